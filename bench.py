@@ -1,0 +1,194 @@
+#!/usr/bin/env python
+"""Two-tower training-step benchmark on MI355X (driver contract: one JSON line from rank 0).
+
+Workload (BASELINE.json configs[2], C3): V = 200k, E = H = d = 256, L = 64, B = 8192 queries per
+GPU, each with one positive and one negative document (MS-MARCO-shaped synthetic ids resident
+in HBM), tied mean-pool towers, in-batch sampled softmax over all 2B documents of the step
+(candidates all-gathered across ranks when N > 1: configs[3], C4) on the bf16 MFMA scorer,
+fp32 embedding gradient, AdamW over every parameter.  A step = forward (3 towers) + loss +
+backward + gradient sync + optimizer step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import twotower_amd as tt  # noqa: E402
+from twotower_amd import _lib  # noqa: E402
+
+CONFIGS = {
+    # name: V, E(=H), L, B, scorer dtype
+    "c3": dict(V=200_000, d=256, L=64, B=8192, dtype="bf16", workload="C3: vocab 200k, d 256, seq 64, batch 8192, "
+               "in-batch negatives (M = 2B), bf16 MFMA scorer, fp32 embedding grad"),
+    "c2": dict(V=50_000, d=128, L=32, B=4096, dtype="fp32", workload="C2: vocab 50k, d 128, seq 32, batch 4096, "
+               "in-batch negatives (M = 2B), fp32"),
+}
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--scorer-dtype", default=None, help="override: fp32 | bf16 | bf16_fast")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-batch", type=int, default=1024)
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank
+
+
+def main():
+    args = parse()
+    world, rank = setup_dist()
+    cfg = CONFIGS[args.config]
+    V, d, L, B = cfg["V"], cfg["d"], cfg["L"], cfg["B"]
+    scorer_dtype = args.scorer_dtype or cfg["dtype"]
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=d)
+    model = tt.build_two_tower("mean", emb, hidden_dim=d, tied_weights=True).to(dev)
+    loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
+                              cross_device_negatives=world > 1)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=world == 1, tables=[emb])
+    step = tt.TrainStep(model, loss_fn, opt)
+
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev) for k in range(4)]
+    nnz = sum(int((t > 0).sum()) for b in batches for t in b) / len(batches)  # tokens per step
+
+    for k in range(args.warmup):
+        step(*batches[k % len(batches)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    _lib.TIMER.reset()
+    _lib.TIMER.enabled = True
+    t0 = time.perf_counter()
+    loss = None
+    for k in range(args.steps):
+        loss = step(*batches[k % len(batches)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _lib.TIMER.enabled = False
+    ops_t = _lib.TIMER.summary()
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = B * world * args.steps / elapsed
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    # ---- per-op device times (HIP events on the launch stream) -> rooflines
+    nseq = 3 * B
+    M = 2 * B * world
+    kernels = []
+
+    def add(name, key, algo, unit, peak, bound, per_launch_note):
+        if key not in ops_t:
+            return
+        ms = ops_t[key]["mean_ms"]
+        achieved = algo / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+        kernels.append({"op": name, "abi": key, "bound": bound, "mean_ms": round(ms, 4),
+                        "calls_per_step": ops_t[key]["calls"] / args.steps, "achieved": round(achieved, 2),
+                        "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "algorithmic": algo,
+                        "per_launch": per_launch_note})
+
+    id_bytes = 4  # int32 ids on device
+    add("embedding bag forward (gather + masked mean)", "tt_bag_mean_fwd",
+        nseq * L * id_bytes + nnz * d * 4 + nseq * d * 4 + nseq * 4, "GB/s", HBM_PEAK_GBS, "hbm",
+        "ids N*L*4 + gathered rows nnz*E*4 + pooled N*E*4 + denom N*4 bytes")
+    add("embedding bag backward fused with table AdamW", "tt_bag_mean_bwd_adamw",
+        nseq * d * 4 + nseq * (L + 1) * 4 + 24 * V * d, "GB/s", HBM_PEAK_GBS, "hbm",
+        "d_pooled N*E*4 + ids/denom N*(L+1)*4 + AdamW p,m,v read+write 24*V*E bytes")
+    add("embedding bag backward (dense grad)", "tt_bag_mean_bwd",
+        nseq * d * 4 + nseq * (L + 1) * 4 + 2 * V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
+        "d_pooled + ids/denom + V*E*4 grad write + its read")
+    pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
+    add("in-batch scorer forward (S=QD^T, lse, P.D)", "tt_inbatch_fwd", 2.0 * B * M * d, "TFLOP/s", pk, "mfma",
+        "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ")
+    add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
+        "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q)")
+    add("dense AdamW (tower FF)", "tt_adamw", 28 * sum(p.numel() for n_, p in model.named_parameters()
+                                                      if "embedding" not in n_), "GB/s", HBM_PEAK_GBS, "hbm",
+        "28 bytes per parameter")
+    dominant = max(kernels, key=lambda k: k["mean_ms"] * k["calls_per_step"]) if kernels else None
+    roofline = None
+    if dominant:
+        roofline = {"bound": dominant["bound"], "achieved": dominant["achieved"], "peak": dominant["peak"],
+                    "unit": dominant["unit"], "frac": dominant["frac"], "traffic": None, "op": dominant["op"]}
+    gather = next((k for k in kernels if k["abi"] == "tt_bag_mean_fwd"), None)
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle.cpu_step import time_cpu_step  # CPU baseline only: the measured GPU path never uses it
+
+        cb = args.cpu_batch
+        cpu_batches = [tuple(t[:cb].to("cpu", torch.int64) for t in b) for b in batches[:2]]
+        r = time_cpu_step(V, d, d, cpu_batches, loss="in_batch", min_seconds=args.cpu_seconds)
+        cpu = {"value": round(r["pairs_per_s"], 1), "unit": "pairs/s", "cores": r["threads"], "kind": "port",
+               "sample": f"torch-CPU restatement of the reference step (oracle/cpu_step.py), same V/d/L, batch "
+                         f"{cb} instead of {B}, in-batch loss fp32, {r['steps']} steps in {r['seconds']:.1f}s"}
+
+    line = {
+        "metric": "(query,doc) pairs/sec whole node at B=8192 d=256; HBM GB/s on embed gather",
+        "value": round(value, 1),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if scorer_dtype != "fp32" else "fp32",
+        "data": "synthetic MS-MARCO-shaped id triplets (q 3-12 tokens, docs L/2-L), random-init weights",
+        "config": {"workload": cfg["workload"] + ("; candidates all-gathered over ranks" if world > 1 else ""),
+                   "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
+                   "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype},
+        "gather_hbm_gbs": gather["achieved"] if gather else None,
+        "roofline": roofline,
+        "kernels": kernels,
+        "cpu_baseline": cpu,
+        "final_loss": float(loss.item()) if loss is not None else None,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+/*
+ * twotower_amd.h — C ABI of the MI355X (gfx950) two-tower training-step library
+ * (libtwotower_amd.so).
+ *
+ * Every entry point replaces one device op that the reference (k0r1g/two-towers, pure
+ * PyTorch) reaches through ATen on its hot path.  The reference has no FFI of its own;
+ * the Python host package `twotower_amd` binds these symbols with ctypes behind the
+ * reference's plugin surface (BaseEmbedding / BaseTower / LOSS_REGISTRY).  Each
+ * declaration cites the reference call site it replaces.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers owned by the caller (PyTorch's caching allocator).
+ *     The library never allocates; scratch comes in through `ws`/`ws_bytes`.
+ *   - `stream` is the caller's hipStream_t (the torch current stream); every launch is
+ *     asynchronous on it, nothing synchronises, so calls are graph-capturable.
+ *   - Return value: 0 = success; > 0 = hipError_t of a failed launch; < 0 = TT_ERR_*
+ *     argument validation failure.  tt_last_error() returns the thread's last message.
+ *   - fp32 matrices are row-major, contiguous (leading dimension = row length) unless a
+ *     leading-dimension argument says otherwise.
+ */
+#ifndef TWOTOWER_AMD_H
+#define TWOTOWER_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* tt_stream_t; /* layout-compatible with hipStream_t */
+
+enum tt_status { TT_OK = 0, TT_ERR_INVALID = -1, TT_ERR_WORKSPACE = -2, TT_ERR_UNSUPPORTED = -3 };
+enum tt_index_dtype { TT_IDS_I32 = 0, TT_IDS_I64 = 1 };
+enum tt_compute_dtype { TT_F32 = 0, TT_BF16 = 1, TT_BF16_FAST = 2 };
+enum tt_scatter_mode {
+  TT_SCATTER_SORTED = 0, /* deterministic: stable radix sort + segmented row reduce; writes every row */
+  TT_SCATTER_ATOMIC = 1  /* global_atomic_add_f32 into caller-zeroed grad; order-dependent */
+};
+
+/* ---- library ------------------------------------------------------------------ */
+int tt_version(void);
+const char* tt_last_error(void);
+
+/* ---- embedding bag: lookup + masked mean-pool -----------------------------------
+ * Replaces, per tower call:
+ *   LookupEmbedding.forward  -> nn.Embedding(V,E,padding_idx=0)(ids)   twotower/embeddings.py:30,40
+ *   MeanPoolingTower.forward  mask=(ids>0) :62, emb*mask :67, sum(1)/(mask.sum(1)+1e-9) :72
+ *                                                                    twotower/encoders.py:62-72
+ * pooled[s,:] = sum_{t: ids[s,t]>0} table[ids[s,t],:] / denom[s],  denom[s] = count + 1e-9f.
+ * ids are (nseq, L) with row stride ld_ids elements, int32 or int64 (the reference feeds int64,
+ * twotower/dataset.py:274-278).  Ids >= V are treated as masked (the reference raises). */
+int tt_bag_mean_fwd(const float* table, int64_t V, int E,
+                    const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                    float* pooled, float* denom, tt_stream_t stream);
+
+/* Backward of the above w.r.t. the table (autograd of encoders.py:67-72 +
+ * embedding_dense_backward with padding_idx, reached from twotower/train.py:138):
+ *   G[id,:] += d_pooled[s,:] / denom[s] for every token with 0 < id < V, id != padding_idx.
+ * TT_SCATTER_SORTED overwrites all V rows of grad_table (untouched rows -> 0);
+ * TT_SCATTER_ATOMIC accumulates into grad_table (caller zeroes it; ws may be NULL). */
+size_t tt_bag_mean_bwd_ws_size(int64_t nseq, int L, int64_t V, int E);
+int tt_bag_mean_bwd(const float* d_pooled, const float* denom,
+                    const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                    int64_t V, int E, int64_t padding_idx, float* grad_table, int mode,
+                    void* ws, size_t ws_bytes, tt_stream_t stream);
+
+/* Sorted scatter fused with a dense AdamW step on the table (exactly the math of
+ * tt_bag_mean_bwd(SORTED) followed by tt_adamw on the table, without materialising G):
+ * replaces embedding_dense_backward + torch.optim.AdamW.step for the table,
+ * twotower/train.py:138-139,359.  Every row is updated (rows without tokens see g = 0). */
+int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom,
+                          const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                          int64_t V, int E, int64_t padding_idx,
+                          float* table, float* exp_avg, float* exp_avg_sq,
+                          float lr, float beta1, float beta2, float eps, float weight_decay,
+                          int64_t step, void* ws, size_t ws_bytes, tt_stream_t stream);
+
+/* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
+ * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
+ * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps).   step is 1-based. */
+int tt_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+             float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
+             tt_stream_t stream);
+
+/* ---- row L2 normalise (F.normalize(x, dim=-1), eps 1e-12; twotower/encoders.py:77) -- */
+int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, tt_stream_t stream);
+int tt_l2norm_bwd(const float* dout, const float* out, const float* norm, int64_t rows, int H,
+                  float* dx, tt_stream_t stream);
+
+/* ---- triplet hinge on cosine (contrastive_triplet_loss, twotower/losses.py:9-44) ----
+ * loss = mean_i relu(margin - cos(q_i,p_i) + cos(q_i,n_i)), cosine eps 1e-8.
+ * fwd writes loss_rows[B] and loss[1]; bwd reads the upstream scalar grad from grad_loss
+ * (device) and writes dq, dp, dn. */
+int tt_triplet_fwd(const float* q, const float* p, const float* n, int64_t B, int H,
+                   float margin, float* loss_rows, float* loss, tt_stream_t stream);
+int tt_triplet_bwd(const float* q, const float* p, const float* n, int64_t B, int H,
+                   float margin, const float* grad_loss, float* dq, float* dp, float* dn,
+                   tt_stream_t stream);
+
+/* ---- InfoNCE with N negatives (multiple_negatives_loss, twotower/losses.py:47-85) ----
+ * logits[i,k] = cos(q_i, [p_i, negs_i,0..N-1][k]) / tau; loss = mean_i CE(logits_i, 0). */
+int tt_multi_neg_fwd(const float* q, const float* p, const float* negs, int64_t B, int N, int H,
+                     float inv_tau, float* loss_rows, float* loss, tt_stream_t stream);
+int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t B, int N, int H,
+                     float inv_tau, const float* grad_loss, float* dq, float* dp, float* dnegs,
+                     tt_stream_t stream);
+
+/* ---- in-batch sampled softmax (in_batch_sampled_softmax_loss, twotower/losses.py:88-118)
+ * S = q d^T (B x M, never materialised), logits = S * inv_tau, label of row i is column
+ * i + label_off (reference: arange(B), label_off = 0; data-parallel: rank * local M).
+ * loss = mean_i (lse_i - logits[i, i+label_off]).
+ * compute dtype TT_F32 (exact fp32 MFMA), TT_BF16 (bf16 operands, P split hi+lo bf16 so the
+ * second product keeps ~16 mantissa bits) or TT_BF16_FAST (P rounded once to bf16).
+ * fwd (want_grad != 0) also leaves dq_unscaled = sum_j P_ij d~_j - d~_label (B x H) so the
+ * backward needs only the dD pass.  ws must stay untouched between fwd and bwd. */
+size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype);
+int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+                   float inv_tau, int64_t label_off, int want_grad,
+                   float* lse, float* loss_rows, float* loss, float* dq_unscaled,
+                   void* ws, size_t ws_bytes, tt_stream_t stream);
+/* dq = grad_loss[0]*grad_scale*inv_tau*dq_unscaled;
+ * dd[j] = grad_loss[0]*grad_scale*inv_tau * sum_i (P_ij - [j == i+label_off]) q~_i.
+ * grad_scale is 1/B for the reference's mean reduction. */
+int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+                   float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
+                   const float* grad_loss, float grad_scale, float* dq, float* dd,
+                   void* ws, size_t ws_bytes, tt_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TWOTOWER_AMD_H */

@@ -1,0 +1,68 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py): the CPU baseline.
+
+A torch-on-CPU restatement of the reference's training step exactly as the reference computes
+it (twotower/train.py:120-139 driving embeddings.py:30,40, encoders.py:62-77, losses.py,
+torch.optim.AdamW): nn.Embedding gather -> mask multiply -> sum / (count + 1e-9) ->
+Linear-ReLU-Linear -> F.normalize, the loss, dense backward, dense AdamW.  bench.py times it on
+the GPU box's host cores as `cpu_baseline` (kind "port"); the reference source never travels.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class RefTower(nn.Module):
+    def __init__(self, V: int, E: int, H: int):
+        super().__init__()
+        self.embedding = nn.Embedding(V, E, padding_idx=0)              # embeddings.py:30
+        self.feed_forward = nn.Sequential(nn.Linear(E, H), nn.ReLU(), nn.Linear(H, H))  # encoders.py:38-42
+
+    def forward(self, ids):
+        mask = (ids > 0).float().unsqueeze(-1)                           # encoders.py:62
+        emb = self.embedding(ids) * mask                                 # :67
+        pooled = emb.sum(1) / (mask.sum(1) + 1e-9)                       # :72
+        return F.normalize(self.feed_forward(pooled), dim=-1)            # :77
+
+
+def ref_loss(name: str, q, p, n, temperature=0.1, margin=0.2):
+    if name == "triplet":                                                # losses.py:9-44
+        return F.relu(margin - F.cosine_similarity(q, p, dim=1) + F.cosine_similarity(q, n, dim=1)).mean()
+    if name == "in_batch":                                               # losses.py:88-118 on cat[p, n]
+        d = torch.cat([p, n])
+        logits = (q @ d.T) / temperature
+        return F.cross_entropy(logits, torch.arange(q.shape[0]))
+    raise ValueError(name)
+
+
+def time_cpu_step(V: int, E: int, H: int, batches, loss: str = "in_batch", threads: int | None = None,
+                  min_seconds: float = 10.0, max_steps: int = 20) -> dict:
+    """Pairs/s of the reference CPU step on `batches` (list of (q, p, n) int64 CPU tensors)."""
+    if threads:
+        torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    tower = RefTower(V, E, H)
+    opt = torch.optim.AdamW(tower.parameters(), lr=1e-3)
+
+    def step(b):
+        q, p, n = b
+        qv, pv, nv = tower(q), tower(p), tower(n)                        # tied towers (char_tower.yml)
+        loss_v = ref_loss(loss, qv, pv, nv)
+        opt.zero_grad()
+        loss_v.backward()
+        opt.step()
+        return loss_v
+
+    step(batches[0])                                                     # warm-up
+    t0 = time.perf_counter()
+    steps, pairs = 0, 0
+    while steps < max_steps and (time.perf_counter() - t0 < min_seconds or steps < 2):
+        b = batches[steps % len(batches)]
+        step(b)
+        steps += 1
+        pairs += b[0].shape[0]
+    dt = time.perf_counter() - t0
+    return {"pairs_per_s": pairs / dt, "steps": steps, "seconds": dt, "threads": torch.get_num_threads()}

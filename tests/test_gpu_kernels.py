@@ -1,0 +1,318 @@
+"""GPU parity: every HIP kernel (called through the C ABI via twotower_amd.ops) against the CPU
+oracle and the reference's golden vectors.  Tolerances: token-id indexing bit-exact (gathered
+rows / pooled values of single-token bags), fp32 loss and gradients within 1e-5 relative
+(max-abs normalised), bf16 scorer within 1e-4 against the oracle on bf16-rounded inputs
+(hi/lo split G) and 2e-2 for the single-rounding fast variant."""
+import numpy as np
+import pytest
+import torch
+
+import twotower_amd as tt
+from twotower_amd import _lib, ops
+from oracle import reference_math as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().double().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def cuda(x, dtype=None):
+    t = torch.as_tensor(np.asarray(x))
+    return t.to(DEV, dtype=dtype) if dtype is not None else t.to(DEV)
+
+
+def edge_ids(N, L, V, rng, dtype=torch.int64):
+    ids = rng.integers(1, V, size=(N, L))
+    lengths = rng.integers(0, L + 1, size=N)
+    ids[np.arange(L)[None, :] >= lengths[:, None]] = 0
+    if N > 3:
+        ids[0, :] = 0                        # all padding
+        ids[1, ::3] = 0                      # interior zeros
+        ids[2, :] = V - 1                    # last row, repeated
+        ids[3, : min(L, 5)] = 1
+    return cuda(ids, dtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# bag forward / backward
+@pytest.mark.parametrize("E", [16, 64, 128, 256, 512, 100])
+@pytest.mark.parametrize("L,dtype", [(12, torch.int64), (64, torch.int32), (100, torch.int64), (1, torch.int32)])
+def test_bag_forward_vs_oracle(E, L, dtype):
+    rng = np.random.default_rng(E * 1000 + L)
+    V, N = 997, 203
+    table = rng.standard_normal((V, E)).astype(np.float32)
+    ids = edge_ids(N, L, V, rng, dtype)
+    pooled, denom = ops.bag_mean_forward(cuda(table), ids)
+    ref, ref_den = O.bag_mean_fwd(table.astype(np.float64), ids.cpu().numpy())
+    assert rel(pooled, ref) < 1e-6
+    np.testing.assert_allclose(denom.cpu().numpy(), ref_den.astype(np.float32), rtol=0, atol=0)
+    assert torch.count_nonzero(pooled[0]) == 0
+
+
+def test_bag_forward_gather_is_bit_exact():
+    """Single-token bags return the table row bit for bit (index path, no arithmetic drift)."""
+    rng = np.random.default_rng(7)
+    V, E, N, L = 5000, 256, 512, 64
+    table = cuda(rng.standard_normal((V, E)).astype(np.float32))
+    ids = torch.zeros(N, L, dtype=torch.int64, device=DEV)
+    rows = torch.as_tensor(rng.integers(1, V, N), device=DEV)
+    pos = torch.as_tensor(rng.integers(0, L, N), device=DEV)
+    ids[torch.arange(N, device=DEV), pos] = rows
+    pooled, _ = ops.bag_mean_forward(table, ids)
+    assert torch.equal(pooled, table[rows])
+
+
+def test_bag_forward_golden(golden):
+    g = golden("bag_tiny")
+    pooled, denom = ops.bag_mean_forward(cuda(g["table"]), cuda(g["ids"]))
+    assert rel(pooled, g["pooled"]) < 1e-6
+
+
+@pytest.mark.parametrize("E", [64, 128, 256, 48])
+@pytest.mark.parametrize("mode", [_lib.TT_SCATTER_SORTED, _lib.TT_SCATTER_ATOMIC])
+def test_bag_backward_vs_oracle(E, mode):
+    rng = np.random.default_rng(E + 17 * mode)
+    V, N, L = 1500, 333, 40
+    ids = edge_ids(N, L, V, rng)
+    d_pooled = rng.standard_normal((N, E)).astype(np.float32)
+    table = cuda(rng.standard_normal((V, E)).astype(np.float32))
+    _, denom = ops.bag_mean_forward(table, ids)
+    grad = ops.bag_mean_backward(cuda(d_pooled), denom, ids, V, 0, mode)
+    ref = O.bag_mean_bwd(d_pooled.astype(np.float64), denom.double().cpu().numpy(), ids.cpu().numpy(), V, 0)
+    assert rel(grad, ref) < 1e-5
+    assert torch.count_nonzero(grad[0]) == 0
+
+
+def test_bag_backward_sorted_is_deterministic_and_hot_rows():
+    """Char-vocab-like contention (V=34, C1) and a Zipf-hot row: sorted path is bitwise
+    reproducible and matches the oracle."""
+    rng = np.random.default_rng(3)
+    V, N, L, E = 34, 2048, 64, 64
+    ids = cuda(rng.integers(0, V, size=(N, L)))
+    ids[:, :8] = 5                                   # one very hot row
+    d_pooled = cuda(rng.standard_normal((N, E)).astype(np.float32))
+    _, denom = ops.bag_mean_forward(cuda(rng.standard_normal((V, E)).astype(np.float32)), ids)
+    g1 = ops.bag_mean_backward(d_pooled, denom, ids, V, 0, _lib.TT_SCATTER_SORTED)
+    g2 = ops.bag_mean_backward(d_pooled, denom, ids, V, 0, _lib.TT_SCATTER_SORTED)
+    assert torch.equal(g1, g2)
+    ref = O.bag_mean_bwd(d_pooled.double().cpu().numpy(), denom.double().cpu().numpy(), ids.cpu().numpy(), V, 0)
+    assert rel(g1, ref) < 1e-5
+
+
+def test_bag_backward_padding_idx_nonzero():
+    rng = np.random.default_rng(4)
+    V, N, L, E = 300, 64, 16, 64
+    ids = edge_ids(N, L, V, rng)
+    ids[:, 2] = 7
+    d_pooled = rng.standard_normal((N, E)).astype(np.float32)
+    _, denom = ops.bag_mean_forward(cuda(rng.standard_normal((V, E)).astype(np.float32)), ids)
+    grad = ops.bag_mean_backward(cuda(d_pooled), denom, ids, V, 7)
+    ref = O.bag_mean_bwd(d_pooled.astype(np.float64), denom.double().cpu().numpy(), ids.cpu().numpy(), V, 7)
+    assert rel(grad, ref) < 1e-5 and torch.count_nonzero(grad[7]) == 0
+
+
+def test_bag_backward_empty_batch():
+    V, E = 50, 64
+    ids = torch.zeros(0, 8, dtype=torch.int64, device=DEV)
+    grad = ops.bag_mean_backward(torch.zeros(0, E, device=DEV), torch.zeros(0, device=DEV), ids, V, 0)
+    assert grad.shape == (V, E) and torch.count_nonzero(grad) == 0
+
+
+# ---------------------------------------------------------------------------------------------
+# AdamW (dense and fused with the sorted scatter)
+def test_adamw_vs_oracle():
+    rng = np.random.default_rng(5)
+    n = 10007
+    p, g = rng.standard_normal(n), rng.standard_normal(n)
+    m, v = rng.standard_normal(n) * 0.1, np.abs(rng.standard_normal(n)) * 0.01
+    P, G, Mt, Vt = (cuda(x.astype(np.float32)) for x in (p, g, m, v))
+    ops.adamw_step(P, G, Mt, Vt, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, step=7)
+    rp, rm, rv = O.adamw(p, g, m, v, 7)
+    assert rel(P, rp) < 1e-6 and rel(Mt, rm) < 1e-6 and rel(Vt, rv) < 1e-6
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(0)
+    w1 = torch.randn(513, 77, device=DEV, requires_grad=True)
+    w2 = torch.nn.Parameter(w1.detach().clone())
+    o1 = torch.optim.AdamW([w1], lr=1e-3)
+    o2 = tt.optim.AdamW([w2], lr=1e-3)
+    for _ in range(3):
+        g = torch.randn_like(w1)
+        w1.grad, w2.grad = g.clone(), g.clone()
+        o1.step()
+        o2.step()
+    assert rel(w2, w1) < 1e-6
+    assert set(o2.state[w2].keys()) == set(o1.state[w1].keys())
+
+
+@pytest.mark.parametrize("E", [64, 256])
+def test_fused_table_adamw_equals_dense_path(E):
+    rng = np.random.default_rng(6)
+    V, N, L = 4000, 300, 32
+    ids = edge_ids(N, L, V, rng)
+    t0 = rng.standard_normal((V, E)).astype(np.float32)
+    d_pooled = cuda(rng.standard_normal((N, E)).astype(np.float32))
+    A, B = cuda(t0), cuda(t0)
+    mA, vA = torch.zeros_like(A), torch.zeros_like(A)
+    mB, vB = torch.zeros_like(B), torch.zeros_like(B)
+    _, denom = ops.bag_mean_forward(A, ids)
+    for step in (1, 2):
+        grad = ops.bag_mean_backward(d_pooled, denom, ids, V, 0)
+        ops.adamw_step(A, grad, mA, vA, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, step=step)
+        ops.bag_mean_backward_adamw(d_pooled, denom, ids, B, mB, vB, 0, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
+                                    weight_decay=0.01, step=step)
+    assert torch.equal(A, B) and torch.equal(mA, mB) and torch.equal(vA, vB)
+
+
+# ---------------------------------------------------------------------------------------------
+# normalize + per-sample losses
+def test_l2norm_vs_oracle():
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((257, 128)).astype(np.float32)
+    x[3] = 0.0
+    dout = rng.standard_normal(x.shape).astype(np.float32)
+    X = cuda(x).requires_grad_(True)
+    out = ops.l2_normalize(X)
+    out.backward(cuda(dout))
+    ro, _ = O.l2norm_fwd(x.astype(np.float64))
+    assert rel(out, ro) < 1e-6
+    assert rel(X.grad, O.l2norm_bwd(dout.astype(np.float64), x.astype(np.float64))) < 1e-5
+
+
+def test_triplet_golden(golden):
+    g = golden("losses")
+    q, p, n = (cuda(g[k]).requires_grad_(True) for k in ("tri_q", "tri_p", "tri_n"))
+    loss = tt.losses.contrastive_triplet_loss(q, p, n, margin=float(g["tri_margin"]))
+    loss.backward()
+    assert abs(loss.item() - g["tri_loss"]) < 1e-5
+    assert rel(q.grad, g["tri_dq"]) < 1e-5 and rel(p.grad, g["tri_dp"]) < 1e-5 and rel(n.grad, g["tri_dn"]) < 1e-5
+
+
+def test_multiple_negatives_golden(golden):
+    g = golden("losses")
+    q, p, negs = (cuda(g[k]).requires_grad_(True) for k in ("mn_q", "mn_p", "mn_negs"))
+    loss = tt.losses.multiple_negatives_loss(q, p, negs, temperature=float(g["mn_tau"]))
+    loss.backward()
+    assert abs(loss.item() - g["mn_loss"]) < 1e-5
+    assert rel(q.grad, g["mn_dq"]) < 1e-5 and rel(p.grad, g["mn_dp"]) < 1e-5 and rel(negs.grad, g["mn_dnegs"]) < 1e-5
+
+
+# ---------------------------------------------------------------------------------------------
+# in-batch scorer
+def test_in_batch_golden(golden):
+    g = golden("losses")
+    for tag in ("ib8", "ib16"):
+        q, d = cuda(g[f"{tag}_q"]).requires_grad_(True), cuda(g[f"{tag}_d"]).requires_grad_(True)
+        loss = tt.losses.in_batch_sampled_softmax_loss(q, d, temperature=0.1)
+        loss.backward()
+        assert abs(loss.item() - g[f"{tag}_loss"]) < 1e-5 * max(1, abs(g[f"{tag}_loss"])), tag
+        assert rel(q.grad, g[f"{tag}_dq"]) < 1e-5 and rel(d.grad, g[f"{tag}_dd"]) < 1e-5, tag
+
+
+def _unit(rng, n, H):
+    x = rng.standard_normal((n, H))
+    return (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
+
+
+@pytest.mark.parametrize("H", [64, 128, 256])
+@pytest.mark.parametrize("B,M,off", [(300, 700, 0), (129, 129, 0), (64, 256, 128), (1000, 2000, 1000)])
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "bf16_fast"])
+def test_in_batch_vs_oracle(H, B, M, off, dt):
+    rng = np.random.default_rng(H + B + M)
+    q, d = _unit(rng, B, H), _unit(rng, M, H)
+    if dt != "fp32":   # the bf16 kernels score bf16-rounded operands: so does the oracle
+        q = torch.as_tensor(q).bfloat16().float().numpy()
+        d = torch.as_tensor(d).bfloat16().float().numpy()
+    Q, D = cuda(q).requires_grad_(True), cuda(d).requires_grad_(True)
+    loss = ops.InBatchSoftmaxLoss.apply(Q, D, 10.0, off, dt, None)
+    g = 0.7
+    loss.backward(torch.tensor(g, device=DEV))
+    rl, (rdq, rdd), _ = O.in_batch_fwd_bwd(q.astype(np.float64), d.astype(np.float64), 0.1, g=g, label_off=off)
+    tol = {"fp32": 1e-5, "bf16": 1e-4, "bf16_fast": 2e-2}[dt]
+    assert abs(loss.item() - rl) < 1e-5 * max(1.0, abs(rl))
+    assert rel(Q.grad, rdq) < tol and rel(D.grad, rdd) < tol
+
+
+def test_in_batch_three_tensor_form_and_zero_copy_candidates():
+    rng = np.random.default_rng(11)
+    B, H = 96, 128
+    allv = cuda(_unit(rng, 3 * B, H)).requires_grad_(True)
+    q, p, n = torch.split(allv, B)
+    loss = tt.losses.build("in_batch", temperature=0.1)(q, p, n)
+    loss.backward()
+    a = allv.detach().double().cpu().numpy()
+    rl, (rdq, rdd), _ = O.in_batch_fwd_bwd(a[:B], a[B:], 0.1)
+    assert abs(loss.item() - rl) < 1e-5
+    assert rel(allv.grad[:B], rdq) < 1e-5 and rel(allv.grad[B:], rdd) < 1e-5
+
+
+def test_in_batch_reports_underflow_as_nan():
+    """Huge-norm rows whose shift bound is far above the true max fail loudly (NaN), never silently."""
+    H = 64
+    q = torch.zeros(4, H, device=DEV)
+    q[:, 0] = -1000.0
+    d = torch.zeros(8, H, device=DEV)
+    d[:, 0] = 1.0
+    d[0, 1] = 1000.0
+    loss = ops.in_batch_softmax_loss(q, d, 0.1)
+    assert torch.isnan(loss)
+
+
+# ---------------------------------------------------------------------------------------------
+# whole model vs the reference's captured step
+def _model_from_fixture(g, V, E, H):
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=H, tied_weights=True).to(DEV)
+    t = model.query_tower
+    with torch.no_grad():
+        t.embedding.embedding.weight.copy_(cuda(g["table"]))
+        t.feed_forward[0].weight.copy_(cuda(g["W1"]))
+        t.feed_forward[0].bias.copy_(cuda(g["b1"]))
+        t.feed_forward[2].weight.copy_(cuda(g["W2"]))
+        t.feed_forward[2].bias.copy_(cuda(g["b2"]))
+    return model
+
+
+@pytest.mark.parametrize("optimizer", ["torch", "tt", "tt_fused"])
+def test_c1_step_matches_reference(golden, optimizer):
+    g = golden("c1_step")
+    V = int(g["V"])
+    model = _model_from_fixture(g, V, 64, 128)
+    t = model.query_tower
+    if optimizer == "torch":
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    else:
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=optimizer == "tt_fused", tables=[t.embedding])
+    loss_fn = tt.losses.build("triplet", margin=0.2)
+    q, p, n = cuda(g["q"]), cuda(g["p"]), cuda(g["n"])
+    qv, pv, nv = model(q, p, n)
+    loss = loss_fn(qv, pv, nv)
+    opt.zero_grad()
+    loss.backward()
+    assert abs(loss.item() - g["loss"]) < 1e-5
+    assert rel(qv, g["qv"]) < 1e-5 and rel(nv, g["nv"]) < 1e-5
+    if optimizer != "tt_fused":
+        assert rel(t.embedding.embedding.weight.grad, g["g_table"]) < 1e-5
+        assert rel(t.feed_forward[0].weight.grad, g["g_W1"]) < 1e-5
+    opt.step()
+    assert rel(t.embedding.embedding.weight, g["after_table"]) < 1e-5
+    assert rel(t.feed_forward[2].weight, g["after_W2"]) < 1e-5
+
+
+def test_trajectory_matches_reference(golden):
+    g = golden("trajectory")
+    model = _model_from_fixture(g, g["table"].shape[0], g["table"].shape[1], g["W1"].shape[0])
+    t = model.query_tower
+    opt = tt.optim.AdamW(model.parameters(), lr=float(g["lr"]), fused_tables=True, tables=[t.embedding])
+    step = tt.TrainStep(model, tt.losses.build("triplet", margin=0.2), opt)
+    for s in range(3):
+        loss = step(cuda(g[f"q{s}"]), cuda(g[f"p{s}"]), cuda(g[f"n{s}"]))
+        assert abs(loss.item() - g[f"loss{s}"]) < 1e-5
+        assert rel(t.embedding.embedding.weight, g[f"step{s}_table"]) < 1e-5
+        assert rel(t.feed_forward[0].weight, g[f"step{s}_W1"]) < 1e-5

@@ -1,0 +1,159 @@
+"""ctypes binding of libtwotower_amd.so (the C ABI declared in include/twotower_amd.h).
+
+The product path has no fallback: if the shared library is missing, or a tensor is not on a
+GPU, the call raises.  Torch only supplies device memory and the current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwotower_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "twotower_amd.h")
+
+TT_IDS_I32, TT_IDS_I64 = 0, 1
+TT_F32, TT_BF16, TT_BF16_FAST = 0, 1, 2
+TT_SCATTER_SORTED, TT_SCATTER_ATOMIC = 0, 1
+
+COMPUTE_DTYPES = {"fp32": TT_F32, "float32": TT_F32, "bf16": TT_BF16, "bfloat16": TT_BF16,
+                  "bf16_fast": TT_BF16_FAST}
+
+_c_i64, _c_int, _c_f32, _c_sz, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+
+# name -> (restype, argtypes); must mirror include/twotower_amd.h
+_SIGNATURES = {
+    "tt_version": (_c_int, []),
+    "tt_last_error": (ctypes.c_char_p, []),
+    "tt_bag_mean_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _c_int, _c_i64, _c_int, _c_i64, _vp, _vp, _vp]),
+    "tt_bag_mean_bwd_ws_size": (_c_sz, [_c_i64, _c_int, _c_i64, _c_int]),
+    "tt_bag_mean_bwd": (_c_int, [_vp, _vp, _vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp, _c_int,
+                                 _vp, _c_sz, _vp]),
+    "tt_bag_mean_bwd_adamw": (_c_int, [_vp, _vp, _vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp,
+                                       _vp, _vp, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_i64, _vp, _c_sz, _vp]),
+    "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_i64, _vp]),
+    "tt_l2norm_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
+    "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),
+    "tt_triplet_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp]),
+    "tt_triplet_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
+    "tt_multi_neg_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp]),
+    "tt_multi_neg_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
+    "tt_inbatch_ws_size": (_c_sz, [_c_i64, _c_i64, _c_int, _c_int]),
+    "tt_inbatch_fwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp, _vp, _vp,
+                                _vp, _c_sz, _vp]),
+    "tt_inbatch_bwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
+                                _vp, _vp, _c_sz, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function the public header declares (used by the ABI export test)."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(tt_\w+)\s*\(", text, flags=re.M)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library once.  Raises if it was not built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"twotower_amd: {LIB_PATH} is missing; build it with `make -C twotower_amd/csrc` "
+                    "(or __graft_entry__.build()).  There is no CPU fallback.")
+            cdll = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in _SIGNATURES.items():
+                fn = getattr(cdll, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = cdll
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().tt_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"twotower_amd: {name} failed (code {rc}): {last_error()}")
+
+
+class OpTimer:
+    """Optional HIP-event bracketing of every C-ABI call on the torch current stream (the stream
+    the call launches on).  bench.py enables it over the timed region to get live per-op device
+    times for the roofline figures."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events: dict[str, list] = {}
+
+    def reset(self):
+        self.events = {}
+
+    def run(self, name: str, fn):
+        if not self.enabled:
+            return fn()
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        rc = fn()
+        end.record()
+        self.events.setdefault(name, []).append((start, end))
+        return rc
+
+    def summary(self) -> dict[str, dict]:
+        torch.cuda.synchronize()
+        out = {}
+        for name, evs in self.events.items():
+            ms = [s.elapsed_time(e) for s, e in evs]
+            out[name] = {"calls": len(ms), "mean_ms": sum(ms) / len(ms), "total_ms": sum(ms)}
+        return out
+
+
+TIMER = OpTimer()
+
+
+def call(name: str, *args) -> None:
+    fn = getattr(lib(), name)
+    check(TIMER.run(name, lambda: fn(*args)), name)
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_gpu(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("twotower_amd: the HIP kernels need GPU tensors (no CPU fallback); "
+                               f"got a tensor on {t.device}")
+
+
+def ids_dtype_code(ids: torch.Tensor) -> int:
+    if ids.dtype == torch.int64:
+        return TT_IDS_I64
+    if ids.dtype == torch.int32:
+        return TT_IDS_I32
+    raise TypeError(f"token ids must be int32 or int64, got {ids.dtype}")
+
+
+def compute_dtype_code(name) -> int:
+    if isinstance(name, int):
+        return name
+    key = str(name).lower()
+    if key not in COMPUTE_DTYPES:
+        raise ValueError(f"unknown compute_dtype {name!r}; choose one of {sorted(COMPUTE_DTYPES)}")
+    return COMPUTE_DTYPES[key]

@@ -1,0 +1,512 @@
+// Embedding bag on gfx950: lookup + masked mean-pool forward, sorted / atomic scatter-add
+// backward, and the sorted backward fused with a dense AdamW step on the table.
+//
+// Reference semantics (k0r1g/two-towers):
+//   twotower/embeddings.py:30,40  nn.Embedding(V, E, padding_idx=0)(ids)
+//   twotower/encoders.py:62       mask = (ids > 0).float()
+//   twotower/encoders.py:67       emb = embedding(ids) * mask
+//   twotower/encoders.py:72       pooled = emb.sum(1) / (mask.sum(1) + 1e-9)
+//   backward (twotower/train.py:138): G[id] += dpooled[s] / denom[s] for non-pad tokens,
+//   dense V x E gradient, padding row excluded (embedding_dense_backward).
+//
+// Layout: the table is V x E fp32 row-major (1 KiB rows at E = 256).  A wavefront owns a
+// sequence (forward) or a table row (backward).  Each lane moves 16 B per row-load so a
+// wave-instruction reads 64 x 16 B = 1 KiB: one E=256 row, two E=128 rows or four E=64 rows.
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "common.hpp"
+
+namespace tt {
+namespace {
+
+constexpr int kBlock = 256;                 // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// ---------------------------------------------------------------------------------------
+// Forward: one wave per sequence.  LPR lanes cover one row with NV float4 each
+// (E = 4 * LPR * NV); RPI = 64 / LPR rows are in flight per wave-instruction and U such
+// instructions are issued before the adds, so each wave keeps U * 1 KiB of gathers in flight.
+// Token order is preserved per sub-row (sequential adds), sub-rows are folded at the end.
+template <typename IdT, int LPR, int NV, int U>
+__global__ __launch_bounds__(kBlock) void bag_fwd_kernel(
+    const float* __restrict__ table, int64_t V, int E, const IdT* __restrict__ ids, int64_t nseq,
+    int L, int64_t ld, float* __restrict__ pooled, float* __restrict__ denom) {
+  constexpr int RPI = kWave / LPR;
+  const int lane = lane_id();
+  const int64_t seq = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (seq >= nseq) return;  // wave-uniform
+  const int sub = lane / LPR, c = lane % LPR;
+  const IdT* rid = ids + seq * ld;
+
+  f32x4 acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int cnt = 0;
+
+  for (int base = 0; base < L; base += kWave) {
+    const int t = base + lane;
+    const int64_t id = (t < L) ? (int64_t)rid[t] : 0;
+    const bool valid = id > 0 && id < V;
+    const int id32 = valid ? (int)id : 0;
+    uint64_t m = __ballot(valid);
+    cnt += __popcll(m);
+    while (m) {
+      int pos[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        int mine = -1;
+#pragma unroll
+        for (int s = 0; s < RPI; ++s) {
+          if (m) {
+            const int q = __builtin_ctzll(m);
+            m &= m - 1;
+            if (s == sub) mine = q;
+          }
+        }
+        pos[u] = mine;
+      }
+      f32x4 v[U][NV];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        int r;
+        if constexpr (RPI == 1) {
+          r = __builtin_amdgcn_readlane(id32, pos[u] < 0 ? 0 : pos[u]);
+        } else {
+          r = __shfl(id32, pos[u] < 0 ? 0 : pos[u]);
+        }
+        const f32x4* rowp = reinterpret_cast<const f32x4*>(table + (int64_t)r * E);
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          v[u][k] = (pos[u] >= 0) ? rowp[k * LPR + c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) acc[k] += v[u][k];
+    }
+  }
+  if constexpr (RPI > 1) {
+#pragma unroll
+    for (int o = LPR; o < kWave; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        acc[k][0] += __shfl_xor(acc[k][0], o);
+        acc[k][1] += __shfl_xor(acc[k][1], o);
+        acc[k][2] += __shfl_xor(acc[k][2], o);
+        acc[k][3] += __shfl_xor(acc[k][3], o);
+      }
+  }
+  const float den = (float)cnt + 1e-9f;  // mask.sum(1) + 1e-9, encoders.py:72
+  if (sub == 0) {
+    f32x4* out = reinterpret_cast<f32x4*>(pooled + seq * E);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k * LPR + c] = acc[k] / den;
+  }
+  if (lane == 0) denom[seq] = den;
+}
+
+// Any E: lanes stride the columns, tokens are walked one at a time (wave-uniform row).
+template <typename IdT>
+__global__ __launch_bounds__(kBlock) void bag_fwd_generic_kernel(
+    const float* __restrict__ table, int64_t V, int E, const IdT* __restrict__ ids, int64_t nseq,
+    int L, int64_t ld, float* __restrict__ pooled, float* __restrict__ denom) {
+  const int lane = lane_id();
+  const int64_t seq = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (seq >= nseq) return;
+  const IdT* rid = ids + seq * ld;
+  int cnt = 0;
+  for (int base = 0; base < L; base += kWave) {
+    const int t = base + lane;
+    const int64_t id = (t < L) ? (int64_t)rid[t] : 0;
+    cnt += __popcll(__ballot(id > 0 && id < V));
+  }
+  const float den = (float)cnt + 1e-9f;
+  for (int c0 = 0; c0 < E; c0 += kWave) {
+    const int c = c0 + lane;
+    float acc = 0.f;
+    for (int base = 0; base < L; base += kWave) {
+      const int t = base + lane;
+      const int64_t id = (t < L) ? (int64_t)rid[t] : 0;
+      const bool valid = id > 0 && id < V;
+      const int id32 = valid ? (int)id : 0;
+      uint64_t m = __ballot(valid);
+      while (m) {
+        const int q = __builtin_ctzll(m);
+        m &= m - 1;
+        const int r = __builtin_amdgcn_readlane(id32, q);
+        if (c < E) acc += table[(int64_t)r * E + c];
+      }
+    }
+    if (c < E) pooled[seq * E + c] = acc / den;
+  }
+  if (lane == 0) denom[seq] = den;
+}
+
+// ---------------------------------------------------------------------------------------
+// Backward, sorted (deterministic) path.
+// prep: per sequence, emit (key = row id or V for masked, value = seq) for each token and the
+// scaled row gs[s] = dpooled[s] / denom[s] (the division autograd applies, encoders.py:72).
+template <typename IdT>
+__global__ __launch_bounds__(kBlock) void bag_bwd_prep_kernel(
+    const float* __restrict__ dpooled, const float* __restrict__ denom, const IdT* __restrict__ ids,
+    int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, int E,
+    uint32_t* __restrict__ keys, int32_t* __restrict__ vals, float* __restrict__ gs) {
+  const int lane = lane_id();
+  const int64_t seq = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (seq >= nseq) return;
+  const IdT* rid = ids + seq * ld;
+  for (int t = lane; t < L; t += kWave) {
+    const int64_t id = (int64_t)rid[t];
+    const bool valid = id > 0 && id < V && id != padding_idx;
+    keys[seq * L + t] = valid ? (uint32_t)id : (uint32_t)V;
+    vals[seq * L + t] = (int32_t)seq;
+  }
+  const float den = denom[seq];
+  const float* src = dpooled + seq * E;
+  float* dst = gs + seq * E;
+  if ((E & 3) == 0) {
+    for (int c = lane; c < E / 4; c += kWave)
+      reinterpret_cast<f32x4*>(dst)[c] = reinterpret_cast<const f32x4*>(src)[c] / den;
+  } else {
+    for (int c = lane; c < E; c += kWave) dst[c] = src[c] / den;
+  }
+}
+
+// Segment bounds of each row id in the sorted key array (rows absent stay [0,0)).
+__global__ __launch_bounds__(kBlock) void bag_bwd_mark_kernel(const uint32_t* __restrict__ keys,
+                                                              int64_t n, uint32_t V,
+                                                              int32_t* __restrict__ seg_start,
+                                                              int32_t* __restrict__ seg_end) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = keys[i];
+  if (k >= V) return;
+  if (i == 0 || keys[i - 1] != k) seg_start[k] = (int32_t)i;
+  if (i == n - 1 || keys[i + 1] != k) seg_end[k] = (int32_t)(i + 1);
+}
+
+// Row reduce: wave owns RPI rows (LPR lanes x NV float4 each); sums gs[seq] over the
+// row's sorted entries (ascending seq => fixed order) and either writes the gradient row or
+// applies AdamW to (table, exp_avg, exp_avg_sq) in place.
+template <int LPR, int NV, int U, bool FUSED>
+__global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
+    const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
+    const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
+    float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
+    float* __restrict__ exp_avg_sq, AdamArgs aa) {
+  constexpr int RPI = kWave / LPR;
+  const int lane = lane_id();
+  const int sub = lane / LPR, c = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  if (row >= V) return;
+  const int st = seg_start[row], en = seg_end[row];
+  f32x4 acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = st; e < en; e += U) {
+    int s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = (e + u < en) ? vals[e + u] : -1;
+    f32x4 v[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f32x4* rp = reinterpret_cast<const f32x4*>(gs + (int64_t)(s[u] < 0 ? 0 : s[u]) * E);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[u][k] = (s[u] >= 0) ? rp[k * LPR + c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] += v[u][k];
+  }
+  if constexpr (!FUSED) {
+    f32x4* out = reinterpret_cast<f32x4*>(grad + row * E);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k * LPR + c] = acc[k];
+  } else {
+    f32x4* pp = reinterpret_cast<f32x4*>(param + row * E);
+    f32x4* mp = reinterpret_cast<f32x4*>(exp_avg + row * E);
+    f32x4* vp = reinterpret_cast<f32x4*>(exp_avg_sq + row * E);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int idx = k * LPR + c;
+      f32x4 p = pp[idx], m = mp[idx], v = vp[idx];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float pj = p[j], mj = m[j], vj = v[j];
+        adam_update(pj, acc[k][j], mj, vj, aa);
+        p[j] = pj;
+        m[j] = mj;
+        v[j] = vj;
+      }
+      pp[idx] = p;
+      mp[idx] = m;
+      vp[idx] = v;
+    }
+  }
+}
+
+// Generic-E row reduce (scalar columns).
+template <bool FUSED>
+__global__ __launch_bounds__(kBlock) void bag_bwd_reduce_generic_kernel(
+    const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
+    const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
+    float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
+    float* __restrict__ exp_avg_sq, AdamArgs aa) {
+  const int lane = lane_id();
+  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (row >= V) return;
+  const int st = seg_start[row], en = seg_end[row];
+  for (int c = lane; c < E; c += kWave) {
+    float acc = 0.f;
+    for (int e = st; e < en; ++e) acc += gs[(int64_t)vals[e] * E + c];
+    if constexpr (!FUSED) {
+      grad[row * E + c] = acc;
+    } else {
+      float p = param[row * E + c], m = exp_avg[row * E + c], v = exp_avg_sq[row * E + c];
+      adam_update(p, acc, m, v, aa);
+      param[row * E + c] = p;
+      exp_avg[row * E + c] = m;
+      exp_avg_sq[row * E + c] = v;
+    }
+  }
+}
+
+// Atomic path: one wave per sequence; lane owns columns lane, lane+64, ... so each
+// global_atomic_add_f32 wave-instruction covers 256 contiguous bytes of the row.
+template <typename IdT>
+__global__ __launch_bounds__(kBlock) void bag_bwd_atomic_kernel(
+    const float* __restrict__ dpooled, const float* __restrict__ denom, const IdT* __restrict__ ids,
+    int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, int E, float* __restrict__ grad) {
+  const int lane = lane_id();
+  const int64_t seq = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (seq >= nseq) return;
+  const IdT* rid = ids + seq * ld;
+  const float den = denom[seq];
+  for (int c0 = 0; c0 < E; c0 += kWave) {
+    const int c = c0 + lane;
+    const float g = (c < E) ? dpooled[seq * E + c] / den : 0.f;
+    for (int base = 0; base < L; base += kWave) {
+      const int t = base + lane;
+      const int64_t id = (t < L) ? (int64_t)rid[t] : 0;
+      const bool valid = id > 0 && id < V && id != padding_idx;
+      const int id32 = valid ? (int)id : 0;
+      uint64_t m = __ballot(valid);
+      while (m) {
+        const int q = __builtin_ctzll(m);
+        m &= m - 1;
+        const int r = __builtin_amdgcn_readlane(id32, q);
+        if (c < E) atomicAdd(grad + (int64_t)r * E + c, g);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side
+int end_bit_for(int64_t V) {
+  int b = 1;
+  while ((int64_t(1) << b) <= V) ++b;  // keys in [0, V] (V = masked sentinel)
+  return b;
+}
+
+struct BwdWs {
+  uint32_t* keys_in;
+  uint32_t* keys_out;
+  int32_t* vals_in;
+  int32_t* vals_out;
+  float* gs;
+  int32_t* seg_start;
+  int32_t* seg_end;
+  void* sort_tmp;
+  size_t sort_bytes;
+  size_t total;
+};
+
+BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes) {
+  BwdWs w{};
+  const size_t n = (size_t)nseq * L;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  char* b = static_cast<char*>(base);
+  const size_t o_ki = take(n * 4), o_ko = take(n * 4), o_vi = take(n * 4), o_vo = take(n * 4);
+  const size_t o_gs = take((size_t)nseq * E * 4);
+  const size_t o_ss = take((size_t)V * 4), o_se = take((size_t)V * 4);
+  const size_t o_tmp = take(sort_bytes);
+  if (b) {
+    w.keys_in = reinterpret_cast<uint32_t*>(b + o_ki);
+    w.keys_out = reinterpret_cast<uint32_t*>(b + o_ko);
+    w.vals_in = reinterpret_cast<int32_t*>(b + o_vi);
+    w.vals_out = reinterpret_cast<int32_t*>(b + o_vo);
+    w.gs = reinterpret_cast<float*>(b + o_gs);
+    w.seg_start = reinterpret_cast<int32_t*>(b + o_ss);
+    w.seg_end = reinterpret_cast<int32_t*>(b + o_se);
+    w.sort_tmp = b + o_tmp;
+  }
+  w.sort_bytes = sort_bytes;
+  w.total = off;
+  return w;
+}
+
+size_t sort_tmp_bytes(int64_t n, int64_t V) {
+  size_t bytes = 0;
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0,
+                                           end_bit_for(V), (hipStream_t)0, false);
+  if (e != hipSuccess) {
+    set_error("rocprim::radix_sort_pairs size query: %s", hipGetErrorString(e));
+    return 0;
+  }
+  return bytes;
+}
+
+template <typename IdT>
+int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nseq, int L, int64_t ld,
+               float* pooled, float* denom, hipStream_t s) {
+  const dim3 grid((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+  switch (E) {
+    case 64: bag_fwd_kernel<IdT, 16, 1, 4><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+    case 128: bag_fwd_kernel<IdT, 32, 1, 4><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+    case 256: bag_fwd_kernel<IdT, 64, 1, 8><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+    case 512: bag_fwd_kernel<IdT, 64, 2, 4><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+    case 1024: bag_fwd_kernel<IdT, 64, 4, 2><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+    default: bag_fwd_generic_kernel<IdT><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+  }
+  TT_LAUNCH_CHECK("tt_bag_mean_fwd");
+  return TT_OK;
+}
+
+template <bool FUSED>
+int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, float* m, float* v,
+                  const AdamArgs& aa, hipStream_t s) {
+  auto grid_for = [&](int rpi) {
+    const int64_t waves = (V + rpi - 1) / rpi;
+    return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+  };
+  const dim3 block(kBlock);
+  switch (E) {
+    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+  }
+  TT_LAUNCH_CHECK("bag_bwd_reduce");
+  return TT_OK;
+}
+
+// prep -> stable radix sort (key = row id, value = seq) -> segment bounds.
+template <typename IdT>
+int sorted_front(const float* dpooled, const float* denom, const IdT* ids, int64_t nseq, int L,
+                 int64_t ld, int64_t V, int64_t padding_idx, int E, const BwdWs& w, hipStream_t s) {
+  const int64_t n = nseq * L;
+  const dim3 block(kBlock);
+  bag_bwd_prep_kernel<IdT><<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block, 0, s>>>(
+      dpooled, denom, ids, nseq, L, ld, V, padding_idx, E, w.keys_in, w.vals_in, w.gs);
+  TT_LAUNCH_CHECK("bag_bwd_prep");
+  size_t tmp = w.sort_bytes;
+  TT_HIP(rocprim::radix_sort_pairs(w.sort_tmp, tmp, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
+                                   (size_t)n, 0, end_bit_for(V), s, false),
+         "rocprim::radix_sort_pairs");
+  TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
+  TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
+  if (n > 0) {
+    bag_bwd_mark_kernel<<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
+        w.keys_out, n, (uint32_t)V, w.seg_start, w.seg_end);
+    TT_LAUNCH_CHECK("bag_bwd_mark");
+  }
+  return TT_OK;
+}
+
+int check_common(int64_t V, int E, const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld) {
+  TT_REQUIRE(V > 0 && V < (int64_t(1) << 31) - 1, "V=%lld out of range", (long long)V);
+  TT_REQUIRE(E > 0, "E=%d must be positive", E);
+  TT_REQUIRE(nseq >= 0 && L >= 0 && ld >= L, "bad ids shape nseq=%lld L=%d ld=%lld", (long long)nseq, L, (long long)ld);
+  TT_REQUIRE(nseq * (int64_t)L < (int64_t(1) << 31), "too many tokens (%lld)", (long long)(nseq * L));
+  TT_REQUIRE(ids_dtype == TT_IDS_I32 || ids_dtype == TT_IDS_I64, "ids_dtype=%d", ids_dtype);
+  TT_REQUIRE(ids != nullptr || nseq * L == 0, "ids is NULL");
+  return TT_OK;
+}
+
+}  // namespace
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" int tt_bag_mean_fwd(const float* table, int64_t V, int E, const void* ids, int ids_dtype,
+                               int64_t nseq, int L, int64_t ld_ids, float* pooled, float* denom,
+                               tt_stream_t stream) {
+  int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
+  if (rc) return rc;
+  TT_REQUIRE(table && pooled && denom, "null pointer");
+  if (nseq == 0) return TT_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ids_dtype == TT_IDS_I32)
+    return launch_fwd(table, V, E, static_cast<const int32_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
+  return launch_fwd(table, V, E, static_cast<const int64_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
+}
+
+extern "C" size_t tt_bag_mean_bwd_ws_size(int64_t nseq, int L, int64_t V, int E) {
+  const size_t sb = sort_tmp_bytes(nseq * (int64_t)L, V);
+  return carve(nullptr, nseq, L, V, E, sb).total + 256;
+}
+
+template <bool FUSED>
+static int bwd_impl(const float* dpooled, const float* denom, const void* ids, int ids_dtype, int64_t nseq,
+                    int L, int64_t ld, int64_t V, int E, int64_t padding_idx, float* grad, float* param,
+                    float* m, float* v, const AdamArgs& aa, void* ws, size_t ws_bytes, hipStream_t s) {
+  const size_t sb = sort_tmp_bytes(nseq * (int64_t)L, V);
+  void* base = reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256));
+  BwdWs w = carve(base, nseq, L, V, E, sb);
+  TT_REQUIRE(ws != nullptr && w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu",
+             w.total + 256, ws_bytes);
+  int rc = (ids_dtype == TT_IDS_I32)
+               ? sorted_front(dpooled, denom, static_cast<const int32_t*>(ids), nseq, L, ld, V, padding_idx, E, w, s)
+               : sorted_front(dpooled, denom, static_cast<const int64_t*>(ids), nseq, L, ld, V, padding_idx, E, w, s);
+  if (rc) return rc;
+  return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, s);
+}
+
+extern "C" int tt_bag_mean_bwd(const float* d_pooled, const float* denom, const void* ids, int ids_dtype,
+                               int64_t nseq, int L, int64_t ld_ids, int64_t V, int E, int64_t padding_idx,
+                               float* grad_table, int mode, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
+  if (rc) return rc;
+  TT_REQUIRE(grad_table && (nseq == 0 || (d_pooled && denom)), "null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (mode == TT_SCATTER_ATOMIC) {
+    if (nseq == 0) return TT_OK;
+    const dim3 grid((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+    if (ids_dtype == TT_IDS_I32)
+      bag_bwd_atomic_kernel<int32_t><<<grid, block, 0, s>>>(d_pooled, denom, static_cast<const int32_t*>(ids), nseq, L, ld_ids, V, padding_idx, E, grad_table);
+    else
+      bag_bwd_atomic_kernel<int64_t><<<grid, block, 0, s>>>(d_pooled, denom, static_cast<const int64_t*>(ids), nseq, L, ld_ids, V, padding_idx, E, grad_table);
+    TT_LAUNCH_CHECK("tt_bag_mean_bwd(atomic)");
+    return TT_OK;
+  }
+  TT_REQUIRE(mode == TT_SCATTER_SORTED, "unknown scatter mode %d", mode);
+  AdamArgs aa{};
+  return bwd_impl<false>(d_pooled, denom, ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, grad_table,
+                         nullptr, nullptr, nullptr, aa, ws, ws_bytes, s);
+}
+
+extern "C" int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom, const void* ids, int ids_dtype,
+                                     int64_t nseq, int L, int64_t ld_ids, int64_t V, int E, int64_t padding_idx,
+                                     float* table, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
+                                     float beta2, float eps, float weight_decay, int64_t step, void* ws,
+                                     size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
+  if (rc) return rc;
+  TT_REQUIRE(table && exp_avg && exp_avg_sq, "null pointer");
+  TT_REQUIRE(step >= 1, "step must be >= 1 (got %lld)", (long long)step);
+  const AdamArgs aa = make_adam(lr, beta1, beta2, eps, weight_decay, step);
+  return bwd_impl<true>(d_pooled, denom, ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, nullptr, table,
+                        exp_avg, exp_avg_sq, aa, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+}

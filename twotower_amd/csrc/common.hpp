@@ -1,0 +1,94 @@
+// Shared device/host helpers for libtwotower_amd (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+#include "../../include/twotower_amd.h"
+
+namespace tt {
+
+void set_error(const char* fmt, ...);
+
+constexpr int kWave = 64;  // CDNA wavefront; never 32
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <typename IdT>
+__device__ __forceinline__ int64_t load_id(const IdT* p) { return (int64_t)(*p); }
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// torch.optim.AdamW (foreach form, amsgrad=False, maximize=False) with the per-step scalars
+// precomputed on the host in double exactly as torch does in Python floats.
+struct AdamArgs {
+  float wd_factor;  // 1 - lr * weight_decay
+  float one_m_b1;   // lerp weight 1 - beta1
+  float beta2;
+  float one_m_b2;   // 1 - beta2
+  float step_size;  // lr / (1 - beta1^step)
+  float bc2_sqrt;   // sqrt(1 - beta2^step)
+  float eps;
+};
+
+inline AdamArgs make_adam(float lr, float beta1, float beta2, float eps, float wd, int64_t step) {
+  AdamArgs a;
+  const double bc1 = 1.0 - __builtin_pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - __builtin_pow((double)beta2, (double)step);
+  a.wd_factor = (float)(1.0 - (double)lr * (double)wd);
+  a.one_m_b1 = (float)(1.0 - (double)beta1);
+  a.beta2 = beta2;
+  a.one_m_b2 = (float)(1.0 - (double)beta2);
+  a.step_size = (float)((double)lr / bc1);
+  a.bc2_sqrt = (float)__builtin_sqrt(bc2);
+  a.eps = eps;
+  return a;
+}
+
+__device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, const AdamArgs& a) {
+  p = p * a.wd_factor;                   // param.mul_(1 - lr * wd)
+  m = m + a.one_m_b1 * (g - m);          // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * a.beta2 + a.one_m_b2 * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+  const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p - a.step_size * (m / den);       // param.addcdiv_(exp_avg, denom, -step_size)
+}
+
+}  // namespace tt
+
+#define TT_REQUIRE(cond, ...)                 \
+  do {                                        \
+    if (!(cond)) {                            \
+      tt::set_error(__VA_ARGS__);             \
+      return TT_ERR_INVALID;                  \
+    }                                         \
+  } while (0)
+
+#define TT_LAUNCH_CHECK(what)                                                   \
+  do {                                                                          \
+    hipError_t _e = hipGetLastError();                                          \
+    if (_e != hipSuccess) {                                                     \
+      tt::set_error("%s: launch failed: %s", what, hipGetErrorString(_e));     \
+      return (int)_e;                                                           \
+    }                                                                           \
+  } while (0)
+
+#define TT_HIP(call, what)                                                      \
+  do {                                                                          \
+    hipError_t _e = (call);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      tt::set_error("%s: %s", what, hipGetErrorString(_e));                    \
+      return (int)_e;                                                           \
+    }                                                                           \
+  } while (0)

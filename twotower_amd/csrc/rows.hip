@@ -1,0 +1,273 @@
+// Row-wise kernels of the tower output and the per-sample losses:
+//   F.normalize(x, dim=-1)                       twotower/encoders.py:77  (eps 1e-12)
+//   contrastive_triplet_loss                     twotower/losses.py:9-44  (cosine eps 1e-8)
+//   multiple_negatives_loss                      twotower/losses.py:47-85
+//   deterministic mean of per-row losses          (.mean() / F.cross_entropy reduction)
+// One wavefront owns one row; rows are <= a few KiB so re-reads within a wave hit L1/L2.
+// Cosine follows ATen's cosine_similarity: sum((x1 / clamp(|x1|, eps)) * (x2 / clamp(|x2|, eps))),
+// whose backward differentiates the norm but not the clamp.
+#include "common.hpp"
+
+namespace tt {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+__device__ __forceinline__ int64_t wave_row() { return (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); }
+
+__global__ __launch_bounds__(kBlock) void l2norm_fwd_kernel(const float* __restrict__ x, int64_t rows, int H,
+                                                            float* __restrict__ out, float* __restrict__ norm) {
+  const int64_t r = wave_row();
+  if (r >= rows) return;
+  const int lane = lane_id();
+  const float* xr = x + r * H;
+  float ss = 0.f;
+  for (int c = lane; c < H; c += kWave) ss += xr[c] * xr[c];
+  ss = wave_sum(ss);
+  const float nrm = sqrtf(ss);
+  const float den = fmaxf(nrm, 1e-12f);
+  for (int c = lane; c < H; c += kWave) out[r * H + c] = xr[c] / den;
+  if (lane == 0) norm[r] = nrm;
+}
+
+__global__ __launch_bounds__(kBlock) void l2norm_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ out,
+                                                            const float* __restrict__ norm, int64_t rows, int H,
+                                                            float* __restrict__ dx) {
+  const int64_t r = wave_row();
+  if (r >= rows) return;
+  const int lane = lane_id();
+  const float nrm = norm[r];
+  const float den = fmaxf(nrm, 1e-12f);
+  // x = out * den; s_x = sum(dout * x)
+  float sx = 0.f;
+  for (int c = lane; c < H; c += kWave) sx += dout[r * H + c] * out[r * H + c];
+  sx = wave_sum(sx) * den;
+  const float coef = (nrm >= 1e-12f && nrm > 0.f) ? sx / (den * den * nrm) : 0.f;
+  for (int c = lane; c < H; c += kWave) {
+    const float xv = out[r * H + c] * den;
+    dx[r * H + c] = dout[r * H + c] / den - coef * xv;
+  }
+}
+
+struct CosStats {
+  float dot, n1, n2;  // raw dot and unclamped norms
+};
+
+__device__ __forceinline__ CosStats cos_stats(const float* a, const float* b, int H) {
+  float d = 0.f, s1 = 0.f, s2 = 0.f;
+  for (int c = lane_id(); c < H; c += kWave) {
+    const float x = a[c], y = b[c];
+    d += x * y;
+    s1 += x * x;
+    s2 += y * y;
+  }
+  return CosStats{wave_sum(d), sqrtf(wave_sum(s1)), sqrtf(wave_sum(s2))};
+}
+
+__device__ __forceinline__ float cos_value(const CosStats& s) {
+  return s.dot / (fmaxf(s.n1, 1e-8f) * fmaxf(s.n2, 1e-8f));
+}
+
+// d cos / d x1 = x2 / (n1c n2c) - cos * x1 / (n1c * n1)   (0 at n1 == 0)
+__device__ __forceinline__ void cos_grad_coefs(const CosStats& s, float cosv, float& a_other, float& a_self1,
+                                               float& a_self2) {
+  const float n1c = fmaxf(s.n1, 1e-8f), n2c = fmaxf(s.n2, 1e-8f);
+  a_other = 1.f / (n1c * n2c);
+  a_self1 = s.n1 > 0.f ? cosv / (n1c * s.n1) : 0.f;
+  a_self2 = s.n2 > 0.f ? cosv / (n2c * s.n2) : 0.f;
+}
+
+__global__ __launch_bounds__(kBlock) void triplet_fwd_kernel(const float* __restrict__ q, const float* __restrict__ p,
+                                                             const float* __restrict__ n, int64_t B, int H, float margin,
+                                                             float* __restrict__ loss_rows) {
+  const int64_t r = wave_row();
+  if (r >= B) return;
+  const CosStats sp = cos_stats(q + r * H, p + r * H, H);
+  const CosStats sn = cos_stats(q + r * H, n + r * H, H);
+  const float h = margin - cos_value(sp) + cos_value(sn);
+  if (lane_id() == 0) loss_rows[r] = fmaxf(h, 0.f);
+}
+
+__global__ __launch_bounds__(kBlock) void triplet_bwd_kernel(const float* __restrict__ q, const float* __restrict__ p,
+                                                             const float* __restrict__ n, int64_t B, int H, float margin,
+                                                             const float* __restrict__ grad_loss,
+                                                             float* __restrict__ dq, float* __restrict__ dp,
+                                                             float* __restrict__ dn) {
+  const int64_t r = wave_row();
+  if (r >= B) return;
+  const float* qr = q + r * H;
+  const float* pr = p + r * H;
+  const float* nr = n + r * H;
+  const CosStats sp = cos_stats(qr, pr, H);
+  const CosStats sn = cos_stats(qr, nr, H);
+  const float cp = cos_value(sp), cn = cos_value(sn);
+  const float h = margin - cp + cn;
+  const float gate = (h > 0.f) ? grad_loss[0] / (float)B : 0.f;  // relu' and mean
+  const float gcp = -gate, gcn = gate;
+  float ap, aqp, app, an, aqn, ann;
+  cos_grad_coefs(sp, cp, ap, aqp, app);
+  cos_grad_coefs(sn, cn, an, aqn, ann);
+  for (int c = lane_id(); c < H; c += kWave) {
+    const float qv = qr[c], pv = pr[c], nv = nr[c];
+    dq[r * H + c] = gcp * (pv * ap - aqp * qv) + gcn * (nv * an - aqn * qv);
+    dp[r * H + c] = gcp * (qv * ap - app * pv);
+    dn[r * H + c] = gcn * (qv * an - ann * nv);
+  }
+}
+
+constexpr int kMaxNeg = 63;
+
+__device__ __forceinline__ const float* mn_doc(const float* p, const float* negs, int64_t r, int k, int N, int H) {
+  return k == 0 ? p + r * H : negs + (r * N + (k - 1)) * (int64_t)H;
+}
+
+__global__ __launch_bounds__(kBlock) void multi_neg_fwd_kernel(const float* __restrict__ q, const float* __restrict__ p,
+                                                               const float* __restrict__ negs, int64_t B, int N, int H,
+                                                               float inv_tau, float* __restrict__ loss_rows) {
+  const int64_t r = wave_row();
+  if (r >= B) return;
+  const float* qr = q + r * H;
+  float mx = -INFINITY, z0 = 0.f;
+  float z[kMaxNeg + 1];
+  for (int k = 0; k <= N; ++k) {
+    z[k] = cos_value(cos_stats(qr, mn_doc(p, negs, r, k, N, H), H)) * inv_tau;
+    mx = fmaxf(mx, z[k]);
+  }
+  z0 = z[0];
+  float se = 0.f;
+  for (int k = 0; k <= N; ++k) se += expf(z[k] - mx);
+  if (lane_id() == 0) loss_rows[r] = mx + logf(se) - z0;
+}
+
+__global__ __launch_bounds__(kBlock) void multi_neg_bwd_kernel(const float* __restrict__ q, const float* __restrict__ p,
+                                                               const float* __restrict__ negs, int64_t B, int N, int H,
+                                                               float inv_tau, const float* __restrict__ grad_loss,
+                                                               float* __restrict__ dq, float* __restrict__ dp,
+                                                               float* __restrict__ dnegs) {
+  const int64_t r = wave_row();
+  if (r >= B) return;
+  const float* qr = q + r * H;
+  CosStats st[kMaxNeg + 1];
+  float cs[kMaxNeg + 1];
+  float mx = -INFINITY;
+  for (int k = 0; k <= N; ++k) {
+    st[k] = cos_stats(qr, mn_doc(p, negs, r, k, N, H), H);
+    cs[k] = cos_value(st[k]);
+    mx = fmaxf(mx, cs[k] * inv_tau);
+  }
+  float se = 0.f;
+  for (int k = 0; k <= N; ++k) se += expf(cs[k] * inv_tau - mx);
+  const float g = grad_loss[0] / (float)B;
+  for (int c = lane_id(); c < H; c += kWave) dq[r * H + c] = 0.f;
+  for (int k = 0; k <= N; ++k) {
+    const float pk = expf(cs[k] * inv_tau - mx) / se;
+    const float gcos = g * (pk - (k == 0 ? 1.f : 0.f)) * inv_tau;
+    float a_other, a_q, a_d;
+    cos_grad_coefs(st[k], cs[k], a_other, a_q, a_d);
+    const float* dr = mn_doc(p, negs, r, k, N, H);
+    float* ddr = (k == 0) ? dp + r * H : dnegs + (r * N + (k - 1)) * (int64_t)H;
+    for (int c = lane_id(); c < H; c += kWave) {
+      const float qv = qr[c], dv = dr[c];
+      dq[r * H + c] += gcos * (dv * a_other - a_q * qv);
+      ddr[c] = gcos * (qv * a_other - a_d * dv);
+    }
+  }
+}
+
+// One workgroup: fixed-order strided partial sums then a fixed tree => bitwise reproducible.
+__global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float part[1024];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) s += x[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = n > 0 ? part[0] / (float)n : NAN;
+}
+
+dim3 rows_grid(int64_t rows) { return dim3((unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock)); }
+
+}  // namespace
+
+int launch_mean(const float* x, int64_t n, float* out, hipStream_t s) {
+  mean_kernel<<<dim3(1), dim3(1024), 0, s>>>(x, n, out);
+  TT_LAUNCH_CHECK("mean");
+  return TT_OK;
+}
+
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, tt_stream_t stream) {
+  TT_REQUIRE(rows >= 0 && H > 0, "bad shape rows=%lld H=%d", (long long)rows, H);
+  if (rows == 0) return TT_OK;
+  TT_REQUIRE(x && out && norm, "null pointer");
+  l2norm_fwd_kernel<<<rows_grid(rows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(x, rows, H, out, norm);
+  TT_LAUNCH_CHECK("tt_l2norm_fwd");
+  return TT_OK;
+}
+
+extern "C" int tt_l2norm_bwd(const float* dout, const float* out, const float* norm, int64_t rows, int H, float* dx,
+                             tt_stream_t stream) {
+  TT_REQUIRE(rows >= 0 && H > 0, "bad shape rows=%lld H=%d", (long long)rows, H);
+  if (rows == 0) return TT_OK;
+  TT_REQUIRE(dout && out && norm && dx, "null pointer");
+  l2norm_bwd_kernel<<<rows_grid(rows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(dout, out, norm, rows,
+                                                                                                 H, dx);
+  TT_LAUNCH_CHECK("tt_l2norm_bwd");
+  return TT_OK;
+}
+
+extern "C" int tt_triplet_fwd(const float* q, const float* p, const float* n, int64_t B, int H, float margin,
+                              float* loss_rows, float* loss, tt_stream_t stream) {
+  TT_REQUIRE(B >= 0 && H > 0, "bad shape B=%lld H=%d", (long long)B, H);
+  TT_REQUIRE(loss, "null loss");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B > 0) {
+    TT_REQUIRE(q && p && n && loss_rows, "null pointer");
+    triplet_fwd_kernel<<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, n, B, H, margin, loss_rows);
+    TT_LAUNCH_CHECK("tt_triplet_fwd");
+  }
+  return launch_mean(loss_rows, B, loss, s);
+}
+
+extern "C" int tt_triplet_bwd(const float* q, const float* p, const float* n, int64_t B, int H, float margin,
+                              const float* grad_loss, float* dq, float* dp, float* dn, tt_stream_t stream) {
+  TT_REQUIRE(B >= 0 && H > 0, "bad shape B=%lld H=%d", (long long)B, H);
+  if (B == 0) return TT_OK;
+  TT_REQUIRE(q && p && n && grad_loss && dq && dp && dn, "null pointer");
+  triplet_bwd_kernel<<<rows_grid(B), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(q, p, n, B, H, margin,
+                                                                                               grad_loss, dq, dp, dn);
+  TT_LAUNCH_CHECK("tt_triplet_bwd");
+  return TT_OK;
+}
+
+extern "C" int tt_multi_neg_fwd(const float* q, const float* p, const float* negs, int64_t B, int N, int H,
+                                float inv_tau, float* loss_rows, float* loss, tt_stream_t stream) {
+  TT_REQUIRE(B >= 0 && H > 0 && N >= 0 && N <= kMaxNeg, "bad shape B=%lld N=%d H=%d", (long long)B, N, H);
+  TT_REQUIRE(loss, "null loss");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B > 0) {
+    TT_REQUIRE(q && p && loss_rows && (N == 0 || negs), "null pointer");
+    multi_neg_fwd_kernel<<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, H, inv_tau, loss_rows);
+    TT_LAUNCH_CHECK("tt_multi_neg_fwd");
+  }
+  return launch_mean(loss_rows, B, loss, s);
+}
+
+extern "C" int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t B, int N, int H,
+                                float inv_tau, const float* grad_loss, float* dq, float* dp, float* dnegs,
+                                tt_stream_t stream) {
+  TT_REQUIRE(B >= 0 && H > 0 && N >= 0 && N <= kMaxNeg, "bad shape B=%lld N=%d H=%d", (long long)B, N, H);
+  if (B == 0) return TT_OK;
+  TT_REQUIRE(q && p && grad_loss && dq && dp && (N == 0 || (negs && dnegs)), "null pointer");
+  multi_neg_bwd_kernel<<<rows_grid(B), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      q, p, negs, B, N, H, inv_tau, grad_loss, dq, dp, dnegs);
+  TT_LAUNCH_CHECK("tt_multi_neg_bwd");
+  return TT_OK;
+}

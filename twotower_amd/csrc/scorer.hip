@@ -1,0 +1,592 @@
+// Fused in-batch sampled-softmax cross entropy on gfx950 MFMA
+// (in_batch_sampled_softmax_loss, twotower/losses.py:88-118):
+//   S = Q D^T (B x M), logits = S / tau, labels = arange(B) (+label_off under data parallel),
+//   loss = mean_i (logsumexp_j logits_ij - logits_i,label_i).
+// B x M is never materialised.  One engine serves both passes:
+//   * a workgroup keeps 4 x 32 "column" rows resident in VGPRs as the MFMA B operand and
+//     streams the other matrix through a double-buffered, XOR-swizzled LDS tile;
+//   * X = R_tile * C^T (32x32 per wave, 32x32x16 bf16 or 32x32x2 f32 MFMA), an elementwise map
+//     G = f(X) in registers, then Acc^T += R_tile^T * G with the X accumulator reused as the
+//     next MFMA's B operand (no LDS round trip) and R_tile^T read with ds_read_b64_tr_b16.
+//   forward  (R = D, C = Q): G = exp2(X*c2 - m) with a lazily rescaled running max, Acc = O^T,
+//            giving lse and O = P D per query => dQ needs no extra pass.
+//   backward (R = Q, C = D): G = exp2(X*c2 - lse2_i) - [j == i + off], Acc = dD^T.
+// The streamed dimension is split over workgroups (blockIdx % S == split, so one split per XCD
+// when S == 8); split partials are merged by small combine kernels.
+#include "common.hpp"
+
+namespace tt {
+int launch_mean(const float* x, int64_t n, float* out, hipStream_t s);
+
+namespace {
+
+constexpr int NW = 4;
+constexpr int NT = NW * kWave;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kShiftGuard = 100.f;  // log2 units: a shift this far above the true max risks underflow
+enum Mode { FWD = 0, DD = 1 };
+
+__device__ __forceinline__ int acc_row(int v, int hh) { return (v & 3) + 8 * (v >> 2) + 4 * hh; }
+
+// ------------------------------------------------------------------------------------------
+// LDS tile image shared by both engines: BJ rows of H elements, row-major, 16-byte chunk c of
+// row r stored at chunk c ^ (r & SWM).  The swizzle makes the 32-rows-same-column ds_read_b128
+// operand reads hit 16 distinct slots; the column reads (ds_read_b32 / ds_read_b64_tr_b16)
+// stay inside one row and remain conflict-free.  Tiles are filled by global_load_lds
+// (16 B per lane, 1 KiB per wave-instruction, no staging VGPRs): the LDS side is written
+// linearly, so the swizzle is applied to the per-lane SOURCE address (rule 21).
+template <typename ET, int H>
+struct Tile {
+  static constexpr int BJ = sizeof(ET) == 2 ? 64 : 32;
+  static constexpr int ROWB = H * (int)sizeof(ET);
+  static constexpr int NCH = ROWB / 16;
+  // bf16: 4-bit XOR (row reads conflict-free).  f32: 3-bit XOR keeps every h-tile of a column
+  // read at a constant byte offset from the first (immediate offsets, no per-tile address
+  // VGPRs) at the price of 2-way conflicts on the 16-byte row reads.
+  static constexpr int SWM = ((sizeof(ET) == 2 && NCH >= 16) ? 16 : (NCH >= 8 ? 8 : NCH)) - 1;
+  static constexpr int STAGE_B = BJ * ROWB;
+  static constexpr int NI = STAGE_B / 1024 / NW;  // glds wave-instructions per wave per stage
+  static_assert(NI * 1024 * NW == STAGE_B, "stage must be a whole number of 1 KiB pieces per wave");
+  static constexpr int LDS_BYTES = 2 * STAGE_B + 2 * 64 * 4;  // two stages + two 64-float lse rows
+  __device__ static __forceinline__ int off(int row, int ch) { return row * ROWB + ((ch ^ (row & SWM)) << 4); }
+};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// Issue the global_load_lds pieces that fill stage `buf` with rows [r0, r0 + BJ) of R (rows at
+// or past row_end are clamped to a real row; their products are masked by the caller).
+template <typename ET, int H, int MODE>
+__device__ __forceinline__ void stage_tile(char* smem, int buf, const ET* __restrict__ R, int64_t r0, int64_t row_end,
+                                           const float* __restrict__ lse_rows) {
+  using T = Tile<ET, H>;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  char* base = smem + buf * T::STAGE_B;
+#pragma unroll
+  for (int c = 0; c < T::NI; ++c) {
+    const int wbase = (c * NW + wid) * 1024;
+    const int p = wbase + lane * 16;
+    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
+    const int ch = slot ^ (row & T::SWM);
+    int64_t g = r0 + row;
+    g = g < row_end ? g : row_end - 1;
+    const char* src = reinterpret_cast<const char*>(R + g * H) + ch * 16;
+    __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(base + wbase), 16, 0, 0);
+  }
+  if constexpr (MODE == DD) {
+    if (wid == 0) {
+      int64_t g = r0 + lane;
+      g = g < row_end ? g : row_end - 1;
+      __builtin_amdgcn_global_load_lds(lse_rows + g, (lds_void_t*)(smem + 2 * T::STAGE_B + buf * 256), 4, 0, 0);
+    }
+  }
+}
+
+// Elementwise map of one 32x32 X tile (rows j = jb + acc_row, column = this lane's my_col).
+template <int MODE>
+struct EltState {
+  float m_run = -INFINITY, l_run = 0.f, diag = 0.f;
+  bool has_diag = false;
+};
+
+template <int MODE>
+__device__ __forceinline__ void elementwise(const f32x16& x, float (&e)[16], EltState<MODE>& st, int64_t jb,
+                                            int64_t row_end, int64_t my_col, int64_t label_off, float c2, float shift,
+                                            const float* lse_tile, int hh) {
+  if constexpr (MODE == FWD) {
+    // Fixed per-column shift (an upper bound of the column's logits, log2 units): no running
+    // max, no accumulator rescale, so the accumulators never leave the MFMA register file.
+    float ls = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t j = jb + acc_row(v, hh);
+      const bool in = j < row_end;
+      const float z = x[v] * c2;
+      st.m_run = in ? fmaxf(st.m_run, z) : st.m_run;
+      e[v] = in ? exp2f(z - shift) : 0.f;
+      ls += e[v];
+      if (in && j == my_col + label_off) {
+        st.diag = x[v];
+        st.has_diag = true;
+      }
+    }
+    st.l_run += ls;
+  } else {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_tile + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int v = 4 * g4 + u;
+        const int64_t i = jb + acc_row(v, hh);
+        float gv = 0.f;
+        if (i < row_end) {
+          gv = exp2f(x[v] * c2 - l4[u] * kLog2e);
+          if (my_col == i + label_off) gv -= 1.f;
+        }
+        e[v] = gv;
+      }
+    }
+  }
+}
+
+template <int MODE, int H>
+__device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], EltState<MODE>& st, int split, int64_t nC,
+                                               int64_t my_col, int hh, float* acc_part, float* m_part, float* l_part,
+                                               float* diag_raw) {
+  if (my_col < nC) {
+    float* dst = acc_part + ((int64_t)split * nC + my_col) * H;
+#pragma unroll
+    for (int ht = 0; ht < H / 32; ++ht)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<f32x4*>(dst + ht * 32 + 8 * g4 + 4 * hh) =
+            f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
+  }
+  if constexpr (MODE == FWD) {
+    st.l_run += __shfl_xor(st.l_run, 32);
+    st.m_run = fmaxf(st.m_run, __shfl_xor(st.m_run, 32));
+    if (my_col < nC) {
+      if (hh == 0) {
+        m_part[(int64_t)split * nC + my_col] = st.m_run;
+        l_part[(int64_t)split * nC + my_col] = st.l_run;
+      }
+      if (st.has_diag) diag_raw[my_col] = st.diag;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 engine (32x32x16 bf16 MFMA).  PRECISE splits G into hi + lo bf16 so the second product
+// carries ~16 mantissa bits; otherwise G is rounded once (flash-attention style).
+template <int MODE, bool PRECISE, int H>
+__global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
+    const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
+    int64_t rows_per_split, float c2, int64_t label_off, const float* __restrict__ lse_rows,
+    const float* __restrict__ col_shift, float* __restrict__ acc_part, float* __restrict__ m_part, float* __restrict__ l_part,
+    float* __restrict__ diag_raw) {
+  using T = Tile<__bf16, H>;
+  constexpr int NK = H / 16;
+  constexpr int NHT = H / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
+  const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
+
+  if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse_rows);
+
+  bf16x8 cf[NK];
+  {
+    const bool ok = my_col < nC;
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(C + (ok ? my_col : 0) * H);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      bf16x8 v = src[2 * kk + hh];
+      if (!ok) v = bf16x8{};
+      cf[kk] = v;
+    }
+  }
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  EltState<MODE> st;
+  __syncthreads();
+
+  // transposed-read lane geometry (T10): group g = lane>>4 reads rows 4*(g>>1)+q, cols 16*(g&1)+4p
+  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
+
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int buf = (int)(t & 1);
+    if (t + 1 < ntiles) stage_tile<__bf16, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse_rows);
+    const char* base = smem + buf * T::STAGE_B;
+    const float* lse_tile = reinterpret_cast<const float*>(smem + 2 * T::STAGE_B + buf * 256);
+#pragma unroll
+    for (int jt = 0; jt < T::BJ / 32; ++jt) {
+      const int64_t jb = row_begin + t * T::BJ + jt * 32;
+      f32x16 x = f32x16{};
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + T::off(jt * 32 + r32, 2 * kk + hh));
+        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cf[kk], x, 0, 0, 0);
+      }
+      float e[16];
+      elementwise<MODE>(x, e, st, jb, row_end, my_col, label_off, c2, shift, lse_tile + jt * 32, hh);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 bh, bl;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float v = e[8 * s2 + jj];
+          const __bf16 h = (__bf16)v;
+          bh[jj] = h;
+          if constexpr (PRECISE) bl[jj] = (__bf16)(v - (float)h);
+        }
+        const int row1 = jt * 32 + 16 * s2 + 4 * (tg >> 1) + tq;
+#pragma unroll
+        for (int ht = 0; ht < NHT; ++ht) {
+          const int hcol = ht * 32 + 16 * (tg & 1) + 4 * tp;
+          const int ch = hcol >> 3, bo = (hcol & 7) * 2;
+          typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+          const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + T::off(row1, ch) + bo));
+          const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + T::off(row1 + 8, ch) + bo));
+          const bf16x8 a = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+          acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc[ht], 0, 0, 0);
+          if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc[ht], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  write_partials<MODE, H>(acc, st, split, nC, my_col, hh, acc_part, m_part, l_part, diag_raw);
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 engine (exact f32 MFMA, 32x32x2).  The k order inside the X product is permuted
+// (k = 8*blk + 4*hh + u) so each lane reads one 16-byte chunk per four MFMAs.
+template <int MODE, int H>
+__global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
+    const float* __restrict__ R, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
+    int64_t rows_per_split, float c2, int64_t label_off, const float* __restrict__ lse_rows,
+    const float* __restrict__ col_shift, float* __restrict__ acc_part, float* __restrict__ m_part, float* __restrict__ l_part,
+    float* __restrict__ diag_raw) {
+  using T = Tile<float, H>;
+  constexpr int NB = H / 8;
+  constexpr int NHT = H / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
+  const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
+
+  if (ntiles > 0) stage_tile<float, H, MODE>(smem, 0, R, row_begin, row_end, lse_rows);
+
+  f32x4 cf[NB];
+  {
+    const bool ok = my_col < nC;
+    const f32x4* src = reinterpret_cast<const f32x4*>(C + (ok ? my_col : 0) * H);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      f32x4 v = src[2 * b + hh];
+      if (!ok) v = f32x4{};
+      cf[b] = v;
+    }
+  }
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  EltState<MODE> st;
+  __syncthreads();
+
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int buf = (int)(t & 1);
+    if (t + 1 < ntiles) stage_tile<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse_rows);
+    const char* base = smem + buf * T::STAGE_B;
+    const float* lse_tile = reinterpret_cast<const float*>(smem + 2 * T::STAGE_B + buf * 256);
+    const int64_t jb = row_begin + t * T::BJ;
+    f32x16 x = f32x16{};
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(base + T::off(r32, 2 * b + hh));
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], cf[b][u], x, 0, 0, 0);
+    }
+    float e[16];
+    elementwise<MODE>(x, e, st, jb, row_end, my_col, label_off, c2, shift, lse_tile, hh);
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = acc_row(v, hh);
+        const float a = *reinterpret_cast<const float*>(base + T::off(row, 8 * ht + (r32 >> 2)) + (r32 & 3) * 4);
+        acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, e[v], acc[ht], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+  write_partials<MODE, H>(acc, st, split, nC, my_col, hh, acc_part, m_part, l_part, diag_raw);
+}
+
+// ------------------------------------------------------------------------------------------
+// Operand prep, one wave per row: optional fp32 -> bf16 (RNE) copy, row L2 norm, and the max
+// norm over rows (atomicMax on the float bits; norms are >= 0 so the integer order is the
+// float order).
+__global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ x, int64_t rows, int H,
+                                                        __bf16* __restrict__ xb, float* __restrict__ norms,
+                                                        unsigned* __restrict__ max_bits) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = lane_id();
+  const f32x4* src = reinterpret_cast<const f32x4*>(x + r * H);
+  float ss = 0.f;
+  for (int c = lane; c < H / 4; c += kWave) {
+    const f32x4 v = src[c];
+    ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    if (xb)
+      reinterpret_cast<bf16x4*>(xb + r * H)[c] = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  }
+  ss = wave_sum(ss);
+  if (lane == 0) {
+    const float n = sqrtf(ss);
+    if (norms) norms[r] = n;
+    if (max_bits) atomicMax(max_bits, __float_as_uint(n));
+  }
+}
+
+// Column shift for the forward: an upper bound of row i's logits in log2 units,
+// |q~_i . d~_j| * c2 <= c2 * |q_i| * max_j |d_j| * (1 + 2^-6) (bf16 rounding slack included).
+__global__ __launch_bounds__(256) void shift_kernel(const float* __restrict__ qn, const unsigned* __restrict__ dmax_bits,
+                                                    int64_t B, float c2, float* __restrict__ shift) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= B) return;
+  shift[i] = fabsf(c2) * qn[i] * __uint_as_float(*dmax_bits) * 1.015625f;
+}
+
+// Merge forward split partials: one wave per query row.  Rows whose shift sits more than
+// kShiftGuard above the true max could have underflowed: they report NaN (fail loudly).
+template <typename DT>
+__global__ __launch_bounds__(256) void fwd_combine_kernel(
+    int64_t B, int H, int S, const float* __restrict__ shift, const float* __restrict__ m_part,
+    const float* __restrict__ l_part, const float* __restrict__ acc_part, const float* __restrict__ diag_raw,
+    float inv_tau, int64_t label_off, const DT* __restrict__ Dmat, float* __restrict__ lse,
+    float* __restrict__ loss_rows, float* __restrict__ dqu) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= B) return;
+  const int lane = lane_id();
+  float mt = -INFINITY, l = 0.f;
+  for (int s = 0; s < S; ++s) {
+    mt = fmaxf(mt, m_part[(int64_t)s * B + i]);
+    l += l_part[(int64_t)s * B + i];
+  }
+  const float sh = shift[i];
+  const bool ok = l > 0.f && sh - mt < kShiftGuard;
+  const float lse_i = ok ? (sh + log2f(l)) * kLn2 : NAN;
+  if (lane == 0) {
+    lse[i] = lse_i;
+    loss_rows[i] = lse_i - diag_raw[i] * inv_tau;
+  }
+  if (dqu) {
+    const float inv_l = ok ? 1.f / l : NAN;
+    const DT* dl = Dmat + (i + label_off) * H;
+    for (int h = lane; h < H; h += kWave) {
+      float o = 0.f;
+      for (int s = 0; s < S; ++s) o += acc_part[((int64_t)s * B + i) * H + h];
+      dqu[i * H + h] = o * inv_l - (float)dl[h];
+    }
+  }
+}
+
+// dd = scale * sum_s part[s]; dq = scale * dqu (scale = grad_loss * grad_scale * inv_tau).
+__global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, int H, int S,
+                                                          const float* __restrict__ acc_part,
+                                                          const float* __restrict__ dqu,
+                                                          const float* __restrict__ grad_loss, float grad_scale,
+                                                          float inv_tau, float* __restrict__ dq,
+                                                          float* __restrict__ dd) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = lane_id();
+  const float scale = grad_loss[0] * grad_scale * inv_tau;
+  if (r < M) {
+    for (int h = lane; h < H; h += kWave) {
+      float a = 0.f;
+      for (int s = 0; s < S; ++s) a += acc_part[((int64_t)s * M + r) * H + h];
+      dd[r * H + h] = a * scale;
+    }
+  }
+  if (r < B) {
+    for (int h = lane; h < H; h += kWave) dq[r * H + h] = dqu[r * H + h] * scale;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side.
+struct Plan {
+  int S;
+  int64_t rows_per_split;
+  int grid;
+};
+
+Plan plan_for(int64_t nR, int64_t nC, int BJ) {
+  const int64_t ncb = (nC + 32 * NW - 1) / (32 * NW);
+  const int64_t row_tiles = (nR + BJ - 1) / BJ;
+  int64_t S = (512 + ncb - 1) / ncb;  // aim for ~2 workgroups per CU
+  if (S > 8) S = 8;
+  if (S > row_tiles) S = row_tiles;
+  if (S < 1) S = 1;
+  int64_t rps = (row_tiles + S - 1) / S * BJ;
+  S = (nR + rps - 1) / rps;
+  if (S < 1) S = 1;
+  return Plan{(int)S, rps, (int)(ncb * S)};
+}
+
+int bj_for(int dtype) { return dtype == TT_F32 ? Tile<float, 64>::BJ : Tile<__bf16, 64>::BJ; }
+
+struct Ws {
+  __bf16* Qb;
+  __bf16* Db;
+  float* qnorm;
+  float* shift;
+  unsigned* dmax;
+  float* diag;
+  float* m_part;
+  float* l_part;
+  float* acc_part;
+  size_t total;
+};
+
+// Layout: [Qb | Db] persist from forward to backward (the backward's MFMA operands);
+// everything else is scratch reused by both passes.
+Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
+  const int BJ = bj_for(dtype);
+  const Plan pf = plan_for(M, B, BJ), pd = plan_for(B, M, BJ);
+  const bool bf = dtype != TT_F32;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  const size_t oq = take(bf ? (size_t)B * H * 2 : 0), od = take(bf ? (size_t)M * H * 2 : 0);
+  const size_t oqn = take((size_t)B * 4), osh = take((size_t)B * 4), omx = take(16);
+  const size_t odg = take((size_t)B * 4), om = take((size_t)pf.S * B * 4), ol = take((size_t)pf.S * B * 4);
+  const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
+  const size_t oa = take(parts);
+  Ws w{};
+  char* b = static_cast<char*>(base);
+  if (b) {
+    w.Qb = reinterpret_cast<__bf16*>(b + oq);
+    w.Db = reinterpret_cast<__bf16*>(b + od);
+    w.qnorm = reinterpret_cast<float*>(b + oqn);
+    w.shift = reinterpret_cast<float*>(b + osh);
+    w.dmax = reinterpret_cast<unsigned*>(b + omx);
+    w.diag = reinterpret_cast<float*>(b + odg);
+    w.m_part = reinterpret_cast<float*>(b + om);
+    w.l_part = reinterpret_cast<float*>(b + ol);
+    w.acc_part = reinterpret_cast<float*>(b + oa);
+  }
+  w.total = off;
+  return w;
+}
+
+template <int MODE, int H>
+int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
+                  int64_t label_off, const float* lse, const Ws& w, hipStream_t s) {
+  if (dtype == TT_F32) {
+    score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
+        static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, label_off,
+        lse, w.shift, w.acc_part, w.m_part, w.l_part, w.diag);
+  } else if (dtype == TT_BF16) {
+    score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
+        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, label_off,
+        lse, w.shift, w.acc_part, w.m_part, w.l_part, w.diag);
+  } else {
+    score_bf16_kernel<MODE, false, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
+        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, label_off,
+        lse, w.shift, w.acc_part, w.m_part, w.l_part, w.diag);
+  }
+  TT_LAUNCH_CHECK(MODE == FWD ? "score_fwd" : "score_dd");
+  return TT_OK;
+}
+
+template <int MODE>
+int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
+                    float c2, int64_t label_off, const float* lse, const Ws& w, hipStream_t s) {
+  switch (H) {
+    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
+    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
+    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
+    default: set_error("in-batch scorer: H=%d unsupported (64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
+  }
+}
+
+int check_args(int64_t B, int64_t M, int H, int dtype, int64_t label_off) {
+  TT_REQUIRE(B > 0 && M > 0, "B=%lld M=%lld must be positive", (long long)B, (long long)M);
+  TT_REQUIRE(H == 64 || H == 128 || H == 256, "H=%d unsupported (64, 128, 256)", H);
+  TT_REQUIRE(dtype == TT_F32 || dtype == TT_BF16 || dtype == TT_BF16_FAST, "dtype=%d", dtype);
+  TT_REQUIRE(label_off >= 0 && label_off + B <= M, "labels [%lld, %lld) fall outside the %lld candidate columns",
+             (long long)label_off, (long long)(label_off + B), (long long)M);
+  return TT_OK;
+}
+
+}  // namespace
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype) {
+  return carve(nullptr, B, M, H, dtype).total + 256;
+}
+
+static Ws carve_user(void* ws, int64_t B, int64_t M, int H, int dtype) {
+  void* base = reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256));
+  return carve(base, B, M, H, dtype);
+}
+
+extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                              int64_t label_off, int want_grad, float* lse, float* loss_rows, float* loss,
+                              float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_args(B, M, H, dtype, label_off);
+  if (rc) return rc;
+  TT_REQUIRE(q && d && lse && loss_rows && loss && ws, "null pointer");
+  TT_REQUIRE(!want_grad || dq_unscaled, "want_grad needs dq_unscaled");
+  TT_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(d)) & 15) == 0, "q/d must be 16-byte aligned");
+  const Ws w = carve_user(ws, B, M, H, dtype);
+  TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const Plan p = plan_for(M, B, bj_for(dtype));
+  const float c2 = inv_tau * kLog2e;
+  const bool bf = dtype != TT_F32;
+  TT_HIP(hipMemsetAsync(w.dmax, 0, 16, s), "memset dmax");
+  prep_rows_kernel<<<dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s>>>(q, B, H, bf ? w.Qb : nullptr, w.qnorm, nullptr);
+  prep_rows_kernel<<<dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s>>>(d, M, H, bf ? w.Db : nullptr, nullptr, w.dmax);
+  shift_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(w.qnorm, w.dmax, B, c2, w.shift);
+  TT_LAUNCH_CHECK("score_prep");
+  const void* Rm = bf ? (const void*)w.Db : (const void*)d;
+  const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
+  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, label_off, nullptr, w, s))) return rc;
+  const dim3 grid((unsigned)((B + 3) / 4)), block(256);
+  if (!bf)
+    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, w.shift, w.m_part, w.l_part, w.acc_part, w.diag,
+                                                    inv_tau, label_off, d, lse, loss_rows,
+                                                    want_grad ? dq_unscaled : nullptr);
+  else
+    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, w.shift, w.m_part, w.l_part, w.acc_part, w.diag,
+                                                     inv_tau, label_off, w.Db, lse, loss_rows,
+                                                     want_grad ? dq_unscaled : nullptr);
+  TT_LAUNCH_CHECK("score_fwd_combine");
+  return launch_mean(loss_rows, B, loss, s);
+}
+
+extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                              int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
+                              float grad_scale, float* dq, float* dd, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_args(B, M, H, dtype, label_off);
+  if (rc) return rc;
+  TT_REQUIRE(q && d && lse && dq_unscaled && grad_loss && dq && dd && ws, "null pointer");
+  const Ws w = carve_user(ws, B, M, H, dtype);
+  TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const Plan p = plan_for(B, M, bj_for(dtype));
+  const float c2 = inv_tau * kLog2e;
+  const void* Rm = (dtype == TT_F32) ? (const void*)q : (const void*)w.Qb;  // operands left by the forward
+  const void* Cm = (dtype == TT_F32) ? (const void*)d : (const void*)w.Db;
+  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, label_off, lse, w, s))) return rc;
+  const int64_t rows = std::max(B, M);
+  bwd_combine_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(B, M, H, p.S, w.acc_part, dq_unscaled,
+                                                                           grad_loss, grad_scale, inv_tau, dq, dd);
+  TT_LAUNCH_CHECK("score_bwd_combine");
+  return TT_OK;
+}

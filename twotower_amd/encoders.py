@@ -1,0 +1,165 @@
+"""Tower registry and TwoTower, mirroring twotower/encoders.py (BaseTower :12-22,
+MeanPoolingTower :25-81, AveragePoolingTower :84-155, TwoTower :158-224, TOWER_REGISTRY
+:228-232, build_tower :234-249, build_two_tower :251-272).
+
+Parameter names match the reference (`embedding.embedding.weight`, `feed_forward.{0,2}.*`,
+`projection.{0,2}.*`) so state_dicts load in either direction.  The pooled lookup runs on the
+fused HIP bag kernel; TwoTower.forward pools the query, positive and negative ids of a step in
+ONE launch over the shared table (the towers always share it, encoders.py:265,270).
+"""
+from __future__ import annotations
+
+import logging
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .embeddings import BaseEmbedding
+
+logger = logging.getLogger("twotower_amd.encoders")
+
+
+def pool_mean(embedding: nn.Module, input_ids: torch.Tensor) -> torch.Tensor:
+    """Fused gather + masked mean (encoders.py:62-72).  Accepts this package's embeddings and
+    any reference-style embedding that holds an nn.Embedding at `.embedding`."""
+    if hasattr(embedding, "pool_mean"):
+        return embedding.pool_mean(input_ids)
+    inner = getattr(embedding, "embedding", None)
+    if isinstance(inner, nn.Embedding):
+        return ops.bag_mean_pool(inner.weight, input_ids, inner.padding_idx)
+    raise TypeError(f"{type(embedding).__name__} exposes no lookup table for the fused bag kernel")
+
+
+def _table_of(embedding: nn.Module) -> torch.Tensor | None:
+    inner = getattr(embedding, "embedding", None)
+    return inner.weight if isinstance(inner, nn.Embedding) else None
+
+
+class BaseTower(nn.Module):
+    """Base class for tower/encoder architectures (encoders.py:12-22)."""
+
+    def __init__(self, embedding: BaseEmbedding, hidden_dim: int):
+        super().__init__()
+        self.embedding = embedding
+        self.hidden_dim = hidden_dim
+
+    def log_params(self):
+        n = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        logger.info(f"Tower parameters: {n:,}")
+
+    def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    def forward(self, input_ids: torch.Tensor) -> torch.Tensor:
+        return self.encode_pooled(pool_mean(self.embedding, input_ids))
+
+
+class MeanPoolingTower(BaseTower):
+    """Masked mean-pool -> Linear-ReLU-Linear -> L2 normalise (encoders.py:25-81)."""
+
+    def __init__(self, embedding: BaseEmbedding, hidden_dim: int):
+        super().__init__(embedding, hidden_dim)
+        embedding_dim = embedding.embedding_dim
+        self.feed_forward = nn.Sequential(
+            nn.Linear(embedding_dim, hidden_dim),
+            nn.ReLU(),
+            nn.Linear(hidden_dim, hidden_dim),
+        )
+        self.log_params()
+
+    def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:
+        return ops.l2_normalize(self.feed_forward(pooled))  # encoders.py:77
+
+
+class AveragePoolingTower(BaseTower):
+    """Masked mean-pool -> optional Linear-Dropout-LayerNorm -> L2 normalise (encoders.py:84-155)."""
+
+    def __init__(self, embedding: BaseEmbedding, hidden_dim: int, dropout: float = 0.1):
+        super().__init__(embedding, hidden_dim)
+        embedding_dim = embedding.embedding_dim
+        self.has_projection = hidden_dim != embedding_dim
+        if self.has_projection:
+            self.projection = nn.Sequential(
+                nn.Linear(embedding_dim, hidden_dim),
+                nn.Dropout(dropout),
+                nn.LayerNorm(hidden_dim),
+            )
+        self.log_params()
+
+    def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:
+        out = self.projection(pooled) if self.has_projection else pooled
+        return ops.l2_normalize(out.contiguous())  # encoders.py:150
+
+
+class TwoTower(nn.Module):
+    """Query and document towers (encoders.py:158-224)."""
+
+    def __init__(self, query_tower: BaseTower, document_tower: BaseTower | None = None, tied_weights: bool = False):
+        super().__init__()
+        self.query_tower = query_tower
+        if tied_weights:
+            self.document_tower = query_tower
+        else:
+            self.document_tower = document_tower if document_tower is not None else query_tower
+        total = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        logger.info(f"Total trainable parameters: {total:,}")
+
+    def _fusable(self) -> bool:
+        qt, dt = self.query_tower, self.document_tower
+        if not (isinstance(qt, BaseTower) and isinstance(dt, BaseTower)):
+            return False
+        tq, td = _table_of(qt.embedding), _table_of(dt.embedding)
+        return tq is not None and tq is td
+
+    def forward(self, query_input, document_input=None, negative_input=None):
+        inputs = [t for t in (query_input, document_input, negative_input) if t is not None]
+        if len(inputs) > 1 and self._fusable():
+            outs = self._forward_fused(inputs)
+        else:
+            outs = [self.query_tower(query_input)]
+            outs += [self.document_tower(t) for t in inputs[1:]]
+        return outs[0] if len(outs) == 1 else tuple(outs)
+
+    def _forward_fused(self, inputs: list[torch.Tensor]) -> list[torch.Tensor]:
+        """One bag launch over all sequences of the step, then the towers' heads."""
+        L = max(t.shape[1] for t in inputs)
+        ids = [t if t.shape[1] == L else F.pad(t, (0, L - t.shape[1])) for t in inputs]
+        dtype = torch.int64 if any(t.dtype == torch.int64 for t in ids) else ids[0].dtype
+        all_ids = torch.cat([t.to(dtype) for t in ids], dim=0)
+        pooled = pool_mean(self.query_tower.embedding, all_ids)
+        sizes = [t.shape[0] for t in inputs]
+        nq = sizes[0]
+        if self.query_tower is self.document_tower:
+            return list(torch.split(self.query_tower.encode_pooled(pooled), sizes, dim=0))
+        q = self.query_tower.encode_pooled(pooled[:nq])
+        docs = self.document_tower.encode_pooled(pooled[nq:])
+        return [q] + list(torch.split(docs, sizes[1:], dim=0))
+
+    def encode_query(self, query_input):
+        return self.query_tower(query_input)
+
+    def encode_document(self, document_input):
+        return self.document_tower(document_input)
+
+
+TOWER_REGISTRY = {
+    "mean": MeanPoolingTower,
+    "avg_pool": AveragePoolingTower,
+}
+
+
+def build_tower(name: str, embedding: BaseEmbedding, **kwargs) -> BaseTower:
+    """Build a tower by name (encoders.py:234-249)."""
+    if name not in TOWER_REGISTRY:
+        raise ValueError(f"Unknown tower architecture: {name}. Available options: {list(TOWER_REGISTRY.keys())}")
+    return TOWER_REGISTRY[name](embedding=embedding, **kwargs)
+
+
+def build_two_tower(tower_name: str, embedding: BaseEmbedding, hidden_dim: int, tied_weights: bool = False,
+                    **kwargs) -> TwoTower:
+    """Build a complete two-tower model (encoders.py:251-272)."""
+    query_tower = build_tower(tower_name, embedding, hidden_dim=hidden_dim, **kwargs)
+    document_tower = None if tied_weights else build_tower(tower_name, embedding, hidden_dim=hidden_dim, **kwargs)
+    return TwoTower(query_tower, document_tower, tied_weights=tied_weights)

@@ -1,0 +1,86 @@
+"""Loss registry mirroring twotower/losses.py (contrastive_triplet_loss :9-44,
+multiple_negatives_loss :47-85, in_batch_sampled_softmax_loss :88-118, LOSS_REGISTRY :122-127,
+build :129-150), every loss on HIP kernels.
+
+The reference training loop always calls ``loss_fn(q, p, n)`` (twotower/train.py:133), which
+its own ``multiple_negatives`` / ``in_batch`` entries cannot take.  Here both also accept that
+call: ``multiple_negatives`` treats a (B, H) negative as N = 1, and ``in_batch`` scores every
+query against all positives and negatives of the batch (candidates = cat[p, n], label of query
+i = column i), which is the reference function applied to ``d_emb = cat[p, n]``.  Their
+reference signatures keep working unchanged.
+"""
+from __future__ import annotations
+
+import logging
+from functools import partial
+from typing import Callable
+
+import torch
+
+from . import ops
+
+logger = logging.getLogger("twotower_amd.losses")
+
+
+def contrastive_triplet_loss(q_emb: torch.Tensor, d_pos_emb: torch.Tensor, d_neg_emb: torch.Tensor,
+                             margin: float = 0.2) -> torch.Tensor:
+    """mean(relu(margin - cos(q, d+) + cos(q, d-))) (losses.py:9-44)."""
+    return ops.TripletLoss.apply(q_emb, d_pos_emb, d_neg_emb, margin)
+
+
+def multiple_negatives_loss(q_emb: torch.Tensor, d_pos_emb: torch.Tensor, d_neg_embs: torch.Tensor,
+                            temperature: float = 0.1) -> torch.Tensor:
+    """InfoNCE over [d+, d-_1..N] by cosine / temperature, label 0 (losses.py:47-85)."""
+    if d_neg_embs.dim() == 2:
+        d_neg_embs = d_neg_embs.unsqueeze(1)
+    return ops.MultiNegLoss.apply(q_emb, d_pos_emb, d_neg_embs, 1.0 / float(temperature))
+
+
+def _candidates(p: torch.Tensor, n: torch.Tensor) -> torch.Tensor:
+    """cat([p, n]) without a copy when p and n are consecutive row blocks of one tensor
+    (TwoTower's fused output): a narrow() of their common base, so autograd stays exact."""
+    base = p._base
+    if (base is not None and base is n._base and base.dim() == 2 and base.is_contiguous() and p.dim() == 2
+            and p.is_contiguous() and n.is_contiguous() and p.shape[1] == base.shape[1] == n.shape[1]):
+        row = base.shape[1] * base.element_size()
+        start = (p.data_ptr() - base.data_ptr()) // row
+        if (p.data_ptr() - base.data_ptr()) % row == 0 and n.data_ptr() == p.data_ptr() + p.shape[0] * row:
+            return base.narrow(0, start, p.shape[0] + n.shape[0])
+    return torch.cat([p, n], dim=0)
+
+
+def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *args, temperature: float = 0.1,
+                                  compute_dtype: str = "fp32", cross_device_negatives: bool = False,
+                                  group=None) -> torch.Tensor:
+    """CE over S = q d^T / temperature with labels arange(B) (losses.py:88-118), on the fused
+    MFMA scorer.  Third positional argument: a negatives tensor (train.py:133 call) or the
+    reference's positional temperature.  ``cross_device_negatives`` all-gathers the candidates
+    of every data-parallel rank (RCCL) and offsets the labels by this rank's slot."""
+    if args:
+        if isinstance(args[0], torch.Tensor):
+            d_emb = _candidates(d_emb, args[0])
+            if len(args) > 1:
+                temperature = args[1]
+        else:
+            temperature = args[0]
+    label_off = 0
+    if cross_device_negatives:
+        from .distributed import gather_candidates
+
+        d_emb, label_off = gather_candidates(d_emb, group=group)
+    return ops.in_batch_softmax_loss(q_emb, d_emb, temperature, label_off=label_off, compute_dtype=compute_dtype)
+
+
+LOSS_REGISTRY = {
+    "triplet": contrastive_triplet_loss,
+    "multiple_negatives": multiple_negatives_loss,
+    "in_batch": in_batch_sampled_softmax_loss,
+}
+
+
+def build(name: str, **kwargs) -> Callable:
+    """Loss by name with bound kwargs (losses.py:129-150)."""
+    if name not in LOSS_REGISTRY:
+        raise ValueError(f"Unknown loss function: {name}. Available options: {list(LOSS_REGISTRY.keys())}")
+    fn = LOSS_REGISTRY[name]
+    return partial(fn, **kwargs) if kwargs else fn

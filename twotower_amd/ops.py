@@ -1,0 +1,274 @@
+"""Autograd wrappers over the C ABI.  Every forward/backward here launches HIP kernels from
+libtwotower_amd.so on the tensor's current stream; nothing falls back to ATen compute.
+
+Reference call sites each op replaces are cited per function (paths inside k0r1g/two-towers).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, require_gpu, stream_of
+
+_FLOAT = torch.float32
+
+
+def _contig_f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != _FLOAT:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    return t.contiguous()
+
+
+# --------------------------------------------------------------------------------------------
+# Embedding bag: gather + masked mean-pool   (twotower/embeddings.py:30,40; encoders.py:62-72)
+class _Workspace:
+    """Per-device scratch buffers grown on demand (the C side never allocates)."""
+
+    def __init__(self):
+        self._bufs: dict[tuple, torch.Tensor] = {}
+
+    def get(self, key: str, nbytes: int, device: torch.device) -> torch.Tensor:
+        k = (key, device)
+        buf = self._bufs.get(k)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+            self._bufs[k] = buf
+        return buf
+
+
+WORKSPACE = _Workspace()
+
+
+def bag_mean_forward(weight: torch.Tensor, ids: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """pooled (N, E) and denom (N,) = count of ids > 0 plus 1e-9 (encoders.py:62-72)."""
+    require_gpu(weight, ids)
+    if ids.dim() != 2:
+        raise ValueError(f"ids must be (batch, seq_len), got shape {tuple(ids.shape)}")
+    ids = ids.contiguous()
+    V, E = weight.shape
+    N, L = ids.shape
+    pooled = torch.empty(N, E, dtype=_FLOAT, device=weight.device)
+    denom = torch.empty(N, dtype=_FLOAT, device=weight.device)
+    call("tt_bag_mean_fwd", ptr(weight), V, E, ptr(ids), _lib.ids_dtype_code(ids), N, L, L, ptr(pooled), ptr(denom),
+         stream_of(weight))
+    return pooled, denom
+
+
+def bag_mean_backward(d_pooled: torch.Tensor, denom: torch.Tensor, ids: torch.Tensor, V: int,
+                      padding_idx: int | None, mode: int = _lib.TT_SCATTER_SORTED) -> torch.Tensor:
+    """Dense (V, E) table gradient (embedding_dense_backward of the pooled lookup)."""
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    N, E = d_pooled.shape
+    L = ids.shape[1]
+    dev = d_pooled.device
+    pad = -1 if padding_idx is None else int(padding_idx)
+    if mode == _lib.TT_SCATTER_ATOMIC:
+        grad = torch.zeros(V, E, dtype=_FLOAT, device=dev)
+        call("tt_bag_mean_bwd", ptr(d_pooled), ptr(denom), ptr(ids), _lib.ids_dtype_code(ids), N, L, L, V, E, pad,
+             ptr(grad), mode, None, 0, stream_of(d_pooled))
+        return grad
+    grad = torch.empty(V, E, dtype=_FLOAT, device=dev)
+    nbytes = _lib.lib().tt_bag_mean_bwd_ws_size(N, L, V, E)
+    ws = WORKSPACE.get("bag_bwd", nbytes, dev)
+    call("tt_bag_mean_bwd", ptr(d_pooled), ptr(denom), ptr(ids), _lib.ids_dtype_code(ids), N, L, L, V, E, pad,
+         ptr(grad), mode, ptr(ws), ws.numel(), stream_of(d_pooled))
+    return grad
+
+
+class DeferredTableGrad:
+    """Table gradient kept in its factored form (ids, d_pooled, denom) so a fused optimizer can
+    apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer."""
+
+    __slots__ = ("parts", "padding_idx")
+
+    def __init__(self, padding_idx: int | None = 0):
+        self.parts: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
+        self.padding_idx = padding_idx
+
+
+class BagMeanPool(torch.autograd.Function):
+    """pooled = masked mean of weight[ids] over the sequence (ids > 0 are real tokens)."""
+
+    @staticmethod
+    def forward(ctx, weight, ids, padding_idx, scatter_mode):
+        pooled, denom = bag_mean_forward(weight, ids)
+        ctx.save_for_backward(ids, denom)
+        ctx.V = weight.shape[0]
+        ctx.padding_idx = padding_idx
+        ctx.scatter_mode = scatter_mode
+        ctx.weight_ref = weight
+        return pooled
+
+    @staticmethod
+    def backward(ctx, d_pooled):
+        ids, denom = ctx.saved_tensors
+        weight = ctx.weight_ref
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        deferred = getattr(weight, "_tt_deferred", None)
+        if deferred is not None:
+            # A fused optimizer owns this table: hand it the factored gradient.
+            deferred.parts.append((ids, d_pooled.contiguous(), denom))
+            return None, None, None, None
+        grad = bag_mean_backward(d_pooled, denom, ids, ctx.V, ctx.padding_idx, ctx.scatter_mode)
+        return grad, None, None, None
+
+
+def bag_mean_pool(weight: torch.Tensor, ids: torch.Tensor, padding_idx: int | None = 0,
+                  scatter_mode: int = _lib.TT_SCATTER_SORTED) -> torch.Tensor:
+    return BagMeanPool.apply(weight, ids, padding_idx, scatter_mode)
+
+
+# --------------------------------------------------------------------------------------------
+# F.normalize(x, dim=-1), eps 1e-12   (twotower/encoders.py:77)
+class L2Normalize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        require_gpu(x)
+        x = _contig_f32(x, "x")
+        rows, H = x.shape
+        out = torch.empty_like(x)
+        norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
+        call("tt_l2norm_fwd", ptr(x), rows, H, ptr(out), ptr(norm), stream_of(x))
+        ctx.save_for_backward(out, norm)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        out, norm = ctx.saved_tensors
+        dout = _contig_f32(dout, "dout")
+        dx = torch.empty_like(out)
+        call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dx), stream_of(out))
+        return dx
+
+
+def l2_normalize(x: torch.Tensor) -> torch.Tensor:
+    return L2Normalize.apply(x)
+
+
+# --------------------------------------------------------------------------------------------
+# contrastive_triplet_loss   (twotower/losses.py:9-44)
+class TripletLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, p, n, margin):
+        require_gpu(q, p, n)
+        q, p, n = (_contig_f32(t, nm) for t, nm in ((q, "q"), (p, "p"), (n, "n")))
+        B, H = q.shape
+        rows = torch.empty(B, dtype=_FLOAT, device=q.device)
+        loss = torch.empty((), dtype=_FLOAT, device=q.device)
+        call("tt_triplet_fwd", ptr(q), ptr(p), ptr(n), B, H, float(margin), ptr(rows), ptr(loss), stream_of(q))
+        ctx.save_for_backward(q, p, n)
+        ctx.margin = float(margin)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        q, p, n = ctx.saved_tensors
+        B, H = q.shape
+        g = g.to(_FLOAT).contiguous().reshape(1)
+        dq, dp, dn = torch.empty_like(q), torch.empty_like(p), torch.empty_like(n)
+        call("tt_triplet_bwd", ptr(q), ptr(p), ptr(n), B, H, ctx.margin, ptr(g), ptr(dq), ptr(dp), ptr(dn),
+             stream_of(q))
+        return dq, dp, dn, None
+
+
+# --------------------------------------------------------------------------------------------
+# multiple_negatives_loss   (twotower/losses.py:47-85)
+class MultiNegLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, p, negs, inv_tau):
+        require_gpu(q, p, negs)
+        q, p, negs = _contig_f32(q, "q"), _contig_f32(p, "p"), _contig_f32(negs, "negs")
+        B, H = q.shape
+        N = negs.shape[1]
+        rows = torch.empty(B, dtype=_FLOAT, device=q.device)
+        loss = torch.empty((), dtype=_FLOAT, device=q.device)
+        call("tt_multi_neg_fwd", ptr(q), ptr(p), ptr(negs), B, N, H, float(inv_tau), ptr(rows), ptr(loss),
+             stream_of(q))
+        ctx.save_for_backward(q, p, negs)
+        ctx.inv_tau = float(inv_tau)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        q, p, negs = ctx.saved_tensors
+        B, H = q.shape
+        N = negs.shape[1]
+        g = g.to(_FLOAT).contiguous().reshape(1)
+        dq, dp, dnegs = torch.empty_like(q), torch.empty_like(p), torch.empty_like(negs)
+        call("tt_multi_neg_bwd", ptr(q), ptr(p), ptr(negs), B, N, H, ctx.inv_tau, ptr(g), ptr(dq), ptr(dp),
+             ptr(dnegs), stream_of(q))
+        return dq, dp, dnegs, None
+
+
+# --------------------------------------------------------------------------------------------
+# in_batch_sampled_softmax_loss   (twotower/losses.py:88-118), fused MFMA scorer
+class InBatchSoftmaxLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale):
+        require_gpu(q, d)
+        q, d = _contig_f32(q, "q"), _contig_f32(d, "d")
+        B, H = q.shape
+        M = d.shape[0]
+        if d.shape[1] != H:
+            raise ValueError(f"q is (B, {H}) but d is {tuple(d.shape)}")
+        dt = _lib.compute_dtype_code(compute_dtype)
+        dev = q.device
+        want_grad = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        nbytes = _lib.lib().tt_inbatch_ws_size(B, M, H, dt)
+        # The workspace carries the bf16 operands from forward to backward: one per call.
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        lse = torch.empty(B, dtype=_FLOAT, device=dev)
+        rows = torch.empty(B, dtype=_FLOAT, device=dev)
+        loss = torch.empty((), dtype=_FLOAT, device=dev)
+        dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
+        call("tt_inbatch_fwd", ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
+             ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
+        if want_grad:
+            ctx.save_for_backward(q, d, lse, dqu, ws)
+        ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off),
+                    float(1.0 / B) if grad_scale is None else float(grad_scale))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        q, d, lse, dqu, ws = ctx.saved_tensors
+        B, M, H, dt, inv_tau, label_off, grad_scale = ctx.meta
+        g = g.to(_FLOAT).contiguous().reshape(1)
+        dq, dd = torch.empty_like(q), torch.empty_like(d)
+        call("tt_inbatch_bwd", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g),
+             grad_scale, ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(q))
+        return dq, dd, None, None, None, None
+
+
+def in_batch_softmax_loss(q: torch.Tensor, d: torch.Tensor, temperature: float = 0.1, label_off: int = 0,
+                          compute_dtype="fp32", grad_scale: float | None = None) -> torch.Tensor:
+    return InBatchSoftmaxLoss.apply(q, d, 1.0 / float(temperature), label_off, compute_dtype, grad_scale)
+
+
+# --------------------------------------------------------------------------------------------
+# torch.optim.AdamW step (twotower/train.py:359, :139)
+def adamw_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,
+               lr: float, beta1: float, beta2: float, eps: float, weight_decay: float, step: int) -> None:
+    require_gpu(param, grad, exp_avg, exp_avg_sq)
+    for t, nm in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        if not t.is_contiguous() or t.dtype != _FLOAT:
+            raise ValueError(f"{nm} must be a contiguous float32 tensor")
+    call("tt_adamw", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), lr, beta1, beta2, eps,
+         weight_decay, step, stream_of(param))
+
+
+def bag_mean_backward_adamw(d_pooled, denom, ids, table, exp_avg, exp_avg_sq, padding_idx, *, lr, beta1, beta2,
+                            eps, weight_decay, step) -> None:
+    """Sorted scatter of the pooled gradient fused with the table's AdamW step."""
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    N, E = d_pooled.shape
+    V = table.shape[0]
+    L = ids.shape[1]
+    dev = table.device
+    nbytes = _lib.lib().tt_bag_mean_bwd_ws_size(N, L, V, E)
+    ws = WORKSPACE.get("bag_bwd", nbytes, dev)
+    pad = -1 if padding_idx is None else int(padding_idx)
+    call("tt_bag_mean_bwd_adamw", ptr(d_pooled), ptr(denom), ptr(ids), _lib.ids_dtype_code(ids), N, L, L, V, E,
+         pad, ptr(table), ptr(exp_avg), ptr(exp_avg_sq), lr, beta1, beta2, eps, weight_decay, step, ptr(ws),
+         ws.numel(), stream_of(table))
