@@ -73,14 +73,16 @@ int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom,
                           const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
                           int64_t V, int E, int64_t padding_idx,
                           float* table, float* exp_avg, float* exp_avg_sq,
-                          float lr, float beta1, float beta2, float eps, float weight_decay,
+                          double lr, double beta1, double beta2, double eps, double weight_decay,
                           int64_t step, void* ws, size_t ws_bytes, tt_stream_t stream);
 
 /* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
  * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
- * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps).   step is 1-based. */
+ * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps).   step is 1-based.
+ * Hyper-parameters are double: like torch, the per-step scalars (1-b2, bias corrections) are
+ * formed in double and rounded to float once (1 - (float)0.999 would be off by 1.3e-5). */
 int tt_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
-             float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
+             double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
              tt_stream_t stream);
 
 /* ---- row L2 normalise (F.normalize(x, dim=-1), eps 1e-12; twotower/encoders.py:77) -- */

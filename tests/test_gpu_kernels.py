@@ -49,7 +49,7 @@ def test_bag_forward_vs_oracle(E, L, dtype):
     ids = edge_ids(N, L, V, rng, dtype)
     pooled, denom = ops.bag_mean_forward(cuda(table), ids)
     ref, ref_den = O.bag_mean_fwd(table.astype(np.float64), ids.cpu().numpy())
-    assert rel(pooled, ref) < 1e-6
+    assert rel(pooled, ref) < 1e-5
     np.testing.assert_allclose(denom.cpu().numpy(), ref_den.astype(np.float32), rtol=0, atol=0)
     assert torch.count_nonzero(pooled[0]) == 0
 

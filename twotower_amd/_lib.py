@@ -23,6 +23,7 @@ COMPUTE_DTYPES = {"fp32": TT_F32, "float32": TT_F32, "bf16": TT_BF16, "bfloat16"
                   "bf16_fast": TT_BF16_FAST}
 
 _c_i64, _c_int, _c_f32, _c_sz, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+_c_f64 = ctypes.c_double
 
 # name -> (restype, argtypes); must mirror include/twotower_amd.h
 _SIGNATURES = {
@@ -33,8 +34,8 @@ _SIGNATURES = {
     "tt_bag_mean_bwd": (_c_int, [_vp, _vp, _vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp, _c_int,
                                  _vp, _c_sz, _vp]),
     "tt_bag_mean_bwd_adamw": (_c_int, [_vp, _vp, _vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp,
-                                       _vp, _vp, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_i64, _vp, _c_sz, _vp]),
-    "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f32, _c_f32, _c_f32, _c_f32, _c_f32, _c_i64, _vp]),
+                                       _vp, _vp, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp, _c_sz, _vp]),
+    "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
     "tt_l2norm_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_triplet_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp]),

@@ -44,8 +44,8 @@ __global__ __launch_bounds__(kBlock) void adamw_scalar_kernel(float* __restrict_
 
 using namespace tt;
 
-extern "C" int tt_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr,
-                        float beta1, float beta2, float eps, float weight_decay, int64_t step, tt_stream_t stream) {
+extern "C" int tt_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                        double beta1, double beta2, double eps, double weight_decay, int64_t step, tt_stream_t stream) {
   TT_REQUIRE(n >= 0, "n=%lld", (long long)n);
   TT_REQUIRE(step >= 1, "step must be >= 1 (got %lld)", (long long)step);
   if (n == 0) return TT_OK;

@@ -202,9 +202,13 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
   const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   if (row >= V) return;
   const int st = seg_start[row], en = seg_end[row];
-  f32x4 acc[NV];
+  // U interleaved partial sums (entry e goes to partial (e - st) % U), folded in a fixed order:
+  // deterministic, ~U x shorter dependent add chains and error growth on hot (Zipf) rows.
+  f32x4 part[U][NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) part[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int e = st; e < en; e += U) {
     int s[U];
 #pragma unroll
@@ -219,7 +223,14 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < NV; ++k) acc[k] += v[u][k];
+      for (int k = 0; k < NV; ++k) part[u][k] += v[u][k];
+  }
+  f32x4 acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    acc[k] = part[0][k];
+#pragma unroll
+    for (int u = 1; u < U; ++u) acc[k] += part[u][k];
   }
   if constexpr (!FUSED) {
     f32x4* out = reinterpret_cast<f32x4*>(grad + row * E);
@@ -462,11 +473,17 @@ template <bool FUSED>
 static int bwd_impl(const float* dpooled, const float* denom, const void* ids, int ids_dtype, int64_t nseq,
                     int L, int64_t ld, int64_t V, int E, int64_t padding_idx, float* grad, float* param,
                     float* m, float* v, const AdamArgs& aa, void* ws, size_t ws_bytes, hipStream_t s) {
-  const size_t sb = sort_tmp_bytes(nseq * (int64_t)L, V);
+  if (nseq == 0 || L == 0) nseq = 0, L = 0;
+  const size_t sb = nseq > 0 ? sort_tmp_bytes(nseq * (int64_t)L, V) : 0;
   void* base = reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256));
   BwdWs w = carve(base, nseq, L, V, E, sb);
   TT_REQUIRE(ws != nullptr && w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu",
              w.total + 256, ws_bytes);
+  if (nseq == 0) {  // no tokens: every row's gradient is zero (segments stay empty)
+    TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
+    TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
+    return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, s);
+  }
   int rc = (ids_dtype == TT_IDS_I32)
                ? sorted_front(dpooled, denom, static_cast<const int32_t*>(ids), nseq, L, ld, V, padding_idx, E, w, s)
                : sorted_front(dpooled, denom, static_cast<const int64_t*>(ids), nseq, L, ld, V, padding_idx, E, w, s);
@@ -499,8 +516,8 @@ extern "C" int tt_bag_mean_bwd(const float* d_pooled, const float* denom, const 
 
 extern "C" int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom, const void* ids, int ids_dtype,
                                      int64_t nseq, int L, int64_t ld_ids, int64_t V, int E, int64_t padding_idx,
-                                     float* table, float* exp_avg, float* exp_avg_sq, float lr, float beta1,
-                                     float beta2, float eps, float weight_decay, int64_t step, void* ws,
+                                     float* table, float* exp_avg, float* exp_avg_sq, double lr, double beta1,
+                                     double beta2, double eps, double weight_decay, int64_t step, void* ws,
                                      size_t ws_bytes, tt_stream_t stream) {
   int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
   if (rc) return rc;

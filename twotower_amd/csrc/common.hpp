@@ -43,17 +43,17 @@ struct AdamArgs {
   float eps;
 };
 
-inline AdamArgs make_adam(float lr, float beta1, float beta2, float eps, float wd, int64_t step) {
+inline AdamArgs make_adam(double lr, double beta1, double beta2, double eps, double wd, int64_t step) {
   AdamArgs a;
-  const double bc1 = 1.0 - __builtin_pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - __builtin_pow((double)beta2, (double)step);
-  a.wd_factor = (float)(1.0 - (double)lr * (double)wd);
-  a.one_m_b1 = (float)(1.0 - (double)beta1);
-  a.beta2 = beta2;
-  a.one_m_b2 = (float)(1.0 - (double)beta2);
-  a.step_size = (float)((double)lr / bc1);
+  const double bc1 = 1.0 - __builtin_pow(beta1, (double)step);
+  const double bc2 = 1.0 - __builtin_pow(beta2, (double)step);
+  a.wd_factor = (float)(1.0 - lr * wd);
+  a.one_m_b1 = (float)(1.0 - beta1);
+  a.beta2 = (float)beta2;
+  a.one_m_b2 = (float)(1.0 - beta2);
+  a.step_size = (float)(lr / bc1);
   a.bc2_sqrt = (float)__builtin_sqrt(bc2);
-  a.eps = eps;
+  a.eps = (float)eps;
   return a;
 }
 

@@ -505,16 +505,17 @@ template <int MODE>
 int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
                     float c2, int64_t label_off, const float* lse, const Ws& w, hipStream_t s) {
   switch (H) {
+    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
     case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
     case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
     case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
-    default: set_error("in-batch scorer: H=%d unsupported (64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
+    default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
 }
 
 int check_args(int64_t B, int64_t M, int H, int dtype, int64_t label_off) {
   TT_REQUIRE(B > 0 && M > 0, "B=%lld M=%lld must be positive", (long long)B, (long long)M);
-  TT_REQUIRE(H == 64 || H == 128 || H == 256, "H=%d unsupported (64, 128, 256)", H);
+  TT_REQUIRE(H == 32 || H == 64 || H == 128 || H == 256, "H=%d unsupported (32, 64, 128, 256)", H);
   TT_REQUIRE(dtype == TT_F32 || dtype == TT_BF16 || dtype == TT_BF16_FAST, "dtype=%d", dtype);
   TT_REQUIRE(label_off >= 0 && label_off + B <= M, "labels [%lld, %lld) fall outside the %lld candidate columns",
              (long long)label_off, (long long)(label_off + B), (long long)M);
