@@ -24,7 +24,6 @@ constexpr int NW = 4;
 constexpr int NT = NW * kWave;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
-constexpr float kShiftGuard = 100.f;  // log2 units: a shift this far above the true max risks underflow
 enum Mode { FWD = 0, DD = 1 };
 
 __device__ __forceinline__ int acc_row(int v, int hh) { return (v & 3) + 8 * (v >> 2) + 4 * hh; }
@@ -121,7 +120,7 @@ __device__ __forceinline__ void elementwise(const f32x16& x, float (&e)[16], Elt
         const int64_t i = jb + acc_row(v, hh);
         float gv = 0.f;
         if (i < row_end) {
-          gv = exp2f(x[v] * c2 - l4[u] * kLog2e);
+          gv = exp2f(x[v] * c2 - l4[u]);
           if (my_col == i + label_off) gv -= 1.f;
         }
         e[v] = gv;
@@ -159,16 +158,125 @@ __device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], EltS
 // ------------------------------------------------------------------------------------------
 // bf16 engine (32x32x16 bf16 MFMA).  PRECISE splits G into hi + lo bf16 so the second product
 // carries ~16 mantissa bits; otherwise G is rounded once (flash-attention style).
+//
+// Schedule per 64-row stage (two 32-row X tiles, one barrier): S(0); then for each tile j the
+// next tile's S MFMA chain is issued beside tile j's elementwise map, and tile j's Acc MFMAs
+// beside nothing but their own LDS transposed reads: the VALU work (exp, bf16 packing) sits in
+// the MFMA issue gaps of an independent chain instead of between dependent ones.  All LDS
+// addressing is 32-bit; full tiles skip every mask, and the label compare runs only in the one
+// tile per column that holds the label.
+typedef __attribute__((address_space(3))) char lds_char_t;
+typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8_t;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4_t;
+
+template <int H>
+__device__ __forceinline__ f32x16 s_chain(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16]) {
+  using T = Tile<__bf16, H>;
+  constexpr int NK = H / 16;
+  const int rowb = row * T::ROWB, x = row & T::SWM;
+  f32x16 acc = f32x16{};
+  bf16x8 a[4];
+#pragma unroll
+  for (int k = 0; k < 4 && k < NK; ++k)
+    a[k] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * k + hh) ^ x) << 4));
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
+    if (kk + 4 < NK)
+      a[kk & 3] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * (kk + 4) + hh) ^ x) << 4));
+  }
+  return acc;
+}
+
+// Map one X tile to packed bf16 B operands (hi, lo) for the Acc product.
+template <int MODE, bool PRECISE>
+__device__ __forceinline__ void map_tile(const f32x16& x, bf16x8 (&bh)[2], bf16x8 (&bl)[2], int nvalid, int drel,
+                                         float c2, float shift, const lds_f32x4_t* lse4, int hh, float& l_run,
+                                         float& diag, bool& has_diag) {
+  float e[16];
+  if constexpr (MODE == FWD) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(x[v] * c2 - shift);
+  } else {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 l4 = lse4[2 * g4 + hh];  // lse of rows 8*g4 + 4*hh + u (log2 units)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[4 * g4 + u] = __builtin_amdgcn_exp2f(x[4 * g4 + u] * c2 - l4[u]);
+    }
+  }
+  if (nvalid < 32) {  // wave-uniform: only the last tile of a split
+#pragma unroll
+    for (int v = 0; v < 16; ++v) e[v] = acc_row(v, hh) < nvalid ? e[v] : 0.f;
+  }
+  if (__any(drel >= 0 && drel < 32)) {  // the label column of some lane falls in this tile
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      if (acc_row(v, hh) == drel) {
+        if constexpr (MODE == FWD) {
+          diag = x[v];
+          has_diag = true;
+        } else {
+          e[v] -= 1.f;
+        }
+      }
+    }
+  }
+  if constexpr (MODE == FWD) {
+    float ls = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) ls += e[v];
+    l_run += ls;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const float v = e[8 * s2 + jj];
+      const __bf16 h = (__bf16)v;
+      bh[s2][jj] = h;
+      if constexpr (PRECISE) bl[s2][jj] = (__bf16)(v - (float)h);
+    }
+}
+
+// Acc^T[h][col] += tile^T[h][rows] * G[rows][col] for one 32-row X tile.
+template <bool PRECISE, int H>
+__device__ __forceinline__ void acc_chain(const lds_char_t* tile, int jt, int lane, const bf16x8 (&bh)[2],
+                                          const bf16x8 (&bl)[2], f32x16 (&acc)[H / 32]) {
+  using T = Tile<__bf16, H>;
+  constexpr int NHT = H / 32;
+  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
+  const int r0 = jt * 32 + 4 * (tg >> 1) + tq;  // + 16*s2 (+8 for the second read): same (row & SWM)
+  const int x0 = r0 & T::SWM, x1 = (r0 + 8) & T::SWM;
+  const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int rb0 = (r0 + 16 * s2) * T::ROWB + bo, rb1 = (r0 + 16 * s2 + 8) * T::ROWB + bo;
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht) {
+      const int ch = 4 * ht + cbase;
+      const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb0 + ((ch ^ x0) << 4)));
+      const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb1 + ((ch ^ x1) << 4)));
+      const bf16x8 a = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+      acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh[s2], acc[ht], 0, 0, 0);
+      if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl[s2], acc[ht], 0, 0, 0);
+    }
+  }
+}
+
 template <int MODE, bool PRECISE, int H>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, int64_t label_off, const float* __restrict__ lse_rows,
-    const float* __restrict__ col_shift, float* __restrict__ acc_part, float* __restrict__ m_part, float* __restrict__ l_part,
-    float* __restrict__ diag_raw) {
+    const float* __restrict__ col_shift, float* __restrict__ acc_part, float* __restrict__ m_part,
+    float* __restrict__ l_part, float* __restrict__ diag_raw) {
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
   constexpr int NHT = H / 32;
+  constexpr int NJ = T::BJ / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;  // addrspacecast: 32-bit LDS offsets from here on
 
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -179,6 +287,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
   const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
+  // label of this column, relative to the split (FWD: row index of D; DD: row index of Q)
+  const int64_t lab = (MODE == FWD) ? my_col + label_off : my_col - label_off;
 
   if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse_rows);
 
@@ -196,55 +306,49 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   f32x16 acc[NHT];
 #pragma unroll
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  EltState<MODE> st;
+  float l_run = 0.f, diag = 0.f;
+  bool has_diag = false;
   __syncthreads();
-
-  // transposed-read lane geometry (T10): group g = lane>>4 reads rows 4*(g>>1)+q, cols 16*(g&1)+4p
-  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
 
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 1);
     if (t + 1 < ntiles) stage_tile<__bf16, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse_rows);
-    const char* base = smem + buf * T::STAGE_B;
-    const float* lse_tile = reinterpret_cast<const float*>(smem + 2 * T::STAGE_B + buf * 256);
+    const lds_char_t* tile = lds + buf * T::STAGE_B;
+    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + 2 * T::STAGE_B + buf * 256);
+    const int64_t jb0 = row_begin + t * T::BJ;
+    f32x16 xa = s_chain<H>(tile, r32, hh, cf);
 #pragma unroll
-    for (int jt = 0; jt < T::BJ / 32; ++jt) {
-      const int64_t jb = row_begin + t * T::BJ + jt * 32;
-      f32x16 x = f32x16{};
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + T::off(jt * 32 + r32, 2 * kk + hh));
-        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cf[kk], x, 0, 0, 0);
-      }
-      float e[16];
-      elementwise<MODE>(x, e, st, jb, row_end, my_col, label_off, c2, shift, lse_tile + jt * 32, hh);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 bh, bl;
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const float v = e[8 * s2 + jj];
-          const __bf16 h = (__bf16)v;
-          bh[jj] = h;
-          if constexpr (PRECISE) bl[jj] = (__bf16)(v - (float)h);
-        }
-        const int row1 = jt * 32 + 16 * s2 + 4 * (tg >> 1) + tq;
-#pragma unroll
-        for (int ht = 0; ht < NHT; ++ht) {
-          const int hcol = ht * 32 + 16 * (tg & 1) + 4 * tp;
-          const int ch = hcol >> 3, bo = (hcol & 7) * 2;
-          typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-          const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + T::off(row1, ch) + bo));
-          const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(base + T::off(row1 + 8, ch) + bo));
-          const bf16x8 a = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-          acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc[ht], 0, 0, 0);
-          if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc[ht], 0, 0, 0);
-        }
-      }
+    for (int jt = 0; jt < NJ; ++jt) {
+      f32x16 xb = f32x16{};
+      if (jt + 1 < NJ) xb = s_chain<H>(tile, (jt + 1) * 32 + r32, hh, cf);
+      const int64_t jb = jb0 + jt * 32;
+      const int nvalid = (int)min<int64_t>(32, row_end - jb);
+      const int64_t dr = lab - jb;
+      const int drel = (dr >= 0 && dr < nvalid) ? (int)dr : -1;  // labels only on real rows
+      bf16x8 bh[2], bl[2];
+      map_tile<MODE, PRECISE>(xa, bh, bl, nvalid, drel, c2, shift, lse4 + jt * 8, hh, l_run, diag, has_diag);
+      acc_chain<PRECISE, H>(tile, jt, lane, bh, bl, acc);
+      xa = xb;
     }
     __syncthreads();
   }
-  write_partials<MODE, H>(acc, st, split, nC, my_col, hh, acc_part, m_part, l_part, diag_raw);
+
+  if (my_col < nC) {
+    float* dst = acc_part + ((int64_t)split * nC + my_col) * H;
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<f32x4*>(dst + ht * 32 + 8 * g4 + 4 * hh) =
+            f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
+  }
+  if constexpr (MODE == FWD) {
+    l_run += __shfl_xor(l_run, 32);
+    if (my_col < nC) {
+      if (hh == 0) l_part[(int64_t)split * nC + my_col] = l_run;
+      if (has_diag) diag_raw[my_col] = diag;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -321,28 +425,36 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// Operand prep, one wave per row: optional fp32 -> bf16 (RNE) copy, row L2 norm, and the max
-// norm over rows (atomicMax on the float bits; norms are >= 0 so the integer order is the
-// float order).
+// Operand prep: optional fp32 -> bf16 (RNE) copy, row L2 norm, and the max norm over rows.
+// Grid-stride over rows, one wave per row; the max is folded per wave, then per block in LDS,
+// then ONE atomicMax per block (norms >= 0 so float order == unsigned bit order).  A single
+// address hit by every row serialises at the memory side (MI355X_MICROARCH: 14x slower).
 __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ x, int64_t rows, int H,
                                                         __bf16* __restrict__ xb, float* __restrict__ norms,
                                                         unsigned* __restrict__ max_bits) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const int lane = lane_id();
-  const f32x4* src = reinterpret_cast<const f32x4*>(x + r * H);
-  float ss = 0.f;
-  for (int c = lane; c < H / 4; c += kWave) {
-    const f32x4 v = src[c];
-    ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-    if (xb)
-      reinterpret_cast<bf16x4*>(xb + r * H)[c] = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  __shared__ float wmax[4];
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  float mx = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < rows; r += (int64_t)gridDim.x * 4) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(x + r * H);
+    float ss = 0.f;
+    for (int c = lane; c < H / 4; c += kWave) {
+      const f32x4 v = src[c];
+      ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      if (xb)
+        reinterpret_cast<bf16x4*>(xb + r * H)[c] = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    }
+    const float n = sqrtf(wave_sum(ss));
+    if (lane == 0 && norms) norms[r] = n;
+    mx = fmaxf(mx, n);
   }
-  ss = wave_sum(ss);
-  if (lane == 0) {
-    const float n = sqrtf(ss);
-    if (norms) norms[r] = n;
-    if (max_bits) atomicMax(max_bits, __float_as_uint(n));
+  if (max_bits) {
+    if (lane == 0) wmax[wid] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+      atomicMax(max_bits, __float_as_uint(m));
+    }
   }
 }
 
@@ -356,7 +468,7 @@ __global__ __launch_bounds__(256) void shift_kernel(const float* __restrict__ qn
 }
 
 // Merge forward split partials: one wave per query row.  Rows whose shift sits more than
-// kShiftGuard above the true max could have underflowed: they report NaN (fail loudly).
+// so far above the true max that the terms underflow report NaN (fail loudly).
 template <typename DT>
 __global__ __launch_bounds__(256) void fwd_combine_kernel(
     int64_t B, int H, int S, const float* __restrict__ shift, const float* __restrict__ m_part,
@@ -366,13 +478,12 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= B) return;
   const int lane = lane_id();
-  float mt = -INFINITY, l = 0.f;
-  for (int s = 0; s < S; ++s) {
-    mt = fmaxf(mt, m_part[(int64_t)s * B + i]);
-    l += l_part[(int64_t)s * B + i];
-  }
+  float l = 0.f;
+  for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
+  // l = sum_j 2^(z_ij - shift_i) with shift_i >= max_j z_ij.  l >= 2^-100 keeps the dominant
+  // terms normal floats (>= 2^-114 each); below it the bound was too loose: report NaN.
   const float sh = shift[i];
-  const bool ok = l > 0.f && sh - mt < kShiftGuard;
+  const bool ok = l >= 7.888609052210118e-31f;
   const float lse_i = ok ? (sh + log2f(l)) * kLn2 : NAN;
   if (lane == 0) {
     lse[i] = lse_i;
@@ -387,6 +498,11 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
       dqu[i * H + h] = o * inv_l - (float)dl[h];
     }
   }
+}
+
+__global__ __launch_bounds__(256) void to_log2_kernel(const float* __restrict__ lse, int64_t n, float* __restrict__ lse2) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) lse2[i] = lse[i] * kLog2e;
 }
 
 // dd = scale * sum_s part[s]; dq = scale * dqu (scale = grad_loss * grad_scale * inv_tau).
@@ -439,6 +555,7 @@ struct Ws {
   __bf16* Db;
   float* qnorm;
   float* shift;
+  float* lse2;
   unsigned* dmax;
   float* diag;
   float* m_part;
@@ -460,7 +577,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     return o;
   };
   const size_t oq = take(bf ? (size_t)B * H * 2 : 0), od = take(bf ? (size_t)M * H * 2 : 0);
-  const size_t oqn = take((size_t)B * 4), osh = take((size_t)B * 4), omx = take(16);
+  const size_t oqn = take((size_t)B * 4), osh = take((size_t)B * 4), ol2 = take((size_t)B * 4), omx = take(16);
   const size_t odg = take((size_t)B * 4), om = take((size_t)pf.S * B * 4), ol = take((size_t)pf.S * B * 4);
   const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   const size_t oa = take(parts);
@@ -471,6 +588,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.Db = reinterpret_cast<__bf16*>(b + od);
     w.qnorm = reinterpret_cast<float*>(b + oqn);
     w.shift = reinterpret_cast<float*>(b + osh);
+    w.lse2 = reinterpret_cast<float*>(b + ol2);
     w.dmax = reinterpret_cast<unsigned*>(b + omx);
     w.diag = reinterpret_cast<float*>(b + odg);
     w.m_part = reinterpret_cast<float*>(b + om);
@@ -551,8 +669,9 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   const float c2 = inv_tau * kLog2e;
   const bool bf = dtype != TT_F32;
   TT_HIP(hipMemsetAsync(w.dmax, 0, 16, s), "memset dmax");
-  prep_rows_kernel<<<dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s>>>(q, B, H, bf ? w.Qb : nullptr, w.qnorm, nullptr);
-  prep_rows_kernel<<<dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s>>>(d, M, H, bf ? w.Db : nullptr, nullptr, w.dmax);
+  auto prep_grid = [](int64_t rows) { return dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 1024)); };
+  prep_rows_kernel<<<prep_grid(B), dim3(256), 0, s>>>(q, B, H, bf ? w.Qb : nullptr, w.qnorm, nullptr);
+  prep_rows_kernel<<<prep_grid(M), dim3(256), 0, s>>>(d, M, H, bf ? w.Db : nullptr, nullptr, w.dmax);
   shift_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(w.qnorm, w.dmax, B, c2, w.shift);
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
@@ -584,7 +703,9 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   const float c2 = inv_tau * kLog2e;
   const void* Rm = (dtype == TT_F32) ? (const void*)q : (const void*)w.Qb;  // operands left by the forward
   const void* Cm = (dtype == TT_F32) ? (const void*)d : (const void*)w.Db;
-  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, label_off, lse, w, s))) return rc;
+  to_log2_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(lse, B, w.lse2);
+  TT_LAUNCH_CHECK("score_lse2");
+  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, label_off, w.lse2, w, s))) return rc;
   const int64_t rows = std::max(B, M);
   bwd_combine_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(B, M, H, p.S, w.acc_part, dq_unscaled,
                                                                            grad_loss, grad_scale, inv_tau, dq, dd);
