@@ -5,14 +5,18 @@
 // B x M is never materialised.  One engine serves both passes:
 //   * a workgroup keeps 4 x 32 "column" rows resident in VGPRs as the MFMA B operand and
 //     streams the other matrix through a double-buffered, XOR-swizzled LDS tile;
-//   * X = R_tile * C^T (32x32 per wave, 32x32x16 bf16 or 32x32x2 f32 MFMA), an elementwise map
-//     G = f(X) in registers, then Acc^T += R_tile^T * G with the X accumulator reused as the
-//     next MFMA's B operand (no LDS round trip) and R_tile^T read with ds_read_b64_tr_b16.
-//   forward  (R = D, C = Q): G = exp2(X*c2 - m) with a lazily rescaled running max, Acc = O^T,
-//            giving lse and O = P D per query => dQ needs no extra pass.
-//   backward (R = Q, C = D): G = exp2(X*c2 - lse2_i) - [j == i + off], Acc = dD^T.
-// The streamed dimension is split over workgroups (blockIdx % S == split, so one split per XCD
-// when S == 8); split partials are merged by small combine kernels.
+//   * X = R_tile C^T (32x32 per wave; 32x32x16 bf16 or 32x32x2 f32 MFMA), an elementwise map
+//     G = f(X) in registers, then Acc^T += R_tile^T G with the X accumulator reused as the next
+//     MFMA's B operand (no LDS round trip) and R_tile^T read with ds_read_b64_tr_b16.
+//   forward  (R = D, C = Q): G = 2^(X c2 - shift_i), shift_i >= max_j X_ij c2 a per-query bound
+//            (no running max, no accumulator rescale); Acc = O^T, so dQ needs no extra pass.
+//   backward (R = Q, C = D): G = 2^(X c2 - lse2_i); Acc = dD^T.
+// The inner loop has no masks and no label logic: rows past the end are zero rows staged from
+// a pad buffer (backward: their lse = +inf, so G = 0); in the forward each pad row adds exactly
+// 2^-shift_i to l_i and nothing to O, removed by the combine.  The label terms (the diagonal
+// logit, the -q_i contribution to dD) are applied by the combine kernels.
+// The streamed dimension is split over workgroups (blockIdx % S == split: one split per XCD
+// when S == 8); split partials are merged by the combine kernels.
 #include "common.hpp"
 
 namespace tt {
@@ -24,115 +28,96 @@ constexpr int NW = 4;
 constexpr int NT = NW * kWave;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
+constexpr int kPadBytes = 2048;  // zero row source (>= one 1 KiB row) + one +inf float after it
 enum Mode { FWD = 0, DD = 1 };
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) char lds_char_t;
+typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8_t;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4_t;
+typedef __attribute__((address_space(3))) float lds_float_t;
 
 __device__ __forceinline__ int acc_row(int v, int hh) { return (v & 3) + 8 * (v >> 2) + 4 * hh; }
 
 // ------------------------------------------------------------------------------------------
 // LDS tile image shared by both engines: BJ rows of H elements, row-major, 16-byte chunk c of
 // row r stored at chunk c ^ (r & SWM).  The swizzle makes the 32-rows-same-column ds_read_b128
-// operand reads hit 16 distinct slots; the column reads (ds_read_b32 / ds_read_b64_tr_b16)
-// stay inside one row and remain conflict-free.  Tiles are filled by global_load_lds
-// (16 B per lane, 1 KiB per wave-instruction, no staging VGPRs): the LDS side is written
-// linearly, so the swizzle is applied to the per-lane SOURCE address (rule 21).
+// operand reads hit distinct slots; the column reads (ds_read_b32 / ds_read_b64_tr_b16) stay
+// inside one row.  Tiles are filled by global_load_lds (16 B per lane, 1 KiB per wave-
+// instruction, no staging VGPRs): the LDS side is written linearly, so the swizzle is applied
+// to the per-lane SOURCE address (cdna_hip_programming.md rule 21).
 template <typename ET, int H>
 struct Tile {
   static constexpr int BJ = sizeof(ET) == 2 ? 64 : 32;
   static constexpr int ROWB = H * (int)sizeof(ET);
   static constexpr int NCH = ROWB / 16;
   // bf16: 4-bit XOR (row reads conflict-free).  f32: 3-bit XOR keeps every h-tile of a column
-  // read at a constant byte offset from the first (immediate offsets, no per-tile address
-  // VGPRs) at the price of 2-way conflicts on the 16-byte row reads.
+  // read at a constant byte offset from the first, at the price of 2-way row-read conflicts.
   static constexpr int SWM = ((sizeof(ET) == 2 && NCH >= 16) ? 16 : (NCH >= 8 ? 8 : NCH)) - 1;
   static constexpr int STAGE_B = BJ * ROWB;
   static constexpr int NI = STAGE_B / 1024 / NW;  // glds wave-instructions per wave per stage
   static_assert(NI * 1024 * NW == STAGE_B, "stage must be a whole number of 1 KiB pieces per wave");
   static constexpr int LDS_BYTES = 2 * STAGE_B + 2 * 64 * 4;  // two stages + two 64-float lse rows
-  __device__ static __forceinline__ int off(int row, int ch) { return row * ROWB + ((ch ^ (row & SWM)) << 4); }
+  // Chunk XOR of a row.  bf16 rows of >= 256 B use the dual-use swizzle (cdna_hip_programming.md
+  // T10 (b)): bits 0-1 of the row go to chunk bits 2-3 and bits 2-3 to chunk bits 0-1, so both
+  // the 16-row ds_read_b128 operand reads and the 4-row x 64-B transposed reads of a 32-lane half
+  // cover all 64 banks once (a plain (row & 15) XOR leaves the transposed reads 4-way conflicted).
+  __device__ static __forceinline__ int swz(int row) {
+    if constexpr (sizeof(ET) == 2 && NCH >= 16) return ((row & 3) << 2) | ((row >> 2) & 3);
+    else return row & SWM;
+  }
 };
 
-typedef __attribute__((address_space(3))) void lds_void_t;
+// LDS-DMA issued through inline asm: hipcc treats a builtin global_load_lds as a pending write
+// to ALL of LDS and waits vmcnt(0) before the next transposed LDS read, which would drain the
+// next stage's prefetch right after issuing it.  The asm form is invisible to that pass; the
+// kernels drain it themselves with one explicit vmcnt(0) in front of the stage barrier (the
+// compiler's own counted waits stay correct: extra older VMEM ops only make them wait longer).
+__device__ __forceinline__ void glds_dwordx4(const void* gsrc, unsigned lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_base)
+               : "memory");  // m0 is reserved (no live compiler value: no other LDS-DMA here)
+}
+__device__ __forceinline__ void glds_dword(const void* gsrc, unsigned lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(gsrc), "s"(lds_base)
+               : "memory");  // m0 is reserved (no live compiler value: no other LDS-DMA here)
+}
+__device__ __forceinline__ void drain_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Issue the global_load_lds pieces that fill stage `buf` with rows [r0, r0 + BJ) of R (rows at
-// or past row_end are clamped to a real row; their products are masked by the caller).
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const lds_char_t*)p;  // 32-bit LDS byte address
+}
+
+// Fill stage `buf` with rows [r0, r0 + BJ) of R; rows at or past row_end come from the zero pad
+// (and, backward, an lse of +inf).
 template <typename ET, int H, int MODE>
 __device__ __forceinline__ void stage_tile(char* smem, int buf, const ET* __restrict__ R, int64_t r0, int64_t row_end,
-                                           const float* __restrict__ lse_rows) {
+                                           const float* __restrict__ lse2_rows, const char* __restrict__ pad) {
   using T = Tile<ET, H>;
   const int lane = lane_id(), wid = threadIdx.x >> 6;
-  char* base = smem + buf * T::STAGE_B;
+  const unsigned base = lds_addr(smem) + buf * T::STAGE_B;
 #pragma unroll
   for (int c = 0; c < T::NI; ++c) {
     const int wbase = (c * NW + wid) * 1024;
     const int p = wbase + lane * 16;
     const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
-    const int ch = slot ^ (row & T::SWM);
-    int64_t g = r0 + row;
-    g = g < row_end ? g : row_end - 1;
-    const char* src = reinterpret_cast<const char*>(R + g * H) + ch * 16;
-    __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(base + wbase), 16, 0, 0);
+    const int ch = slot ^ T::swz(row);
+    const int64_t g = r0 + row;
+    const char* src = (g < row_end) ? reinterpret_cast<const char*>(R + g * H) + ch * 16 : pad + ch * 16;
+    glds_dwordx4(src, __builtin_amdgcn_readfirstlane(base + wbase));
   }
   if constexpr (MODE == DD) {
     if (wid == 0) {
-      int64_t g = r0 + lane;
-      g = g < row_end ? g : row_end - 1;
-      __builtin_amdgcn_global_load_lds(lse_rows + g, (lds_void_t*)(smem + 2 * T::STAGE_B + buf * 256), 4, 0, 0);
-    }
-  }
-}
-
-// Elementwise map of one 32x32 X tile (rows j = jb + acc_row, column = this lane's my_col).
-template <int MODE>
-struct EltState {
-  float m_run = -INFINITY, l_run = 0.f, diag = 0.f;
-  bool has_diag = false;
-};
-
-template <int MODE>
-__device__ __forceinline__ void elementwise(const f32x16& x, float (&e)[16], EltState<MODE>& st, int64_t jb,
-                                            int64_t row_end, int64_t my_col, int64_t label_off, float c2, float shift,
-                                            const float* lse_tile, int hh) {
-  if constexpr (MODE == FWD) {
-    // Fixed per-column shift (an upper bound of the column's logits, log2 units): no running
-    // max, no accumulator rescale, so the accumulators never leave the MFMA register file.
-    float ls = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int64_t j = jb + acc_row(v, hh);
-      const bool in = j < row_end;
-      const float z = x[v] * c2;
-      st.m_run = in ? fmaxf(st.m_run, z) : st.m_run;
-      e[v] = in ? exp2f(z - shift) : 0.f;
-      ls += e[v];
-      if (in && j == my_col + label_off) {
-        st.diag = x[v];
-        st.has_diag = true;
-      }
-    }
-    st.l_run += ls;
-  } else {
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_tile + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int v = 4 * g4 + u;
-        const int64_t i = jb + acc_row(v, hh);
-        float gv = 0.f;
-        if (i < row_end) {
-          gv = exp2f(x[v] * c2 - l4[u]);
-          if (my_col == i + label_off) gv -= 1.f;
-        }
-        e[v] = gv;
-      }
+      const int64_t g = r0 + lane;
+      const float* src = (g < row_end) ? lse2_rows + g : reinterpret_cast<const float*>(pad + kPadBytes - 16);
+      glds_dword(src, __builtin_amdgcn_readfirstlane(lds_addr(smem) + 2 * T::STAGE_B + buf * 256));
     }
   }
 }
 
 template <int MODE, int H>
-__device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], EltState<MODE>& st, int split, int64_t nC,
-                                               int64_t my_col, int hh, float* acc_part, float* m_part, float* l_part,
-                                               float* diag_raw) {
+__device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], float l_run, int split, int64_t nC,
+                                               int64_t my_col, int hh, float* acc_part, float* l_part) {
   if (my_col < nC) {
     float* dst = acc_part + ((int64_t)split * nC + my_col) * H;
 #pragma unroll
@@ -143,14 +128,29 @@ __device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], EltS
             f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
   }
   if constexpr (MODE == FWD) {
-    st.l_run += __shfl_xor(st.l_run, 32);
-    st.m_run = fmaxf(st.m_run, __shfl_xor(st.m_run, 32));
-    if (my_col < nC) {
-      if (hh == 0) {
-        m_part[(int64_t)split * nC + my_col] = st.m_run;
-        l_part[(int64_t)split * nC + my_col] = st.l_run;
-      }
-      if (st.has_diag) diag_raw[my_col] = st.diag;
+    l_run += __shfl_xor(l_run, 32);
+    if (my_col < nC && hh == 0) l_part[(int64_t)split * nC + my_col] = l_run;
+  }
+}
+
+// G for one 32x32 X tile: forward 2^(x c2 - shift) (accumulating l), backward 2^(x c2 - lse2_row).
+template <int MODE>
+__device__ __forceinline__ void map_tile(const f32x16& x, float (&e)[16], float c2, float shift,
+                                         const lds_f32x4_t* lse4, int hh, float& l_run) {
+  if constexpr (MODE == FWD) {
+    float ls = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      e[v] = __builtin_amdgcn_exp2f(x[v] * c2 - shift);
+      ls += e[v];
+    }
+    l_run += ls;
+  } else {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 l4 = lse4[2 * g4 + hh];  // lse2 of rows 8*g4 + 4*hh + u
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[4 * g4 + u] = __builtin_amdgcn_exp2f(x[4 * g4 + u] * c2 - l4[u]);
     }
   }
 }
@@ -158,23 +158,14 @@ __device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], EltS
 // ------------------------------------------------------------------------------------------
 // bf16 engine (32x32x16 bf16 MFMA).  PRECISE splits G into hi + lo bf16 so the second product
 // carries ~16 mantissa bits; otherwise G is rounded once (flash-attention style).
-//
-// Schedule per 64-row stage (two 32-row X tiles, one barrier): S(0); then for each tile j the
-// next tile's S MFMA chain is issued beside tile j's elementwise map, and tile j's Acc MFMAs
-// beside nothing but their own LDS transposed reads: the VALU work (exp, bf16 packing) sits in
-// the MFMA issue gaps of an independent chain instead of between dependent ones.  All LDS
-// addressing is 32-bit; full tiles skip every mask, and the label compare runs only in the one
-// tile per column that holds the label.
-typedef __attribute__((address_space(3))) char lds_char_t;
-typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8_t;
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
-typedef __attribute__((address_space(3))) f32x4 lds_f32x4_t;
-
+// Schedule per 64-row stage (two 32-row X tiles, one barrier): S(0); then per tile j the next
+// tile's S chain is issued beside tile j's elementwise map (independent: the VALU fills the
+// MFMA issue gaps), then tile j's Acc chain.
 template <int H>
 __device__ __forceinline__ f32x16 s_chain(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16]) {
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
-  const int rowb = row * T::ROWB, x = row & T::SWM;
+  const int rowb = row * T::ROWB, x = T::swz(row);
   f32x16 acc = f32x16{};
   bf16x8 a[4];
 #pragma unroll
@@ -189,46 +180,8 @@ __device__ __forceinline__ f32x16 s_chain(const lds_char_t* tile, int row, int h
   return acc;
 }
 
-// Map one X tile to packed bf16 B operands (hi, lo) for the Acc product.
-template <int MODE, bool PRECISE>
-__device__ __forceinline__ void map_tile(const f32x16& x, bf16x8 (&bh)[2], bf16x8 (&bl)[2], int nvalid, int drel,
-                                         float c2, float shift, const lds_f32x4_t* lse4, int hh, float& l_run,
-                                         float& diag, bool& has_diag) {
-  float e[16];
-  if constexpr (MODE == FWD) {
-#pragma unroll
-    for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(x[v] * c2 - shift);
-  } else {
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 l4 = lse4[2 * g4 + hh];  // lse of rows 8*g4 + 4*hh + u (log2 units)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) e[4 * g4 + u] = __builtin_amdgcn_exp2f(x[4 * g4 + u] * c2 - l4[u]);
-    }
-  }
-  if (nvalid < 32) {  // wave-uniform: only the last tile of a split
-#pragma unroll
-    for (int v = 0; v < 16; ++v) e[v] = acc_row(v, hh) < nvalid ? e[v] : 0.f;
-  }
-  if (__any(drel >= 0 && drel < 32)) {  // the label column of some lane falls in this tile
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      if (acc_row(v, hh) == drel) {
-        if constexpr (MODE == FWD) {
-          diag = x[v];
-          has_diag = true;
-        } else {
-          e[v] -= 1.f;
-        }
-      }
-    }
-  }
-  if constexpr (MODE == FWD) {
-    float ls = 0.f;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) ls += e[v];
-    l_run += ls;
-  }
+template <bool PRECISE>
+__device__ __forceinline__ void pack_g(const float (&e)[16], bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -240,15 +193,17 @@ __device__ __forceinline__ void map_tile(const f32x16& x, bf16x8 (&bh)[2], bf16x
     }
 }
 
-// Acc^T[h][col] += tile^T[h][rows] * G[rows][col] for one 32-row X tile.
+// Acc^T[h][col] += tile^T[h][rows] * G[rows][col] for one 32-row X tile.  k order inside a
+// step follows the accumulator layout: element j of lane half h is row 16 s + 8 (j>>2) + 4 h
+// + (j&3) (cdna_hip_programming.md §3), read as two 4-row transposed blocks.
 template <bool PRECISE, int H>
 __device__ __forceinline__ void acc_chain(const lds_char_t* tile, int jt, int lane, const bf16x8 (&bh)[2],
                                           const bf16x8 (&bl)[2], f32x16 (&acc)[H / 32]) {
   using T = Tile<__bf16, H>;
   constexpr int NHT = H / 32;
   const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
-  const int r0 = jt * 32 + 4 * (tg >> 1) + tq;  // + 16*s2 (+8 for the second read): same (row & SWM)
-  const int x0 = r0 & T::SWM, x1 = (r0 + 8) & T::SWM;
+  const int r0 = jt * 32 + 4 * (tg >> 1) + tq;  // (+16 s2 leaves swz unchanged: it reads row & 15)
+  const int x0 = T::swz(r0), x1 = T::swz(r0 + 8);
   const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
@@ -268,9 +223,8 @@ __device__ __forceinline__ void acc_chain(const lds_char_t* tile, int jt, int la
 template <int MODE, bool PRECISE, int H>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
-    int64_t rows_per_split, float c2, int64_t label_off, const float* __restrict__ lse_rows,
-    const float* __restrict__ col_shift, float* __restrict__ acc_part, float* __restrict__ m_part,
-    float* __restrict__ l_part, float* __restrict__ diag_raw) {
+    int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ col_shift,
+    const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part) {
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
   constexpr int NHT = H / 32;
@@ -287,10 +241,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
   const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
-  // label of this column, relative to the split (FWD: row index of D; DD: row index of Q)
-  const int64_t lab = (MODE == FWD) ? my_col + label_off : my_col - label_off;
 
-  if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse_rows);
+  if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
 
   bf16x8 cf[NK];
   {
@@ -306,64 +258,49 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   f32x16 acc[NHT];
 #pragma unroll
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  float l_run = 0.f, diag = 0.f;
-  bool has_diag = false;
+  float l_run = 0.f;
+  drain_dma();
   __syncthreads();
 
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 1);
-    if (t + 1 < ntiles) stage_tile<__bf16, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse_rows);
+    if (t + 1 < ntiles)
+      stage_tile<__bf16, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
     const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + 2 * T::STAGE_B + buf * 256);
-    const int64_t jb0 = row_begin + t * T::BJ;
     f32x16 xa = s_chain<H>(tile, r32, hh, cf);
 #pragma unroll
     for (int jt = 0; jt < NJ; ++jt) {
       f32x16 xb = f32x16{};
       if (jt + 1 < NJ) xb = s_chain<H>(tile, (jt + 1) * 32 + r32, hh, cf);
-      const int64_t jb = jb0 + jt * 32;
-      const int nvalid = (int)min<int64_t>(32, row_end - jb);
-      const int64_t dr = lab - jb;
-      const int drel = (dr >= 0 && dr < nvalid) ? (int)dr : -1;  // labels only on real rows
+      float e[16];
+      map_tile<MODE>(xa, e, c2, shift, lse4 + jt * 8, hh, l_run);
       bf16x8 bh[2], bl[2];
-      map_tile<MODE, PRECISE>(xa, bh, bl, nvalid, drel, c2, shift, lse4 + jt * 8, hh, l_run, diag, has_diag);
+      pack_g<PRECISE>(e, bh, bl);
+      __builtin_amdgcn_sched_barrier(0);  // [S(next) || map] ; [Acc chain]
       acc_chain<PRECISE, H>(tile, jt, lane, bh, bl, acc);
       xa = xb;
     }
+    drain_dma();  // next stage landed (issued a whole stage of MFMAs ago)
     __syncthreads();
   }
-
-  if (my_col < nC) {
-    float* dst = acc_part + ((int64_t)split * nC + my_col) * H;
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-        *reinterpret_cast<f32x4*>(dst + ht * 32 + 8 * g4 + 4 * hh) =
-            f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
-  }
-  if constexpr (MODE == FWD) {
-    l_run += __shfl_xor(l_run, 32);
-    if (my_col < nC) {
-      if (hh == 0) l_part[(int64_t)split * nC + my_col] = l_run;
-      if (has_diag) diag_raw[my_col] = diag;
-    }
-  }
+  write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 }
 
 // ------------------------------------------------------------------------------------------
 // fp32 engine (exact f32 MFMA, 32x32x2).  The k order inside the X product is permuted
-// (k = 8*blk + 4*hh + u) so each lane reads one 16-byte chunk per four MFMAs.
+// (k = 8*blk + 4*hh + u) so each lane reads one 16-byte chunk per four MFMAs; the Acc product
+// consumes X register t directly as its B operand (k = row of X held by register t).
 template <int MODE, int H>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
     const float* __restrict__ R, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
-    int64_t rows_per_split, float c2, int64_t label_off, const float* __restrict__ lse_rows,
-    const float* __restrict__ col_shift, float* __restrict__ acc_part, float* __restrict__ m_part, float* __restrict__ l_part,
-    float* __restrict__ diag_raw) {
+    int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ col_shift,
+    const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part) {
   using T = Tile<float, H>;
   constexpr int NB = H / 8;
   constexpr int NHT = H / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;
 
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -375,7 +312,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
   const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
 
-  if (ntiles > 0) stage_tile<float, H, MODE>(smem, 0, R, row_begin, row_end, lse_rows);
+  if (ntiles > 0) stage_tile<float, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
 
   f32x4 cf[NB];
   {
@@ -391,37 +328,41 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
   f32x16 acc[NHT];
 #pragma unroll
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  EltState<MODE> st;
+  float l_run = 0.f;
+  const int rx = T::swz(r32);
+  drain_dma();
   __syncthreads();
 
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 1);
-    if (t + 1 < ntiles) stage_tile<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse_rows);
-    const char* base = smem + buf * T::STAGE_B;
-    const float* lse_tile = reinterpret_cast<const float*>(smem + 2 * T::STAGE_B + buf * 256);
-    const int64_t jb = row_begin + t * T::BJ;
+    if (t + 1 < ntiles)
+      stage_tile<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad);
+    const lds_char_t* tile = lds + buf * T::STAGE_B;
+    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + 2 * T::STAGE_B + buf * 256);
     f32x16 x = f32x16{};
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(base + T::off(r32, 2 * b + hh));
+      const f32x4 a = *reinterpret_cast<const lds_f32x4_t*>(tile + r32 * T::ROWB + (((2 * b + hh) ^ rx) << 4));
 #pragma unroll
       for (int u = 0; u < 4; ++u) x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], cf[b][u], x, 0, 0, 0);
     }
     float e[16];
-    elementwise<MODE>(x, e, st, jb, row_end, my_col, label_off, c2, shift, lse_tile, hh);
+    map_tile<MODE>(x, e, c2, shift, lse4, hh, l_run);
 #pragma unroll
     for (int ht = 0; ht < NHT; ++ht) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int row = acc_row(v, hh);
-        const float a = *reinterpret_cast<const float*>(base + T::off(row, 8 * ht + (r32 >> 2)) + (r32 & 3) * 4);
+        const float a = *reinterpret_cast<const lds_float_t*>(
+            tile + row * T::ROWB + (((8 * ht + (r32 >> 2)) ^ T::swz(row)) << 4) + (r32 & 3) * 4);
         acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, e[v], acc[ht], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    drain_dma();
     __syncthreads();
   }
-  write_partials<MODE, H>(acc, st, split, nC, my_col, hh, acc_part, m_part, l_part, diag_raw);
+  write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -458,40 +399,62 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict_
   }
 }
 
+// Pad source for rows past the end: kPadBytes - 16 zero bytes, then +inf (backward lse2).
+__device__ __forceinline__ void write_pad(char* pad) {
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
+      reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
+  }
+}
+
 // Column shift for the forward: an upper bound of row i's logits in log2 units,
 // |q~_i . d~_j| * c2 <= c2 * |q_i| * max_j |d_j| * (1 + 2^-6) (bf16 rounding slack included).
 __global__ __launch_bounds__(256) void shift_kernel(const float* __restrict__ qn, const unsigned* __restrict__ dmax_bits,
-                                                    int64_t B, float c2, float* __restrict__ shift) {
+                                                    int64_t B, float c2, float* __restrict__ shift, char* pad) {
+  write_pad(pad);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= B) return;
   shift[i] = fabsf(c2) * qn[i] * __uint_as_float(*dmax_bits) * 1.015625f;
 }
 
-// Merge forward split partials: one wave per query row.  Rows whose shift sits more than
-// so far above the true max that the terms underflow report NaN (fail loudly).
+__global__ __launch_bounds__(256) void to_log2_kernel(const float* __restrict__ lse, int64_t n, float* __restrict__ lse2,
+                                                      char* pad) {
+  write_pad(pad);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) lse2[i] = lse[i] * kLog2e;
+}
+
+// Merge forward split partials, one wave per query row:
+//   l_i    = sum_s l_s,i - n_pad 2^-shift_i             (pad rows: X = 0 exactly)
+//   lse_i  = (shift_i + log2 l_i) ln 2
+//   loss_i = lse_i - (q~_i . d~_label) inv_tau           (diagonal logit, fp32 dot of the operands)
+//   dqu_i  = O_i / l_i - d~_label,   O_i = sum_s Acc_s,i
+// Rows whose bound sits so far above the true max that l underflows (l < 2^-100) report NaN.
 template <typename DT>
 __global__ __launch_bounds__(256) void fwd_combine_kernel(
-    int64_t B, int H, int S, const float* __restrict__ shift, const float* __restrict__ m_part,
-    const float* __restrict__ l_part, const float* __restrict__ acc_part, const float* __restrict__ diag_raw,
-    float inv_tau, int64_t label_off, const DT* __restrict__ Dmat, float* __restrict__ lse,
-    float* __restrict__ loss_rows, float* __restrict__ dqu) {
+    int64_t B, int H, int S, int n_pad, const float* __restrict__ shift, const float* __restrict__ l_part,
+    const float* __restrict__ acc_part, float inv_tau, int64_t label_off, const DT* __restrict__ Qmat,
+    const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ loss_rows, float* __restrict__ dqu) {
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= B) return;
   const int lane = lane_id();
+  const float sh = shift[i];
   float l = 0.f;
   for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
-  // l = sum_j 2^(z_ij - shift_i) with shift_i >= max_j z_ij.  l >= 2^-100 keeps the dominant
-  // terms normal floats (>= 2^-114 each); below it the bound was too loose: report NaN.
-  const float sh = shift[i];
-  const bool ok = l >= 7.888609052210118e-31f;
+  l -= (float)n_pad * __builtin_amdgcn_exp2f(-sh);
+  const bool ok = l >= 7.888609052210118e-31f;  // 2^-100
   const float lse_i = ok ? (sh + log2f(l)) * kLn2 : NAN;
+  const DT* qr = Qmat + i * H;
+  const DT* dl = Dmat + (i + label_off) * H;
+  float dot = 0.f;
+  for (int h = lane; h < H; h += kWave) dot += (float)qr[h] * (float)dl[h];
+  dot = wave_sum(dot);
   if (lane == 0) {
     lse[i] = lse_i;
-    loss_rows[i] = lse_i - diag_raw[i] * inv_tau;
+    loss_rows[i] = lse_i - dot * inv_tau;
   }
   if (dqu) {
     const float inv_l = ok ? 1.f / l : NAN;
-    const DT* dl = Dmat + (i + label_off) * H;
     for (int h = lane; h < H; h += kWave) {
       float o = 0.f;
       for (int s = 0; s < S; ++s) o += acc_part[((int64_t)s * B + i) * H + h];
@@ -500,15 +463,12 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void to_log2_kernel(const float* __restrict__ lse, int64_t n, float* __restrict__ lse2) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) lse2[i] = lse[i] * kLog2e;
-}
-
-// dd = scale * sum_s part[s]; dq = scale * dqu (scale = grad_loss * grad_scale * inv_tau).
-__global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, int H, int S,
+// dd_j = scale (sum_s Acc_s,j - [0 <= j - off < B] q~_{j-off});  dq = scale * dqu;
+// scale = grad_loss * grad_scale * inv_tau.
+template <typename DT>
+__global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, int H, int S, int64_t label_off,
                                                           const float* __restrict__ acc_part,
-                                                          const float* __restrict__ dqu,
+                                                          const DT* __restrict__ Qmat, const float* __restrict__ dqu,
                                                           const float* __restrict__ grad_loss, float grad_scale,
                                                           float inv_tau, float* __restrict__ dq,
                                                           float* __restrict__ dd) {
@@ -516,9 +476,12 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
   const int lane = lane_id();
   const float scale = grad_loss[0] * grad_scale * inv_tau;
   if (r < M) {
+    const int64_t qi = r - label_off;
+    const bool lab = qi >= 0 && qi < B;
     for (int h = lane; h < H; h += kWave) {
       float a = 0.f;
       for (int s = 0; s < S; ++s) a += acc_part[((int64_t)s * M + r) * H + h];
+      if (lab) a -= (float)Qmat[qi * H + h];
       dd[r * H + h] = a * scale;
     }
   }
@@ -533,6 +496,7 @@ struct Plan {
   int S;
   int64_t rows_per_split;
   int grid;
+  int n_pad;  // zero rows processed past the end of the last split
 };
 
 Plan plan_for(int64_t nR, int64_t nC, int BJ) {
@@ -542,10 +506,12 @@ Plan plan_for(int64_t nR, int64_t nC, int BJ) {
   if (S > 8) S = 8;
   if (S > row_tiles) S = row_tiles;
   if (S < 1) S = 1;
-  int64_t rps = (row_tiles + S - 1) / S * BJ;
+  const int64_t rps = (row_tiles + S - 1) / S * BJ;
   S = (nR + rps - 1) / rps;
   if (S < 1) S = 1;
-  return Plan{(int)S, rps, (int)(ncb * S)};
+  const int64_t last = nR - (S - 1) * rps;
+  const int64_t n_pad = (last + BJ - 1) / BJ * BJ - last;
+  return Plan{(int)S, rps, (int)(ncb * S), (int)n_pad};
 }
 
 int bj_for(int dtype) { return dtype == TT_F32 ? Tile<float, 64>::BJ : Tile<__bf16, 64>::BJ; }
@@ -557,8 +523,7 @@ struct Ws {
   float* shift;
   float* lse2;
   unsigned* dmax;
-  float* diag;
-  float* m_part;
+  char* pad;
   float* l_part;
   float* acc_part;
   size_t total;
@@ -578,7 +543,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   };
   const size_t oq = take(bf ? (size_t)B * H * 2 : 0), od = take(bf ? (size_t)M * H * 2 : 0);
   const size_t oqn = take((size_t)B * 4), osh = take((size_t)B * 4), ol2 = take((size_t)B * 4), omx = take(16);
-  const size_t odg = take((size_t)B * 4), om = take((size_t)pf.S * B * 4), ol = take((size_t)pf.S * B * 4);
+  const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   const size_t oa = take(parts);
   Ws w{};
@@ -590,8 +555,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.shift = reinterpret_cast<float*>(b + osh);
     w.lse2 = reinterpret_cast<float*>(b + ol2);
     w.dmax = reinterpret_cast<unsigned*>(b + omx);
-    w.diag = reinterpret_cast<float*>(b + odg);
-    w.m_part = reinterpret_cast<float*>(b + om);
+    w.pad = b + opad;
     w.l_part = reinterpret_cast<float*>(b + ol);
     w.acc_part = reinterpret_cast<float*>(b + oa);
   }
@@ -601,19 +565,19 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
 
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
-                  int64_t label_off, const float* lse, const Ws& w, hipStream_t s) {
+                  const float* lse2, const Ws& w, hipStream_t s) {
   if (dtype == TT_F32) {
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
-        static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, label_off,
-        lse, w.shift, w.acc_part, w.m_part, w.l_part, w.diag);
+        static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
+        w.shift, w.pad, w.acc_part, w.l_part);
   } else if (dtype == TT_BF16) {
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
-        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, label_off,
-        lse, w.shift, w.acc_part, w.m_part, w.l_part, w.diag);
+        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
+        w.shift, w.pad, w.acc_part, w.l_part);
   } else {
     score_bf16_kernel<MODE, false, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
-        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, label_off,
-        lse, w.shift, w.acc_part, w.m_part, w.l_part, w.diag);
+        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
+        w.shift, w.pad, w.acc_part, w.l_part);
   }
   TT_LAUNCH_CHECK(MODE == FWD ? "score_fwd" : "score_dd");
   return TT_OK;
@@ -621,12 +585,12 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
 
 template <int MODE>
 int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
-                    float c2, int64_t label_off, const float* lse, const Ws& w, hipStream_t s) {
+                    float c2, const float* lse2, const Ws& w, hipStream_t s) {
   switch (H) {
-    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
-    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
-    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
-    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, label_off, lse, w, s);
+    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
+    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
+    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
+    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
 }
@@ -640,6 +604,11 @@ int check_args(int64_t B, int64_t M, int H, int dtype, int64_t label_off) {
   return TT_OK;
 }
 
+Ws carve_user(void* ws, int64_t B, int64_t M, int H, int dtype) {
+  void* base = reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256));
+  return carve(base, B, M, H, dtype);
+}
+
 }  // namespace
 }  // namespace tt
 
@@ -647,11 +616,6 @@ using namespace tt;
 
 extern "C" size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype) {
   return carve(nullptr, B, M, H, dtype).total + 256;
-}
-
-static Ws carve_user(void* ws, int64_t B, int64_t M, int H, int dtype) {
-  void* base = reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256));
-  return carve(base, B, M, H, dtype);
 }
 
 extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
@@ -672,20 +636,19 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   auto prep_grid = [](int64_t rows) { return dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 1024)); };
   prep_rows_kernel<<<prep_grid(B), dim3(256), 0, s>>>(q, B, H, bf ? w.Qb : nullptr, w.qnorm, nullptr);
   prep_rows_kernel<<<prep_grid(M), dim3(256), 0, s>>>(d, M, H, bf ? w.Db : nullptr, nullptr, w.dmax);
-  shift_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(w.qnorm, w.dmax, B, c2, w.shift);
+  shift_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(w.qnorm, w.dmax, B, c2, w.shift, w.pad);
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
-  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, label_off, nullptr, w, s))) return rc;
+  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, s))) return rc;
   const dim3 grid((unsigned)((B + 3) / 4)), block(256);
+  float* dqu = want_grad ? dq_unscaled : nullptr;
   if (!bf)
-    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, w.shift, w.m_part, w.l_part, w.acc_part, w.diag,
-                                                    inv_tau, label_off, d, lse, loss_rows,
-                                                    want_grad ? dq_unscaled : nullptr);
+    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, w.shift, w.l_part, w.acc_part, inv_tau,
+                                                    label_off, q, d, lse, loss_rows, dqu);
   else
-    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, w.shift, w.m_part, w.l_part, w.acc_part, w.diag,
-                                                     inv_tau, label_off, w.Db, lse, loss_rows,
-                                                     want_grad ? dq_unscaled : nullptr);
+    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, w.shift, w.l_part, w.acc_part, inv_tau,
+                                                     label_off, w.Qb, w.Db, lse, loss_rows, dqu);
   TT_LAUNCH_CHECK("score_fwd_combine");
   return launch_mean(loss_rows, B, loss, s);
 }
@@ -701,14 +664,20 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const Plan p = plan_for(B, M, bj_for(dtype));
   const float c2 = inv_tau * kLog2e;
-  const void* Rm = (dtype == TT_F32) ? (const void*)q : (const void*)w.Qb;  // operands left by the forward
-  const void* Cm = (dtype == TT_F32) ? (const void*)d : (const void*)w.Db;
-  to_log2_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(lse, B, w.lse2);
+  const bool bf = dtype != TT_F32;
+  to_log2_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(lse, B, w.lse2, w.pad);
   TT_LAUNCH_CHECK("score_lse2");
-  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, label_off, w.lse2, w, s))) return rc;
+  const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
+  const void* Cm = bf ? (const void*)w.Db : (const void*)d;
+  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, w.lse2, w, s))) return rc;
   const int64_t rows = std::max(B, M);
-  bwd_combine_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(B, M, H, p.S, w.acc_part, dq_unscaled,
-                                                                           grad_loss, grad_scale, inv_tau, dq, dd);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  if (!bf)
+    bwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, w.acc_part, q, dq_unscaled, grad_loss,
+                                                    grad_scale, inv_tau, dq, dd);
+  else
+    bwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, w.acc_part, w.Qb, dq_unscaled,
+                                                     grad_loss, grad_scale, inv_tau, dq, dd);
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
