@@ -90,6 +90,12 @@ int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, 
 int tt_l2norm_bwd(const float* dout, const float* out, const float* norm, int64_t rows, int H,
                   float* dx, tt_stream_t stream);
 
+/* ---- column sum (bias gradient of nn.Linear: grad_out.sum(0); twotower/encoders.py:38-42) ----
+ * out[c] = sum_r x[r, c] in a fixed order (deterministic): per-block partial sums over row
+ * chunks into ws (>= tt_colsum_ws_size bytes), then one fixed-order pass over the partials. */
+size_t tt_colsum_ws_size(int64_t rows, int cols);
+int tt_colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes, tt_stream_t stream);
+
 /* ---- triplet hinge on cosine (contrastive_triplet_loss, twotower/losses.py:9-44) ----
  * loss = mean_i relu(margin - cos(q_i,p_i) + cos(q_i,n_i)), cosine eps 1e-8.
  * fwd writes loss_rows[B] and loss[1]; bwd reads the upstream scalar grad from grad_loss

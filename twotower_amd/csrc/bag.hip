@@ -202,6 +202,17 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
   const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   if (row >= V) return;
   const int st = seg_start[row], en = seg_end[row];
+  // AdamW operands first: independent of the segment, so their HBM reads overlap the gather chain.
+  f32x4 pv[NV], mv[NV], vv[NV];
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int idx = k * LPR + c;
+      pv[k] = reinterpret_cast<const f32x4*>(param + row * E)[idx];
+      mv[k] = reinterpret_cast<const f32x4*>(exp_avg + row * E)[idx];
+      vv[k] = reinterpret_cast<const f32x4*>(exp_avg_sq + row * E)[idx];
+    }
+  }
   // U interleaved partial sums (entry e goes to partial (e - st) % U), folded in a fixed order:
   // deterministic, ~U x shorter dependent add chains and error growth on hot (Zipf) rows.
   f32x4 part[U][NV];
@@ -237,13 +248,10 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k * LPR + c] = acc[k];
   } else {
-    f32x4* pp = reinterpret_cast<f32x4*>(param + row * E);
-    f32x4* mp = reinterpret_cast<f32x4*>(exp_avg + row * E);
-    f32x4* vp = reinterpret_cast<f32x4*>(exp_avg_sq + row * E);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int idx = k * LPR + c;
-      f32x4 p = pp[idx], m = mp[idx], v = vp[idx];
+      f32x4 p = pv[k], m = mv[k], v = vv[k];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float pj = p[j], mj = m[j], vj = v[j];
@@ -252,9 +260,9 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
         m[j] = mj;
         v[j] = vj;
       }
-      pp[idx] = p;
-      mp[idx] = m;
-      vp[idx] = v;
+      reinterpret_cast<f32x4*>(param + row * E)[idx] = p;
+      reinterpret_cast<f32x4*>(exp_avg + row * E)[idx] = m;
+      reinterpret_cast<f32x4*>(exp_avg_sq + row * E)[idx] = v;
     }
   }
 }

@@ -189,6 +189,30 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) out[0] = n > 0 ? part[0] / (float)n : NAN;
 }
 
+// Column sums: block b sums rows [b*R, (b+1)*R) for 256 columns per block-column; then a second
+// kernel adds the per-block partials in block order.
+constexpr int kColRows = 128;
+
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int64_t rows, int cols,
+                                                             float* __restrict__ part) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kColRows;
+  if (c >= cols) return;
+  float s = 0.f;
+  const int64_t r1 = min<int64_t>(rows, r0 + kColRows);
+  for (int64_t r = r0; r < r1; ++r) s += x[r * cols + c];
+  part[(int64_t)blockIdx.x * cols + c] = s;
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int cols,
+                                                           float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * cols + c];
+  out[c] = s;
+}
+
 dim3 rows_grid(int64_t rows) { return dim3((unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock)); }
 
 }  // namespace
@@ -220,6 +244,29 @@ extern "C" int tt_l2norm_bwd(const float* dout, const float* out, const float* n
   l2norm_bwd_kernel<<<rows_grid(rows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(dout, out, norm, rows,
                                                                                                  H, dx);
   TT_LAUNCH_CHECK("tt_l2norm_bwd");
+  return TT_OK;
+}
+
+extern "C" size_t tt_colsum_ws_size(int64_t rows, int cols) {
+  const int64_t nblk = (rows + kColRows - 1) / kColRows;
+  return (size_t)std::max<int64_t>(nblk, 1) * (size_t)cols * sizeof(float);
+}
+
+extern "C" int tt_colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes,
+                         tt_stream_t stream) {
+  TT_REQUIRE(rows >= 0 && cols > 0, "bad shape rows=%lld cols=%d", (long long)rows, cols);
+  TT_REQUIRE(out && (rows == 0 || (x && ws)), "null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    TT_HIP(hipMemsetAsync(out, 0, (size_t)cols * 4, s), "memset colsum");
+    return TT_OK;
+  }
+  TT_REQUIRE(ws_bytes >= tt_colsum_ws_size(rows, cols), "workspace too small");
+  const int nblk = (int)((rows + kColRows - 1) / kColRows);
+  const int cblk = (cols + 255) / 256;
+  colsum_partial_kernel<<<dim3(nblk, cblk), dim3(256), 0, s>>>(x, rows, cols, static_cast<float*>(ws));
+  colsum_final_kernel<<<dim3(cblk), dim3(256), 0, s>>>(static_cast<const float*>(ws), nblk, cols, out);
+  TT_LAUNCH_CHECK("tt_colsum");
   return TT_OK;
 }
 

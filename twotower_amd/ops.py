@@ -147,6 +147,59 @@ def l2_normalize(x: torch.Tensor) -> torch.Tensor:
 
 
 # --------------------------------------------------------------------------------------------
+# Tower feed-forward Linear(E,H) - ReLU - Linear(H,H)   (twotower/encoders.py:38-42)
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """x.sum(0) on the deterministic HIP column-sum (the nn.Linear bias gradient)."""
+    require_gpu(x)
+    x = _contig_f32(x, "x")
+    rows, cols = x.shape
+    out = torch.empty(cols, dtype=_FLOAT, device=x.device)
+    nbytes = _lib.lib().tt_colsum_ws_size(rows, cols)
+    ws = WORKSPACE.get("colsum", nbytes, x.device)
+    call("tt_colsum", ptr(x), rows, cols, ptr(out), ptr(ws), ws.numel(), stream_of(x))
+    return out
+
+
+def _weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dy^T x for tall N x H / N x E operands, K-split into S slabs (bmm) and summed: the
+    library GEMM picks a 32x64 tile grid for the 256 x 256 output and leaves most CUs idle."""
+    N = dy.shape[0]
+    S = 1
+    for cand in (16, 8, 4, 2):
+        if N % cand == 0 and N // cand >= 1024:
+            S = cand
+            break
+    if S == 1:
+        return dy.t() @ x
+    return torch.bmm(dy.view(S, N // S, -1).transpose(1, 2), x.view(S, N // S, -1)).sum(0)
+
+
+class TowerFF(torch.autograd.Function):
+    """y = relu(x W1^T + b1) W2^T + b2 with weight gradients on K-split GEMMs, bias gradients on
+    tt_colsum and the ReLU mask fused into the backward product."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        require_gpu(x)
+        h = torch.relu(torch.addmm(b1, x, W1.t()))
+        y = torch.addmm(b2, h, W2.t())
+        ctx.save_for_backward(x, h, W1, W2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, h, W1, W2 = ctx.saved_tensors
+        dy = dy.contiguous()
+        dh = (dy @ W2).mul_(h > 0)
+        dx = dh @ W1 if ctx.needs_input_grad[0] else None
+        return dx, _weight_grad(dh, x), colsum(dh), _weight_grad(dy, h), colsum(dy)
+
+
+def tower_ff(x, W1, b1, W2, b2):
+    return TowerFF.apply(x, W1, b1, W2, b2)
+
+
+# --------------------------------------------------------------------------------------------
 # contrastive_triplet_loss   (twotower/losses.py:9-44)
 class TripletLoss(torch.autograd.Function):
     @staticmethod
