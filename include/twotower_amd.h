@@ -96,6 +96,10 @@ int tt_l2norm_bwd(const float* dout, const float* out, const float* norm, int64_
 size_t tt_colsum_ws_size(int64_t rows, int cols);
 int tt_colsum(const float* x, int64_t rows, int cols, float* out, void* ws, size_t ws_bytes, tt_stream_t stream);
 
+/* ---- ReLU backward in place (nn.ReLU between the tower Linears, encoders.py:40):
+ * dh[i] = h[i] > 0 ? dh[i] : 0 (16-byte vectors when n % 4 == 0 and both are aligned). */
+int tt_relu_bwd(float* dh, const float* h, int64_t n, tt_stream_t stream);
+
 /* ---- triplet hinge on cosine (contrastive_triplet_loss, twotower/losses.py:9-44) ----
  * loss = mean_i relu(margin - cos(q_i,p_i) + cos(q_i,n_i)), cosine eps 1e-8.
  * fwd writes loss_rows[B] and loss[1]; bwd reads the upstream scalar grad from grad_loss

@@ -252,6 +252,47 @@ def test_in_batch_three_tensor_form_and_zero_copy_candidates():
     assert rel(allv.grad[:B], rdq) < 1e-5 and rel(allv.grad[B:], rdd) < 1e-5
 
 
+def test_packed_losses_equal_separate_tensors():
+    """[q; p; n] in one tensor (TwoTower's fused output) takes the packed kernels; results must
+    equal the separate-tensor path exactly (same kernels, same operands)."""
+    rng = np.random.default_rng(12)
+    B, H = 200, 64
+    base = _unit(rng, 3 * B, H)
+    for name, kw in (("triplet", {"margin": 0.2}), ("in_batch", {"temperature": 0.05})):
+        fn = tt.losses.build(name, **kw)
+        packed = cuda(base).requires_grad_(True)
+        lp = fn(*torch.split(packed, B))
+        lp.backward()
+        sep = [cuda(base[i * B:(i + 1) * B]).requires_grad_(True) for i in range(3)]
+        ls = fn(*sep)
+        ls.backward()
+        assert lp.item() == ls.item(), name
+        assert torch.equal(packed.grad, torch.cat([t.grad for t in sep])), name
+    # views that are not the whole base in order fall back to the separate path
+    packed = cuda(base).requires_grad_(True)
+    q, p, n = torch.split(packed, B)
+    lr_ = tt.losses.build("triplet", margin=0.2)(q, n, p)
+    rl, _ = O.triplet_fwd_bwd(base[:B], base[2 * B:], base[B:2 * B], 0.2)
+    assert abs(lr_.item() - rl) < 1e-5
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 4), (255, 24), (257, 128), (24576, 256), (3000, 1028), (0, 64)])
+def test_colsum_vs_torch(rows, cols):
+    x = torch.randn(rows, cols, device=DEV)
+    got = ops.colsum(x)
+    want = x.double().sum(0)
+    assert torch.allclose(got.double(), want, rtol=1e-5, atol=1e-4 * max(1.0, rows ** 0.5))
+
+
+def test_relu_bwd_matches_mask():
+    for n in (4 * 1000, 1001):
+        h = torch.randn(n, device=DEV).clamp_min(0)
+        dh = torch.randn(n, device=DEV)
+        want = dh * (h > 0)
+        ops._lib.call("tt_relu_bwd", dh.data_ptr(), h.data_ptr(), n, _lib.stream_of(dh))
+        assert torch.equal(dh, want)
+
+
 def test_in_batch_reports_underflow_as_nan():
     """Huge-norm rows whose shift bound is far above the true max fail loudly (NaN), never silently."""
     H = 64

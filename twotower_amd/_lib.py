@@ -40,6 +40,7 @@ _SIGNATURES = {
     "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_colsum_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_colsum": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_sz, _vp]),
+    "tt_relu_bwd": (_c_int, [_vp, _vp, _c_i64, _vp]),
     "tt_triplet_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp]),
     "tt_triplet_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
     "tt_multi_neg_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp]),

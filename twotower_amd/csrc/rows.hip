@@ -189,28 +189,56 @@ __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x,
   if (threadIdx.x == 0) out[0] = n > 0 ? part[0] / (float)n : NAN;
 }
 
-// Column sums: block b sums rows [b*R, (b+1)*R) for 256 columns per block-column; then a second
-// kernel adds the per-block partials in block order.
-constexpr int kColRows = 128;
+// Column sums, deterministic, two levels.  Level 1: block b owns rows [b*kColRows, ...): 256
+// threads = 4 row groups x 64 float4 columns (cols % 4 == 0, cols <= 256 per block column),
+// each thread keeps 4 independent partial sums (16 loads in flight), the 4 row groups are added
+// in a fixed order through LDS.  Level 2: 4 threads per column add the block partials (strided,
+// 4 accumulators each) and fold them in a fixed order.
+constexpr int kColRows = 256;
 
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ x, int64_t rows, int cols,
                                                              float* __restrict__ part) {
-  const int c = blockIdx.y * 256 + threadIdx.x;
+  __shared__ f32x4 red[4][64];
+  const int cq = threadIdx.x & 63, rg = threadIdx.x >> 6;  // float4 column, row group
+  const int c4 = blockIdx.y * 64 + cq;
+  const bool ok = c4 * 4 < cols;
   const int64_t r0 = (int64_t)blockIdx.x * kColRows;
-  if (c >= cols) return;
-  float s = 0.f;
   const int64_t r1 = min<int64_t>(rows, r0 + kColRows);
-  for (int64_t r = r0; r < r1; ++r) s += x[r * cols + c];
-  part[(int64_t)blockIdx.x * cols + c] = s;
+  f32x4 a[4] = {f32x4{}, f32x4{}, f32x4{}, f32x4{}};
+  if (ok) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(x) + c4;
+    const int stride4 = cols / 4;
+    int64_t r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += src[(r + 4 * u) * stride4];
+    }
+    for (int u = 0; r < r1; r += 4, ++u) a[u & 3] += src[r * stride4];
+  }
+  red[rg][cq] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (rg == 0 && ok)
+    reinterpret_cast<f32x4*>(part + (int64_t)blockIdx.x * cols)[c4] =
+        (red[0][cq] + red[1][cq]) + (red[2][cq] + red[3][cq]);
 }
 
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nblk, int cols,
                                                            float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * cols + c];
-  out[c] = s;
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int b = g;
+    for (; b + 12 < nblk; b += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += part[(int64_t)(b + 4 * u) * cols + c];
+    }
+    for (int u = 0; b < nblk; b += 4, ++u) a[u & 3] += part[(int64_t)b * cols + c];
+  }
+  red[g][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (g == 0 && c < cols) out[c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
 dim3 rows_grid(int64_t rows) { return dim3((unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock)); }
@@ -247,6 +275,36 @@ extern "C" int tt_l2norm_bwd(const float* dout, const float* out, const float* n
   return TT_OK;
 }
 
+__global__ __launch_bounds__(256) void relu_bwd_kernel(float* __restrict__ dh, const float* __restrict__ h, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f32x4 d = reinterpret_cast<f32x4*>(dh)[i];
+    const f32x4 v = reinterpret_cast<const f32x4*>(h)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = v[j] > 0.f ? d[j] : 0.f;
+    reinterpret_cast<f32x4*>(dh)[i] = d;
+  }
+}
+
+__global__ __launch_bounds__(256) void relu_bwd_scalar_kernel(float* __restrict__ dh, const float* __restrict__ h,
+                                                               int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    dh[i] = h[i] > 0.f ? dh[i] : 0.f;
+}
+
+extern "C" int tt_relu_bwd(float* dh, const float* h, int64_t n, tt_stream_t stream) {
+  TT_REQUIRE(n >= 0, "tt_relu_bwd: n=%lld", (long long)n);
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(dh && h, "tt_relu_bwd: null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(dh) | reinterpret_cast<uintptr_t>(h)) & 15) == 0;
+  if (vec)
+    relu_bwd_kernel<<<dim3((unsigned)std::min<int64_t>((n / 4 + 255) / 256, 2048)), dim3(256), 0, s>>>(dh, h, n / 4);
+  else
+    relu_bwd_scalar_kernel<<<dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)), dim3(256), 0, s>>>(dh, h, n);
+  TT_LAUNCH_CHECK("tt_relu_bwd");
+  return TT_OK;
+}
+
 extern "C" size_t tt_colsum_ws_size(int64_t rows, int cols) {
   const int64_t nblk = (rows + kColRows - 1) / kColRows;
   return (size_t)std::max<int64_t>(nblk, 1) * (size_t)cols * sizeof(float);
@@ -262,10 +320,11 @@ extern "C" int tt_colsum(const float* x, int64_t rows, int cols, float* out, voi
     return TT_OK;
   }
   TT_REQUIRE(ws_bytes >= tt_colsum_ws_size(rows, cols), "workspace too small");
+  TT_REQUIRE(cols % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0,
+             "tt_colsum needs cols %% 4 == 0 and a 16-byte aligned x");
   const int nblk = (int)((rows + kColRows - 1) / kColRows);
-  const int cblk = (cols + 255) / 256;
-  colsum_partial_kernel<<<dim3(nblk, cblk), dim3(256), 0, s>>>(x, rows, cols, static_cast<float*>(ws));
-  colsum_final_kernel<<<dim3(cblk), dim3(256), 0, s>>>(static_cast<const float*>(ws), nblk, cols, out);
+  colsum_partial_kernel<<<dim3(nblk, (cols + 255) / 256), dim3(256), 0, s>>>(x, rows, cols, static_cast<float*>(ws));
+  colsum_final_kernel<<<dim3((cols + 63) / 64), dim3(256), 0, s>>>(static_cast<const float*>(ws), nblk, cols, out);
   TT_LAUNCH_CHECK("tt_colsum");
   return TT_OK;
 }

@@ -72,9 +72,10 @@ class MeanPoolingTower(BaseTower):
     def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:
         ff = self.feed_forward
         if (len(ff) == 3 and isinstance(ff[0], nn.Linear) and isinstance(ff[1], nn.ReLU)
-                and isinstance(ff[2], nn.Linear) and ff[0].bias is not None and ff[2].bias is not None):
+                and isinstance(ff[2], nn.Linear) and ff[0].bias is not None and ff[2].bias is not None
+                and ff[0].out_features % 4 == 0 and ff[2].out_features % 4 == 0):
             y = ops.tower_ff(pooled.contiguous(), ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
-        else:  # a user-modified head: run it as given
+        else:  # a user-modified head (or widths off the vec4 column-sum): run it as given
             y = ff(pooled)
         return ops.l2_normalize(y)  # encoders.py:77
 

@@ -22,9 +22,31 @@ from . import ops
 logger = logging.getLogger("twotower_amd.losses")
 
 
+def _packed(*views: torch.Tensor) -> torch.Tensor | None:
+    """The common base when the views are consecutive, equally wide row blocks of one contiguous
+    2-D tensor in order (TwoTower's fused output split into q, p, n); else None."""
+    base = views[0]._base
+    if base is None or base.dim() != 2 or not base.is_contiguous():
+        return None
+    row = base.shape[1] * base.element_size()
+    at = base.data_ptr()
+    for v in views:
+        if v._base is not base or v.dim() != 2 or not v.is_contiguous() or v.shape[1] != base.shape[1]:
+            return None
+        if v.data_ptr() != at:
+            return None
+        at += v.shape[0] * row
+    if at != base.data_ptr() + base.shape[0] * row:
+        return None
+    return base
+
+
 def contrastive_triplet_loss(q_emb: torch.Tensor, d_pos_emb: torch.Tensor, d_neg_emb: torch.Tensor,
                              margin: float = 0.2) -> torch.Tensor:
     """mean(relu(margin - cos(q, d+) + cos(q, d-))) (losses.py:9-44)."""
+    base = _packed(q_emb, d_pos_emb, d_neg_emb)
+    if base is not None and q_emb.shape[0] == d_pos_emb.shape[0] == d_neg_emb.shape[0]:
+        return ops.TripletLossPacked.apply(base, margin)
     return ops.TripletLoss.apply(q_emb, d_pos_emb, d_neg_emb, margin)
 
 
@@ -58,9 +80,13 @@ def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *arg
     of every data-parallel rank (RCCL) and offsets the labels by this rank's slot."""
     if args:
         if isinstance(args[0], torch.Tensor):
-            d_emb = _candidates(d_emb, args[0])
             if len(args) > 1:
                 temperature = args[1]
+            base = None if cross_device_negatives else _packed(q_emb, d_emb, args[0])
+            if base is not None:  # [q; p; n] in one tensor: zero-copy candidates and gradient
+                return ops.InBatchSoftmaxLossPacked.apply(base, q_emb.shape[0], 1.0 / float(temperature),
+                                                          compute_dtype, None)
+            d_emb = _candidates(d_emb, args[0])
         else:
             temperature = args[0]
     label_off = 0

@@ -153,6 +153,8 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     require_gpu(x)
     x = _contig_f32(x, "x")
     rows, cols = x.shape
+    if cols % 4:
+        raise ValueError(f"colsum: hidden size {cols} must be a multiple of 4")
     out = torch.empty(cols, dtype=_FLOAT, device=x.device)
     nbytes = _lib.lib().tt_colsum_ws_size(rows, cols)
     ws = WORKSPACE.get("colsum", nbytes, x.device)
@@ -190,7 +192,8 @@ class TowerFF(torch.autograd.Function):
     def backward(ctx, dy):
         x, h, W1, W2 = ctx.saved_tensors
         dy = dy.contiguous()
-        dh = (dy @ W2).mul_(h > 0)
+        dh = dy @ W2
+        call("tt_relu_bwd", ptr(dh), ptr(h), dh.numel(), stream_of(dh))
         dx = dh @ W1 if ctx.needs_input_grad[0] else None
         return dx, _weight_grad(dh, x), colsum(dh), _weight_grad(dy, h), colsum(dy)
 
@@ -201,28 +204,56 @@ def tower_ff(x, W1, b1, W2, b2):
 
 # --------------------------------------------------------------------------------------------
 # contrastive_triplet_loss   (twotower/losses.py:9-44)
+def _triplet_fwd(q, p, n, margin):
+    B, H = q.shape
+    rows = torch.empty(B, dtype=_FLOAT, device=q.device)
+    loss = torch.empty((), dtype=_FLOAT, device=q.device)
+    call("tt_triplet_fwd", ptr(q), ptr(p), ptr(n), B, H, float(margin), ptr(rows), ptr(loss), stream_of(q))
+    return loss
+
+
+def _triplet_bwd(q, p, n, margin, g, dq, dp, dn):
+    B, H = q.shape
+    g = g.to(_FLOAT).contiguous().reshape(1)
+    call("tt_triplet_bwd", ptr(q), ptr(p), ptr(n), B, H, margin, ptr(g), ptr(dq), ptr(dp), ptr(dn), stream_of(q))
+
+
 class TripletLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, p, n, margin):
         require_gpu(q, p, n)
         q, p, n = (_contig_f32(t, nm) for t, nm in ((q, "q"), (p, "p"), (n, "n")))
-        B, H = q.shape
-        rows = torch.empty(B, dtype=_FLOAT, device=q.device)
-        loss = torch.empty((), dtype=_FLOAT, device=q.device)
-        call("tt_triplet_fwd", ptr(q), ptr(p), ptr(n), B, H, float(margin), ptr(rows), ptr(loss), stream_of(q))
         ctx.save_for_backward(q, p, n)
         ctx.margin = float(margin)
-        return loss
+        return _triplet_fwd(q, p, n, margin)
 
     @staticmethod
     def backward(ctx, g):
         q, p, n = ctx.saved_tensors
-        B, H = q.shape
-        g = g.to(_FLOAT).contiguous().reshape(1)
         dq, dp, dn = torch.empty_like(q), torch.empty_like(p), torch.empty_like(n)
-        call("tt_triplet_bwd", ptr(q), ptr(p), ptr(n), B, H, ctx.margin, ptr(g), ptr(dq), ptr(dp), ptr(dn),
-             stream_of(q))
+        _triplet_bwd(q, p, n, ctx.margin, g, dq, dp, dn)
         return dq, dp, dn, None
+
+
+class TripletLossPacked(torch.autograd.Function):
+    """Same loss on one (3B, H) tensor holding [q; p; n] (TwoTower's fused output): the gradient
+    is written as one tensor, so autograd never runs the split backward (zeros + cat)."""
+
+    @staticmethod
+    def forward(ctx, qpn, margin):
+        require_gpu(qpn)
+        qpn = _contig_f32(qpn, "qpn")
+        q, p, n = torch.chunk(qpn, 3)
+        ctx.save_for_backward(qpn)
+        ctx.margin = float(margin)
+        return _triplet_fwd(q, p, n, margin)
+
+    @staticmethod
+    def backward(ctx, g):
+        (qpn,) = ctx.saved_tensors
+        grad = torch.empty_like(qpn)
+        _triplet_bwd(*torch.chunk(qpn, 3), ctx.margin, g, *torch.chunk(grad, 3))
+        return grad, None
 
 
 # --------------------------------------------------------------------------------------------
@@ -256,42 +287,74 @@ class MultiNegLoss(torch.autograd.Function):
 
 # --------------------------------------------------------------------------------------------
 # in_batch_sampled_softmax_loss   (twotower/losses.py:88-118), fused MFMA scorer
+def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad):
+    B, H = q.shape
+    M = d.shape[0]
+    if d.shape[1] != H:
+        raise ValueError(f"q is (B, {H}) but d is {tuple(d.shape)}")
+    dt = _lib.compute_dtype_code(compute_dtype)
+    dev = q.device
+    nbytes = _lib.lib().tt_inbatch_ws_size(B, M, H, dt)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)  # carries the bf16 operands to backward
+    lse = torch.empty(B, dtype=_FLOAT, device=dev)
+    rows = torch.empty(B, dtype=_FLOAT, device=dev)
+    loss = torch.empty((), dtype=_FLOAT, device=dev)
+    dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
+    call("tt_inbatch_fwd", ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
+         ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
+    ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off), float(1.0 / B) if grad_scale is None else float(grad_scale))
+    return loss, lse, dqu, ws
+
+
+def _inbatch_bwd(meta, q, d, lse, dqu, ws, g, dq, dd):
+    B, M, H, dt, inv_tau, label_off, grad_scale = meta
+    g = g.to(_FLOAT).contiguous().reshape(1)
+    call("tt_inbatch_bwd", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g), grad_scale,
+         ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(q))
+
+
 class InBatchSoftmaxLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale):
         require_gpu(q, d)
         q, d = _contig_f32(q, "q"), _contig_f32(d, "d")
-        B, H = q.shape
-        M = d.shape[0]
-        if d.shape[1] != H:
-            raise ValueError(f"q is (B, {H}) but d is {tuple(d.shape)}")
-        dt = _lib.compute_dtype_code(compute_dtype)
-        dev = q.device
         want_grad = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
-        nbytes = _lib.lib().tt_inbatch_ws_size(B, M, H, dt)
-        # The workspace carries the bf16 operands from forward to backward: one per call.
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        lse = torch.empty(B, dtype=_FLOAT, device=dev)
-        rows = torch.empty(B, dtype=_FLOAT, device=dev)
-        loss = torch.empty((), dtype=_FLOAT, device=dev)
-        dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
-        call("tt_inbatch_fwd", ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
-             ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
+        loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad)
         if want_grad:
             ctx.save_for_backward(q, d, lse, dqu, ws)
-        ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off),
-                    float(1.0 / B) if grad_scale is None else float(grad_scale))
         return loss
 
     @staticmethod
     def backward(ctx, g):
         q, d, lse, dqu, ws = ctx.saved_tensors
-        B, M, H, dt, inv_tau, label_off, grad_scale = ctx.meta
-        g = g.to(_FLOAT).contiguous().reshape(1)
         dq, dd = torch.empty_like(q), torch.empty_like(d)
-        call("tt_inbatch_bwd", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g),
-             grad_scale, ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(q))
+        _inbatch_bwd(ctx.meta, q, d, lse, dqu, ws, g, dq, dd)
         return dq, dd, None, None, None, None
+
+
+class InBatchSoftmaxLossPacked(torch.autograd.Function):
+    """In-batch loss on one (B + M, H) tensor [q; candidates] (TwoTower's fused output): dq and
+    dd are written into one gradient tensor (no split backward)."""
+
+    @staticmethod
+    def forward(ctx, qd, nq, inv_tau, compute_dtype, grad_scale):
+        require_gpu(qd)
+        qd = _contig_f32(qd, "qd")
+        q, d = qd[:nq], qd[nq:]
+        want_grad = bool(ctx.needs_input_grad[0])
+        loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad)
+        if want_grad:
+            ctx.save_for_backward(qd, lse, dqu, ws)
+        ctx.nq = nq
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        qd, lse, dqu, ws = ctx.saved_tensors
+        grad = torch.empty_like(qd)
+        nq = ctx.nq
+        _inbatch_bwd(ctx.meta, qd[:nq], qd[nq:], lse, dqu, ws, g, grad[:nq], grad[nq:])
+        return grad, None, None, None, None
 
 
 def in_batch_softmax_loss(q: torch.Tensor, d: torch.Tensor, temperature: float = 0.1, label_off: int = 0,
