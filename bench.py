@@ -38,6 +38,21 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 
 
+def pmc_traffic(abi: str, config: str) -> dict:
+    """roofline.traffic: HBM bytes per launch of the dominant op from the newest committed PMC
+    profile of this workload (profiles/<tag>_pmc_traffic.json, written by tools/profile_round.sh:
+    FETCH_SIZE x2 + WRITE_SIZE over the op's kernels).  PMC counters cannot be read inside this
+    process, so the figure comes from a separate rocprofv3 pass of this same command."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{config}*_pmc_traffic.json")))
+    for f in reversed(files):
+        ops = json.load(open(f)).get("ops", {})
+        if abi in ops and ops[abi].get("hbm_bytes_per_call"):
+            return {"traffic": round(ops[abi]["hbm_bytes_per_call"]), "traffic_source": os.path.relpath(f, ROOT)}
+    return {"traffic": None}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -46,6 +61,9 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--scorer-dtype", default=None, help="override: fp32 | bf16 | bf16_fast")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the step as one HIP graph (auto: on for a single GPU)")
+    ap.add_argument("--timing-steps", type=int, default=10, help="eager steps timed per op after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=1024)
     return ap.parse_args()
@@ -74,8 +92,9 @@ def main():
     model = tt.build_two_tower("mean", emb, hidden_dim=d, tied_weights=True).to(dev)
     loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
                               cross_device_negatives=world > 1)
-    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=world == 1, tables=[emb])
-    step = tt.TrainStep(model, loss_fn, opt)
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=world == 1, tables=[emb], capturable=True)
+    step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
     batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev) for k in range(4)]
     nnz = sum(int((t > 0).sum()) for b in batches for t in b) / len(batches)  # tokens per step
@@ -87,8 +106,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    _lib.TIMER.reset()
-    _lib.TIMER.enabled = True
     t0 = time.perf_counter()
     loss = None
     for k in range(args.steps):
@@ -98,8 +115,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+
+    # Per-op device times for the rooflines: HIP events around every C-ABI call on its launch
+    # stream, over an eager pass of the same step (events cannot be timed inside a graph replay;
+    # the kernels and their inputs are the same).
+    _lib.TIMER.reset()
+    _lib.TIMER.enabled = True
+    for k in range(args.timing_steps):
+        step.eager(*batches[k % len(batches)])
+    torch.cuda.synchronize()
     _lib.TIMER.enabled = False
     ops_t = _lib.TIMER.summary()
+    timing_steps = args.timing_steps
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -123,7 +150,7 @@ def main():
         ms = ops_t[key]["mean_ms"]
         achieved = algo / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         kernels.append({"op": name, "abi": key, "bound": bound, "mean_ms": round(ms, 4),
-                        "calls_per_step": ops_t[key]["calls"] / args.steps, "achieved": round(achieved, 2),
+                        "calls_per_step": ops_t[key]["calls"] / timing_steps, "achieved": round(achieved, 2),
                         "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "algorithmic": algo,
                         "per_launch": per_launch_note})
 
@@ -131,18 +158,20 @@ def main():
     add("embedding bag forward (gather + masked mean)", "tt_bag_mean_fwd",
         nseq * L * id_bytes + nnz * d * 4 + nseq * d * 4 + nseq * 4, "GB/s", HBM_PEAK_GBS, "hbm",
         "ids N*L*4 + gathered rows nnz*E*4 + pooled N*E*4 + denom N*4 bytes")
-    add("embedding bag backward fused with table AdamW", "tt_bag_mean_bwd_adamw",
-        nseq * d * 4 + nseq * (L + 1) * 4 + 24 * V * d, "GB/s", HBM_PEAK_GBS, "hbm",
-        "d_pooled N*E*4 + ids/denom N*(L+1)*4 + AdamW p,m,v read+write 24*V*E bytes")
-    add("embedding bag backward (dense grad)", "tt_bag_mean_bwd",
-        nseq * d * 4 + nseq * (L + 1) * 4 + 2 * V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
-        "d_pooled + ids/denom + V*E*4 grad write + its read")
+    add("embedding bag backward fused with table AdamW (apply half: scale rows + per-row reduce + AdamW)",
+        "tt_bag_mean_bwd_adamw_planned", nseq * d * 4 + nseq * 4 + 24 * V * d, "GB/s", HBM_PEAK_GBS, "hbm",
+        "d_pooled N*E*4 + denom N*4 + AdamW p,m,v read+write 24*V*E bytes")
+    add("embedding bag backward sort plan (ids -> sorted (row, seq) + segments; side stream, overlaps the towers)",
+        "tt_bag_plan", nseq * L * 4 + nnz * 8 + V * 8, "GB/s", HBM_PEAK_GBS, "hbm",
+        "ids N*L*4 + sorted (row, seq) pairs nnz*8 + segment bounds V*8 bytes (latency-bound radix sort)")
+    add("embedding bag backward (dense grad, apply half)", "tt_bag_mean_bwd_planned",
+        nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
     pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
     add("in-batch scorer forward (S=QD^T, lse, P.D)", "tt_inbatch_fwd", 2.0 * B * M * d, "TFLOP/s", pk, "mfma",
         "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ")
     add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
         "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q)")
-    add("dense AdamW (tower FF)", "tt_adamw", 28 * sum(p.numel() for n_, p in model.named_parameters()
+    add("dense AdamW (tower FF, multi-tensor)", "tt_adamw_multi", 28 * sum(p.numel() for n_, p in model.named_parameters()
                                                       if "embedding" not in n_), "GB/s", HBM_PEAK_GBS, "hbm",
         "28 bytes per parameter")
     dominant = max(kernels, key=lambda k: k["mean_ms"] * k["calls_per_step"]) if kernels else None
@@ -150,6 +179,7 @@ def main():
     if dominant:
         roofline = {"bound": dominant["bound"], "achieved": dominant["achieved"], "peak": dominant["peak"],
                     "unit": dominant["unit"], "frac": dominant["frac"], "traffic": None, "op": dominant["op"]}
+        roofline.update(pmc_traffic(dominant["abi"], args.config))
     gather = next((k for k in kernels if k["abi"] == "tt_bag_mean_fwd"), None)
 
     cpu = None
@@ -178,7 +208,8 @@ def main():
         "data": "synthetic MS-MARCO-shaped id triplets (q 3-12 tokens, docs L/2-L), random-init weights",
         "config": {"workload": cfg["workload"] + ("; candidates all-gathered over ranks" if world > 1 else ""),
                    "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
-                   "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype},
+                   "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
+                   "hip_graph": use_graph},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "roofline": roofline,
         "kernels": kernels,

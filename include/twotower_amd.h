@@ -76,6 +76,26 @@ int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom,
                           double lr, double beta1, double beta2, double eps, double weight_decay,
                           int64_t step, void* ws, size_t ws_bytes, tt_stream_t stream);
 
+/* Split form of the sorted backward, so the id-only half can run early (beside the forward, on
+ * another stream) and a step can be captured in a HIP graph:
+ *   tt_bag_plan         ids -> sorted (row, seq) pairs + per-row segment bounds, into `plan`
+ *                       (tt_bag_plan_ws_size bytes; it also holds the scaled-row scratch);
+ *   tt_bag_mean_bwd_planned        dense grad_table from d_pooled/denom and the plan;
+ *   tt_bag_mean_bwd_adamw_planned  fused AdamW with the per-step scalars read from device
+ *                       memory (`adam_args`, written by tt_adam_prepare).
+ * Plan + apply compute exactly what tt_bag_mean_bwd / tt_bag_mean_bwd_adamw compute. */
+size_t tt_bag_plan_ws_size(int64_t nseq, int L, int64_t V, int E);
+int tt_bag_plan(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                int64_t V, int E, int64_t padding_idx, void* plan, size_t plan_bytes,
+                tt_stream_t stream);
+int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                            int64_t V, int E, const void* plan, size_t plan_bytes,
+                            float* grad_table, tt_stream_t stream);
+int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                  int64_t V, int E, const void* plan, size_t plan_bytes,
+                                  float* table, float* exp_avg, float* exp_avg_sq,
+                                  const void* adam_args, tt_stream_t stream);
+
 /* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
  * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
  * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps).   step is 1-based.
@@ -84,6 +104,29 @@ int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom,
 int tt_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
              double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
              tt_stream_t stream);
+
+/* Device-resident form (graph-capturable; torch's capturable=True convention of a device `step`):
+ * tt_adam_prepare increments each slot's fp32 step counter on the device and writes that
+ * tensor's per-step scalars (same double-precision formulas as above) into `args`
+ * (TT_ADAM_ARGS_BYTES device bytes, 4-byte aligned); tt_adamw_multi then updates up to
+ * TT_ADAM_MAX_TENSORS tensors in one launch, each with its own args. */
+#define TT_ADAM_ARGS_BYTES 32
+#define TT_ADAM_MAX_TENSORS 16
+typedef struct {
+  float* step;
+  void* args;
+} tt_adam_slot;
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+  const void* args;
+} tt_adamw_tensor;
+int tt_adam_prepare(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
+                    double eps, double weight_decay, tt_stream_t stream);
+int tt_adamw_multi(const tt_adamw_tensor* tensors, int count, tt_stream_t stream);
 
 /* ---- row L2 normalise (F.normalize(x, dim=-1), eps 1e-12; twotower/encoders.py:77) -- */
 int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, tt_stream_t stream);

@@ -357,3 +357,88 @@ def test_trajectory_matches_reference(golden):
         assert abs(loss.item() - g[f"loss{s}"]) < 1e-5
         assert rel(t.embedding.embedding.weight, g[f"step{s}_table"]) < 1e-5
         assert rel(t.feed_forward[0].weight, g[f"step{s}_W1"]) < 1e-5
+
+
+# ---------------------------------------------------------------------------------------------
+# split (planned) backward, device-resident AdamW scalars, graph-captured step
+@pytest.mark.parametrize("E", [64, 256, 48])
+def test_planned_backward_equals_one_shot(E):
+    rng = np.random.default_rng(21)
+    V, N, L = 3001, 300, 40
+    ids = edge_ids(N, L, V, rng, torch.int32)
+    dp = cuda(rng.standard_normal((N, E)).astype(np.float32))
+    den = cuda((rng.integers(1, L, N) + 1e-9).astype(np.float32))
+    want = ops.bag_mean_backward(dp, den, ids, V, 0)
+    plan = ops.BagPlan(ids, V, E, 0)
+    got = ops.bag_mean_backward_planned(dp, den, plan)
+    assert torch.equal(got, want)
+    # fused AdamW from the plan with device scalars == one-shot fused call with host scalars
+    tbl = cuda(rng.standard_normal((V, E)).astype(np.float32))
+    m = cuda(rng.standard_normal((V, E)).astype(np.float32) * 0.01)
+    v = cuda(np.abs(rng.standard_normal((V, E))).astype(np.float32) * 1e-4)
+    t1, m1, v1 = tbl.clone(), m.clone(), v.clone()
+    ops.bag_mean_backward_adamw(dp, den, ids, t1, m1, v1, 0, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
+                                weight_decay=0.01, step=3)
+    step = torch.tensor(2.0, device=DEV)
+    args = torch.zeros(8, device=DEV)
+    ops.adam_prepare([(step, args)], lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01)
+    assert step.item() == 3.0
+    t2, m2, v2 = tbl.clone(), m.clone(), v.clone()
+    ops.bag_mean_backward_adamw_planned(dp, den, ops.BagPlan(ids, V, E, 0), t2, m2, v2, args)
+    assert torch.equal(t1, t2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
+def test_planned_backward_empty_batch():
+    V, E = 50, 64
+    ids = torch.zeros(0, 8, dtype=torch.int32, device=DEV)
+    plan = ops.BagPlan(ids, V, E, 0)
+    g = ops.bag_mean_backward_planned(torch.zeros(0, E, device=DEV), torch.zeros(0, device=DEV), plan)
+    assert torch.equal(g, torch.zeros(V, E, device=DEV))
+
+
+def test_adamw_multi_matches_host_adamw():
+    rng = np.random.default_rng(22)
+    shapes = [(256, 256), (256,), (7,), (1000, 3), (5, 5)]
+    params = [cuda(rng.standard_normal(s).astype(np.float32)) for s in shapes]
+    grads = [cuda(rng.standard_normal(s).astype(np.float32)) for s in shapes]
+    a = [torch.nn.Parameter(p.clone()) for p in params]
+    b = [torch.nn.Parameter(p.clone()) for p in params]
+    oa = tt.optim.AdamW(a, lr=3e-3, weight_decay=0.05)
+    ob = tt.optim.AdamW(b, lr=3e-3, weight_decay=0.05, capturable=True)
+    ref = torch.optim.AdamW([torch.nn.Parameter(p.clone()) for p in params], lr=3e-3, weight_decay=0.05)
+    for _ in range(4):
+        for ps, o in ((a, oa), (b, ob), (ref.param_groups[0]["params"], ref)):
+            for p, g in zip(ps, grads):
+                p.grad = g.clone()
+            o.step()
+    for x, y, z in zip(a, b, ref.param_groups[0]["params"]):
+        assert rel(y, x) < 1e-7
+        assert rel(y, z) < 1e-6
+    assert ob.state[b[0]]["step"].device.type == "cuda" and ob.state[b[0]]["step"].item() == 4.0
+
+
+@pytest.mark.parametrize("loss_name", ["in_batch", "triplet"])
+def test_graph_step_equals_eager(loss_name):
+    """The graph-replayed step computes exactly what the eager step computes."""
+    V, E, B, L = 5000, 64, 96, 20
+
+    def build():
+        torch.manual_seed(5)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        kw = {"temperature": 0.1} if loss_name == "in_batch" else {"margin": 0.2}
+        return model, opt, tt.losses.build(loss_name, **kw)
+
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=k, device=DEV) for k in range(5)]
+    m1, o1, l1 = build()
+    s1 = tt.TrainStep(m1, l1, o1)
+    m2, o2, l2 = build()
+    s2 = tt.TrainStep(m2, l2, o2, graph=True, eager_steps=1)
+    for b in batches:
+        x1 = s1(*b).clone()
+        x2 = s2(*b).clone()
+        assert torch.equal(x1, x2)
+    assert len(s2._graphs) == 1
+    for (n_, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), n_

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round profile of the bench step: a kernel-trace/stats pass and two PMC passes (FETCH_SIZE and
+# WRITE_SIZE cannot share a pass on gfx950), each its own rocprofv3 run with --kernel-trace only
+# (never combined with sys/runtime/hip/hsa traces).  Usage: tools/profile_round.sh TAG [bench args]
+set -e
+TAG=${1:?tag}; shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+ARGS=${*:---steps 10 --warmup 3 --no-cpu-baseline}
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace" -o run -- \
+  python3 bench.py $ARGS > "$OUT/ktrace.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
+  python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
+  python3 bench.py $ARGS > "$OUT/write.log" 2>&1
+python3 tools/summarize_profile.py "$OUT" "$TAG"

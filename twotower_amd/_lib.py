@@ -25,6 +25,20 @@ COMPUTE_DTYPES = {"fp32": TT_F32, "float32": TT_F32, "bf16": TT_BF16, "bfloat16"
 _c_i64, _c_int, _c_f32, _c_sz, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 _c_f64 = ctypes.c_double
 
+TT_ADAM_ARGS_BYTES = 32
+TT_ADAM_MAX_TENSORS = 16
+
+
+class AdamSlot(ctypes.Structure):
+    """tt_adam_slot"""
+    _fields_ = [("step", _vp), ("args", _vp)]
+
+
+class AdamwTensor(ctypes.Structure):
+    """tt_adamw_tensor"""
+    _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("n", _c_i64), ("args", _vp)]
+
+
 # name -> (restype, argtypes); must mirror include/twotower_amd.h
 _SIGNATURES = {
     "tt_version": (_c_int, []),
@@ -35,6 +49,13 @@ _SIGNATURES = {
                                  _vp, _c_sz, _vp]),
     "tt_bag_mean_bwd_adamw": (_c_int, [_vp, _vp, _vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp,
                                        _vp, _vp, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp, _c_sz, _vp]),
+    "tt_bag_plan_ws_size": (_c_sz, [_c_i64, _c_int, _c_i64, _c_int]),
+    "tt_bag_plan": (_c_int, [_vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp, _c_sz, _vp]),
+    "tt_bag_mean_bwd_planned": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _vp, _vp]),
+    "tt_bag_mean_bwd_adamw_planned": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _vp, _vp, _vp,
+                                               _vp, _vp]),
+    "tt_adam_prepare": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _vp]),
+    "tt_adamw_multi": (_c_int, [ctypes.POINTER(AdamwTensor), _c_int, _vp]),
     "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
     "tt_l2norm_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),
@@ -60,6 +81,18 @@ def header_symbols(path: str = HEADER_PATH) -> list[str]:
     """Every function the public header declares (used by the ABI export test)."""
     text = open(path).read()
     return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(tt_\w+)\s*\(", text, flags=re.M)))
+
+
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    """A per-device auxiliary stream (id-only work that can run beside the forward)."""
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    st = _SIDE.get(key)
+    if st is None:
+        st = _SIDE[key] = torch.cuda.Stream(device=key)
+    return st
+
+
+_SIDE: dict[int, torch.cuda.Stream] = {}
 
 
 def lib() -> ctypes.CDLL:
@@ -105,7 +138,7 @@ class OpTimer:
         self.events = {}
 
     def run(self, name: str, fn):
-        if not self.enabled:
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
             return fn()
         start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         start.record()

@@ -145,24 +145,30 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_generic_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// Backward, sorted (deterministic) path.
-// prep: per sequence, emit (key = row id or V for masked, value = seq) for each token and the
-// scaled row gs[s] = dpooled[s] / denom[s] (the division autograd applies, encoders.py:72).
+// Backward, sorted (deterministic) path, in two halves:
+//   plan  (ids only, may run as soon as the ids exist, e.g. beside the forward):
+//         keys = row id (V for masked tokens), vals = seq -> stable radix sort -> segment bounds;
+//   apply (needs d_pooled): gs[s] = dpooled[s] / denom[s] (the division autograd applies,
+//         encoders.py:72), then the per-row reduce (optionally fused with AdamW).
 template <typename IdT>
-__global__ __launch_bounds__(kBlock) void bag_bwd_prep_kernel(
-    const float* __restrict__ dpooled, const float* __restrict__ denom, const IdT* __restrict__ ids,
-    int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, int E,
-    uint32_t* __restrict__ keys, int32_t* __restrict__ vals, float* __restrict__ gs) {
-  const int lane = lane_id();
+__global__ __launch_bounds__(kBlock) void bag_plan_keys_kernel(
+    const IdT* __restrict__ ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx,
+    uint32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= nseq * L) return;
+  const int64_t seq = i / L, t = i - seq * L;
+  const int64_t id = (int64_t)ids[seq * ld + t];
+  const bool valid = id > 0 && id < V && id != padding_idx;
+  keys[i] = valid ? (uint32_t)id : (uint32_t)V;
+  vals[i] = (int32_t)seq;
+}
+
+__global__ __launch_bounds__(kBlock) void bag_scale_rows_kernel(const float* __restrict__ dpooled,
+                                                                const float* __restrict__ denom, int64_t nseq,
+                                                                int E, float* __restrict__ gs) {
   const int64_t seq = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (seq >= nseq) return;
-  const IdT* rid = ids + seq * ld;
-  for (int t = lane; t < L; t += kWave) {
-    const int64_t id = (int64_t)rid[t];
-    const bool valid = id > 0 && id < V && id != padding_idx;
-    keys[seq * L + t] = valid ? (uint32_t)id : (uint32_t)V;
-    vals[seq * L + t] = (int32_t)seq;
-  }
+  const int lane = lane_id();
   const float den = denom[seq];
   const float* src = dpooled + seq * E;
   float* dst = gs + seq * E;
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
     const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
-    float* __restrict__ exp_avg_sq, AdamArgs aa) {
+    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev) {
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
@@ -205,6 +211,7 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
   // AdamW operands first: independent of the segment, so their HBM reads overlap the gather chain.
   f32x4 pv[NV], mv[NV], vv[NV];
   if constexpr (FUSED) {
+    if (aa_dev) aa = *aa_dev;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int idx = k * LPR + c;
@@ -273,10 +280,11 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_generic_kernel(
     const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
-    float* __restrict__ exp_avg_sq, AdamArgs aa) {
+    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev) {
   const int lane = lane_id();
   const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (row >= V) return;
+  if (FUSED && aa_dev) aa = *aa_dev;
   const int st = seg_start[row], en = seg_end[row];
   for (int c = lane; c < E; c += kWave) {
     float acc = 0.f;
@@ -403,45 +411,57 @@ int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nse
 
 template <bool FUSED>
 int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, float* m, float* v,
-                  const AdamArgs& aa, hipStream_t s) {
+                  const AdamArgs& aa, const AdamArgs* aa_dev, hipStream_t s) {
   auto grid_for = [&](int rpi) {
     const int64_t waves = (V + rpi - 1) / rpi;
     return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   };
   const dim3 block(kBlock);
   switch (E) {
-    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
-    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
-    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
-    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
-    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
-    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa); break;
+    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
+    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
+    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
+    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
+    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
+    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
   }
   TT_LAUNCH_CHECK("bag_bwd_reduce");
   return TT_OK;
 }
 
-// prep -> stable radix sort (key = row id, value = seq) -> segment bounds.
+// plan: keys/vals -> stable radix sort (key = row id, value = seq) -> segment bounds.
 template <typename IdT>
-int sorted_front(const float* dpooled, const float* denom, const IdT* ids, int64_t nseq, int L,
-                 int64_t ld, int64_t V, int64_t padding_idx, int E, const BwdWs& w, hipStream_t s) {
+int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, const BwdWs& w,
+               hipStream_t s) {
   const int64_t n = nseq * L;
   const dim3 block(kBlock);
-  bag_bwd_prep_kernel<IdT><<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block, 0, s>>>(
-      dpooled, denom, ids, nseq, L, ld, V, padding_idx, E, w.keys_in, w.vals_in, w.gs);
-  TT_LAUNCH_CHECK("bag_bwd_prep");
+  TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
+  TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
+  if (n == 0) return TT_OK;
+  bag_plan_keys_kernel<IdT><<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
+      ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in);
+  TT_LAUNCH_CHECK("bag_plan_keys");
   size_t tmp = w.sort_bytes;
   TT_HIP(rocprim::radix_sort_pairs(w.sort_tmp, tmp, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
                                    (size_t)n, 0, end_bit_for(V), s, false),
          "rocprim::radix_sort_pairs");
-  TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
-  TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
-  if (n > 0) {
-    bag_bwd_mark_kernel<<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
-        w.keys_out, n, (uint32_t)V, w.seg_start, w.seg_end);
-    TT_LAUNCH_CHECK("bag_bwd_mark");
-  }
+  bag_bwd_mark_kernel<<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
+      w.keys_out, n, (uint32_t)V, w.seg_start, w.seg_end);
+  TT_LAUNCH_CHECK("bag_bwd_mark");
   return TT_OK;
+}
+
+// apply: gs = dpooled / denom, then the row reduce (dense gradient or fused AdamW).
+template <bool FUSED>
+int apply_plan(const float* dpooled, const float* denom, int64_t nseq, int64_t V, int E, const BwdWs& w,
+               float* grad, float* param, float* m, float* v, const AdamArgs& aa, const AdamArgs* aa_dev,
+               hipStream_t s) {
+  if (nseq > 0) {
+    bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
+        dpooled, denom, nseq, E, w.gs);
+    TT_LAUNCH_CHECK("bag_scale_rows");
+  }
+  return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, aa_dev, s);
 }
 
 int check_common(int64_t V, int E, const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld) {
@@ -477,26 +497,68 @@ extern "C" size_t tt_bag_mean_bwd_ws_size(int64_t nseq, int L, int64_t V, int E)
   return carve(nullptr, nseq, L, V, E, sb).total + 256;
 }
 
-template <bool FUSED>
-static int bwd_impl(const float* dpooled, const float* denom, const void* ids, int ids_dtype, int64_t nseq,
-                    int L, int64_t ld, int64_t V, int E, int64_t padding_idx, float* grad, float* param,
-                    float* m, float* v, const AdamArgs& aa, void* ws, size_t ws_bytes, hipStream_t s) {
+static BwdWs plan_layout(void* ws, int64_t nseq, int L, int64_t V, int E) {
   if (nseq == 0 || L == 0) nseq = 0, L = 0;
   const size_t sb = nseq > 0 ? sort_tmp_bytes(nseq * (int64_t)L, V) : 0;
-  void* base = reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256));
-  BwdWs w = carve(base, nseq, L, V, E, sb);
+  void* base = ws ? reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256)) : nullptr;
+  return carve(base, nseq, L, V, E, sb);
+}
+
+static int plan_impl(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld, int64_t V, int E,
+                     int64_t padding_idx, void* ws, size_t ws_bytes, hipStream_t s) {
+  const BwdWs w = plan_layout(ws, nseq, L, V, E);
   TT_REQUIRE(ws != nullptr && w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu",
              w.total + 256, ws_bytes);
-  if (nseq == 0) {  // no tokens: every row's gradient is zero (segments stay empty)
-    TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
-    TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
-    return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, s);
-  }
-  int rc = (ids_dtype == TT_IDS_I32)
-               ? sorted_front(dpooled, denom, static_cast<const int32_t*>(ids), nseq, L, ld, V, padding_idx, E, w, s)
-               : sorted_front(dpooled, denom, static_cast<const int64_t*>(ids), nseq, L, ld, V, padding_idx, E, w, s);
+  if (nseq == 0 || L == 0) return plan_front<int32_t>(nullptr, 0, 0, 0, V, padding_idx, w, s);
+  return ids_dtype == TT_IDS_I32
+             ? plan_front(static_cast<const int32_t*>(ids), nseq, L, ld, V, padding_idx, w, s)
+             : plan_front(static_cast<const int64_t*>(ids), nseq, L, ld, V, padding_idx, w, s);
+}
+
+template <bool FUSED>
+static int apply_impl(const float* dpooled, const float* denom, int64_t nseq, int L, int64_t V, int E, void* ws,
+                      size_t ws_bytes, float* grad, float* param, float* m, float* v, const AdamArgs& aa,
+                      const AdamArgs* aa_dev, hipStream_t s) {
+  const BwdWs w = plan_layout(ws, nseq, L, V, E);
+  TT_REQUIRE(ws != nullptr && w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu",
+             w.total + 256, ws_bytes);
+  return apply_plan<FUSED>(dpooled, denom, (nseq == 0 || L == 0) ? 0 : nseq, V, E, w, grad, param, m, v, aa, aa_dev,
+                           s);
+}
+
+extern "C" size_t tt_bag_plan_ws_size(int64_t nseq, int L, int64_t V, int E) {
+  return tt_bag_mean_bwd_ws_size(nseq, L, V, E);
+}
+
+extern "C" int tt_bag_plan(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids, int64_t V, int E,
+                           int64_t padding_idx, void* plan, size_t plan_bytes, tt_stream_t stream) {
+  int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
   if (rc) return rc;
-  return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, s);
+  return plan_impl(ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, plan, plan_bytes,
+                   reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom, int64_t nseq, int L, int64_t V,
+                                       int E, const void* plan, size_t plan_bytes, float* grad_table,
+                                       tt_stream_t stream) {
+  TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
+  TT_REQUIRE(grad_table && (nseq == 0 || (d_pooled && denom)), "null pointer");
+  AdamArgs aa{};
+  return apply_impl<false>(d_pooled, denom, nseq, L, V, E, const_cast<void*>(plan), plan_bytes, grad_table, nullptr,
+                           nullptr, nullptr, aa, nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                             int64_t V, int E, const void* plan, size_t plan_bytes, float* table,
+                                             float* exp_avg, float* exp_avg_sq, const void* adam_args,
+                                             tt_stream_t stream) {
+  TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
+  TT_REQUIRE(table && exp_avg && exp_avg_sq && adam_args, "null pointer");
+  TT_REQUIRE(nseq == 0 || (d_pooled && denom), "null pointer");
+  AdamArgs aa{};
+  return apply_impl<true>(d_pooled, denom, nseq, L, V, E, const_cast<void*>(plan), plan_bytes, nullptr, table,
+                          exp_avg, exp_avg_sq, aa, static_cast<const AdamArgs*>(adam_args),
+                          reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int tt_bag_mean_bwd(const float* d_pooled, const float* denom, const void* ids, int ids_dtype,
@@ -518,8 +580,10 @@ extern "C" int tt_bag_mean_bwd(const float* d_pooled, const float* denom, const 
   }
   TT_REQUIRE(mode == TT_SCATTER_SORTED, "unknown scatter mode %d", mode);
   AdamArgs aa{};
-  return bwd_impl<false>(d_pooled, denom, ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, grad_table,
-                         nullptr, nullptr, nullptr, aa, ws, ws_bytes, s);
+  rc = plan_impl(ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, ws, ws_bytes, s);
+  if (rc) return rc;
+  return apply_impl<false>(d_pooled, denom, nseq, L, V, E, ws, ws_bytes, grad_table, nullptr, nullptr, nullptr, aa,
+                           nullptr, s);
 }
 
 extern "C" int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom, const void* ids, int ids_dtype,
@@ -531,7 +595,11 @@ extern "C" int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom, 
   if (rc) return rc;
   TT_REQUIRE(table && exp_avg && exp_avg_sq, "null pointer");
   TT_REQUIRE(step >= 1, "step must be >= 1 (got %lld)", (long long)step);
+  TT_REQUIRE(nseq * (int64_t)L == 0 || (d_pooled && denom), "null pointer");
   const AdamArgs aa = make_adam(lr, beta1, beta2, eps, weight_decay, step);
-  return bwd_impl<true>(d_pooled, denom, ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, nullptr, table,
-                        exp_avg, exp_avg_sq, aa, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  rc = plan_impl(ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, ws, ws_bytes, s);
+  if (rc) return rc;
+  return apply_impl<true>(d_pooled, denom, nseq, L, V, E, ws, ws_bytes, nullptr, table, exp_avg, exp_avg_sq, aa,
+                          nullptr, s);
 }

@@ -75,14 +75,53 @@ def bag_mean_backward(d_pooled: torch.Tensor, denom: torch.Tensor, ids: torch.Te
     return grad
 
 
+class BagPlan:
+    """The id-only half of the sorted backward (tt_bag_plan), launched on the side stream as soon
+    as the forward has its ids, so its radix sort runs beside the towers and the scorer.  The
+    backward (or the fused optimizer) waits on ``ready`` before using it."""
+
+    __slots__ = ("ids", "buf", "ready", "nseq", "L", "V", "E")
+
+    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None):
+        dev = ids.device
+        self.ids, self.V, self.E = ids, V, E
+        self.nseq, self.L = ids.shape
+        nbytes = _lib.lib().tt_bag_plan_ws_size(self.nseq, self.L, V, E)
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        main = torch.cuda.current_stream(dev)
+        side = _lib.side_stream(dev)
+        side.wait_stream(main)
+        pad = -1 if padding_idx is None else int(padding_idx)
+        with torch.cuda.stream(side):
+            call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, pad,
+                 ptr(self.buf), self.buf.numel(), side.cuda_stream)
+        if not torch.cuda.is_current_stream_capturing():
+            self.buf.record_stream(side)
+            ids.record_stream(side)
+        self.ready = torch.cuda.Event()
+        self.ready.record(side)
+
+    def wait(self) -> None:
+        torch.cuda.current_stream(self.buf.device).wait_event(self.ready)
+
+
+def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan: BagPlan) -> torch.Tensor:
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    plan.wait()
+    grad = torch.empty(plan.V, plan.E, dtype=_FLOAT, device=d_pooled.device)
+    call("tt_bag_mean_bwd_planned", ptr(d_pooled), ptr(denom), plan.nseq, plan.L, plan.V, plan.E, ptr(plan.buf),
+         plan.buf.numel(), ptr(grad), stream_of(d_pooled))
+    return grad
+
+
 class DeferredTableGrad:
-    """Table gradient kept in its factored form (ids, d_pooled, denom) so a fused optimizer can
-    apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer."""
+    """Table gradient kept in its factored form (ids, d_pooled, denom, plan) so a fused optimizer
+    can apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer."""
 
     __slots__ = ("parts", "padding_idx")
 
     def __init__(self, padding_idx: int | None = 0):
-        self.parts: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
+        self.parts: list[tuple] = []
         self.padding_idx = padding_idx
 
 
@@ -90,33 +129,41 @@ class BagMeanPool(torch.autograd.Function):
     """pooled = masked mean of weight[ids] over the sequence (ids > 0 are real tokens)."""
 
     @staticmethod
-    def forward(ctx, weight, ids, padding_idx, scatter_mode):
+    def forward(ctx, weight, ids, padding_idx, scatter_mode, want_plan=False):
         pooled, denom = bag_mean_forward(weight, ids)
+        ids = ids.contiguous()
         ctx.save_for_backward(ids, denom)
         ctx.V = weight.shape[0]
         ctx.padding_idx = padding_idx
         ctx.scatter_mode = scatter_mode
         ctx.weight_ref = weight
+        ctx.plan = None
+        if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
+            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx)
         return pooled
 
     @staticmethod
     def backward(ctx, d_pooled):
         ids, denom = ctx.saved_tensors
         weight = ctx.weight_ref
+        plan, ctx.plan = ctx.plan, None
         if not ctx.needs_input_grad[0]:
-            return None, None, None, None
+            return None, None, None, None, None
         deferred = getattr(weight, "_tt_deferred", None)
         if deferred is not None:
             # A fused optimizer owns this table: hand it the factored gradient.
-            deferred.parts.append((ids, d_pooled.contiguous(), denom))
-            return None, None, None, None
+            deferred.parts.append((ids, d_pooled.contiguous(), denom, plan))
+            return None, None, None, None, None
+        if plan is not None:
+            return bag_mean_backward_planned(d_pooled, denom, plan), None, None, None, None
         grad = bag_mean_backward(d_pooled, denom, ids, ctx.V, ctx.padding_idx, ctx.scatter_mode)
-        return grad, None, None, None
+        return grad, None, None, None, None
 
 
 def bag_mean_pool(weight: torch.Tensor, ids: torch.Tensor, padding_idx: int | None = 0,
                   scatter_mode: int = _lib.TT_SCATTER_SORTED) -> torch.Tensor:
-    return BagMeanPool.apply(weight, ids, padding_idx, scatter_mode)
+    want_plan = torch.is_grad_enabled() and weight.requires_grad
+    return BagMeanPool.apply(weight, ids, padding_idx, scatter_mode, want_plan)
 
 
 # --------------------------------------------------------------------------------------------
@@ -372,6 +419,41 @@ def adamw_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, e
             raise ValueError(f"{nm} must be a contiguous float32 tensor")
     call("tt_adamw", ptr(param), ptr(grad), ptr(exp_avg), ptr(exp_avg_sq), param.numel(), lr, beta1, beta2, eps,
          weight_decay, step, stream_of(param))
+
+
+def adam_prepare(slots: list[tuple[torch.Tensor, torch.Tensor]], *, lr: float, beta1: float, beta2: float, eps: float,
+                 weight_decay: float) -> None:
+    """Device step += 1 and per-step scalars for each (step, args) pair (tt_adam_prepare)."""
+    if not slots:
+        return
+    stream = stream_of(slots[0][0])
+    for i in range(0, len(slots), _lib.TT_ADAM_MAX_TENSORS):
+        chunk = slots[i:i + _lib.TT_ADAM_MAX_TENSORS]
+        arr = (_lib.AdamSlot * len(chunk))(*[_lib.AdamSlot(ptr(st), ptr(a)) for st, a in chunk])
+        call("tt_adam_prepare", arr, len(chunk), lr, beta1, beta2, eps, weight_decay, stream)
+
+
+def adamw_multi(items: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]]) -> None:
+    """(param, grad, exp_avg, exp_avg_sq, args) tensors updated in launches of up to 16."""
+    if not items:
+        return
+    stream = stream_of(items[0][0])
+    for i in range(0, len(items), _lib.TT_ADAM_MAX_TENSORS):
+        chunk = items[i:i + _lib.TT_ADAM_MAX_TENSORS]
+        arr = (_lib.AdamwTensor * len(chunk))(
+            *[_lib.AdamwTensor(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(a)) for p, g, m, v, a in chunk])
+        call("tt_adamw_multi", arr, len(chunk), stream)
+
+
+def bag_mean_backward_adamw_planned(d_pooled, denom, plan: BagPlan, table, exp_avg, exp_avg_sq,
+                                    adam_args: torch.Tensor) -> None:
+    """Fused scatter + AdamW from a BagPlan, per-step scalars read from device memory."""
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    if table.shape[0] != plan.V or table.shape[1] != plan.E:
+        raise ValueError("plan was built for a different table shape")
+    plan.wait()
+    call("tt_bag_mean_bwd_adamw_planned", ptr(d_pooled), ptr(denom), plan.nseq, plan.L, plan.V, plan.E, ptr(plan.buf),
+         plan.buf.numel(), ptr(table), ptr(exp_avg), ptr(exp_avg_sq), ptr(adam_args), stream_of(table))
 
 
 def bag_mean_backward_adamw(d_pooled, denom, ids, table, exp_avg, exp_avg_sq, padding_idx, *, lr, beta1, beta2,

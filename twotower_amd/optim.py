@@ -4,26 +4,35 @@ same per-parameter state keys ('step', 'exp_avg', 'exp_avg_sq') so optimizer sta
 interchange.
 
 ``fused_tables=True`` lets the embedding tables skip their dense V x E gradient: the bag
-backward leaves its factored gradient (ids, d_pooled, denom) on the table and ``step`` runs
-the sorted scatter fused with the AdamW update (tt_bag_mean_bwd_adamw).  The result equals the
-dense path exactly in math (every row is decayed and its moments updated, rows without tokens
-with g = 0), it just never writes or re-reads the dense gradient.
+backward leaves its factored gradient (ids, d_pooled, denom, sort plan) on the table and
+``step`` runs the sorted scatter fused with the AdamW update.  The result equals the dense path
+exactly in math (every row is decayed and its moments updated, rows without tokens with g = 0),
+it just never writes or re-reads the dense gradient.
+
+``capturable=True`` follows torch's convention of the same name: each ``state['step']`` lives on
+the parameter's device and is advanced there (tt_adam_prepare), the per-step scalars are read
+from device memory, and the small parameters are updated by one multi-tensor launch, so a whole
+training step can be captured in a HIP graph and replayed (train_step.TrainStep(graph=True)).
 """
 from __future__ import annotations
+
+import math
 
 import torch
 import torch.nn.functional as F
 
-from . import ops
+from . import _lib, ops
 
 
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 fused_tables: bool = False, tables=()):
+                 fused_tables: bool = False, tables=(), capturable: bool = False):
         if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
             raise ValueError("invalid AdamW hyper-parameter")
-        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                                      capturable=bool(capturable)))
         self._tables: list[torch.Tensor] = []
+        self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         if fused_tables:
             ids = {id(p) for g in self.param_groups for p in g["params"]}
             for t in tables:
@@ -42,13 +51,21 @@ class AdamW(torch.optim.Optimizer):
                 del w._tt_deferred
         self._tables = []
 
-    def _state(self, p: torch.Tensor) -> dict:
+    def _state(self, p: torch.Tensor, capturable: bool) -> dict:
         st = self.state[p]
         if not st:
-            st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            st["step"] = torch.tensor(0.0, dtype=torch.float32, device=p.device if capturable else "cpu")
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        elif capturable and st["step"].device != p.device:
+            st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
         return st
+
+    def _adam_args(self, p: torch.Tensor) -> torch.Tensor:
+        a = self._args.get(id(p))
+        if a is None:
+            a = self._args[id(p)] = torch.zeros(_lib.TT_ADAM_ARGS_BYTES // 4, dtype=torch.float32, device=p.device)
+        return a
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -57,32 +74,82 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for group in self.param_groups:
-            lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
-            for p in group["params"]:
-                deferred = getattr(p, "_tt_deferred", None)
-                if deferred is not None and deferred.parts:
-                    st = self._state(p)
-                    st["step"] += 1
-                    ids, dp, den = _merge_parts(deferred.parts)
-                    deferred.parts.clear()
-                    ops.bag_mean_backward_adamw(dp, den, ids, p.data, st["exp_avg"], st["exp_avg_sq"],
-                                                deferred.padding_idx, lr=lr,
-                                                beta1=b1, beta2=b2, eps=eps, weight_decay=wd, step=int(st["step"]))
-                    continue
-                if p.grad is None:
-                    continue
-                if p.grad.is_sparse:
-                    raise RuntimeError("AdamW does not support sparse gradients")
-                st = self._state(p)
-                st["step"] += 1
-                ops.adamw_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], lr=lr, beta1=b1,
-                               beta2=b2, eps=eps, weight_decay=wd, step=int(st["step"]))
+            if group["capturable"]:
+                self._step_device(group)
+            else:
+                self._step_host(group)
         return loss
 
+    def _step_host(self, group: dict) -> None:
+        """torch's default (non-capturable) form: step counters on the host."""
+        lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+        for p in group["params"]:
+            deferred = getattr(p, "_tt_deferred", None)
+            if deferred is not None and deferred.parts:
+                st = self._state(p, False)
+                st["step"] += 1
+                ids, dp, den, plan = _merge_parts(deferred.parts, p, deferred.padding_idx)
+                deferred.parts.clear()
+                args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
+                ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"], args)
+                continue
+            if p.grad is None:
+                continue
+            if p.grad.is_sparse:
+                raise RuntimeError("AdamW does not support sparse gradients")
+            st = self._state(p, False)
+            st["step"] += 1
+            ops.adamw_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], lr=lr, beta1=b1,
+                           beta2=b2, eps=eps, weight_decay=wd, step=int(st["step"]))
 
-def _merge_parts(parts):
+    def _step_device(self, group: dict) -> None:
+        """Capturable form: one tt_adam_prepare launch, one multi-tensor launch per 16 dense
+        parameters, one fused scatter + AdamW launch per table."""
+        slots, dense, fused = [], [], []
+        for p in group["params"]:
+            deferred = getattr(p, "_tt_deferred", None)
+            if deferred is not None and deferred.parts:
+                st = self._state(p, True)
+                slots.append((st["step"], self._adam_args(p)))
+                fused.append((p, st, _merge_parts(deferred.parts, p, deferred.padding_idx)))
+                deferred.parts.clear()
+                continue
+            if p.grad is None:
+                continue
+            if p.grad.is_sparse:
+                raise RuntimeError("AdamW does not support sparse gradients")
+            for t, nm in ((p, "param"), (p.grad, "grad")):
+                if not t.is_cuda or t.dtype != torch.float32:
+                    raise ValueError(f"capturable AdamW needs float32 GPU tensors ({nm} is {t.dtype} on {t.device})")
+            st = self._state(p, True)
+            a = self._adam_args(p)
+            slots.append((st["step"], a))
+            dense.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], a))
+        lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+        ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd)
+        ops.adamw_multi(dense)
+        for p, st, (ids, dp, den, plan) in fused:
+            ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
+                                                self._adam_args(p))
+
+
+def _host_adam_args(lr, b1, b2, eps, wd, step, device) -> torch.Tensor:
+    """The per-step scalars of make_adam (csrc/common.hpp) formed in Python doubles, rounded to
+    fp32 once, as a TT_ADAM_ARGS_BYTES device buffer."""
+    vals = [1.0 - lr * wd, 1.0 - b1, b2, 1.0 - b2, lr / (1.0 - b1 ** step), math.sqrt(1.0 - b2 ** step), eps, 0.0]
+    return torch.tensor(vals, dtype=torch.float32).to(device)
+
+
+def _merge_parts(parts, table: torch.Tensor, padding_idx):
+    """One (ids, d_pooled, denom, plan) for every bag call on the table this step (a single call
+    in the fused TwoTower path; separate tower calls are concatenated and re-planned)."""
     if len(parts) == 1:
-        return parts[0]
-    L = max(ids.shape[1] for ids, _, _ in parts)
-    ids = torch.cat([F.pad(i.to(torch.int64), (0, L - i.shape[1])) for i, _, _ in parts], 0)
-    return ids, torch.cat([d for _, d, _ in parts], 0), torch.cat([n for _, _, n in parts], 0)
+        ids, dp, den, plan = parts[0]
+        if plan is None and table.is_cuda:
+            plan = ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx)
+        return ids, dp, den, plan
+    L = max(p[0].shape[1] for p in parts)
+    ids = torch.cat([F.pad(p[0].to(torch.int64), (0, L - p[0].shape[1])) for p in parts], 0)
+    dp = torch.cat([p[1] for p in parts], 0)
+    den = torch.cat([p[2] for p in parts], 0)
+    return ids, dp, den, ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx)

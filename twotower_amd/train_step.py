@@ -2,6 +2,13 @@
 (twotower/train.py:103-139: forward :120-122, loss :133, zero_grad/backward/step :137-139),
 with optional data parallelism.  Returns the loss as a device tensor (no host sync; the
 reference's per-step .item() monitors at :144-154 are left to the caller).
+
+``graph=True`` captures the whole step (forward, loss, backward, optimizer) in one HIP graph
+after ``eager_steps`` ordinary steps and replays it for every later batch of the same shape:
+the step's ~40 kernel launches then cost one graph launch, and the GPU no longer idles while
+Python issues short kernels.  Each call is still exactly one training step on its own batch
+(the batch is copied into the graph's static input buffers first).  Needs a capturable
+optimizer (optim.AdamW(capturable=True)); a new input shape is captured anew.
 """
 from __future__ import annotations
 
@@ -11,14 +18,20 @@ from .distributed import GradSync, is_active
 
 
 class TrainStep:
-    def __init__(self, model: torch.nn.Module, loss_fn, optimizer: torch.optim.Optimizer, group=None):
+    def __init__(self, model: torch.nn.Module, loss_fn, optimizer: torch.optim.Optimizer, group=None,
+                 graph: bool = False, eager_steps: int = 2):
         self.model = model
         self.loss_fn = loss_fn
         self.optimizer = optimizer
         self.group = group
         self.sync = GradSync(model.parameters(), group=group) if is_active(group) else None
+        self.graph = graph
+        if graph and not all(g.get("capturable", False) for g in optimizer.param_groups):
+            raise ValueError("TrainStep(graph=True) needs an optimizer built with capturable=True")
+        self._eager_left = max(1, int(eager_steps))  # >= 1: lazy library/workspace set-up happens eagerly
+        self._graphs: dict[tuple, tuple] = {}
 
-    def __call__(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
+    def eager(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
         q, p, n = self.model(queries, positive_docs, negative_docs)
         loss = self.loss_fn(q, p, n)
         self.optimizer.zero_grad(set_to_none=True)
@@ -29,3 +42,28 @@ class TrainStep:
             loss.backward()
         self.optimizer.step()
         return loss.detach()
+
+    def __call__(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
+        if not self.graph:
+            return self.eager(queries, positive_docs, negative_docs)
+        inputs = (queries, positive_docs, negative_docs)
+        key = tuple((tuple(t.shape), t.dtype, t.device) for t in inputs)
+        hit = self._graphs.get(key)
+        if hit is None:
+            if self._eager_left > 0:
+                self._eager_left -= 1
+                return self.eager(*inputs)
+            hit = self._graphs[key] = self._capture(inputs)
+        graph, static_in, static_loss = hit
+        for dst, src in zip(static_in, inputs):
+            dst.copy_(src)
+        graph.replay()
+        return static_loss
+
+    def _capture(self, inputs):
+        static_in = tuple(t.clone() for t in inputs)
+        graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph):
+            static_loss = self.eager(*static_in)
+        return graph, static_in, static_loss
