@@ -63,25 +63,32 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the step as one HIP graph (auto: on for a single GPU)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--timing-steps", type=int, default=10, help="eager steps timed per op after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=1024)
     return ap.parse_args()
 
 
-def setup_dist():
+def setup_dist(backend: str):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "gloo":  # rehearsal of the DP path on one GPU (ranks share it); RCCL is the real path
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank
 
 
 def main():
     args = parse()
-    world, rank = setup_dist()
+    world, rank = setup_dist(args.dist_backend)
     cfg = CONFIGS[args.config]
     V, d, L, B = cfg["V"], cfg["d"], cfg["L"], cfg["B"]
     scorer_dtype = args.scorer_dtype or cfg["dtype"]
@@ -93,7 +100,9 @@ def main():
     loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
                               cross_device_negatives=world > 1)
     use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
-    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=world == 1, tables=[emb], capturable=True)
+    # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
+    # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
     step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
     batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev) for k in range(4)]

@@ -1,0 +1,165 @@
+"""Data-parallel logic on CPU: gloo, world_size 2, one process per rank (the same code runs over
+RCCL on the GPU node).  Each check compares the 2-rank computation against the single-process
+computation on the concatenated global batch, with torch CPU math standing in for the HIP
+kernels (which need a GPU): the collectives, the row sharding, the label offsets and the loss
+scaling are what is under test here."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from twotower_amd import distributed as D
+
+WORLD = 2
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(fn, *args):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_entry, args=(r, port, fn, q, args)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r for r in results if isinstance(r, str)]
+    assert not errs, errs[0]
+
+
+def _entry(rank, port, fn, q, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        torch.manual_seed(0)
+        fn(rank, *args)
+        q.put(None)
+    except Exception as e:  # reported to the parent
+        import traceback
+
+        q.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------------------------
+def _collectives(rank):
+    x = torch.arange(6 * 3, dtype=torch.float32).view(6, 3) * (rank + 1)
+    out = torch.empty(3, 3)
+    D.reduce_scatter_rows(out, x)
+    full = torch.arange(18, dtype=torch.float32).view(6, 3) * 3  # (1 + 2) x
+    assert torch.equal(out, full[rank * 3:(rank + 1) * 3])
+    g = torch.empty(4, 2)
+    D.all_gather_rows(g, torch.full((2, 2), float(rank)))
+    assert torch.equal(g, torch.tensor([[0., 0.], [0., 0.], [1., 1.], [1., 1.]]))
+    # in place: the input is this rank's slab of the output
+    buf = torch.zeros(4, 2)
+    buf[rank * 2:(rank + 1) * 2] = rank + 5
+    D.all_gather_rows(buf, buf[rank * 2:(rank + 1) * 2])
+    assert torch.equal(buf, torch.tensor([[5., 5.], [5., 5.], [6., 6.], [6., 6.]]))
+
+
+def test_collectives_gloo():
+    _run(_collectives)
+
+
+# ---------------------------------------------------------------------------------------------
+def _ref_adamw(p, g, m, v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, wd=0.01):
+    p.mul_(1 - lr * wd)
+    m.lerp_(g, 1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    denom = (v.sqrt() / (1 - b2 ** step) ** 0.5).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / (1 - b1 ** step))
+
+
+def _sharded_table(rank, V):
+    """Row-sharded AdamW on the reduce-scattered gradient == full AdamW on the global gradient."""
+    E = 4
+    torch.manual_seed(1)
+    table0 = torch.randn(V, E)
+    grads = [torch.randn(V, E) for _ in range(WORLD)]  # each rank's local (pre-scaled) gradient
+    w = torch.nn.Parameter(table0.clone())
+    sh = D.ShardedRows(w, None)
+    assert sh.Vp % WORLD == 0 and sh.Vp >= V and w.shape == (V, E)
+    m = torch.zeros(sh.Vs, E)
+    v = torch.zeros(sh.Vs, E)
+    ref_p, ref_m, ref_v = table0.clone(), torch.zeros(V, E), torch.zeros(V, E)
+    for step in (1, 2, 3):
+        gbuf = sh.new_grad_buffer()
+        gbuf[:V] = grads[rank] * step
+        g_shard = sh.reduce_scatter(gbuf)
+        _ref_adamw(sh.rows(sh.storage()), g_shard, m, v, step)
+        sh.all_gather_params()
+        _ref_adamw(ref_p, sum(g * step for g in grads), ref_m, ref_v, step)
+        assert torch.allclose(w.data, ref_p, rtol=0, atol=1e-6), step
+    if sh.Vp > V:
+        assert torch.equal(sh.storage()[V:], torch.zeros(sh.Vp - V, E))  # padding rows stay zero
+
+
+@pytest.mark.parametrize("V", [10, 11])
+def test_sharded_table_adamw_equals_global(V):
+    _run(_sharded_table, V)
+
+
+# ---------------------------------------------------------------------------------------------
+def _inbatch_ref(q, d, tau, off):
+    s = q @ d.t() / tau
+    return F.cross_entropy(s, torch.arange(q.shape[0]) + off)
+
+
+def _cross_device_negatives(rank):
+    """Local loss on all-gathered candidates with offset labels, pre-scaled by 1/world and
+    summed over ranks == the global-batch in-batch loss; gradients flow back to the owners."""
+    B, H, tau = 5, 8, 0.1
+    torch.manual_seed(2)
+    qg = torch.randn(WORLD * B, H)
+    dg = torch.randn(WORLD * 2 * B, H)  # each rank holds 2B candidates (its p and n)
+    q = qg[rank * B:(rank + 1) * B].clone().requires_grad_(True)
+    d = dg[rank * 2 * B:(rank + 1) * 2 * B].clone().requires_grad_(True)
+    dall, off = D.gather_candidates(d)
+    assert off == rank * 2 * B and dall.shape[0] == WORLD * 2 * B
+    # labels: query i of rank r is positive for candidate row off + i (its own p)
+    loss = _inbatch_ref(q, dall, tau, off)
+    (loss / WORLD).backward()
+    total = loss.detach().clone()
+    dist.all_reduce(total)
+    # global reference: the same candidates, labels = each query's own positive row
+    qr = qg.clone().requires_grad_(True)
+    dr = dg.clone().requires_grad_(True)
+    labels = torch.cat([torch.arange(B) + r * 2 * B for r in range(WORLD)])
+    ref = F.cross_entropy(qr @ dr.t() / tau, labels)
+    ref.backward()
+    assert torch.allclose(total / WORLD, ref.detach(), atol=1e-6)
+    assert torch.allclose(q.grad, qr.grad[rank * B:(rank + 1) * B], atol=1e-6)
+    assert torch.allclose(d.grad, dr.grad[rank * 2 * B:(rank + 1) * 2 * B], atol=1e-6)
+
+
+def test_cross_device_negatives_equal_global_batch():
+    _run(_cross_device_negatives)
+
+
+def _grad_sync(rank):
+    lin = torch.nn.Linear(3, 2)
+    sync = D.GradSync(lin.parameters())
+    assert sync.loss_scale() == 0.5
+    x = torch.full((4, 3), float(rank + 1))
+    (lin(x).sum() * sync.loss_scale()).backward()
+    sync.sync()
+    # mean over the two ranks' gradients
+    assert torch.allclose(lin.weight.grad, torch.full((2, 3), 4 * 1.5))
+    assert torch.allclose(lin.bias.grad, torch.full((2,), 4.0))
+
+
+def test_grad_sync_mean():
+    _run(_grad_sync)

@@ -1,0 +1,116 @@
+"""Data-parallel step on the real HIP kernels: two ranks share cuda:0 over gloo (RCCL will not
+put two ranks on one GPU; the round-end 8-GPU run uses RCCL with the same code), and their
+parameters after each step must equal a single process stepping on the global batch.
+
+The DP step: each rank pools/scores its half, the in-batch candidates are all-gathered with
+rank-offset labels, the loss is pre-scaled by 1/world, tower gradients are all-reduced, and
+the table gradient is reduce-scattered into row shards, updated by AdamW per shard and
+all-gathered.  Sum orders differ from the single process (two partial sums), so the bar is the
+fp32 1e-5 relative tolerance on the parameter change.  AdamW normalises every element's update,
+which turns rounding-level differences of near-cancelled gradients (|g| ~ eps) into O(lr)
+parameter differences; with eps = 1 and no decay the first update is -lr g / (|g| + 1), so the
+parameter change measures the synchronised gradient itself, checked against the float64 oracle."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+LR = 1e6  # the parameter change dominates the O(1) parameters, so it is read back at fp32 precision
+V, E, B, L = 3001, 64, 64, 24
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _build(loss_name, world):
+    import twotower_amd as tt
+
+    torch.manual_seed(7)
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to("cuda:0")
+    kw = {"temperature": 0.1, "cross_device_negatives": world > 1} if loss_name == "in_batch" else {"margin": 0.2}
+    opt = tt.optim.AdamW(model.parameters(), lr=LR, eps=1.0, weight_decay=0.0, fused_tables=True, tables=[emb],
+                         capturable=True)
+    return model, tt.TrainStep(model, tt.losses.build(loss_name, **kw), opt)
+
+
+def _batch():
+    import twotower_amd as tt
+
+    return tt.data.synthetic_triplets(WORLD * B, L, V, seed=3, device="cuda:0")
+
+
+def _worker(rank, port, loss_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        if rank >= 0:
+            dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        model, step = _build(loss_name, WORLD if rank >= 0 else 1)
+        init = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
+        full = _batch()
+        b = full if rank < 0 else tuple(t[rank * B:(rank + 1) * B] for t in full)
+        loss = step(*b).clone()
+        if rank >= 0:
+            dist.all_reduce(loss)
+            loss /= WORLD
+        # numpy arrays travel by value (torch CPU tensors would travel as fds of a dying process)
+        delta = {n: p.detach().cpu().numpy() - init[n] for n, p in model.named_parameters()}
+        q.put((rank, float(loss), init, delta, [t.cpu().numpy() for t in full]))
+    except Exception as e:
+        import traceback
+
+        q.put((rank, f"{e!r}\n{traceback.format_exc()}", None, None, None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+KEYS = {"table": "query_tower.embedding.embedding.weight", "W1": "query_tower.feed_forward.0.weight",
+        "b1": "query_tower.feed_forward.0.bias", "W2": "query_tower.feed_forward.2.weight",
+        "b2": "query_tower.feed_forward.2.bias"}
+
+
+@pytest.mark.parametrize("loss_name", ["in_batch", "triplet"])
+def test_dp_step_equals_global_batch(loss_name):
+    """One step, eps 1, no decay: delta = -lr g / (|g| + 1), so g is recovered from the parameter
+    change and compared with the float64 oracle on the global batch."""
+    from oracle import reference_math as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, q))
+    ref.start()
+    _, r_loss, init, r_delta, ids = q.get(timeout=300)
+    ref.join(timeout=60)
+    assert init is not None, r_loss
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    params = {k: init[v] for k, v in KEYS.items()}
+    kw = {"temperature": 0.1} if loss_name == "in_batch" else {"margin": 0.2}
+    o_loss, _, o_grads = O.tied_step_grads(params, *ids, loss=loss_name, **kw)
+    assert abs(r_loss - o_loss) < 1e-5
+    runs = [("single", r_loss, r_delta)] + [(f"rank{r}", l_, d_) for r, l_, _, d_, _ in out]
+    for name, loss, delta in runs:
+        assert delta is not None, loss
+        assert abs(loss - o_loss) < 1e-5, (name, loss, o_loss)
+        for k, key in KEYS.items():
+            d = delta[key].astype("float64")
+            u = -d / LR
+            g = u / (1.0 - abs(u))
+            err = abs(g - o_grads[k]).max() / abs(o_grads[k]).max()
+            assert err < 1e-5, (name, k, float(err))

@@ -105,10 +105,14 @@ class BagPlan:
         torch.cuda.current_stream(self.buf.device).wait_event(self.ready)
 
 
-def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan: BagPlan) -> torch.Tensor:
+def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan: BagPlan,
+                              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Dense (V, E) table gradient from a BagPlan (every row written), into `out` if given."""
     d_pooled = _contig_f32(d_pooled, "d_pooled")
     plan.wait()
-    grad = torch.empty(plan.V, plan.E, dtype=_FLOAT, device=d_pooled.device)
+    grad = torch.empty(plan.V, plan.E, dtype=_FLOAT, device=d_pooled.device) if out is None else out
+    if tuple(grad.shape) != (plan.V, plan.E) or not grad.is_contiguous() or grad.dtype != _FLOAT:
+        raise ValueError("out must be a contiguous float32 (V, E) tensor")
     call("tt_bag_mean_bwd_planned", ptr(d_pooled), ptr(denom), plan.nseq, plan.L, plan.V, plan.E, ptr(plan.buf),
          plan.buf.numel(), ptr(grad), stream_of(d_pooled))
     return grad

@@ -21,18 +21,19 @@ import math
 import torch
 import torch.nn.functional as F
 
-from . import _lib, ops
+from . import _lib, distributed, ops
 
 
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 fused_tables: bool = False, tables=(), capturable: bool = False):
+                 fused_tables: bool = False, tables=(), capturable: bool = False, group=None):
         if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
             raise ValueError("invalid AdamW hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                                       capturable=bool(capturable)))
         self._tables: list[torch.Tensor] = []
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
+        self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
         if fused_tables:
             ids = {id(p) for g in self.param_groups for p in g["params"]}
             for t in tables:
@@ -43,6 +44,8 @@ class AdamW(torch.optim.Optimizer):
                     raise ValueError("fused table is not among the optimizer's parameters")
                 w._tt_deferred = ops.DeferredTableGrad(pad)
                 self._tables.append(w)
+                if distributed.is_active(group):
+                    self._shards[id(w)] = distributed.ShardedRows(w, group)
 
     def release_tables(self) -> None:
         """Return the tables to ordinary dense gradients."""
@@ -55,8 +58,10 @@ class AdamW(torch.optim.Optimizer):
         st = self.state[p]
         if not st:
             st["step"] = torch.tensor(0.0, dtype=torch.float32, device=p.device if capturable else "cpu")
-            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            sh = self._shards.get(id(p))
+            like = p if sh is None else p.new_empty(sh.Vs, sh.E)  # sharded table: this rank's rows only
+            st["exp_avg"] = torch.zeros_like(like, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(like, memory_format=torch.preserve_format)
         elif capturable and st["step"].device != p.device:
             st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
         return st
@@ -90,6 +95,13 @@ class AdamW(torch.optim.Optimizer):
                 st["step"] += 1
                 ids, dp, den, plan = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
+                sh = self._shards.get(id(p))
+                if sh is not None:
+                    g_shard = self._table_grad_shard(sh, dp, den, plan)
+                    ops.adamw_step(sh.rows(sh.storage()), g_shard, st["exp_avg"], st["exp_avg_sq"], lr=lr,
+                                   beta1=b1, beta2=b2, eps=eps, weight_decay=wd, step=int(st["step"]))
+                    sh.all_gather_params()
+                    continue
                 args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
                 ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"], args)
                 continue
@@ -105,14 +117,22 @@ class AdamW(torch.optim.Optimizer):
     def _step_device(self, group: dict) -> None:
         """Capturable form: one tt_adam_prepare launch, one multi-tensor launch per 16 dense
         parameters, one fused scatter + AdamW launch per table."""
-        slots, dense, fused = [], [], []
+        slots, dense, fused, gathers = [], [], [], []
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
             if deferred is not None and deferred.parts:
                 st = self._state(p, True)
-                slots.append((st["step"], self._adam_args(p)))
-                fused.append((p, st, _merge_parts(deferred.parts, p, deferred.padding_idx)))
+                a = self._adam_args(p)
+                slots.append((st["step"], a))
+                parts = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
+                sh = self._shards.get(id(p))
+                if sh is not None:  # data parallel: reduce-scatter, AdamW on own rows, all-gather
+                    g_shard = self._table_grad_shard(sh, parts[1], parts[2], parts[3])
+                    dense.append((sh.rows(sh.storage()), g_shard, st["exp_avg"], st["exp_avg_sq"], a))
+                    gathers.append(sh)
+                else:
+                    fused.append((p, st, parts))
                 continue
             if p.grad is None:
                 continue
@@ -131,6 +151,15 @@ class AdamW(torch.optim.Optimizer):
         for p, st, (ids, dp, den, plan) in fused:
             ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
                                                 self._adam_args(p))
+        for sh in gathers:
+            sh.all_gather_params()
+
+    @staticmethod
+    def _table_grad_shard(sh, d_pooled, denom, plan) -> torch.Tensor:
+        """This rank's rows of the summed table gradient (the loss is pre-scaled by 1/world)."""
+        gbuf = sh.new_grad_buffer()
+        ops.bag_mean_backward_planned(d_pooled, denom, plan, out=gbuf[:sh.V])
+        return sh.reduce_scatter(gbuf)
 
 
 def _host_adam_args(lr, b1, b2, eps, wd, step, device) -> torch.Tensor:
