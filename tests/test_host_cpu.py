@@ -1,0 +1,167 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports every symbol the public
+header declares, its argument validation answers without touching a device, and the Python
+surface mirrors the reference's plugin API (registries, builders and their errors, parameter
+names, install() into a reference-shaped package, packed-view detection)."""
+import ctypes
+import subprocess
+import sys
+import types
+
+import pytest
+import torch
+
+import twotower_amd as tt
+from twotower_amd import _lib, losses
+
+
+# ---------------------------------------------------------------------------------------------
+# C ABI
+def test_library_exports_every_header_symbol():
+    lib = _lib.lib()
+    names = _lib.header_symbols()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the ctypes table binds exactly the declared functions
+    assert sorted(_lib._SIGNATURES) == names
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = {ln.split()[-1] for ln in out.stdout.splitlines() if " T " in ln}
+    assert set(names) <= exported
+    assert lib.tt_version() == 1
+
+
+def test_library_is_gfx950_only():
+    """Every offload bundle embedded in the library targets gfx950 (no other ISA, no fallback)."""
+    import re
+
+    blob = open(_lib.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+@pytest.mark.parametrize("call,msg", [
+    (lambda L: L.tt_bag_mean_fwd(None, 0, 64, None, 0, 1, 4, 4, None, None, None), "V=0"),
+    (lambda L: L.tt_bag_mean_fwd(None, 10, 64, None, 7, 1, 4, 4, None, None, None), "ids_dtype"),
+    (lambda L: L.tt_bag_mean_fwd(None, 10, 64, None, 0, 2, 4, 3, None, None, None), "bad ids shape"),
+    (lambda L: L.tt_adamw(None, None, None, None, 16, 1e-3, 0.9, 0.999, 1e-8, 0.01, 0, None), "step must be"),
+    (lambda L: L.tt_adamw_multi(None, 17, None), "count=17"),
+    (lambda L: L.tt_colsum(ctypes.c_void_p(16), 8, 6, ctypes.c_void_p(16), ctypes.c_void_p(16), 1 << 20, None), "cols % 4"),
+    (lambda L: L.tt_inbatch_fwd(None, None, 8, 4, 64, 0, 10.0, 0, 1, None, None, None, None, None, 0, None),
+     "label"),
+])
+def test_validation_without_a_device(call, msg):
+    rc = call(_lib.lib())
+    assert rc != 0
+    assert msg in _lib.last_error(), _lib.last_error()
+
+
+def test_ops_refuse_cpu_tensors():
+    w = torch.zeros(10, 4)
+    ids = torch.ones(2, 3, dtype=torch.int64)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        tt.ops.bag_mean_pool(w, ids)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        tt.ops.in_batch_softmax_loss(torch.zeros(2, 64), torch.zeros(4, 64))
+
+
+# ---------------------------------------------------------------------------------------------
+# plugin surface (twotower/embeddings.py:159-181, encoders.py:228-272, losses.py:122-150)
+def test_registries_and_builder_errors():
+    assert set(tt.embeddings.REGISTRY) == {"lookup", "word2vec", "glove"}
+    assert set(tt.TOWER_REGISTRY) == {"mean", "avg_pool"}
+    assert set(tt.LOSS_REGISTRY) == {"triplet", "multiple_negatives", "in_batch"}
+    with pytest.raises(ValueError, match=r"Unknown embedding: nope\. Available options: \['lookup'"):
+        tt.embeddings.build("nope", vocab_size=10)
+    with pytest.raises(ValueError, match=r"Unknown tower architecture: nope\. Available options"):
+        tt.build_tower("nope", tt.embeddings.build("lookup", vocab_size=10, embedding_dim=8))
+    with pytest.raises(ValueError, match=r"Unknown loss function: nope\. Available options"):
+        losses.build("nope")
+    f = losses.build("triplet", margin=0.3)
+    assert f.func is losses.contrastive_triplet_loss and f.keywords == {"margin": 0.3}
+    assert losses.build("in_batch") is losses.in_batch_sampled_softmax_loss
+    with pytest.raises(ImportError):
+        tt.embeddings.build("glove", vocab_size=10, embedding_dim=8)
+
+
+def test_lookup_embedding_layout_and_state_dict_names():
+    emb = tt.embeddings.build("lookup", vocab_size=50, embedding_dim=8)
+    assert (emb.vocab_size, emb.embedding_dim, emb.padding_idx) == (50, 8, 0)
+    assert isinstance(emb.embedding, torch.nn.Embedding) and emb.embedding.padding_idx == 0
+    assert torch.equal(emb.embedding.weight[0], torch.zeros(8))  # nn.Embedding zeroes the padding row
+    model = tt.build_two_tower("mean", emb, hidden_dim=16, tied_weights=True)
+    keys = sorted(model.state_dict())
+    tower = ["embedding.embedding.weight", "feed_forward.0.bias", "feed_forward.0.weight", "feed_forward.2.bias",
+             "feed_forward.2.weight"]
+    assert keys == sorted([f"query_tower.{k}" for k in tower] + [f"document_tower.{k}" for k in tower])
+    assert model.document_tower is model.query_tower
+    untied = tt.build_two_tower("mean", emb, hidden_dim=16, tied_weights=False)
+    assert untied.document_tower is not untied.query_tower
+    assert untied.document_tower.embedding is untied.query_tower.embedding  # one shared table (encoders.py:265,270)
+    avg = tt.build_tower("avg_pool", emb, hidden_dim=16)
+    assert sorted(k for k in avg.state_dict() if k.startswith("projection")) == [
+        "projection.0.bias", "projection.0.weight", "projection.2.bias", "projection.2.weight"]
+
+
+def test_optimizer_state_dict_interchanges_with_torch():
+    p = [torch.nn.Parameter(torch.randn(4, 4)), torch.nn.Parameter(torch.randn(4))]
+    ref = torch.optim.AdamW(p, lr=1e-3)
+    for x in p:
+        x.grad = torch.ones_like(x)
+    ref.step()
+    mine = tt.optim.AdamW(p, lr=1e-3, capturable=True)
+    mine.load_state_dict(ref.state_dict())
+    st = mine.state[p[0]]
+    assert set(st) == {"step", "exp_avg", "exp_avg_sq"} and float(st["step"]) == 1.0
+    assert mine.param_groups[0]["capturable"] is True
+    # and back: torch reads ours
+    ref2 = torch.optim.AdamW(p, lr=1e-3)
+    ref2.load_state_dict(mine.state_dict())
+    assert torch.equal(ref2.state[p[0]]["exp_avg"], st["exp_avg"])
+
+
+def test_install_into_reference_shaped_package():
+    pkg = "fake_twotower_ref"
+    mods = {}
+    for sub in ("", ".embeddings", ".encoders", ".losses", ".train"):
+        m = types.ModuleType(pkg + sub)
+        mods[pkg + sub] = m
+    mods[pkg].__path__ = []
+    mods[pkg + ".embeddings"].REGISTRY = {"lookup": object}
+    mods[pkg + ".encoders"].TOWER_REGISTRY = {"mean": object}
+    mods[pkg + ".losses"].LOSS_REGISTRY = {"triplet": None}
+    mods[pkg + ".train"].build_two_tower = None
+    sys.modules.update(mods)
+    try:
+        tt.install(pkg)
+        assert mods[pkg + ".embeddings"].REGISTRY["lookup"] is tt.LookupEmbedding
+        assert mods[pkg + ".encoders"].TOWER_REGISTRY["mean"] is tt.MeanPoolingTower
+        assert mods[pkg + ".encoders"].build_two_tower is tt.build_two_tower
+        assert mods[pkg + ".train"].build_two_tower is tt.build_two_tower
+        assert mods[pkg + ".losses"].LOSS_REGISTRY["in_batch"] is tt.in_batch_sampled_softmax_loss
+    finally:
+        for k in mods:
+            sys.modules.pop(k, None)
+
+
+def test_packed_view_detection():
+    base = torch.randn(9, 4)
+    q, p, n = torch.split(base, 3)
+    assert losses._packed(q, p, n) is base
+    assert losses._packed(q, n, p) is None           # out of order
+    assert losses._packed(q, p) is None              # not the whole base
+    assert losses._packed(q.clone(), p, n) is None   # not views of one tensor
+    cand = losses._candidates(p, n)
+    assert cand.data_ptr() == p.data_ptr() and cand.shape == (6, 4)
+
+
+def test_synthetic_triplets_shape_and_padding():
+    q, p, n = tt.data.synthetic_triplets(64, 16, 1000, seed=1, device="cpu")
+    for t, (lo, hi) in ((q, (3, 12)), (p, (8, 16)), (n, (8, 16))):
+        assert t.shape == (64, 16) and t.dtype == torch.int32
+        lens = (t > 0).sum(1)
+        assert int(lens.min()) >= lo and int(lens.max()) <= hi
+        # trailing padding: no real token after the first pad
+        pos = torch.arange(16)
+        assert bool(((t > 0) == (pos < lens[:, None])).all())
+        assert int(t.max()) < 1000
+    assert tt.data.tokens_per_triplet(16) == pytest.approx(7.5 + 2 * 12)

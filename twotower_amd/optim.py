@@ -62,9 +62,24 @@ class AdamW(torch.optim.Optimizer):
             like = p if sh is None else p.new_empty(sh.Vs, sh.E)  # sharded table: this rank's rows only
             st["exp_avg"] = torch.zeros_like(like, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(like, memory_format=torch.preserve_format)
-        elif capturable and st["step"].device != p.device:
-            st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+        else:
+            if capturable and st["step"].device != p.device:
+                st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+            sh = self._shards.get(id(p))
+            if sh is not None and st["exp_avg"].shape[0] == sh.V:  # full-table state loaded: keep own rows
+                for k in ("exp_avg", "exp_avg_sq"):
+                    full = torch.zeros(sh.Vp, sh.E, dtype=st[k].dtype, device=st[k].device)
+                    full[:sh.V] = st[k]
+                    st[k] = sh.rows(full).clone()
         return st
+
+    def load_state_dict(self, state_dict) -> None:
+        """torch semantics, except that `capturable` stays what this optimizer was built with (it
+        selects the execution path, not the math); step counters move on first use."""
+        modes = [g["capturable"] for g in self.param_groups]
+        super().load_state_dict(state_dict)
+        for g, c in zip(self.param_groups, modes):
+            g["capturable"] = c
 
     def _adam_args(self, p: torch.Tensor) -> torch.Tensor:
         a = self._args.get(id(p))
