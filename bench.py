@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--scorer-dtype", default=None, help="override: fp32 | bf16 | bf16_fast")
+    ap.add_argument("--scorer-dtype", default=None, help="override: fp32 | bf16 | bf16_split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the step as one HIP graph (auto: on for a single GPU)")

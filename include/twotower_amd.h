@@ -32,7 +32,7 @@ typedef struct ihipStream_t* tt_stream_t; /* layout-compatible with hipStream_t 
 
 enum tt_status { TT_OK = 0, TT_ERR_INVALID = -1, TT_ERR_WORKSPACE = -2, TT_ERR_UNSUPPORTED = -3 };
 enum tt_index_dtype { TT_IDS_I32 = 0, TT_IDS_I64 = 1 };
-enum tt_compute_dtype { TT_F32 = 0, TT_BF16 = 1, TT_BF16_FAST = 2 };
+enum tt_compute_dtype { TT_F32 = 0, TT_BF16 = 1, TT_BF16_SPLIT = 2 };
 enum tt_scatter_mode {
   TT_SCATTER_SORTED = 0, /* deterministic: stable radix sort + segmented row reduce; writes every row */
   TT_SCATTER_ATOMIC = 1  /* global_atomic_add_f32 into caller-zeroed grad; order-dependent */
@@ -165,8 +165,10 @@ int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t 
  * S = q d^T (B x M, never materialised), logits = S * inv_tau, label of row i is column
  * i + label_off (reference: arange(B), label_off = 0; data-parallel: rank * local M).
  * loss = mean_i (lse_i - logits[i, i+label_off]).
- * compute dtype TT_F32 (exact fp32 MFMA), TT_BF16 (bf16 operands, P split hi+lo bf16 so the
- * second product keeps ~16 mantissa bits) or TT_BF16_FAST (P rounded once to bf16).
+ * compute dtype TT_F32 (exact fp32 MFMA), TT_BF16 (bf16 MFMA operands, P rounded once to bf16,
+ * fp32 accumulation) or TT_BF16_SPLIT (P split hi + lo bf16 so the P.D / dS^T.Q products keep
+ * ~16 mantissa bits, at 1.5x the MFMA work; the q/d rounding to bf16 still dominates the error
+ * against fp32 inputs: both bf16 forms land ~3-4e-3 from the fp32 reference's gradients at C3).
  * fwd (want_grad != 0) also leaves dq_unscaled = sum_j P_ij d~_j - d~_label (B x H) so the
  * backward needs only the dD pass.  ws must stay untouched between fwd and bwd. */
 size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype);

@@ -16,11 +16,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwotower
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "twotower_amd.h")
 
 TT_IDS_I32, TT_IDS_I64 = 0, 1
-TT_F32, TT_BF16, TT_BF16_FAST = 0, 1, 2
+TT_F32, TT_BF16, TT_BF16_SPLIT = 0, 1, 2
 TT_SCATTER_SORTED, TT_SCATTER_ATOMIC = 0, 1
 
 COMPUTE_DTYPES = {"fp32": TT_F32, "float32": TT_F32, "bf16": TT_BF16, "bfloat16": TT_BF16,
-                  "bf16_fast": TT_BF16_FAST}
+                  "bf16_split": TT_BF16_SPLIT}
 
 _c_i64, _c_int, _c_f32, _c_sz, _vp = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 _c_f64 = ctypes.c_double

@@ -570,7 +570,7 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.shift, w.pad, w.acc_part, w.l_part);
-  } else if (dtype == TT_BF16) {
+  } else if (dtype == TT_BF16_SPLIT) {
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.shift, w.pad, w.acc_part, w.l_part);
@@ -598,7 +598,7 @@ int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, 
 int check_args(int64_t B, int64_t M, int H, int dtype, int64_t label_off) {
   TT_REQUIRE(B > 0 && M > 0, "B=%lld M=%lld must be positive", (long long)B, (long long)M);
   TT_REQUIRE(H == 32 || H == 64 || H == 128 || H == 256, "H=%d unsupported (32, 64, 128, 256)", H);
-  TT_REQUIRE(dtype == TT_F32 || dtype == TT_BF16 || dtype == TT_BF16_FAST, "dtype=%d", dtype);
+  TT_REQUIRE(dtype == TT_F32 || dtype == TT_BF16 || dtype == TT_BF16_SPLIT, "dtype=%d", dtype);
   TT_REQUIRE(label_off >= 0 && label_off + B <= M, "labels [%lld, %lld) fall outside the %lld candidate columns",
              (long long)label_off, (long long)(label_off + B), (long long)M);
   return TT_OK;

@@ -100,6 +100,20 @@ class AveragePoolingTower(BaseTower):
         return ops.l2_normalize(out.contiguous())  # encoders.py:150
 
 
+def _packed_ids(inputs: list[torch.Tensor]) -> torch.Tensor | None:
+    """The common (N, L) base when the id tensors are consecutive row blocks of it in order
+    (TrainStep's packed static batch), so the fused forward needs no concatenation."""
+    base = inputs[0]._base
+    if base is None or base.dim() != 2 or not base.is_contiguous():
+        return None
+    at, row = base.data_ptr(), base.shape[1] * base.element_size()
+    for t in inputs:
+        if t._base is not base or not t.is_contiguous() or t.shape[1] != base.shape[1] or t.data_ptr() != at:
+            return None
+        at += t.shape[0] * row
+    return base if at == base.data_ptr() + base.shape[0] * row else None
+
+
 class TwoTower(nn.Module):
     """Query and document towers (encoders.py:158-224)."""
 
@@ -131,10 +145,12 @@ class TwoTower(nn.Module):
 
     def _forward_fused(self, inputs: list[torch.Tensor]) -> list[torch.Tensor]:
         """One bag launch over all sequences of the step, then the towers' heads."""
-        L = max(t.shape[1] for t in inputs)
-        ids = [t if t.shape[1] == L else F.pad(t, (0, L - t.shape[1])) for t in inputs]
-        dtype = torch.int64 if any(t.dtype == torch.int64 for t in ids) else ids[0].dtype
-        all_ids = torch.cat([t.to(dtype) for t in ids], dim=0)
+        all_ids = _packed_ids(inputs)
+        if all_ids is None:
+            L = max(t.shape[1] for t in inputs)
+            ids = [t if t.shape[1] == L else F.pad(t, (0, L - t.shape[1])) for t in inputs]
+            dtype = torch.int64 if any(t.dtype == torch.int64 for t in ids) else ids[0].dtype
+            all_ids = torch.cat([t.to(dtype) for t in ids], dim=0)
         pooled = pool_mean(self.query_tower.embedding, all_ids)
         sizes = [t.shape[0] for t in inputs]
         nq = sizes[0]

@@ -234,7 +234,7 @@ class TowerFF(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2):
         require_gpu(x)
-        h = torch.relu(torch.addmm(b1, x, W1.t()))
+        h = torch._addmm_activation(b1, x, W1.t())  # bias + ReLU in the hipBLASLt epilogue
         y = torch.addmm(b2, h, W2.t())
         ctx.save_for_backward(x, h, W1, W2)
         return y

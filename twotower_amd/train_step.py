@@ -30,16 +30,21 @@ class TrainStep:
             raise ValueError("TrainStep(graph=True) needs an optimizer built with capturable=True")
         self._eager_left = max(1, int(eager_steps))  # >= 1: lazy library/workspace set-up happens eagerly
         self._graphs: dict[tuple, tuple] = {}
+        self._seed: dict[torch.device, torch.Tensor] = {}  # d(loss) seed of backward, kept on device
 
     def eager(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
         q, p, n = self.model(queries, positive_docs, negative_docs)
         loss = self.loss_fn(q, p, n)
         self.optimizer.zero_grad(set_to_none=True)
+        # backward seeded with the (1/world pre-scaled) unit gradient from a resident tensor:
+        # no fill / scale kernels per step
+        seed = self._seed.get(loss.device)
+        if seed is None:
+            scale = self.sync.loss_scale() if self.sync is not None else 1.0
+            seed = self._seed[loss.device] = torch.full((), scale, dtype=loss.dtype, device=loss.device)
+        loss.backward(seed)
         if self.sync is not None:
-            (loss * self.sync.loss_scale()).backward()
             self.sync.sync()
-        else:
-            loss.backward()
         self.optimizer.step()
         return loss.detach()
 
@@ -54,16 +59,37 @@ class TrainStep:
                 self._eager_left -= 1
                 return self.eager(*inputs)
             hit = self._graphs[key] = self._capture(inputs)
-        graph, static_in, static_loss = hit
-        for dst, src in zip(static_in, inputs):
-            dst.copy_(src)
+        graph, static_all, static_loss = hit
+        if all(t.shape[1:] == inputs[0].shape[1:] and t.dtype == inputs[0].dtype for t in inputs):
+            torch.cat(inputs, 0, out=static_all)  # one copy into the packed static buffer
+        else:
+            for dst, src in zip(_views(static_all, inputs), inputs):
+                dst.copy_(src)
         graph.replay()
         return static_loss
 
     def _capture(self, inputs):
-        static_in = tuple(t.clone() for t in inputs)
+        # the static inputs are consecutive row blocks of one buffer, so the fused TwoTower
+        # forward uses them in place (no concatenation inside the step)
+        static_all = _packed_like(inputs)
+        static_in = tuple(_views(static_all, inputs))
+        for dst, src in zip(static_in, inputs):
+            dst.copy_(src)
         graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
         with torch.cuda.graph(graph):
             static_loss = self.eager(*static_in)
-        return graph, static_in, static_loss
+        return graph, static_all, static_loss
+
+
+def _packed_like(inputs):
+    if all(t.shape[1:] == inputs[0].shape[1:] and t.dtype == inputs[0].dtype for t in inputs):
+        return torch.empty((sum(t.shape[0] for t in inputs),) + tuple(inputs[0].shape[1:]), dtype=inputs[0].dtype,
+                           device=inputs[0].device)
+    return [t.clone() for t in inputs]
+
+
+def _views(static_all, inputs):
+    if isinstance(static_all, list):
+        return static_all
+    return torch.split(static_all, [t.shape[0] for t in inputs], 0)
