@@ -170,7 +170,9 @@ int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t 
  * ~16 mantissa bits, at 1.5x the MFMA work; the q/d rounding to bf16 still dominates the error
  * against fp32 inputs: both bf16 forms land ~3-4e-3 from the fp32 reference's gradients at C3).
  * fwd (want_grad != 0) also leaves dq_unscaled = sum_j P_ij d~_j - d~_label (B x H) so the
- * backward needs only the dD pass.  ws must stay untouched between fwd and bwd. */
+ * backward needs only the dD pass.  ws must stay untouched between fwd and bwd: it carries the
+ * bf16 operands, the pad rows and lse in log2 units, which the backward engine reads (the lse
+ * argument of tt_inbatch_bwd is the same quantity, validated but not re-read). */
 size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype);
 int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
                    float inv_tau, int64_t label_off, int want_grad,

@@ -1,0 +1,24 @@
+"""Summarise tools/pmc_scorer.sh output: per scorer kernel, average duration and counter values."""
+import csv, glob, sys, collections, re
+out = sys.argv[1]
+ks = list(csv.DictReader(open(glob.glob(f"{out}/ks/**/*kernel_stats.csv", recursive=True)[0])))
+for r in ks:
+    n = re.sub(r"\(.*", "", r["Name"].replace("tt::(anonymous namespace)::", "").replace("void ", ""))[:60]
+    print(f"{n:62s} calls {r['Calls']:>4s} avg {float(r['AverageNs'])/1e3:8.1f} us")
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "score_" in r["Kernel_Name"]:
+            k = "fwd" if "Li0E" in r["Kernel_Name"] or "<0," in r["Kernel_Name"] else "bwd"
+            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in vals.items():
+    a = {c: sum(v) / len(v) for c, v in d.items()}
+    print(k, {c: f"{v:.3g}" for c, v in sorted(a.items())})
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in a and "GRBM_GUI_ACTIVE" in a:
+        # MFMA busy cycles summed over SIMDs vs (GUI_ACTIVE/8 XCDs) x 1024 SIMDs
+        print(f"  MFMA util {a['SQ_VALU_MFMA_BUSY_CYCLES'] / (a['GRBM_GUI_ACTIVE'] / 8 * 1024):.3f}")
+    if "SQ_LDS_BANK_CONFLICT" in a:
+        print(f"  LDS conflict frac {a['SQ_LDS_BANK_CONFLICT'] / max(a['SQ_LDS_IDX_ACTIVE'], 1):.3f}")
+    if "SQ_WAVE_CYCLES" in a:
+        w = a["SQ_WAVE_CYCLES"]
+        print(f"  wait_any {a['SQ_WAIT_ANY']/w:.3f} wait_inst {a['SQ_WAIT_INST_ANY']/w:.3f} active {a['SQ_ACTIVE_INST_ANY']/w:.3f}")

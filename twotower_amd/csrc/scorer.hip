@@ -58,7 +58,9 @@ struct Tile {
   static constexpr int STAGE_B = BJ * ROWB;
   static constexpr int NI = STAGE_B / 1024 / NW;  // glds wave-instructions per wave per stage
   static_assert(NI * 1024 * NW == STAGE_B, "stage must be a whole number of 1 KiB pieces per wave");
-  static constexpr int LDS_BYTES = 2 * STAGE_B + 2 * 64 * 4;  // two stages + two 64-float lse rows
+  static constexpr int NSTAGE = sizeof(ET) == 2 ? 3 : 2;  // bf16: triple-buffered (see the engine)
+  static constexpr int LSE_OFF = NSTAGE * STAGE_B;
+  static constexpr int LDS_BYTES = NSTAGE * STAGE_B + NSTAGE * 64 * 4;  // stages + one 64-float lse row each
   // Chunk XOR of a row.  bf16 rows of >= 256 B use the dual-use swizzle (cdna_hip_programming.md
   // T10 (b)): bits 0-1 of the row go to chunk bits 2-3 and bits 2-3 to chunk bits 0-1, so both
   // the 16-row ds_read_b128 operand reads and the 4-row x 64-B transposed reads of a 32-lane half
@@ -83,6 +85,20 @@ __device__ __forceinline__ void glds_dword(const void* gsrc, unsigned lds_base) 
                : "memory");  // m0 is reserved (no live compiler value: no other LDS-DMA here)
 }
 __device__ __forceinline__ void drain_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// max_j |d_j| from the per-block maxima (every lane of the calling wave gets it).
+__device__ __forceinline__ float fold_dmax(const float* __restrict__ part, int n) {
+  float m = 0.f;
+  for (int i = lane_id(); i < n; i += kWave) m = fmaxf(m, part[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  return m;
+}
+
+// Column shift for the forward: an upper bound of row i's logits in log2 units,
+// |q~_i . d~_j| * c2 <= c2 * |q_i| * max_j |d_j| * (1 + 2^-6) (bf16 rounding slack included).
+// Computed where it is used (engine and combine) from the same floats, so both agree exactly.
+__device__ __forceinline__ float col_shift(float c2, float qn, float dmax) { return fabsf(c2) * qn * dmax * 1.015625f; }
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const lds_char_t*)p;  // 32-bit LDS byte address
@@ -110,7 +126,7 @@ __device__ __forceinline__ void stage_tile(char* smem, int buf, const ET* __rest
     if (wid == 0) {
       const int64_t g = r0 + lane;
       const float* src = (g < row_end) ? lse2_rows + g : reinterpret_cast<const float*>(pad + kPadBytes - 16);
-      glds_dword(src, __builtin_amdgcn_readfirstlane(lds_addr(smem) + 2 * T::STAGE_B + buf * 256));
+      glds_dword(src, __builtin_amdgcn_readfirstlane(lds_addr(smem) + T::LSE_OFF + buf * 256));
     }
   }
 }
@@ -220,10 +236,100 @@ __device__ __forceinline__ void acc_chain(const lds_char_t* tile, int jt, int la
   }
 }
 
+// S chain of the next X tile fused, step by step, with the map of the current one: each step is
+// one MFMA, the operand read for the step four ahead, and the exp (+ bf16 pack) of 16/NK
+// elements of the current tile, fenced by sched_barrier(0) so the compiler keeps that interleave
+// (at one wave per SIMD nothing else hides a clump of transcendentals or an unprefetched read).
+template <int MODE, bool PRECISE, int H>
+__device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16],
+                                              const f32x16& xa, float c2, float shift, const lds_f32x4_t* lse4,
+                                              float& l_run, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
+  using T = Tile<__bf16, H>;
+  constexpr int NK = H / 16;
+  constexpr int EPS = 16 / NK;  // map elements per step
+  const int rowb = row * T::ROWB, x = T::swz(row);
+  float sub[16];
+  if constexpr (MODE == FWD) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) sub[v] = shift;
+  } else {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 l4 = lse4[2 * g4 + hh];  // lse2 of rows 8*g4 + 4*hh + u
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sub[4 * g4 + u] = l4[u];
+    }
+  }
+  f32x16 acc = f32x16{};
+  bf16x8 a[4];
+#pragma unroll
+  for (int k = 0; k < 4 && k < NK; ++k)
+    a[k] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * k + hh) ^ x) << 4));
+  float e[16];
+  float ls = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
+    if (kk + 4 < NK)
+      a[kk & 3] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * (kk + 4) + hh) ^ x) << 4));
+#pragma unroll
+    for (int u = 0; u < EPS; ++u) {
+      const int v = kk * EPS + u;
+      e[v] = __builtin_amdgcn_exp2f(xa[v] * c2 - sub[v]);
+      asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
+      if constexpr (MODE == FWD) ls += e[v];
+      if (v & 1) {
+#pragma unroll
+        for (int w = v - 1; w <= v; ++w) {
+          const __bf16 h = (__bf16)e[w];
+          bh[w >> 3][w & 7] = h;
+          if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  l_run += ls;
+  return acc;
+}
+
+// Acc chain with the transposed operand reads of each step issued two steps ahead.
+template <bool PRECISE, int H>
+__device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, int lane, const bf16x8 (&bh)[2],
+                                                    const bf16x8 (&bl)[2], f32x16 (&acc)[H / 32]) {
+  using T = Tile<__bf16, H>;
+  constexpr int NHT = H / 32;
+  constexpr int NS = 2 * NHT;  // steps: (s2, ht)
+  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
+  const int r0 = jt * 32 + 4 * (tg >> 1) + tq;
+  const int x0 = T::swz(r0), x1 = T::swz(r0 + 8);
+  const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
+  auto load = [&](int st) {
+    const int s2 = st / NHT, ht = st % NHT, ch = 4 * ht + cbase;
+    const int rb0 = (r0 + 16 * s2) * T::ROWB + bo, rb1 = (r0 + 16 * s2 + 8) * T::ROWB + bo;
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb0 + ((ch ^ x0) << 4)));
+    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb1 + ((ch ^ x1) << 4)));
+    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  };
+  bf16x8 op[3];
+  op[0] = load(0);
+  if (NS > 1) op[1] = load(1);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    if (st + 2 < NS) op[(st + 2) % 3] = load(st + 2);
+    const int s2 = st / NHT, ht = st % NHT;
+    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], bh[s2], acc[ht], 0, 0, 0);
+    if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], bl[s2], acc[ht], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int MODE, bool PRECISE, int H>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
-    int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ col_shift,
+    int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
+    const float* __restrict__ dmax_part, int n_dmax,
     const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part) {
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
@@ -240,9 +346,14 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const int64_t row_begin = (int64_t)split * rows_per_split;
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
-  const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
+  const float dmax = MODE == FWD ? fold_dmax(dmax_part, n_dmax) : 0.f;  // wave-uniform call
+  const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
 
+  // Three LDS stages: stage t+2 is filled while stage t is consumed and stage t+1 waits, so the
+  // first S chain of stage t+1 can run beside the map of stage t's last tile (one barrier per
+  // stage, placed right before that S chain).
   if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
+  if (ntiles > 1) stage_tile<__bf16, H, MODE>(smem, 1, R, row_begin + T::BJ, row_end, lse2_rows, pad);
 
   bf16x8 cf[NK];
   {
@@ -262,27 +373,33 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   drain_dma();
   __syncthreads();
 
+  f32x16 xa = ntiles > 0 ? s_chain<H>(lds, r32, hh, cf) : f32x16{};
+  int buf = 0;
   for (int64_t t = 0; t < ntiles; ++t) {
-    const int buf = (int)(t & 1);
-    if (t + 1 < ntiles)
-      stage_tile<__bf16, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
-    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + 2 * T::STAGE_B + buf * 256);
-    f32x16 xa = s_chain<H>(tile, r32, hh, cf);
+    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
+    const int nbuf = buf == 2 ? 0 : buf + 1;
 #pragma unroll
     for (int jt = 0; jt < NJ; ++jt) {
-      f32x16 xb = f32x16{};
-      if (jt + 1 < NJ) xb = s_chain<H>(tile, (jt + 1) * 32 + r32, hh, cf);
-      float e[16];
-      map_tile<MODE>(xa, e, c2, shift, lse4 + jt * 8, hh, l_run);
+      f32x16 xb;
       bf16x8 bh[2], bl[2];
-      pack_g<PRECISE>(e, bh, bl);
-      __builtin_amdgcn_sched_barrier(0);  // [S(next) || map] ; [Acc chain]
-      acc_chain<PRECISE, H>(tile, jt, lane, bh, bl, acc);
+      if (jt + 1 < NJ) {
+        xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32 + r32, hh, cf, xa, c2, shift, lse4 + jt * 8, l_run,
+                                           bh, bl);
+      } else {
+        drain_dma();      // stage t+1 landed (the only fill in flight)
+        __syncthreads();  // ... in every wave, and every wave is past stage t-1
+        if (t + 2 < ntiles)
+          stage_tile<__bf16, H, MODE>(smem, nbuf == 2 ? 0 : nbuf + 1, R, row_begin + (t + 2) * T::BJ, row_end,
+                                      lse2_rows, pad);
+        // (after the last stage this scores a stale stage; the result is dropped)
+        xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, r32, hh, cf, xa, c2, shift, lse4 + jt * 8, l_run,
+                                           bh, bl);
+      }
+      acc_chain_pipelined<PRECISE, H>(tile, jt, lane, bh, bl, acc);
       xa = xb;
     }
-    drain_dma();  // next stage landed (issued a whole stage of MFMAs ago)
-    __syncthreads();
+    buf = nbuf;
   }
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 }
@@ -294,7 +411,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 template <int MODE, int H>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
     const float* __restrict__ R, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
-    int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ col_shift,
+    int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
+    const float* __restrict__ dmax_part, int n_dmax,
     const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part) {
   using T = Tile<float, H>;
   constexpr int NB = H / 8;
@@ -310,7 +428,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
   const int64_t row_begin = (int64_t)split * rows_per_split;
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
-  const float shift = (MODE == FWD && my_col < nC) ? col_shift[my_col] : 0.f;
+  const float dmax = MODE == FWD ? fold_dmax(dmax_part, n_dmax) : 0.f;  // wave-uniform call
+  const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
 
   if (ntiles > 0) stage_tile<float, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
 
@@ -338,7 +457,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
     if (t + 1 < ntiles)
       stage_tile<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
-    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + 2 * T::STAGE_B + buf * 256);
+    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
     f32x16 x = f32x16{};
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -366,17 +485,17 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
-// Operand prep: optional fp32 -> bf16 (RNE) copy, row L2 norm, and the max norm over rows.
-// Grid-stride over rows, one wave per row; the max is folded per wave, then per block in LDS,
-// then ONE atomicMax per block (norms >= 0 so float order == unsigned bit order).  A single
-// address hit by every row serialises at the memory side (MI355X_MICROARCH: 14x slower).
-__global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ x, int64_t rows, int H,
-                                                        __bf16* __restrict__ xb, float* __restrict__ norms,
-                                                        unsigned* __restrict__ max_bits) {
-  __shared__ float wmax[4];
+// Operand prep, one launch for both matrices: blocks [0, gq) take the q rows, blocks [gq, grid)
+// the d rows (grid-stride, one wave per row).  Optional fp32 -> bf16 (RNE) copy, the row L2
+// norms of q, and for d one max norm per block (dmax_part[b]; readers fold the <= kMaxPrepBlocks
+// values themselves: no zero-initialised accumulator, no atomics).  Block 0 also writes the pad
+// rows (kPadBytes - 16 zero bytes, then +inf for the backward lse2).
+constexpr int kMaxPrepBlocks = 512;
+
+__device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t rows, int H, __bf16* __restrict__ xb,
+                                          float* __restrict__ norms, int64_t b0, int64_t nb, float& mx) {
   const int lane = lane_id(), wid = threadIdx.x >> 6;
-  float mx = 0.f;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + wid; r < rows; r += (int64_t)gridDim.x * 4) {
+  for (int64_t r = b0 * 4 + wid; r < rows; r += nb * 4) {
     const f32x4* src = reinterpret_cast<const f32x4*>(x + r * H);
     float ss = 0.f;
     for (int c = lane; c < H / 4; c += kWave) {
@@ -389,40 +508,31 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict_
     if (lane == 0 && norms) norms[r] = n;
     mx = fmaxf(mx, n);
   }
-  if (max_bits) {
-    if (lane == 0) wmax[wid] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
-      atomicMax(max_bits, __float_as_uint(m));
-    }
-  }
 }
 
-// Pad source for rows past the end: kPadBytes - 16 zero bytes, then +inf (backward lse2).
-__device__ __forceinline__ void write_pad(char* pad) {
+__global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ q, int64_t B,
+                                                      const float* __restrict__ d, int64_t M, int H, int gq,
+                                                      __bf16* __restrict__ qb, __bf16* __restrict__ db,
+                                                      float* __restrict__ qnorm, float* __restrict__ dmax_part,
+                                                      char* __restrict__ pad) {
+  __shared__ float wmax[4];
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
   }
+  float mx = 0.f;
+  if ((int)blockIdx.x < gq) {
+    prep_rows(q, B, H, qb, qnorm, blockIdx.x, gq, mx);
+    return;
+  }
+  const int b = blockIdx.x - gq, gd = gridDim.x - gq;
+  prep_rows(d, M, H, db, nullptr, b, gd, mx);
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  if (lane == 0) wmax[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) dmax_part[b] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
 }
 
-// Column shift for the forward: an upper bound of row i's logits in log2 units,
-// |q~_i . d~_j| * c2 <= c2 * |q_i| * max_j |d_j| * (1 + 2^-6) (bf16 rounding slack included).
-__global__ __launch_bounds__(256) void shift_kernel(const float* __restrict__ qn, const unsigned* __restrict__ dmax_bits,
-                                                    int64_t B, float c2, float* __restrict__ shift, char* pad) {
-  write_pad(pad);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= B) return;
-  shift[i] = fabsf(c2) * qn[i] * __uint_as_float(*dmax_bits) * 1.015625f;
-}
-
-__global__ __launch_bounds__(256) void to_log2_kernel(const float* __restrict__ lse, int64_t n, float* __restrict__ lse2,
-                                                      char* pad) {
-  write_pad(pad);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) lse2[i] = lse[i] * kLog2e;
-}
 
 // Merge forward split partials, one wave per query row:
 //   l_i    = sum_s l_s,i - n_pad 2^-shift_i             (pad rows: X = 0 exactly)
@@ -432,18 +542,20 @@ __global__ __launch_bounds__(256) void to_log2_kernel(const float* __restrict__ 
 // Rows whose bound sits so far above the true max that l underflows (l < 2^-100) report NaN.
 template <typename DT>
 __global__ __launch_bounds__(256) void fwd_combine_kernel(
-    int64_t B, int H, int S, int n_pad, const float* __restrict__ shift, const float* __restrict__ l_part,
-    const float* __restrict__ acc_part, float inv_tau, int64_t label_off, const DT* __restrict__ Qmat,
-    const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ loss_rows, float* __restrict__ dqu) {
+    int64_t B, int H, int S, int n_pad, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part,
+    int n_dmax, const float* __restrict__ l_part, const float* __restrict__ acc_part, float inv_tau, int64_t label_off,
+    const DT* __restrict__ Qmat, const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2,
+    float* __restrict__ loss_rows, float* __restrict__ dqu) {
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= B) return;
   const int lane = lane_id();
-  const float sh = shift[i];
+  const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
   float l = 0.f;
   for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
   l -= (float)n_pad * __builtin_amdgcn_exp2f(-sh);
   const bool ok = l >= 7.888609052210118e-31f;  // 2^-100
-  const float lse_i = ok ? (sh + log2f(l)) * kLn2 : NAN;
+  const float lse2_i = ok ? sh + log2f(l) : NAN;  // log2 units, for the backward engine
+  const float lse_i = lse2_i * kLn2;
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
   float dot = 0.f;
@@ -451,6 +563,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   dot = wave_sum(dot);
   if (lane == 0) {
     lse[i] = lse_i;
+    lse2[i] = lse2_i;
     loss_rows[i] = lse_i - dot * inv_tau;
   }
   if (dqu) {
@@ -499,10 +612,13 @@ struct Plan {
   int n_pad;  // zero rows processed past the end of the last split
 };
 
-Plan plan_for(int64_t nR, int64_t nC, int BJ) {
+// Split the streamed rows so the grid is one round of resident workgroups (256 CUs x wg_per_cu):
+// a second round would only add prologues/epilogues and twice the split partials.
+Plan plan_for(int64_t nR, int64_t nC, int BJ, int wg_per_cu) {
   const int64_t ncb = (nC + 32 * NW - 1) / (32 * NW);
   const int64_t row_tiles = (nR + BJ - 1) / BJ;
-  int64_t S = (512 + ncb - 1) / ncb;  // aim for ~2 workgroups per CU
+  const int64_t target = 256 * wg_per_cu;
+  int64_t S = (target + ncb - 1) / ncb;
   if (S > 8) S = 8;
   if (S > row_tiles) S = row_tiles;
   if (S < 1) S = 1;
@@ -516,13 +632,15 @@ Plan plan_for(int64_t nR, int64_t nC, int BJ) {
 
 int bj_for(int dtype) { return dtype == TT_F32 ? Tile<float, 64>::BJ : Tile<__bf16, 64>::BJ; }
 
+// resident workgroups per CU (register-limited: launch_bounds min-blocks of the engines)
+int wg_per_cu(int H) { return H <= 128 ? 2 : 1; }
+
 struct Ws {
   __bf16* Qb;
   __bf16* Db;
   float* qnorm;
-  float* shift;
   float* lse2;
-  unsigned* dmax;
+  float* dmax_part;
   char* pad;
   float* l_part;
   float* acc_part;
@@ -533,7 +651,7 @@ struct Ws {
 // everything else is scratch reused by both passes.
 Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const int BJ = bj_for(dtype);
-  const Plan pf = plan_for(M, B, BJ), pd = plan_for(B, M, BJ);
+  const Plan pf = plan_for(M, B, BJ, wg_per_cu(H)), pd = plan_for(B, M, BJ, wg_per_cu(H));
   const bool bf = dtype != TT_F32;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -542,7 +660,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     return o;
   };
   const size_t oq = take(bf ? (size_t)B * H * 2 : 0), od = take(bf ? (size_t)M * H * 2 : 0);
-  const size_t oqn = take((size_t)B * 4), osh = take((size_t)B * 4), ol2 = take((size_t)B * 4), omx = take(16);
+  const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)B * 4), omx = take(kMaxPrepBlocks * 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   const size_t oa = take(parts);
@@ -552,9 +670,8 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.Qb = reinterpret_cast<__bf16*>(b + oq);
     w.Db = reinterpret_cast<__bf16*>(b + od);
     w.qnorm = reinterpret_cast<float*>(b + oqn);
-    w.shift = reinterpret_cast<float*>(b + osh);
     w.lse2 = reinterpret_cast<float*>(b + ol2);
-    w.dmax = reinterpret_cast<unsigned*>(b + omx);
+    w.dmax_part = reinterpret_cast<float*>(b + omx);
     w.pad = b + opad;
     w.l_part = reinterpret_cast<float*>(b + ol);
     w.acc_part = reinterpret_cast<float*>(b + oa);
@@ -565,19 +682,19 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
 
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
-                  const float* lse2, const Ws& w, hipStream_t s) {
+                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
   if (dtype == TT_F32) {
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-        w.shift, w.pad, w.acc_part, w.l_part);
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
   } else if (dtype == TT_BF16_SPLIT) {
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-        w.shift, w.pad, w.acc_part, w.l_part);
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
   } else {
     score_bf16_kernel<MODE, false, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-        w.shift, w.pad, w.acc_part, w.l_part);
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
   }
   TT_LAUNCH_CHECK(MODE == FWD ? "score_fwd" : "score_dd");
   return TT_OK;
@@ -585,12 +702,12 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
 
 template <int MODE>
 int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
-                    float c2, const float* lse2, const Ws& w, hipStream_t s) {
+                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
   switch (H) {
-    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
-    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
-    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
-    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, s);
+    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
+    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
+    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
+    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
 }
@@ -629,26 +746,26 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Plan p = plan_for(M, B, bj_for(dtype));
+  const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   const bool bf = dtype != TT_F32;
-  TT_HIP(hipMemsetAsync(w.dmax, 0, 16, s), "memset dmax");
-  auto prep_grid = [](int64_t rows) { return dim3((unsigned)std::min<int64_t>((rows + 3) / 4, 1024)); };
-  prep_rows_kernel<<<prep_grid(B), dim3(256), 0, s>>>(q, B, H, bf ? w.Qb : nullptr, w.qnorm, nullptr);
-  prep_rows_kernel<<<prep_grid(M), dim3(256), 0, s>>>(d, M, H, bf ? w.Db : nullptr, nullptr, w.dmax);
-  shift_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(w.qnorm, w.dmax, B, c2, w.shift, w.pad);
+  const int gq = (int)std::min<int64_t>((B + 3) / 4, 512);
+  const int gd = (int)std::min<int64_t>((M + 3) / 4, kMaxPrepBlocks);
+  prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
+                                                                 bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad);
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
-  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, s))) return rc;
+  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, gd, s))) return rc;
   const dim3 grid((unsigned)((B + 3) / 4)), block(256);
   float* dqu = want_grad ? dq_unscaled : nullptr;
   if (!bf)
-    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, w.shift, w.l_part, w.acc_part, inv_tau,
-                                                    label_off, q, d, lse, loss_rows, dqu);
+    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, w.qnorm, w.dmax_part, gd, w.l_part,
+                                                    w.acc_part, inv_tau, label_off, q, d, lse, w.lse2, loss_rows, dqu);
   else
-    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, w.shift, w.l_part, w.acc_part, inv_tau,
-                                                     label_off, w.Qb, w.Db, lse, loss_rows, dqu);
+    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, w.qnorm, w.dmax_part, gd, w.l_part,
+                                                     w.acc_part, inv_tau, label_off, w.Qb, w.Db, lse, w.lse2,
+                                                     loss_rows, dqu);
   TT_LAUNCH_CHECK("score_fwd_combine");
   return launch_mean(loss_rows, B, loss, s);
 }
@@ -662,14 +779,13 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Plan p = plan_for(B, M, bj_for(dtype));
+  const Plan p = plan_for(B, M, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   const bool bf = dtype != TT_F32;
-  to_log2_kernel<<<dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s>>>(lse, B, w.lse2, w.pad);
-  TT_LAUNCH_CHECK("score_lse2");
+  // lse in log2 units (ws.lse2) and the pad rows were left in the workspace by the forward
   const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
   const void* Cm = bf ? (const void*)w.Db : (const void*)d;
-  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, w.lse2, w, s))) return rc;
+  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, w.lse2, w, 0, s))) return rc;
   const int64_t rows = std::max(B, M);
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   if (!bf)
