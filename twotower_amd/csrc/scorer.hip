@@ -265,31 +265,54 @@ __device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int row, i
 #pragma unroll
   for (int k = 0; k < 4 && k < NK; ++k)
     a[k] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * k + hh) ^ x) << 4));
+  // the map works on element pairs: v_pk_fma_f32 / v_pk_add_f32 do two lanes' worth each
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const f32x2 c2v = {c2, c2};
   float e[16];
-  float ls = 0.f;
+  f32x2 ls = {0.f, 0.f}, yv = {0.f, 0.f};
+  auto pack2 = [&](int v) {
+#pragma unroll
+    for (int w = v; w <= v + 1; ++w) {
+      const __bf16 h = (__bf16)e[w];
+      bh[w >> 3][w & 7] = h;
+      if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
+    }
+  };
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
     if (kk + 4 < NK)
       a[kk & 3] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * (kk + 4) + hh) ^ x) << 4));
+    if constexpr (EPS == 1) {
+      // one exp per step; the pair's packed fma on its even step, packed sum + bf16 pack on the odd
+      const int v = kk & ~1;
+      if ((kk & 1) == 0) {
+        const f32x2 xv = {xa[v], xa[v + 1]}, sv = {sub[v], sub[v + 1]};
+        yv = xv * c2v - sv;
+        e[v] = __builtin_amdgcn_exp2f(yv[0]);
+        asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
+      } else {
+        e[v + 1] = __builtin_amdgcn_exp2f(yv[1]);
+        asm volatile("" : "+v"(e[v + 1]));
+        if constexpr (MODE == FWD) ls += f32x2{e[v], e[v + 1]};
+        pack2(v);
+      }
+    } else {
 #pragma unroll
-    for (int u = 0; u < EPS; ++u) {
-      const int v = kk * EPS + u;
-      e[v] = __builtin_amdgcn_exp2f(xa[v] * c2 - sub[v]);
-      asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
-      if constexpr (MODE == FWD) ls += e[v];
-      if (v & 1) {
-#pragma unroll
-        for (int w = v - 1; w <= v; ++w) {
-          const __bf16 h = (__bf16)e[w];
-          bh[w >> 3][w & 7] = h;
-          if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
-        }
+      for (int u = 0; u < EPS / 2; ++u) {
+        const int v = kk * EPS + 2 * u;
+        const f32x2 xv = {xa[v], xa[v + 1]}, sv = {sub[v], sub[v + 1]};
+        const f32x2 y = xv * c2v - sv;
+        e[v] = __builtin_amdgcn_exp2f(y[0]);
+        e[v + 1] = __builtin_amdgcn_exp2f(y[1]);
+        asm volatile("" : "+v"(e[v]), "+v"(e[v + 1]));
+        if constexpr (MODE == FWD) ls += f32x2{e[v], e[v + 1]};
+        pack2(v);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  l_run += ls;
+  l_run += ls[0] + ls[1];
   return acc;
 }
 
@@ -351,7 +374,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 
   // Three LDS stages: stage t+2 is filled while stage t is consumed and stage t+1 waits, so the
   // first S chain of stage t+1 can run beside the map of stage t's last tile (one barrier per
-  // stage, placed right before that S chain).
+  // stage, placed right before that S chain).  (A fourth stage filled one stage earlier measured
+  // no faster: the fills are not what the waves wait on.)
   if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
   if (ntiles > 1) stage_tile<__bf16, H, MODE>(smem, 1, R, row_begin + T::BJ, row_end, lse2_rows, pad);
 
