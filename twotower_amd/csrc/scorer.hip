@@ -84,6 +84,16 @@ __device__ __forceinline__ void glds_dword(const void* gsrc, unsigned lds_base) 
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(gsrc), "s"(lds_base)
                : "memory");  // m0 is reserved (no live compiler value: no other LDS-DMA here)
 }
+// saddr forms: wave-uniform 64-bit base in SGPRs + a 32-bit per-lane byte offset (no per-lane
+// 64-bit address arithmetic per load).
+__device__ __forceinline__ void glds_dwordx4_s(unsigned voff, const void* sbase, unsigned lds_base) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base)
+               : "memory");
+}
+__device__ __forceinline__ void glds_dword_s(unsigned voff, const void* sbase, unsigned lds_base) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_base)
+               : "memory");
+}
 __device__ __forceinline__ void drain_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // max_j |d_j| from the per-block maxima (every lane of the calling wave gets it).
@@ -128,6 +138,50 @@ __device__ __forceinline__ void stage_tile(char* smem, int buf, const ET* __rest
       const float* src = (g < row_end) ? lse2_rows + g : reinterpret_cast<const float*>(pad + kPadBytes - 16);
       glds_dword(src, __builtin_amdgcn_readfirstlane(lds_addr(smem) + T::LSE_OFF + buf * 256));
     }
+  }
+}
+
+// Per-lane source byte offsets of the NI pieces of a stage, relative to the stage's first row:
+// the same for every stage, so they are computed once per kernel.
+template <typename ET, int H>
+struct FillOffs {
+  unsigned v[Tile<ET, H>::NI];
+};
+
+template <typename ET, int H>
+__device__ __forceinline__ FillOffs<ET, H> make_fill_offs() {
+  using T = Tile<ET, H>;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  FillOffs<ET, H> o;
+#pragma unroll
+  for (int c = 0; c < T::NI; ++c) {
+    const int p = (c * NW + wid) * 1024 + lane * 16;
+    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
+    o.v[c] = (unsigned)(row * T::ROWB + ((slot ^ T::swz(row)) << 4));
+  }
+  return o;
+}
+
+// Stage fill for a stage whose BJ rows all exist: scalar stage base + precomputed lane offsets.
+// A stage that reaches past row_end takes stage_tile (per-lane pad redirection).
+template <typename ET, int H, int MODE>
+__device__ __forceinline__ void stage_fill(char* smem, int buf, const ET* __restrict__ R, int64_t r0, int64_t row_end,
+                                           const float* __restrict__ lse2_rows, const char* __restrict__ pad,
+                                           const FillOffs<ET, H>& fo) {
+  using T = Tile<ET, H>;
+  if (r0 + T::BJ > row_end) {
+    stage_tile<ET, H, MODE>(smem, buf, R, r0, row_end, lse2_rows, pad);
+    return;
+  }
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const unsigned base = lds_addr(smem) + buf * T::STAGE_B;
+  const char* src = reinterpret_cast<const char*>(R + r0 * H);
+#pragma unroll
+  for (int c = 0; c < T::NI; ++c) glds_dwordx4_s(fo.v[c], src, __builtin_amdgcn_readfirstlane(base + (c * NW + wid) * 1024));
+  if constexpr (MODE == DD) {
+    if (wid == 0)
+      glds_dword_s((unsigned)lane * 4, lse2_rows + r0,
+                   __builtin_amdgcn_readfirstlane(lds_addr(smem) + T::LSE_OFF + buf * 256));
   }
 }
 
@@ -376,8 +430,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   // first S chain of stage t+1 can run beside the map of stage t's last tile (one barrier per
   // stage, placed right before that S chain).  (A fourth stage filled one stage earlier measured
   // no faster: the fills are not what the waves wait on.)
-  if (ntiles > 0) stage_tile<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
-  if (ntiles > 1) stage_tile<__bf16, H, MODE>(smem, 1, R, row_begin + T::BJ, row_end, lse2_rows, pad);
+  const FillOffs<__bf16, H> fo = make_fill_offs<__bf16, H>();
+  if (ntiles > 0) stage_fill<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad, fo);
+  if (ntiles > 1) stage_fill<__bf16, H, MODE>(smem, 1, R, row_begin + T::BJ, row_end, lse2_rows, pad, fo);
 
   bf16x8 cf[NK];
   {
@@ -414,8 +469,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
         drain_dma();      // stage t+1 landed (the only fill in flight)
         __syncthreads();  // ... in every wave, and every wave is past stage t-1
         if (t + 2 < ntiles)
-          stage_tile<__bf16, H, MODE>(smem, nbuf == 2 ? 0 : nbuf + 1, R, row_begin + (t + 2) * T::BJ, row_end,
-                                      lse2_rows, pad);
+          stage_fill<__bf16, H, MODE>(smem, nbuf == 2 ? 0 : nbuf + 1, R, row_begin + (t + 2) * T::BJ, row_end,
+                                      lse2_rows, pad, fo);
         // (after the last stage this scores a stale stage; the result is dropped)
         xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, r32, hh, cf, xa, c2, shift, lse4 + jt * 8, l_run,
                                            bh, bl);
@@ -455,7 +510,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
   const float dmax = MODE == FWD ? fold_dmax(dmax_part, n_dmax) : 0.f;  // wave-uniform call
   const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
 
-  if (ntiles > 0) stage_tile<float, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad);
+  const FillOffs<float, H> fo = make_fill_offs<float, H>();
+  if (ntiles > 0) stage_fill<float, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad, fo);
 
   f32x4 cf[NB];
   {
@@ -479,7 +535,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 1);
     if (t + 1 < ntiles)
-      stage_tile<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad);
+      stage_fill<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad, fo);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
     const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
     f32x16 x = f32x16{};
