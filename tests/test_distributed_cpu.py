@@ -163,3 +163,19 @@ def _grad_sync(rank):
 
 def test_grad_sync_mean():
     _run(_grad_sync)
+
+
+def _sync_modes(rank):
+    assert D.table_sync_mode("auto") == "gather"  # 2 ranks
+    assert D.table_sync_mode("shard") == "shard"
+    try:
+        D.table_sync_mode("bogus")
+    except ValueError:
+        pass
+    else:
+        raise AssertionError("bad mode accepted")
+
+
+def test_table_sync_mode_selection():
+    assert D.table_sync_mode("auto") == "local"  # no process group
+    _run(_sync_modes)

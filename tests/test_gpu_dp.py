@@ -3,9 +3,9 @@ put two ranks on one GPU; the round-end 8-GPU run uses RCCL with the same code),
 parameters after each step must equal a single process stepping on the global batch.
 
 The DP step: each rank pools/scores its half, the in-batch candidates are all-gathered with
-rank-offset labels, the loss is pre-scaled by 1/world, tower gradients are all-reduced, and
-the table gradient is reduce-scattered into row shards, updated by AdamW per shard and
-all-gathered.  Sum orders differ from the single process (two partial sums), so the bar is the
+rank-offset labels, the loss is pre-scaled by 1/world, tower gradients are all-reduced, and the
+table is updated either from the all-gathered factored gradient on every rank ("gather") or by
+reduce-scatter into row shards, AdamW per shard and all-gather ("shard").  Sum orders differ from the single process (two partial sums), so the bar is the
 fp32 1e-5 relative tolerance on the parameter change.  AdamW normalises every element's update,
 which turns rounding-level differences of near-cancelled gradients (|g| ~ eps) into O(lr)
 parameter differences; with eps = 1 and no decay the first update is -lr g / (|g| + 1), so the
@@ -31,7 +31,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _build(loss_name, world):
+def _build(loss_name, world, table_sync="auto"):
     import twotower_amd as tt
 
     torch.manual_seed(7)
@@ -39,7 +39,7 @@ def _build(loss_name, world):
     model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to("cuda:0")
     kw = {"temperature": 0.1, "cross_device_negatives": world > 1} if loss_name == "in_batch" else {"margin": 0.2}
     opt = tt.optim.AdamW(model.parameters(), lr=LR, eps=1.0, weight_decay=0.0, fused_tables=True, tables=[emb],
-                         capturable=True)
+                         capturable=True, table_sync=table_sync)
     return model, tt.TrainStep(model, tt.losses.build(loss_name, **kw), opt)
 
 
@@ -49,13 +49,13 @@ def _batch():
     return tt.data.synthetic_triplets(WORLD * B, L, V, seed=3, device="cuda:0")
 
 
-def _worker(rank, port, loss_name, q):
+def _worker(rank, port, loss_name, table_sync, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
         torch.cuda.set_device(0)
         if rank >= 0:
             dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-        model, step = _build(loss_name, WORLD if rank >= 0 else 1)
+        model, step = _build(loss_name, WORLD if rank >= 0 else 1, table_sync)
         init = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
         full = _batch()
         b = full if rank < 0 else tuple(t[rank * B:(rank + 1) * B] for t in full)
@@ -80,21 +80,22 @@ KEYS = {"table": "query_tower.embedding.embedding.weight", "W1": "query_tower.fe
         "b2": "query_tower.feed_forward.2.bias"}
 
 
-@pytest.mark.parametrize("loss_name", ["in_batch", "triplet"])
-def test_dp_step_equals_global_batch(loss_name):
+@pytest.mark.parametrize("loss_name,table_sync", [("in_batch", "gather"), ("in_batch", "shard"),
+                                                  ("triplet", "gather"), ("triplet", "shard")])
+def test_dp_step_equals_global_batch(loss_name, table_sync):
     """One step, eps 1, no decay: delta = -lr g / (|g| + 1), so g is recovered from the parameter
     change and compared with the float64 oracle on the global batch."""
     from oracle import reference_math as O
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, q))
+    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, table_sync, q))
     ref.start()
     _, r_loss, init, r_delta, ids = q.get(timeout=300)
     ref.join(timeout=60)
     assert init is not None, r_loss
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, table_sync, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in procs]

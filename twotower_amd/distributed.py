@@ -23,6 +23,25 @@ def is_active(group=None) -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
 
 
+def table_sync_mode(requested: str, group=None) -> str:
+    """How an embedding table's gradient crosses ranks:
+      "local"  -- one rank (no exchange);
+      "gather" -- all-gather the factored gradient (ids in the forward, d_pooled/denom after the
+                  backward: ~31 MB per rank at C3) and run the fused scatter + AdamW on every rank
+                  over all ranks' entries (replicated table and moments, no parameter exchange);
+      "shard"  -- reduce-scatter the dense table gradient by row range, AdamW on own rows,
+                  all-gather the rows (2 x 205 MB x (N-1)/N per rank at C3).
+    "auto": gather up to 4 ranks (its bytes grow with N; at N <= 4 a rank pair shares few xGMI
+    links, where the dense exchange is link-bound), shard beyond."""
+    if not is_active(group):
+        return "local"
+    if requested == "auto":
+        return "gather" if dist.get_world_size(group) <= 4 else "shard"
+    if requested not in ("gather", "shard"):
+        raise ValueError(f"table_sync must be 'auto', 'gather' or 'shard', got {requested!r}")
+    return requested
+
+
 def _is_gloo(group=None) -> bool:
     return dist.get_backend(group) == "gloo"
 

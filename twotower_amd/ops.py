@@ -82,17 +82,27 @@ class BagPlan:
 
     __slots__ = ("ids", "buf", "ready", "nseq", "L", "V", "E")
 
-    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None):
+    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None, gather_group=None):
+        """gather_group: data parallel with a replicated table update -- the plan covers the ids
+        of every rank (all-gathered here, on the side stream, rank-major)."""
         dev = ids.device
-        self.ids, self.V, self.E = ids, V, E
-        self.nseq, self.L = ids.shape
-        nbytes = _lib.lib().tt_bag_plan_ws_size(self.nseq, self.L, V, E)
-        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        self.V, self.E = V, E
         main = torch.cuda.current_stream(dev)
         side = _lib.side_stream(dev)
         side.wait_stream(main)
         pad = -1 if padding_idx is None else int(padding_idx)
         with torch.cuda.stream(side):
+            if gather_group is not None:
+                from .distributed import all_gather_rows
+
+                world = torch.distributed.get_world_size(gather_group)
+                ids_all = ids.new_empty((world * ids.shape[0],) + tuple(ids.shape[1:]))
+                all_gather_rows(ids_all, ids, gather_group)
+                ids = ids_all
+            self.ids = ids
+            self.nseq, self.L = ids.shape
+            nbytes = _lib.lib().tt_bag_plan_ws_size(self.nseq, self.L, V, E)
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
             call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, pad,
                  ptr(self.buf), self.buf.numel(), side.cuda_stream)
         if not torch.cuda.is_current_stream_capturing():
@@ -120,13 +130,15 @@ def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan:
 
 class DeferredTableGrad:
     """Table gradient kept in its factored form (ids, d_pooled, denom, plan) so a fused optimizer
-    can apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer."""
+    can apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer.
+    gather_group: data parallel, replicated table update (the plan covers every rank's ids)."""
 
-    __slots__ = ("parts", "padding_idx")
+    __slots__ = ("parts", "padding_idx", "gather_group")
 
-    def __init__(self, padding_idx: int | None = 0):
+    def __init__(self, padding_idx: int | None = 0, gather_group=None):
         self.parts: list[tuple] = []
         self.padding_idx = padding_idx
+        self.gather_group = gather_group
 
 
 class BagMeanPool(torch.autograd.Function):
@@ -143,7 +155,9 @@ class BagMeanPool(torch.autograd.Function):
         ctx.weight_ref = weight
         ctx.plan = None
         if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
-            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx)
+            deferred = getattr(weight, "_tt_deferred", None)
+            group = deferred.gather_group if deferred is not None else None
+            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
         return pooled
 
     @staticmethod

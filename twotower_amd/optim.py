@@ -26,7 +26,8 @@ from . import _lib, distributed, ops
 
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2,
-                 fused_tables: bool = False, tables=(), capturable: bool = False, group=None):
+                 fused_tables: bool = False, tables=(), capturable: bool = False, group=None,
+                 table_sync: str = "auto"):
         if lr < 0.0 or eps < 0.0 or weight_decay < 0.0:
             raise ValueError("invalid AdamW hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
@@ -42,9 +43,12 @@ class AdamW(torch.optim.Optimizer):
                 pad = getattr(inner, "padding_idx", 0) if inner is not None else 0
                 if id(w) not in ids:
                     raise ValueError("fused table is not among the optimizer's parameters")
-                w._tt_deferred = ops.DeferredTableGrad(pad)
+                mode = distributed.table_sync_mode(table_sync, group)
+                # (None is the "no exchange" sentinel there: name the default group explicitly)
+                gg = (group if group is not None else torch.distributed.group.WORLD) if mode == "gather" else None
+                w._tt_deferred = ops.DeferredTableGrad(pad, gather_group=gg)
                 self._tables.append(w)
-                if distributed.is_active(group):
+                if mode == "shard":
                     self._shards[id(w)] = distributed.ShardedRows(w, group)
 
     def release_tables(self) -> None:
@@ -110,6 +114,8 @@ class AdamW(torch.optim.Optimizer):
                 st["step"] += 1
                 ids, dp, den, plan = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
+                if deferred.gather_group is not None:
+                    ids, dp, den, plan = _gather_parts((ids, dp, den, plan), deferred.gather_group)
                 sh = self._shards.get(id(p))
                 if sh is not None:
                     g_shard = self._table_grad_shard(sh, dp, den, plan)
@@ -147,6 +153,8 @@ class AdamW(torch.optim.Optimizer):
                     dense.append((sh.rows(sh.storage()), g_shard, st["exp_avg"], st["exp_avg_sq"], a))
                     gathers.append(sh)
                 else:
+                    if deferred.gather_group is not None:  # data parallel: every rank's factored grad
+                        parts = _gather_parts(parts, deferred.gather_group)
                     fused.append((p, st, parts))
                 continue
             if p.grad is None:
@@ -177,6 +185,21 @@ class AdamW(torch.optim.Optimizer):
         return sh.reduce_scatter(gbuf)
 
 
+def _gather_parts(parts, group):
+    """Replicated table update under data parallelism: all-gather d_pooled and denom (rank-major,
+    matching the plan's all-gathered ids); with the loss pre-scaled by 1/world the sum over all
+    ranks' entries is the global-batch mean gradient, applied identically on every rank."""
+    ids, dp, den, plan = parts
+    world = torch.distributed.get_world_size(group)
+    dp_all = dp.new_empty((world * dp.shape[0],) + tuple(dp.shape[1:]))
+    den_all = den.new_empty((world * den.shape[0],))
+    distributed.all_gather_rows(dp_all, dp.contiguous(), group)
+    distributed.all_gather_rows(den_all, den.contiguous(), group)
+    if plan is None or plan.nseq != dp_all.shape[0]:
+        raise RuntimeError("replicated table sync needs the all-ranks plan built in the forward")
+    return plan.ids, dp_all, den_all, plan
+
+
 def _host_adam_args(lr, b1, b2, eps, wd, step, device) -> torch.Tensor:
     """The per-step scalars of make_adam (csrc/common.hpp) formed in Python doubles, rounded to
     fp32 once, as a TT_ADAM_ARGS_BYTES device buffer."""
@@ -187,13 +210,14 @@ def _host_adam_args(lr, b1, b2, eps, wd, step, device) -> torch.Tensor:
 def _merge_parts(parts, table: torch.Tensor, padding_idx):
     """One (ids, d_pooled, denom, plan) for every bag call on the table this step (a single call
     in the fused TwoTower path; separate tower calls are concatenated and re-planned)."""
+    group = getattr(getattr(table, "_tt_deferred", None), "gather_group", None)
     if len(parts) == 1:
         ids, dp, den, plan = parts[0]
         if plan is None and table.is_cuda:
-            plan = ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx)
+            plan = ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx, gather_group=group)
         return ids, dp, den, plan
     L = max(p[0].shape[1] for p in parts)
     ids = torch.cat([F.pad(p[0].to(torch.int64), (0, L - p[0].shape[1])) for p in parts], 0)
     dp = torch.cat([p[1] for p in parts], 0)
     den = torch.cat([p[2] for p in parts], 0)
-    return ids, dp, den, ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx)
+    return ids, dp, den, ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx, gather_group=group)
