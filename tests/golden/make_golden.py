@@ -187,12 +187,71 @@ def case_losses(R):
     return out
 
 
+def case_state_dict(R):
+    """Parameter names/shapes of the reference models (mean tied/untied, avg_pool with and without
+    projection) and the layout of its AdamW state_dict: checkpoint compatibility
+    (twotower/utils.py:231-330 saves model.state_dict() / optimizer.state_dict())."""
+    import json
+
+    out = {}
+    emb = R["embeddings"].build("lookup", vocab_size=50, embedding_dim=16)
+    models = {
+        "mean_tied": R["encoders"].build_two_tower("mean", emb, hidden_dim=24, tied_weights=True),
+        "mean_untied": R["encoders"].build_two_tower("mean", emb, hidden_dim=24, tied_weights=False),
+        "avg_proj": R["encoders"].build_two_tower("avg_pool", emb, hidden_dim=24, tied_weights=True),
+        "avg_noproj": R["encoders"].build_two_tower("avg_pool", emb, hidden_dim=16, tied_weights=True),
+    }
+    layout = {k: [[n, list(t.shape)] for n, t in m.state_dict().items()] for k, m in models.items()}
+    m = models["mean_tied"]
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    for prm in m.parameters():
+        prm.grad = torch.ones_like(prm)
+    opt.step()
+    sd = opt.state_dict()
+    layout["optimizer"] = {"param_group_keys": sorted(sd["param_groups"][0].keys()),
+                           "state_keys": sorted(sd["state"][0].keys()), "n_state": len(sd["state"])}
+    out["layout_json"] = np.array(json.dumps(layout))
+    return out
+
+
+def case_avg_pool(R):
+    """AveragePoolingTower (encoders.py:84-155) in eval mode (dropout = identity): output and
+    parameter gradients of sum(out * w) for a seeded batch, with and without the projection."""
+    out = {}
+    for tag, H in (("proj", 24), ("noproj", 16)):
+        torch.manual_seed(11)
+        emb = R["embeddings"].build("lookup", vocab_size=40, embedding_dim=16)
+        tower = R["encoders"].build_tower("avg_pool", emb, hidden_dim=H)
+        tower.eval()
+        g = torch.Generator().manual_seed(12)
+        ids = torch.randint(1, 40, (6, 9), generator=g)
+        ids[0, :] = 0
+        ids[1, 4:] = 0
+        ids[2, ::2] = 0
+        y = tower(ids)
+        w = torch.randn(y.shape, generator=g)
+        (y * w).sum().backward()
+        out[f"{tag}_ids"] = ids.numpy()
+        out[f"{tag}_w"] = w.numpy()
+        out[f"{tag}_out"] = y.detach().numpy()
+        for n, prm in tower.named_parameters():
+            out[f"{tag}_param_{n}"] = prm.detach().numpy()
+            out[f"{tag}_grad_{n}"] = prm.grad.numpy()
+    return out
+
+
+CASES = (("bag_tiny", case_bag_tiny), ("c1_step", case_c1_step), ("trajectory", case_trajectory),
+         ("losses", case_losses), ("state_dict", case_state_dict), ("avg_pool", case_avg_pool))
+
+
 def main():
-    root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    root = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else "/root/reference"
+    only = [a[2:] for a in sys.argv[1:] if a.startswith("--")]  # e.g. --avg_pool
     torch.set_num_threads(1)
     R = load_reference(root)
-    for name, fn in (("bag_tiny", case_bag_tiny), ("c1_step", case_c1_step), ("trajectory", case_trajectory),
-                     ("losses", case_losses)):
+    for name, fn in CASES:
+        if only and name not in only:
+            continue
         data = fn(R)
         data["torch_version"] = np.array(torch.__version__)
         path = os.path.join(HERE, f"{name}.npz")

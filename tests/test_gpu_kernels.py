@@ -442,3 +442,20 @@ def test_graph_step_equals_eager(loss_name):
     assert len(s2._graphs) == 1
     for (n_, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
         assert torch.equal(p1, p2), n_
+
+
+@pytest.mark.parametrize("tag,H", [("proj", 24), ("noproj", 16)])
+def test_avg_pool_tower_golden(golden, tag, H):
+    """AveragePoolingTower (encoders.py:84-155), eval mode, against the reference's output and
+    parameter gradients (tests/golden/avg_pool.npz)."""
+    g = golden("avg_pool")
+    emb = tt.embeddings.build("lookup", vocab_size=40, embedding_dim=16)
+    tower = tt.build_tower("avg_pool", emb, hidden_dim=H).to(DEV).eval()
+    with torch.no_grad():
+        for n, p in tower.named_parameters():
+            p.copy_(cuda(g[f"{tag}_param_{n}"]))
+    y = tower(cuda(g[f"{tag}_ids"]))
+    (y * cuda(g[f"{tag}_w"])).sum().backward()
+    assert rel(y, g[f"{tag}_out"]) < 1e-5
+    for n, p in tower.named_parameters():
+        assert rel(p.grad, g[f"{tag}_grad_{n}"]) < 1e-5, n

@@ -3,6 +3,7 @@ header declares, its argument validation answers without touching a device, and 
 surface mirrors the reference's plugin API (registries, builders and their errors, parameter
 names, install() into a reference-shaped package, packed-view detection)."""
 import ctypes
+import os
 import subprocess
 import sys
 import types
@@ -165,3 +166,56 @@ def test_synthetic_triplets_shape_and_padding():
         assert bool(((t > 0) == (pos < lens[:, None])).all())
         assert int(t.max()) < 1000
     assert tt.data.tokens_per_triplet(16) == pytest.approx(7.5 + 2 * 12)
+
+
+# ---------------------------------------------------------------------------------------------
+# checkpoints (twotower/utils.py:231-330; parameter layout pinned by tests/golden/state_dict.npz)
+def _layout(golden):
+    import json
+
+    return json.loads(str(golden("state_dict")["layout_json"]))
+
+
+def test_state_dict_layout_matches_reference(golden):
+    L = _layout(golden)
+    emb = tt.embeddings.build("lookup", vocab_size=50, embedding_dim=16)
+    ours = {
+        "mean_tied": tt.build_two_tower("mean", emb, hidden_dim=24, tied_weights=True),
+        "mean_untied": tt.build_two_tower("mean", emb, hidden_dim=24, tied_weights=False),
+        "avg_proj": tt.build_two_tower("avg_pool", emb, hidden_dim=24, tied_weights=True),
+        "avg_noproj": tt.build_two_tower("avg_pool", emb, hidden_dim=16, tied_weights=True),
+    }
+    for k, m in ours.items():
+        assert [[n, list(t.shape)] for n, t in m.state_dict().items()] == L[k], k
+    m = ours["mean_tied"]
+    opt = tt.optim.AdamW(m.parameters(), lr=1e-3)
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+        opt._state(p, False)  # materialise state without a kernel launch
+    sd = opt.state_dict()
+    assert sorted(sd["state"][0]) == L["optimizer"]["state_keys"]
+    assert len(sd["state"]) == L["optimizer"]["n_state"]
+
+
+def test_checkpoint_round_trip_reference_format(tmp_path):
+    emb = tt.embeddings.build("lookup", vocab_size=30, embedding_dim=8)
+    model = tt.build_two_tower("mean", emb, hidden_dim=12, tied_weights=True)
+    ref_opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    for p in model.parameters():
+        p.grad = torch.randn_like(p)
+    ref_opt.step()
+    path = tt.checkpoint.save_checkpoint(model, {"<PAD>": 0, "a": 1}, ref_opt, epoch=3, loss=0.5,
+                                         checkpoint_dir=str(tmp_path))
+    assert os.path.exists(path) and os.path.exists(tmp_path / "best_model.pt")
+    raw = torch.load(path, weights_only=True)
+    assert set(raw) == {"model", "vocab", "epoch", "loss", "timestamp", "optimizer"}
+    assert raw["epoch"] == 3 and raw["vocab"]["a"] == 1
+    emb2 = tt.embeddings.build("lookup", vocab_size=30, embedding_dim=8)
+    model2 = tt.build_two_tower("mean", emb2, hidden_dim=12, tied_weights=True)
+    opt2 = tt.optim.AdamW(model2.parameters(), lr=1e-3, capturable=True)
+    ck = tt.checkpoint.load_checkpoint(path, model2, opt2)
+    assert ck["loss"] == 0.5
+    for (n, a), b in zip(model.state_dict().items(), model2.state_dict().values()):
+        assert torch.equal(a, b), n
+    p0 = next(model2.parameters())
+    assert torch.equal(opt2.state[p0]["exp_avg"], ref_opt.state[next(model.parameters())]["exp_avg"])

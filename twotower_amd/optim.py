@@ -77,6 +77,26 @@ class AdamW(torch.optim.Optimizer):
                     st[k] = sh.rows(full).clone()
         return st
 
+    def state_dict(self):
+        """torch's layout; a row-sharded table (data parallel "shard" sync) reports its full-size
+        moments (all-gathered over the ranks), so the state loads into torch.optim.AdamW and
+        into a differently sharded run."""
+        sd = super().state_dict()
+        if not self._shards:
+            return sd
+        index = {id(p): i for i, p in enumerate(p for g in self.param_groups for p in g["params"])}
+        for p in (p for g in self.param_groups for p in g["params"]):
+            sh = self._shards.get(id(p))
+            st = sd["state"].get(index[id(p)])
+            if sh is None or st is None:
+                continue
+            st = sd["state"][index[id(p)]] = dict(st)  # the packed dict aliases the live state
+            for k in ("exp_avg", "exp_avg_sq"):
+                full = st[k].new_empty(sh.Vp, sh.E)
+                distributed.all_gather_rows(full, st[k].contiguous(), sh.group)
+                st[k] = full[:sh.V].clone()
+        return sd
+
     def load_state_dict(self, state_dict) -> None:
         """torch semantics, except that `capturable` stays what this optimizer was built with (it
         selects the execution path, not the math); step counters move on first use."""
