@@ -186,6 +186,16 @@ int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, 
                    const float* grad_loss, float grad_scale, float* dq, float* dd,
                    void* ws, size_t ws_bytes, tt_stream_t stream);
 
+/* ---- search over indexed documents (inference/search/two_tower.py:72-115, evaluate.py:159-199)
+ * tt_cosine_scores: scores[i*nd + j] = F.cosine_similarity(q_i, d_j) with eps 1e-8 (each side
+ *   divided by max(|x|, eps), then summed products); q (nq x H), docs (nd x H) fp32, H % 4 == 0.
+ * tt_topk_rows: per row of a (nrows x ncols) score matrix the k largest values, descending, and
+ *   their column indices (torch.topk; ties broken by the lower index), 1 <= k <= min(1024, ncols). */
+int tt_cosine_scores(const float* q, int64_t nq, const float* docs, int64_t nd, int H, float* scores,
+                     tt_stream_t stream);
+int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float* out_vals, int64_t* out_idx,
+                 tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -459,3 +459,54 @@ def test_avg_pool_tower_golden(golden, tag, H):
     assert rel(y, g[f"{tag}_out"]) < 1e-5
     for n, p in tower.named_parameters():
         assert rel(p.grad, g[f"{tag}_grad_{n}"]) < 1e-5, n
+
+
+# ---------------------------------------------------------------------------------------------
+# search: cosine scores + top-k (inference/search/two_tower.py:92-103)
+@pytest.mark.parametrize("nq,nd,H,k", [(1, 5000, 256, 5), (3, 1000, 128, 64), (17, 3001, 64, 10), (2, 70000, 256, 1000)])
+def test_cosine_topk_vs_reference_math(nq, nd, H, k):
+    rng = np.random.default_rng(nq + nd)
+    q = rng.standard_normal((nq, H)).astype(np.float32)
+    d = rng.standard_normal((nd, H)).astype(np.float32)
+    d[7] = 0.0                      # zero row: eps clamp
+    d[11] = d[10]                   # exact tie: lower index first
+    Q, D = cuda(q), cuda(d)
+    s = ops.cosine_scores(Q, D)
+    ref = torch.nn.functional.cosine_similarity(torch.as_tensor(q).double()[:, None], torch.as_tensor(d).double()[None],
+                                                dim=2).numpy()
+    assert np.abs(s.cpu().numpy() - ref).max() < 1e-6
+    vals, idx = ops.topk_rows(s, k)
+    sc = s.cpu().numpy()
+    order = np.lexsort((np.arange(nd)[None].repeat(nq, 0), -sc), axis=1)[:, :k]  # desc value, asc index
+    assert np.array_equal(idx.cpu().numpy(), order)
+    assert np.array_equal(vals.cpu().numpy(), np.take_along_axis(sc, order, 1))
+
+
+def test_topk_ties_and_extremes():
+    x = torch.tensor([[1.0, 3.0, 3.0, -2.0, 3.0, float("-inf"), 0.0, -0.0]], device=DEV)
+    vals, idx = ops.topk_rows(x, 4)
+    assert idx.tolist() == [[1, 2, 4, 0]] and vals.tolist() == [[3.0, 3.0, 3.0, 1.0]]
+    vals, idx = ops.topk_rows(x, 8)
+    assert idx[0, -1].item() == 5
+
+
+def test_search_index_and_query(tmp_path):
+    torch.manual_seed(0)
+    V, E = 500, 64
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+    docs = torch.randint(1, V, (300, 16), device=DEV, dtype=torch.int32)
+    engine = tt.search.TwoTowerSearch(model, device=DEV)
+    engine.index_document_ids(docs)
+    qids = docs[[5, 42]].clone()
+    scores, idx = engine.search_ids(qids, top_k=3)
+    assert idx[:, 0].tolist() == [5, 42]          # a document is its own nearest neighbour (tied towers)
+    assert torch.allclose(scores[:, 0], torch.ones(2, device=DEV), atol=1e-5)
+    with torch.no_grad():
+        ref = torch.nn.functional.cosine_similarity(model.query_tower(qids.long())[:, None],
+                                                    engine.document_embeddings[None], dim=2)
+    assert torch.allclose(torch.topk(ref, 3).values, scores, atol=1e-5)
+    engine.save_index(str(tmp_path / "idx.pt"))
+    e2 = tt.search.TwoTowerSearch(model, device=DEV)
+    e2.load_index(str(tmp_path / "idx.pt"))
+    assert torch.equal(e2.document_embeddings, engine.document_embeddings)

@@ -13,7 +13,7 @@ from __future__ import annotations
 import importlib
 import sys
 
-from . import checkpoint, data, distributed, embeddings, encoders, losses, ops, optim
+from . import checkpoint, data, distributed, embeddings, encoders, losses, ops, optim, search
 from .embeddings import BaseEmbedding, LookupEmbedding
 from .encoders import (AveragePoolingTower, BaseTower, MeanPoolingTower, TOWER_REGISTRY, TwoTower, build_tower,
                        build_two_tower)
@@ -25,7 +25,7 @@ __all__ = [
     "BaseEmbedding", "LookupEmbedding", "BaseTower", "MeanPoolingTower", "AveragePoolingTower", "TwoTower",
     "TOWER_REGISTRY", "LOSS_REGISTRY", "build_tower", "build_two_tower", "contrastive_triplet_loss",
     "multiple_negatives_loss", "in_batch_sampled_softmax_loss", "TrainStep", "install", "data", "distributed",
-    "embeddings", "encoders", "losses", "ops", "optim", "checkpoint",
+    "embeddings", "encoders", "losses", "ops", "optim", "checkpoint", "search",
 ]
 
 

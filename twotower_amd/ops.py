@@ -488,3 +488,36 @@ def bag_mean_backward_adamw(d_pooled, denom, ids, table, exp_avg, exp_avg_sq, pa
     call("tt_bag_mean_bwd_adamw", ptr(d_pooled), ptr(denom), ptr(ids), _lib.ids_dtype_code(ids), N, L, L, V, E,
          pad, ptr(table), ptr(exp_avg), ptr(exp_avg_sq), lr, beta1, beta2, eps, weight_decay, step, ptr(ws),
          ws.numel(), stream_of(table))
+
+
+# --------------------------------------------------------------------------------------------
+# search: cosine scores + top-k   (inference/search/two_tower.py:92-103, evaluate.py:176-183)
+def cosine_scores(q: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
+    """(nq, nd) F.cosine_similarity(q_i, d_j) (eps 1e-8) on the HBM-streaming HIP kernel."""
+    require_gpu(q, docs)
+    q, docs = _contig_f32(q, "q"), _contig_f32(docs, "docs")
+    if q.dim() == 1:
+        q = q.unsqueeze(0)
+    nq, H = q.shape
+    if docs.shape[1] != H:
+        raise ValueError(f"query width {H} != document width {docs.shape[1]}")
+    out = torch.empty(nq, docs.shape[0], dtype=_FLOAT, device=q.device)
+    call("tt_cosine_scores", ptr(q), nq, ptr(docs), docs.shape[0], H, ptr(out), stream_of(q))
+    return out
+
+
+def topk_rows(scores: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """torch.topk(scores, k, dim=1) (descending; ties to the lower index) on the HIP radix select."""
+    require_gpu(scores)
+    scores = _contig_f32(scores, "scores")
+    if scores.dim() == 1:
+        scores = scores.unsqueeze(0)
+    n, m = scores.shape
+    vals = torch.empty(n, k, dtype=_FLOAT, device=scores.device)
+    idx = torch.empty(n, k, dtype=torch.int64, device=scores.device)
+    call("tt_topk_rows", ptr(scores), n, m, int(k), ptr(vals), ptr(idx), stream_of(scores))
+    return vals, idx
+
+
+def cosine_topk(q: torch.Tensor, docs: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]:
+    return topk_rows(cosine_scores(q, docs), k)
