@@ -133,6 +133,15 @@ int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, 
 int tt_l2norm_bwd(const float* dout, const float* out, const float* norm, int64_t rows, int H,
                   float* dx, tt_stream_t stream);
 
+/* ---- LayerNorm + L2 normalise (AveragePoolingTower projection tail: nn.LayerNorm(H) then
+ * F.normalize, twotower/encoders.py:95-97,150).  fwd: out and per-row stats (mean, rstd, |y|,
+ * 3 floats per row).  bwd: dx, and the per-row gamma / beta gradient terms gx = dy*xhat, gb = dy
+ * (rows x H each; their column sums are dgamma / dbeta, tt_colsum). */
+int tt_ln_l2_fwd(const float* x, int64_t rows, int H, const float* gamma, const float* beta, float eps, float* out,
+                 float* stats, tt_stream_t stream);
+int tt_ln_l2_bwd(const float* dout, const float* x, int64_t rows, int H, const float* gamma, const float* beta,
+                 const float* stats, float* dx, float* gx, float* gb, tt_stream_t stream);
+
 /* ---- column sum (bias gradient of nn.Linear: grad_out.sum(0); twotower/encoders.py:38-42) ----
  * out[c] = sum_r x[r, c] in a fixed order (deterministic): per-block partial sums over row
  * chunks into ws (>= tt_colsum_ws_size bytes), then one fixed-order pass over the partials. */
@@ -195,6 +204,12 @@ int tt_cosine_scores(const float* q, int64_t nq, const float* docs, int64_t nd, 
                      tt_stream_t stream);
 int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float* out_vals, int64_t* out_idx,
                  tt_stream_t stream);
+
+/* ---- device-resident batch feeder (TripletDataset.__getitem__ + DataLoader collate,
+ * twotower/dataset.py:262-285, twotower/train.py:411-417): dst[r, :L] = src[idx[r], :L] for int32
+ * id rows; an index outside [0, n_src) yields an all-padding row and sets *bad to 1 (caller zeroes). */
+int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n, int L,
+                       int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -510,3 +510,53 @@ def test_search_index_and_query(tmp_path):
     e2 = tt.search.TwoTowerSearch(model, device=DEV)
     e2.load_index(str(tmp_path / "idx.pt"))
     assert torch.equal(e2.document_embeddings, engine.document_embeddings)
+
+
+# ---------------------------------------------------------------------------------------------
+# device-resident feeder (TripletDataset + DataLoader collate)
+class _FakeTripletDataset(torch.utils.data.Dataset):
+    """Shaped like the reference's TripletDataset: __getitem__ -> three int64 (L,) tensors."""
+
+    def __init__(self, n, L, V, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.data = [tuple(torch.randint(0, V, (L,), generator=g) for _ in range(3)) for _ in range(n)]
+
+    def __len__(self):
+        return len(self.data)
+
+    def __getitem__(self, i):
+        return self.data[i]
+
+
+def test_device_feeder_matches_dataloader_collate():
+    ds = _FakeTripletDataset(103, 12, 500, seed=0)
+    store = tt.data.DeviceTripletStore.from_dataset(ds, DEV)
+    perm = torch.randperm(len(ds), generator=torch.Generator().manual_seed(3))
+    loader = torch.utils.data.DataLoader(ds, batch_size=16, sampler=perm.tolist())
+    got = list(store.batches(16, order=perm))
+    assert len(got) == len(loader)
+    for (q, p, n), (rq, rp, rn) in zip(got, loader):
+        assert torch.equal(q.cpu().long(), rq) and torch.equal(p.cpu().long(), rp) and torch.equal(n.cpu().long(), rn)
+        assert q.dtype == torch.int32 and q._base is p._base  # packed [q; p; n]
+    assert int(store._bad.item()) == 0
+    # out-of-range index: padding row + flag
+    q, p, n = store.gather(torch.tensor([0, 1000], device=DEV))
+    assert torch.equal(q[1], torch.zeros_like(q[1])) and int(store._bad.item()) == 1
+
+
+@pytest.mark.parametrize("rows,H", [(37, 24), (1000, 256), (5, 1024)])
+def test_layernorm_l2_normalize_vs_torch_fp64(rows, H):
+    rng = np.random.default_rng(rows + H)
+    x = rng.standard_normal((rows, H)).astype(np.float32) * 3 + 1
+    x[0] = 2.5  # constant row: var 0
+    gm = rng.standard_normal(H).astype(np.float32)
+    bt = rng.standard_normal(H).astype(np.float32)
+    w = rng.standard_normal((rows, H)).astype(np.float32)
+    X, G, Bt = (cuda(a).requires_grad_(True) for a in (x, gm, bt))
+    out = ops.layernorm_l2_normalize(X, G, Bt, 1e-5)
+    (out * cuda(w)).sum().backward()
+    Xr, Gr, Br = (torch.as_tensor(a).double().requires_grad_(True) for a in (x, gm, bt))
+    ref = torch.nn.functional.normalize(torch.nn.functional.layer_norm(Xr, (H,), Gr, Br, 1e-5), dim=-1)
+    (ref * torch.as_tensor(w).double()).sum().backward()
+    assert rel(out, ref) < 1e-5
+    assert rel(X.grad, Xr.grad) < 1e-5 and rel(G.grad, Gr.grad) < 1e-5 and rel(Bt.grad, Br.grad) < 1e-5

@@ -58,6 +58,9 @@ _SIGNATURES = {
     "tt_adamw_multi": (_c_int, [ctypes.POINTER(AdamwTensor), _c_int, _vp]),
     "tt_cosine_scores": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
+    "tt_gather_rows_i32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
+    "tt_ln_l2_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_f32, _vp, _vp, _vp]),
+    "tt_ln_l2_bwd": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
     "tt_l2norm_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),

@@ -1,0 +1,59 @@
+// Device-resident batch feeder: the encoded (query, doc+, doc-) rows of a dataset live in HBM;
+// each batch is gathered by a (shuffled) index list straight into the packed [q; p; n] int32
+// buffer the fused TwoTower forward reads (replaces TripletDataset.__getitem__ + DataLoader
+// collate + .to(device), twotower/dataset.py:262-285, twotower/train.py:411-417).
+//
+// One wave per destination row: L int32 ids (L*4 bytes) copied with 16-byte loads when the
+// rows are 16-byte aligned, HBM-bound (a batch of 3 x 8192 x 64 ids is 6.3 MB).
+#include "common.hpp"
+
+namespace tt {
+namespace {
+
+constexpr int kBlock = 256;
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(const int32_t* __restrict__ src, int64_t ld_src,
+                                                             int64_t n_src, const int64_t* __restrict__ idx,
+                                                             int64_t n, int L, int32_t* __restrict__ dst,
+                                                             int64_t ld_dst, int* __restrict__ bad) {
+  const int64_t r = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = lane_id();
+  const int64_t s = idx[r];
+  int32_t* out = dst + r * ld_dst;
+  if (s < 0 || s >= n_src) {  // out of range: a zero (all padding) row, and the flag is raised
+    for (int c = lane; c < L; c += kWave) out[c] = 0;
+    if (lane == 0) atomicOr(bad, 1);
+    return;
+  }
+  const int32_t* in = src + s * ld_src;
+  if constexpr (VEC) {
+    for (int c = lane; c < L / 4; c += kWave)
+      reinterpret_cast<int4*>(out)[c] = reinterpret_cast<const int4*>(in)[c];
+  } else {
+    for (int c = lane; c < L; c += kWave) out[c] = in[c];
+  }
+}
+
+}  // namespace
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n,
+                                  int L, int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream) {
+  TT_REQUIRE(n >= 0 && L >= 0 && n_src >= 0 && ld_src >= L && ld_dst >= L, "bad shape");
+  if (n == 0 || L == 0) return TT_OK;
+  TT_REQUIRE(src && idx && dst && bad, "null pointer");
+  const bool vec = (L % 4 == 0) && (ld_src % 4 == 0) && (ld_dst % 4 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  const dim3 grid((unsigned)((n + kBlock / kWave - 1) / (kBlock / kWave))), block(kBlock);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (vec)
+    gather_rows_kernel<true><<<grid, block, 0, s>>>(src, ld_src, n_src, idx, n, L, dst, ld_dst, bad);
+  else
+    gather_rows_kernel<false><<<grid, block, 0, s>>>(src, ld_src, n_src, idx, n, L, dst, ld_dst, bad);
+  TT_LAUNCH_CHECK("tt_gather_rows_i32");
+  return TT_OK;
+}

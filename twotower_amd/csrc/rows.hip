@@ -50,6 +50,73 @@ __global__ __launch_bounds__(kBlock) void l2norm_bwd_kernel(const float* __restr
   }
 }
 
+// ---- LayerNorm -> L2 normalise (AveragePoolingTower's projection tail, encoders.py:95-97,150):
+// y = (x - mean) * rstd * gamma + beta (biased variance, rstd = 1/sqrt(var + eps) as ATen),
+// out = y / max(|y|, 1e-12).  stats per row: mean, rstd, |y|.
+__global__ __launch_bounds__(kBlock) void ln_l2_fwd_kernel(const float* __restrict__ x, int64_t rows, int H,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps,
+                                                           float* __restrict__ out, float* __restrict__ stats) {
+  const int64_t r = wave_row();
+  if (r >= rows) return;
+  const int lane = lane_id();
+  const float* xr = x + r * H;
+  float s = 0.f;
+  for (int c = lane; c < H; c += kWave) s += xr[c];
+  const float mean = wave_sum(s) / (float)H;
+  float v = 0.f;
+  for (int c = lane; c < H; c += kWave) v += (xr[c] - mean) * (xr[c] - mean);
+  const float rstd = 1.f / sqrtf(fmaxf(wave_sum(v) / (float)H, 0.f) + eps);
+  float ss = 0.f;
+  for (int c = lane; c < H; c += kWave) {
+    const float y = (xr[c] - mean) * rstd * gamma[c] + beta[c];
+    ss += y * y;
+  }
+  const float nrm = sqrtf(wave_sum(ss)), den = fmaxf(nrm, 1e-12f);
+  for (int c = lane; c < H; c += kWave) out[r * H + c] = ((xr[c] - mean) * rstd * gamma[c] + beta[c]) / den;
+  if (lane == 0) {
+    stats[3 * r] = mean;
+    stats[3 * r + 1] = rstd;
+    stats[3 * r + 2] = nrm;
+  }
+}
+
+// Backward: dy = F.normalize backward (norm differentiated, clamp not); LayerNorm backward
+// dx = rstd (dxhat - mean(dxhat) - xhat mean(dxhat xhat)), dxhat = dy gamma; the per-row
+// gamma/beta contributions (dy xhat, dy) go to gx / gb for fixed-order column sums.
+__global__ __launch_bounds__(kBlock) void ln_l2_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ x,
+                                                           int64_t rows, int H, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ stats, float* __restrict__ dx,
+                                                           float* __restrict__ gx, float* __restrict__ gb) {
+  const int64_t r = wave_row();
+  if (r >= rows) return;
+  const int lane = lane_id();
+  const float mean = stats[3 * r], rstd = stats[3 * r + 1], nrm = stats[3 * r + 2];
+  const float den = fmaxf(nrm, 1e-12f);
+  const float* xr = x + r * H;
+  const float* dr = dout + r * H;
+  float sy = 0.f;
+  for (int c = lane; c < H; c += kWave) sy += dr[c] * ((xr[c] - mean) * rstd * gamma[c] + beta[c]);
+  const float coef = (nrm >= 1e-12f && nrm > 0.f) ? wave_sum(sy) / (den * den * nrm) : 0.f;
+  float a = 0.f, b = 0.f;
+  for (int c = lane; c < H; c += kWave) {
+    const float xh = (xr[c] - mean) * rstd;
+    const float dy = dr[c] / den - coef * (xh * gamma[c] + beta[c]);
+    gx[r * H + c] = dy * xh;
+    gb[r * H + c] = dy;
+    const float dxh = dy * gamma[c];
+    a += dxh;
+    b += dxh * xh;
+  }
+  a = wave_sum(a) / (float)H;
+  b = wave_sum(b) / (float)H;
+  for (int c = lane; c < H; c += kWave) {
+    const float xh = (xr[c] - mean) * rstd;
+    dx[r * H + c] = rstd * (gb[r * H + c] * gamma[c] - a - xh * b);
+  }
+}
+
 struct CosStats {
   float dot, n1, n2;  // raw dot and unclamped norms
 };
@@ -261,6 +328,29 @@ extern "C" int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, fl
   TT_REQUIRE(x && out && norm, "null pointer");
   l2norm_fwd_kernel<<<rows_grid(rows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(x, rows, H, out, norm);
   TT_LAUNCH_CHECK("tt_l2norm_fwd");
+  return TT_OK;
+}
+
+extern "C" int tt_ln_l2_fwd(const float* x, int64_t rows, int H, const float* gamma, const float* beta, float eps,
+                            float* out, float* stats, tt_stream_t stream) {
+  TT_REQUIRE(rows >= 0 && H > 0, "bad shape rows=%lld H=%d", (long long)rows, H);
+  if (rows == 0) return TT_OK;
+  TT_REQUIRE(x && gamma && beta && out && stats, "null pointer");
+  ln_l2_fwd_kernel<<<rows_grid(rows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(x, rows, H, gamma, beta,
+                                                                                                eps, out, stats);
+  TT_LAUNCH_CHECK("tt_ln_l2_fwd");
+  return TT_OK;
+}
+
+extern "C" int tt_ln_l2_bwd(const float* dout, const float* x, int64_t rows, int H, const float* gamma,
+                            const float* beta, const float* stats, float* dx, float* gx, float* gb,
+                            tt_stream_t stream) {
+  TT_REQUIRE(rows >= 0 && H > 0, "bad shape rows=%lld H=%d", (long long)rows, H);
+  if (rows == 0) return TT_OK;
+  TT_REQUIRE(dout && x && gamma && beta && stats && dx && gx && gb, "null pointer");
+  ln_l2_bwd_kernel<<<rows_grid(rows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      dout, x, rows, H, gamma, beta, stats, dx, gx, gb);
+  TT_LAUNCH_CHECK("tt_ln_l2_bwd");
   return TT_OK;
 }
 

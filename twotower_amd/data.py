@@ -50,3 +50,68 @@ def tokens_per_triplet(L: int, query_len=(3, 12), doc_len=None) -> float:
     ql = (min(query_len[0], L) + min(query_len[1], L)) / 2
     dl = (doc_len[0] + doc_len[1]) / 2
     return ql + 2 * dl
+
+
+class DeviceTripletStore:
+    """Device-resident replacement for the reference's TripletDataset + DataLoader hot loop
+    (twotower/dataset.py:262-285 __getitem__, twotower/train.py:411-417 DataLoader(shuffle=True),
+    collate = torch.stack per field, then .to(device)).
+
+    Every encoded triplet is uploaded once as int32 rows (q, d+, d- stacked: (3, N, L)); HBM
+    holds millions of them (a 64-token triplet is 768 B).  ``batches`` shuffles on the device and
+    gathers each batch with the HIP row-gather (tt_gather_rows_i32) into one packed (3B, L)
+    buffer, yielded as consecutive (q, p, n) views -- the layout the fused TwoTower forward uses
+    in place.  Batch i holds the same triplets, in the same order, as the reference's loader
+    given the same index permutation (``order``)."""
+
+    def __init__(self, rows: torch.Tensor):
+        if rows.dim() != 3 or rows.shape[0] != 3:
+            raise ValueError(f"rows must be (3, N, L), got {tuple(rows.shape)}")
+        self.rows = rows.to(torch.int32).contiguous()
+        self.n, self.L = rows.shape[1], rows.shape[2]
+
+    @classmethod
+    def from_dataset(cls, dataset, device="cuda") -> "DeviceTripletStore":
+        """From a reference TripletDataset: its pre-encoded lists when load_to_memory was set,
+        else one pass of __getitem__ (host tokenisation happens once, not per epoch)."""
+        enc = [getattr(dataset, a, None) for a in ("encoded_queries", "encoded_positive_docs", "encoded_negative_docs")]
+        if all(e is not None and len(e) == len(dataset) for e in enc):
+            rows = torch.tensor(enc, dtype=torch.int32)
+        else:
+            items = [dataset[i] for i in range(len(dataset))]
+            rows = torch.stack([torch.stack([torch.as_tensor(it[k], dtype=torch.int32) for it in items])
+                                for k in range(3)])
+        return cls(rows.to(device))
+
+    def __len__(self) -> int:
+        return self.n
+
+    def gather(self, index: torch.Tensor, out: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(q, p, n) int32 rows of the given triplet indices, packed in one (3B, L) buffer."""
+        from . import _lib
+
+        _lib.require_gpu(self.rows, index)
+        index = index.to(torch.int64).contiguous()
+        B = index.shape[0]
+        if out is None:
+            out = torch.empty(3 * B, self.L, dtype=torch.int32, device=self.rows.device)
+        bad = torch.zeros(1, dtype=torch.int32, device=self.rows.device)
+        for k in range(3):
+            _lib.call("tt_gather_rows_i32", self.rows[k].data_ptr(), self.L, self.n, index.data_ptr(), B, self.L,
+                      out[k * B:].data_ptr(), self.L, bad.data_ptr(), _lib.stream_of(out))
+        self._bad = bad
+        return tuple(torch.split(out, B))
+
+    def order(self, seed: int = 0, shuffle: bool = True) -> torch.Tensor:
+        if not shuffle:
+            return torch.arange(self.n, device=self.rows.device)
+        g = torch.Generator(device=self.rows.device)
+        g.manual_seed(seed)
+        return torch.randperm(self.n, generator=g, device=self.rows.device)
+
+    def batches(self, batch_size: int, shuffle: bool = True, seed: int = 0, drop_last: bool = False,
+                order: torch.Tensor | None = None):
+        perm = self.order(seed, shuffle) if order is None else order.to(self.rows.device)
+        stop = self.n - (self.n % batch_size if drop_last else 0)
+        for i in range(0, stop, batch_size):
+            yield self.gather(perm[i:i + batch_size])

@@ -96,8 +96,14 @@ class AveragePoolingTower(BaseTower):
         self.log_params()
 
     def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:
-        out = self.projection(pooled) if self.has_projection else pooled
-        return ops.l2_normalize(out.contiguous())  # encoders.py:150
+        if not self.has_projection:
+            return ops.l2_normalize(pooled.contiguous())  # encoders.py:150
+        lin, drop, ln = self.projection
+        if (isinstance(lin, nn.Linear) and isinstance(drop, nn.Dropout) and isinstance(ln, nn.LayerNorm)
+                and ln.elementwise_affine and ln.weight.shape[0] % 4 == 0):
+            h = F.dropout(F.linear(pooled, lin.weight, lin.bias), drop.p, self.training)
+            return ops.layernorm_l2_normalize(h, ln.weight, ln.bias, ln.eps)  # one fused row pass
+        return ops.l2_normalize(self.projection(pooled).contiguous())
 
 
 def _packed_ids(inputs: list[torch.Tensor]) -> torch.Tensor | None:

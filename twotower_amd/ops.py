@@ -211,6 +211,36 @@ def l2_normalize(x: torch.Tensor) -> torch.Tensor:
     return L2Normalize.apply(x)
 
 
+class LayerNormL2Normalize(torch.autograd.Function):
+    """F.normalize(layer_norm(x, gamma, beta, eps)) in one row pass each way (the AveragePooling
+    projection tail, encoders.py:95-97,150); gamma/beta gradients by tt_colsum."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        require_gpu(x, gamma, beta)
+        x = _contig_f32(x, "x")
+        rows, H = x.shape
+        out = torch.empty_like(x)
+        stats = torch.empty(rows, 3, dtype=_FLOAT, device=x.device)
+        call("tt_ln_l2_fwd", ptr(x), rows, H, ptr(gamma), ptr(beta), float(eps), ptr(out), ptr(stats), stream_of(x))
+        ctx.save_for_backward(x, gamma, beta, stats)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, gamma, beta, stats = ctx.saved_tensors
+        dout = _contig_f32(dout, "dout")
+        rows, H = x.shape
+        dx, gx, gb = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+        call("tt_ln_l2_bwd", ptr(dout), ptr(x), rows, H, ptr(gamma), ptr(beta), ptr(stats), ptr(dx), ptr(gx),
+             ptr(gb), stream_of(x))
+        return dx, colsum(gx), colsum(gb), None
+
+
+def layernorm_l2_normalize(x, gamma, beta, eps=1e-5):
+    return LayerNormL2Normalize.apply(x, gamma, beta, eps)
+
+
 # --------------------------------------------------------------------------------------------
 # Tower feed-forward Linear(E,H) - ReLU - Linear(H,H)   (twotower/encoders.py:38-42)
 def colsum(x: torch.Tensor) -> torch.Tensor:
