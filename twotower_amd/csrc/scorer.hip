@@ -58,7 +58,7 @@ struct Tile {
   static constexpr int STAGE_B = BJ * ROWB;
   static constexpr int NI = STAGE_B / 1024 / NW;  // glds wave-instructions per wave per stage
   static_assert(NI * 1024 * NW == STAGE_B, "stage must be a whole number of 1 KiB pieces per wave");
-  static constexpr int NSTAGE = sizeof(ET) == 2 ? 3 : 2;  // bf16: triple-buffered (see the engine)
+  static constexpr int NSTAGE = sizeof(ET) == 2 ? 4 : 2;  // bf16: four-stage ring (see the engine)
   static constexpr int LSE_OFF = NSTAGE * STAGE_B;
   static constexpr int LDS_BYTES = NSTAGE * STAGE_B + NSTAGE * 64 * 4;  // stages + one 64-float lse row each
   // Chunk XOR of a row.  bf16 rows of >= 256 B use the dual-use swizzle (cdna_hip_programming.md
@@ -294,86 +294,105 @@ __device__ __forceinline__ void acc_chain(const lds_char_t* tile, int jt, int la
 // one MFMA, the operand read for the step four ahead, and the exp (+ bf16 pack) of 16/NK
 // elements of the current tile, fenced by sched_barrier(0) so the compiler keeps that interleave
 // (at one wave per SIMD nothing else hides a clump of transcendentals or an unprefetched read).
-template <int MODE, bool PRECISE, int H>
-__device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16],
-                                              const f32x16& xa, float c2, float shift, const lds_f32x4_t* lse4,
-                                              float& l_run, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
-  using T = Tile<__bf16, H>;
-  constexpr int NK = H / 16;
-  constexpr int EPS = 16 / NK;  // map elements per step
-  const int rowb = row * T::ROWB, x = T::swz(row);
+struct NoHook {
+  __device__ void operator()(int) const {}
+};
+
+// The softmax map of one 32x32 X tile (16 elements per lane), processed in "slots" of one
+// element: an even slot forms the pair's scaled exponent with one v_pk_fma_f32 and takes the
+// first exp; the odd slot takes the second exp, adds the pair to the row sum (v_pk_add_f32) and
+// packs both to bf16.  Slots 0-7 (G rows 0-15, the B operand of the Acc chain's first half) run
+// beside the next tile's S chain, slots 8-15 beside the first half of this tile's Acc chain,
+// which needs them only from its second half: the vector work is split between both MFMA runs.
+template <int MODE, bool PRECISE>
+struct MapState {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x2 c2v, ls, yv;
   float sub[16];
-  if constexpr (MODE == FWD) {
+  float e[16];
+
+  __device__ __forceinline__ void init(float c2, float shift, const lds_f32x4_t* lse4, int hh) {
+    c2v = f32x2{c2, c2};
+    ls = f32x2{0.f, 0.f};
+    yv = f32x2{0.f, 0.f};
+    if constexpr (MODE == FWD) {
 #pragma unroll
-    for (int v = 0; v < 16; ++v) sub[v] = shift;
-  } else {
+      for (int v = 0; v < 16; ++v) sub[v] = shift;
+    } else {
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 l4 = lse4[2 * g4 + hh];  // lse2 of rows 8*g4 + 4*hh + u
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 l4 = lse4[2 * g4 + hh];  // lse2 of rows 8*g4 + 4*hh + u
 #pragma unroll
-      for (int u = 0; u < 4; ++u) sub[4 * g4 + u] = l4[u];
+        for (int u = 0; u < 4; ++u) sub[4 * g4 + u] = l4[u];
+      }
     }
   }
+
+  __device__ __forceinline__ void slot(int v, const f32x16& xa, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
+    const int p = v & ~1;
+    if ((v & 1) == 0) {
+      const f32x2 xv = {xa[p], xa[p + 1]}, sv = {sub[p], sub[p + 1]};
+      yv = xv * c2v - sv;
+#ifdef TT_ABLATE_EXP
+      e[p] = yv[0];
+#else
+      e[p] = __builtin_amdgcn_exp2f(yv[0]);
+#endif
+      asm volatile("" : "+v"(e[p]));  // side-effecting use: keeps the exp inside this step
+    } else {
+#ifdef TT_ABLATE_EXP
+      e[p + 1] = yv[1];
+#else
+      e[p + 1] = __builtin_amdgcn_exp2f(yv[1]);
+#endif
+      asm volatile("" : "+v"(e[p + 1]));
+      if constexpr (MODE == FWD) ls += f32x2{e[p], e[p + 1]};
+#pragma unroll
+      for (int w = p; w <= p + 1; ++w) {
+        const __bf16 h = (__bf16)e[w];
+        bh[w >> 3][w & 7] = h;
+        if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
+      }
+    }
+  }
+};
+
+// S chain of the next X tile fused, step by step, with map slots 0-7 of the current one: each
+// step is one MFMA, the operand read for the step four ahead and its share of the slots,
+// fenced by sched_barrier(0) so the compiler keeps that interleave (at one wave per SIMD nothing
+// else hides a clump of transcendentals or an unprefetched read).
+template <int MODE, bool PRECISE, int H, class Hook = NoHook>
+__device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16],
+                                              const f32x16& xa, MapState<MODE, PRECISE>& ms, bf16x8 (&bh)[2],
+                                              bf16x8 (&bl)[2], Hook hook = Hook{}) {
+  using T = Tile<__bf16, H>;
+  constexpr int NK = H / 16;
+  const int rowb = row * T::ROWB, x = T::swz(row);
   f32x16 acc = f32x16{};
   bf16x8 a[4];
 #pragma unroll
   for (int k = 0; k < 4 && k < NK; ++k)
     a[k] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * k + hh) ^ x) << 4));
-  // the map works on element pairs: v_pk_fma_f32 / v_pk_add_f32 do two lanes' worth each
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  const f32x2 c2v = {c2, c2};
-  float e[16];
-  f32x2 ls = {0.f, 0.f}, yv = {0.f, 0.f};
-  auto pack2 = [&](int v) {
-#pragma unroll
-    for (int w = v; w <= v + 1; ++w) {
-      const __bf16 h = (__bf16)e[w];
-      bh[w >> 3][w & 7] = h;
-      if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
-    }
-  };
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
+#ifndef TT_ABLATE_SREAD
     if (kk + 4 < NK)
       a[kk & 3] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * (kk + 4) + hh) ^ x) << 4));
-    if constexpr (EPS == 1) {
-      // one exp per step; the pair's packed fma on its even step, packed sum + bf16 pack on the odd
-      const int v = kk & ~1;
-      if ((kk & 1) == 0) {
-        const f32x2 xv = {xa[v], xa[v + 1]}, sv = {sub[v], sub[v + 1]};
-        yv = xv * c2v - sv;
-        e[v] = __builtin_amdgcn_exp2f(yv[0]);
-        asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
-      } else {
-        e[v + 1] = __builtin_amdgcn_exp2f(yv[1]);
-        asm volatile("" : "+v"(e[v + 1]));
-        if constexpr (MODE == FWD) ls += f32x2{e[v], e[v + 1]};
-        pack2(v);
-      }
-    } else {
+#endif
 #pragma unroll
-      for (int u = 0; u < EPS / 2; ++u) {
-        const int v = kk * EPS + 2 * u;
-        const f32x2 xv = {xa[v], xa[v + 1]}, sv = {sub[v], sub[v + 1]};
-        const f32x2 y = xv * c2v - sv;
-        e[v] = __builtin_amdgcn_exp2f(y[0]);
-        e[v + 1] = __builtin_amdgcn_exp2f(y[1]);
-        asm volatile("" : "+v"(e[v]), "+v"(e[v + 1]));
-        if constexpr (MODE == FWD) ls += f32x2{e[v], e[v + 1]};
-        pack2(v);
-      }
-    }
+    for (int v = 8 * kk / NK; v < 8 * (kk + 1) / NK; ++v) ms.slot(v, xa, bh, bl);
+    hook(kk);
     __builtin_amdgcn_sched_barrier(0);
   }
-  l_run += ls[0] + ls[1];
   return acc;
 }
 
 // Acc chain with the transposed operand reads of each step issued two steps ahead.
-template <bool PRECISE, int H>
-__device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, int lane, const bf16x8 (&bh)[2],
-                                                    const bf16x8 (&bl)[2], f32x16 (&acc)[H / 32]) {
+template <int MODE, bool PRECISE, int H, class Hook = NoHook>
+__device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, int lane, bf16x8 (&bh)[2],
+                                                    bf16x8 (&bl)[2], f32x16 (&acc)[H / 32], const f32x16& xa,
+                                                    MapState<MODE, PRECISE>& ms, float& l_run, Hook hook = Hook{}) {
   using T = Tile<__bf16, H>;
   constexpr int NHT = H / 32;
   constexpr int NS = 2 * NHT;  // steps: (s2, ht)
@@ -382,6 +401,9 @@ __device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int 
   const int x0 = T::swz(r0), x1 = T::swz(r0 + 8);
   const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
   auto load = [&](int st) {
+#ifdef TT_ABLATE_ACCREAD
+    return bf16x8{(__bf16)(float)st, 0, 0, 0, 0, 0, 0, (__bf16)(float)lane};
+#endif
     const int s2 = st / NHT, ht = st % NHT, ch = 4 * ht + cbase;
     const int rb0 = (r0 + 16 * s2) * T::ROWB + bo, rb1 = (r0 + 16 * s2 + 8) * T::ROWB + bo;
     const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb0 + ((ch ^ x0) << 4)));
@@ -398,9 +420,27 @@ __device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int 
     const int s2 = st / NHT, ht = st % NHT;
     acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], bh[s2], acc[ht], 0, 0, 0);
     if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], bl[s2], acc[ht], 0, 0, 0);
+    if (st < NHT) {  // map slots 8-15 (G rows 16-31, first used at step NHT)
+#pragma unroll
+      for (int v = 8 + 8 * st / NHT; v < 8 + 8 * (st + 1) / NHT; ++v) ms.slot(v, xa, bh, bl);
+    }
+    hook(st);
     __builtin_amdgcn_sched_barrier(0);
   }
+  if constexpr (MODE == FWD) l_run += ms.ls[0] + ms.ls[1];
 }
+
+#ifdef TT_SCORER_TRACE  // debug builds only (tools/trace_scorer.py): s_memtime at region boundaries
+__device__ long long g_tt_trace[8 * 64];
+#define TT_TRACE(slot)                                                                               \
+  do {                                                                                               \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace[t * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TT_TRACE(slot) \
+  do {                 \
+  } while (0)
+#endif
 
 template <int MODE, bool PRECISE, int H>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
@@ -426,13 +466,30 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const float dmax = MODE == FWD ? fold_dmax(dmax_part, n_dmax) : 0.f;  // wave-uniform call
   const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
 
-  // Three LDS stages: stage t+2 is filled while stage t is consumed and stage t+1 waits, so the
-  // first S chain of stage t+1 can run beside the map of stage t's last tile (one barrier per
-  // stage, placed right before that S chain).  (A fourth stage filled one stage earlier measured
-  // no faster: the fills are not what the waves wait on.)
+  // Four-stage LDS ring.  After the barrier of stage t (which proves every wave is done with
+  // stage t-1's buffer) the fill of stage t+3 goes into that buffer, one 1 KiB piece at a time
+  // spread over the remaining MFMA steps of stage t (a burst of 8 pieces per wave stalled the
+  // issuing wave ~600 cycles per stage on the address/TA queue).  Each fill then has more than
+  // a stage to land.  The R operand (ws bf16 copy) carries a BJ-row zero tail (lse2: +inf), so
+  // every fill is a full stage from one scalar base: no per-lane pad redirection, no branches;
+  // fills past the last stage reload stage 0's rows into a buffer nobody reads again.
+  static_assert(T::NSTAGE == 4, "ring indexing assumes four stages");
+  constexpr int NPC = T::NI + (MODE == DD ? 1 : 0);  // pieces per stage per wave (DD: + lse row)
   const FillOffs<__bf16, H> fo = make_fill_offs<__bf16, H>();
-  if (ntiles > 0) stage_fill<__bf16, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad, fo);
-  if (ntiles > 1) stage_fill<__bf16, H, MODE>(smem, 1, R, row_begin + T::BJ, row_end, lse2_rows, pad, fo);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // scalar per wave
+  auto piece = [&](int c, int b, int64_t r0) {  // piece c of the stage at row r0 into buffer b
+    if (c < T::NI) {
+      glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024);
+    } else if constexpr (MODE == DD) {  // every wave loads the lse row (same bytes): uniform vmcnt
+      glds_dword_s((unsigned)lane * 4, lse2_rows + r0, lds0 + T::LSE_OFF + b * 256);
+    }
+  };
+  auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int c = 0; c < NPC; ++c) piece(c, k, stage_row(k));
 
   bf16x8 cf[NK];
   {
@@ -449,37 +506,59 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 #pragma unroll
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
   float l_run = 0.f;
-  drain_dma();
+  // stage 0 landed (stages 1 and 2 may still be in flight)
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPC) : "memory");
   __syncthreads();
 
   f32x16 xa = ntiles > 0 ? s_chain<H>(lds, r32, hh, cf) : f32x16{};
-  int buf = 0;
   for (int64_t t = 0; t < ntiles; ++t) {
+    const int buf = (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
+    const int64_t frow = stage_row(t + 3);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
     const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
-    const int nbuf = buf == 2 ? 0 : buf + 1;
+    // spread the NPC pieces of stage t+3 over the NK + 2*NHT steps after the barrier
+    constexpr int NSTEP = NK + 2 * NHT;
+    auto hook_s = [&](int step) {
+#pragma unroll
+      for (int c = 0; c < NPC; ++c)
+        if (c * NSTEP / NPC == step) piece(c, fbuf, frow);
+    };
+    auto hook_a = [&](int step) {
+#pragma unroll
+      for (int c = 0; c < NPC; ++c)
+        if (c * NSTEP / NPC == NK + step) piece(c, fbuf, frow);
+    };
 #pragma unroll
     for (int jt = 0; jt < NJ; ++jt) {
+      TT_TRACE(jt * 4);
       f32x16 xb;
       bf16x8 bh[2], bl[2];
       if (jt + 1 < NJ) {
-        xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32 + r32, hh, cf, xa, c2, shift, lse4 + jt * 8, l_run,
-                                           bh, bl);
+        MapState<MODE, PRECISE> ms;
+        ms.init(c2, shift, lse4 + jt * 8, hh);
+        xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32 + r32, hh, cf, xa, ms, bh, bl);
+        TT_TRACE(jt * 4 + 3);
+        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lane, bh, bl, acc, xa, ms, l_run);
       } else {
-        drain_dma();      // stage t+1 landed (the only fill in flight)
+        // stage t+1 landed: all but this wave's two newest fills (t+2, t+3's predecessor t+2 is
+        // newest; t+1 is the third newest) have retired
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
+        TT_TRACE(jt * 4 + 1);
+#ifndef TT_ABLATE_BARRIER  // timing ablations (tools/ablate_scorer.sh); never defined in a real build
         __syncthreads();  // ... in every wave, and every wave is past stage t-1
-        if (t + 2 < ntiles)
-          stage_fill<__bf16, H, MODE>(smem, nbuf == 2 ? 0 : nbuf + 1, R, row_begin + (t + 2) * T::BJ, row_end,
-                                      lse2_rows, pad, fo);
+#endif
+        TT_TRACE(jt * 4 + 2);
         // (after the last stage this scores a stale stage; the result is dropped)
-        xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, r32, hh, cf, xa, c2, shift, lse4 + jt * 8, l_run,
-                                           bh, bl);
+        MapState<MODE, PRECISE> ms;
+        ms.init(c2, shift, lse4 + jt * 8, hh);
+        xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, r32, hh, cf, xa, ms, bh, bl, hook_s);
+        TT_TRACE(jt * 4 + 3);
+        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lane, bh, bl, acc, xa, ms, l_run, hook_a);
       }
-      acc_chain_pipelined<PRECISE, H>(tile, jt, lane, bh, bl, acc);
       xa = xb;
     }
-    buf = nbuf;
   }
+  drain_dma();  // no LDS-DMA may outlive the workgroup
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 }
 
@@ -571,6 +650,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
 // values themselves: no zero-initialised accumulator, no atomics).  Block 0 also writes the pad
 // rows (kPadBytes - 16 zero bytes, then +inf for the backward lse2).
 constexpr int kMaxPrepBlocks = 512;
+constexpr int kTailRows = 64;  // >= the bf16 engine's BJ
 
 __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t rows, int H, __bf16* __restrict__ xb,
                                           float* __restrict__ norms, int64_t b0, int64_t nb, float& mx) {
@@ -594,11 +674,18 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ d, int64_t M, int H, int gq,
                                                       __bf16* __restrict__ qb, __bf16* __restrict__ db,
                                                       float* __restrict__ qnorm, float* __restrict__ dmax_part,
-                                                      char* __restrict__ pad) {
+                                                      char* __restrict__ pad, float* __restrict__ lse2) {
   __shared__ float wmax[4];
   if (blockIdx.x == 0) {
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
+    for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
+    if (qb) {
+      for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x) {
+        qb[B * H + i] = (__bf16)0.f;
+        db[M * H + i] = (__bf16)0.f;
+      }
+    }
   }
   float mx = 0.f;
   if ((int)blockIdx.x < gq) {
@@ -739,8 +826,10 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     off = align_up(off + bytes, 256);
     return o;
   };
-  const size_t oq = take(bf ? (size_t)B * H * 2 : 0), od = take(bf ? (size_t)M * H * 2 : 0);
-  const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)B * 4), omx = take(kMaxPrepBlocks * 4);
+  // bf16 operand copies and lse2 carry a kTailRows tail (zeros / +inf): the engine's stage fills
+  // never need per-lane redirection past the last row
+  const size_t oq = take(bf ? (size_t)(B + kTailRows) * H * 2 : 0), od = take(bf ? (size_t)(M + kTailRows) * H * 2 : 0);
+  const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   const size_t oa = take(parts);
@@ -832,7 +921,8 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   const int gq = (int)std::min<int64_t>((B + 3) / 4, 512);
   const int gd = (int)std::min<int64_t>((M + 3) / 4, kMaxPrepBlocks);
   prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
-                                                                 bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad);
+                                                                 bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad,
+                                                                 w.lse2);
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
@@ -877,3 +967,9 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
+
+#ifdef TT_SCORER_TRACE
+extern "C" int tt_debug_scorer_trace(long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_trace), sizeof(long long) * 8 * 64);
+}
+#endif
