@@ -361,24 +361,54 @@ struct MapState {
 // step is one MFMA, the operand read for the step four ahead and its share of the slots,
 // fenced by sched_barrier(0) so the compiler keeps that interleave (at one wave per SIMD nothing
 // else hides a clump of transcendentals or an unprefetched read).
+// Per-lane LDS byte offsets of the operand reads, relative to a stage base (computed once per
+// kernel).  S chain: chunk (2k + hh) ^ swz(row) of row r32 for k = 0..min(NK,8)-1; k >= 8 adds
+// 16 chunks (+256 B) and tile jt adds 32 rows: immediates.  Acc chain: the transposed 4-row
+// blocks of rows r0 and r0 + 8 at chunk (4 ht + cbase) ^ swz = 4 (ht ^ (swz >> 2)) + (cbase ^
+// (swz & 3)) for ht = 0..3; ht >= 4 (+256 B), the second 16-row half and jt: immediates.
+template <int H>
+struct LdsOffs {
+  using T = Tile<__bf16, H>;
+  static constexpr int NS8 = (H / 16) < 8 ? (H / 16) : 8;
+  static constexpr int NA4 = (H / 32) < 4 ? (H / 32) : 4;
+  unsigned s[NS8];
+  unsigned a0[NA4], a1[NA4];
+  __device__ __forceinline__ void init(int lane) {
+    const int r32 = lane & 31, hh = lane >> 5, x = T::swz(r32);
+#pragma unroll
+    for (int k = 0; k < NS8; ++k) s[k] = r32 * T::ROWB + (((2 * k + hh) ^ x) << 4);
+    const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
+    const int r0 = 4 * (tg >> 1) + tq;
+    const int x0 = T::swz(r0), x1 = T::swz(r0 + 8);
+    const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
+#pragma unroll
+    for (int ht = 0; ht < NA4; ++ht) {
+      a0[ht] = r0 * T::ROWB + bo + (((4 * ht + cbase) ^ x0) << 4);
+      a1[ht] = (r0 + 8) * T::ROWB + bo + (((4 * ht + cbase) ^ x1) << 4);
+    }
+  }
+};
+
 template <int MODE, bool PRECISE, int H, class Hook = NoHook>
-__device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16],
-                                              const f32x16& xa, MapState<MODE, PRECISE>& ms, bf16x8 (&bh)[2],
-                                              bf16x8 (&bl)[2], Hook hook = Hook{}) {
+__device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int jrow, const LdsOffs<H>& lo,
+                                              const bf16x8 (&cf)[H / 16], const f32x16& xa,
+                                              MapState<MODE, PRECISE>& ms, bf16x8 (&bh)[2], bf16x8 (&bl)[2],
+                                              Hook hook = Hook{}) {
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
-  const int rowb = row * T::ROWB, x = T::swz(row);
+  const lds_char_t* tb = tile + jrow * T::ROWB;  // + per-lane offset + immediates
+  auto rd = [&](int k) {
+    return *reinterpret_cast<const lds_bf16x8_t*>(tb + lo.s[k & 7] + (k >= 8 ? 256 : 0));
+  };
   f32x16 acc = f32x16{};
   bf16x8 a[4];
 #pragma unroll
-  for (int k = 0; k < 4 && k < NK; ++k)
-    a[k] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * k + hh) ^ x) << 4));
+  for (int k = 0; k < 4 && k < NK; ++k) a[k] = rd(k);
 #pragma unroll
   for (int kk = 0; kk < NK; ++kk) {
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
 #ifndef TT_ABLATE_SREAD
-    if (kk + 4 < NK)
-      a[kk & 3] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * (kk + 4) + hh) ^ x) << 4));
+    if (kk + 4 < NK) a[kk & 3] = rd(kk + 4);
 #endif
 #pragma unroll
     for (int v = 8 * kk / NK; v < 8 * (kk + 1) / NK; ++v) ms.slot(v, xa, bh, bl);
@@ -390,24 +420,22 @@ __device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int row, i
 
 // Acc chain with the transposed operand reads of each step issued two steps ahead.
 template <int MODE, bool PRECISE, int H, class Hook = NoHook>
-__device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, int lane, bf16x8 (&bh)[2],
-                                                    bf16x8 (&bl)[2], f32x16 (&acc)[H / 32], const f32x16& xa,
-                                                    MapState<MODE, PRECISE>& ms, float& l_run, Hook hook = Hook{}) {
+__device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, const LdsOffs<H>& lo,
+                                                    bf16x8 (&bh)[2], bf16x8 (&bl)[2], f32x16 (&acc)[H / 32],
+                                                    const f32x16& xa, MapState<MODE, PRECISE>& ms, float& l_run,
+                                                    Hook hook = Hook{}) {
   using T = Tile<__bf16, H>;
   constexpr int NHT = H / 32;
   constexpr int NS = 2 * NHT;  // steps: (s2, ht)
-  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
-  const int r0 = jt * 32 + 4 * (tg >> 1) + tq;
-  const int x0 = T::swz(r0), x1 = T::swz(r0 + 8);
-  const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
+  const lds_char_t* tb = tile + jt * 32 * T::ROWB;
   auto load = [&](int st) {
 #ifdef TT_ABLATE_ACCREAD
-    return bf16x8{(__bf16)(float)st, 0, 0, 0, 0, 0, 0, (__bf16)(float)lane};
+    return bf16x8{(__bf16)(float)st, 0, 0, 0, 0, 0, 0, (__bf16)(float)lo.s[0]};
 #endif
-    const int s2 = st / NHT, ht = st % NHT, ch = 4 * ht + cbase;
-    const int rb0 = (r0 + 16 * s2) * T::ROWB + bo, rb1 = (r0 + 16 * s2 + 8) * T::ROWB + bo;
-    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb0 + ((ch ^ x0) << 4)));
-    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb1 + ((ch ^ x1) << 4)));
+    const int s2 = st / NHT, ht = st % NHT;
+    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
+    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
     return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
   };
   bf16x8 op[3];
@@ -476,6 +504,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   static_assert(T::NSTAGE == 4, "ring indexing assumes four stages");
   constexpr int NPC = T::NI + (MODE == DD ? 1 : 0);  // pieces per stage per wave (DD: + lse row)
   const FillOffs<__bf16, H> fo = make_fill_offs<__bf16, H>();
+  LdsOffs<H> lo;
+  lo.init(lane);
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // scalar per wave
   auto piece = [&](int c, int b, int64_t r0) {  // piece c of the stage at row r0 into buffer b
@@ -536,9 +566,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
       if (jt + 1 < NJ) {
         MapState<MODE, PRECISE> ms;
         ms.init(c2, shift, lse4 + jt * 8, hh);
-        xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32 + r32, hh, cf, xa, ms, bh, bl);
+        xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32, lo, cf, xa, ms, bh, bl);
         TT_TRACE(jt * 4 + 3);
-        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lane, bh, bl, acc, xa, ms, l_run);
+        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run);
       } else {
         // stage t+1 landed: all but this wave's two newest fills (t+2, t+3's predecessor t+2 is
         // newest; t+1 is the third newest) have retired
@@ -551,9 +581,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
         // (after the last stage this scores a stale stage; the result is dropped)
         MapState<MODE, PRECISE> ms;
         ms.init(c2, shift, lse4 + jt * 8, hh);
-        xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, r32, hh, cf, xa, ms, bh, bl, hook_s);
+        xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, 0, lo, cf, xa, ms, bh, bl, hook_s);
         TT_TRACE(jt * 4 + 3);
-        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lane, bh, bl, acc, xa, ms, l_run, hook_a);
+        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_a);
       }
       xa = xb;
     }
