@@ -211,6 +211,24 @@ int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float
 int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n, int L,
                        int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream);
 
+/* ---- tower head GEMMs, E = H = 256 (MeanPoolingTower feed_forward + F.normalize,
+ * twotower/encoders.py:38-42,77): fp32 GEMMs run on the bf16 MFMA with each operand split
+ * into three bf16 terms (six cross products, fp32-equivalent).
+ * tt_head_split: W (N x K fp32, or its transpose) -> three bf16 planes [3][N][K]
+ *   (tt_head_planes_bytes bytes);
+ * tt_head_gemm: out[r, n] = epi(sum_k A[r, k] W[n, k]) for the planes of W, with
+ *   epi 0: relu(. + bias)            (Linear + ReLU forward); relu_mask, if not null, receives
+ *          the (out > 0) bits: word r * N/32 + n/32, bit n % 32
+ *   epi 1: (. + bias) / max(|row|, 1e-12), norms[r] = |row|   (Linear + F.normalize forward)
+ *   epi 2: . * mask(r, n)            (ReLU backward fused into dh = dy W2; relu_mask from epi 0)
+ *   epi 3: .                         (dx = dh W1). */
+size_t tt_head_planes_bytes(int N, int K);
+int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream);
+size_t tt_head_gemm_ws_size(int64_t rows, int epi); /* epi 1: per-slice row sums of squares */
+int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,
+                 const float* bias, uint32_t* relu_mask, float* out, float* norms, void* ws, size_t ws_bytes,
+                 tt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

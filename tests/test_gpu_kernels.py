@@ -560,3 +560,43 @@ def test_layernorm_l2_normalize_vs_torch_fp64(rows, H):
     (ref * torch.as_tensor(w).double()).sum().backward()
     assert rel(out, ref) < 1e-5
     assert rel(X.grad, Xr.grad) < 1e-5 and rel(G.grad, Gr.grad) < 1e-5 and rel(Bt.grad, Br.grad) < 1e-5
+
+
+# ---------------------------------------------------------------------------------------------
+# tower head on split-bf16 MFMA GEMMs (E = H = 256)
+@pytest.mark.parametrize("rows", [1, 130, 24576])
+def test_tower_head_vs_oracle(rows):
+    rng = np.random.default_rng(rows)
+    E = H = 256
+    x = rng.standard_normal((rows, E)).astype(np.float32)
+    W1 = (rng.standard_normal((H, E)) / 16).astype(np.float32)
+    b1 = (rng.standard_normal(H) / 16).astype(np.float32)
+    W2 = (rng.standard_normal((H, H)) / 16).astype(np.float32)
+    b2 = (rng.standard_normal(H) / 16).astype(np.float32)
+    g = rng.standard_normal((rows, H)).astype(np.float32)
+    X, A, a, B, b = (cuda(t).requires_grad_(True) for t in (x, W1, b1, W2, b2))
+    out = ops.tower_head(X, A, a, B, b)
+    (out * cuda(g)).sum().backward()
+    xd = x.astype(np.float64)
+    y, cache = O.ff_fwd(xd, W1.astype(np.float64), b1.astype(np.float64), W2.astype(np.float64), b2.astype(np.float64))
+    ref, _ = O.l2norm_fwd(y)
+    assert rel(out, ref) < 1e-5
+    dy = O.l2norm_bwd(g.astype(np.float64), y)
+    dpooled, grads = O.ff_bwd(dy, cache, W1.astype(np.float64), W2.astype(np.float64))
+    assert rel(X.grad, dpooled) < 1e-5
+    for t, k in ((A, "W1"), (a, "b1"), (B, "W2"), (b, "b2")):
+        assert rel(t.grad, grads[k]) < 1e-5, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [1, 45, 1000])
+def test_head_relu_mask_bits(rows):
+    """The forward's ReLU bitmask (word r*8 + n/32, bit n%32) is exactly (h > 0)."""
+    rng = np.random.default_rng(7 + rows)
+    x = cuda(rng.standard_normal((rows, 256)).astype(np.float32))
+    W = cuda((rng.standard_normal((256, 256)) / 16).astype(np.float32))
+    b = cuda((rng.standard_normal(256) / 16).astype(np.float32))
+    mask = torch.full((rows, 8), -1, dtype=torch.int32, device="cuda")
+    h = ops._head_gemm(x, ops._planes(W, False), 0, bias=b, mask=mask)
+    bits = (mask.cpu().numpy().view(np.uint32)[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1
+    assert np.array_equal(bits.reshape(rows, 256).astype(bool), h.cpu().numpy() > 0)

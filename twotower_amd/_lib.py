@@ -61,6 +61,11 @@ _SIGNATURES = {
     "tt_gather_rows_i32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
     "tt_ln_l2_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_f32, _vp, _vp, _vp]),
     "tt_ln_l2_bwd": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "tt_head_planes_bytes": (_c_sz, [_c_int, _c_int]),
+    "tt_head_split": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
+    "tt_head_gemm_ws_size": (_c_sz, [_c_i64, _c_int]),
+    "tt_head_gemm": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_sz,
+                              _vp]),
     "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
     "tt_l2norm_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),

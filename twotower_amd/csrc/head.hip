@@ -1,0 +1,416 @@
+// Tower head GEMMs on gfx950: Linear(E,H)-ReLU-Linear(H,H) + F.normalize of MeanPoolingTower
+// (twotower/encoders.py:38-42,77) and their activation gradients, for E = H = 256.
+//
+// fp32 GEMM on the bf16 MFMA: each fp32 operand is split into three bf16 terms (a = a0 + a1 + a2,
+// exact to 2^-24 relative) and the six cross products whose order is >= 2^-16 are accumulated in
+// fp32 (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0); the dropped terms are <= 2^-24 of the product, so
+// results agree with an fp32 GEMM to rounding of the accumulation order.  Six 32x32x16 bf16 MFMAs
+// (32 cycles each) do the work of eight 32x32x2 f32 MFMAs (64 cycles each): 2.7x the rate.
+//
+// out[r, n] = epi(sum_k A[r, k] W[n, k]), A fp32 row-major (rows x 256), W given as three
+// pre-split bf16 planes [3][256 n][256 k] (tt_head_split: the weight, or its transpose).
+// A workgroup owns a 64-column slice of the output for a group of rows: its slice of the three
+// B planes (96 KiB) is loaded into LDS once (16-B chunks XOR-swizzled by row, so the MFMA operand
+// reads are conflict-free) and stays resident; the four waves stream 32-row tiles of A straight
+// from HBM into registers in the MFMA operand layout (8 consecutive k per lane, a whole tile = 128
+// VGPRs), split them into bf16 terms in registers, and fetch each k chunk of their next tile as
+// soon as the current one is consumed -- a full tile (~3 us) of latency cover with no barrier in
+// the main loop.  The four column slices of a row group run on the same XCD (blockIdx % 8), so
+// A is fetched from HBM once and served to the other three from that XCD's L2.
+// The L2-normalise epilogue needs whole rows: each slice writes its rows' partial sums of
+// squares and head_normalize_kernel finishes the rows in place.
+#include "common.hpp"
+
+namespace tt {
+namespace {
+
+constexpr int kN = 256, kK = 256;  // the specialised head width
+constexpr int kColsWG = 64;                         // output column slice per workgroup
+constexpr int kSlices = kN / kColsWG;               // 4
+constexpr int kPlaneB = kColsWG * kK * 2;           // 32 KiB: one bf16 plane of the slice
+constexpr int kSliceB = 3 * kPlaneB;                // 96 KiB resident in LDS
+constexpr int kKS = 16;                             // k per MFMA step
+constexpr int kSteps = kK / kKS;                    // 16
+constexpr int kWaves = 4;
+constexpr int kTileRows = 32;
+
+enum Epi { EPI_BIAS_RELU = 0, EPI_BIAS_L2 = 1, EPI_RELU_MASK = 2, EPI_PLAIN = 3 };
+
+__device__ __forceinline__ void split3(float x, __bf16& a0, __bf16& a1, __bf16& a2) {
+  a0 = (__bf16)x;
+  const float r1 = x - (float)a0;
+  a1 = (__bf16)r1;
+  a2 = (__bf16)(r1 - (float)a1);
+}
+
+__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ W, int transpose,
+                                                           __bf16* __restrict__ planes) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // output index n * kK + k
+  if (i >= kN * kK) return;
+  const int n = i / kK, k = i % kK;
+  const float x = transpose ? W[k * kN + n] : W[n * kK + k];
+  __bf16 a0, a1, a2;
+  split3(x, a0, a1, a2);
+  planes[i] = a0;
+  planes[kN * kK + i] = a1;
+  planes[2 * kN * kK + i] = a2;
+}
+
+// Workgroup b -> (row group g, column slice c).  Blocks b, b+8, b+16, b+24 share an XCD
+// (round-robin dispatch over the 8 XCDs) and take the four slices of one row group.
+__device__ __forceinline__ void head_block(int b, int& g, int& c) {
+  c = (b >> 3) & 3;
+  g = (b >> 5) * 8 + (b & 7);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restrict__ A, int64_t rows, int64_t lda,
+                                                           const __bf16* __restrict__ planes,
+                                                           const float* __restrict__ bias,
+                                                           unsigned* __restrict__ relu_mask, float* __restrict__ out,
+                                                           float* __restrict__ part, int groups, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8_t;
+  typedef __attribute__((address_space(3))) char lds_char_t;
+  lds_char_t* lds = (lds_char_t*)smem;
+  int g, c;
+  head_block(blockIdx.x, g, c);
+  if (g >= groups) return;
+  const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+
+  // resident B slice: lds[p][n][chunk ^ (n & 31)], chunk = 8 k (16 B), n = local column.
+  // LDS-DMA writes each 1 KiB piece linearly (lane l -> byte 16 l = row n0 + l/32, slot l%32),
+  // so the swizzle goes on the source: slot s of row n holds chunk s ^ (n & 31).  24 pieces per
+  // wave, all in flight together, no staging registers.
+#ifndef TT_HABL_NOFILL
+  {
+    constexpr int kPiecesW = kSliceB / 1024 / kWaves;  // 24
+    const unsigned wl = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
+    const char* src = reinterpret_cast<const char*>(planes);
+#pragma unroll
+    for (int u = 0; u < kPiecesW; ++u) {
+      const int piece = u * kWaves + wid;  // 1 KiB = rows 2 piece, 2 piece + 1 of the slice image
+      const int row = 2 * piece + (lane >> 5), p = row / kColsWG, n = row % kColsWG;
+      const int q = (lane & 31) ^ (n & 31);
+      const unsigned off = (unsigned)(((size_t)p * kN * kK + (size_t)(c * kColsWG + n) * kK + q * 8) * 2);
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(src),
+                   "s"(__builtin_amdgcn_readfirstlane(wl + piece * 1024))
+                   : "memory");
+    }
+  }
+#endif
+  // this wave's tiles: rows g*tiles*128 + t*128 + wid*32 + [0, 32)
+  const int64_t wrow0 = (int64_t)g * tiles * (kWaves * kTileRows) + wid * kTileRows;
+  auto a_src = [&](int t) {
+    int64_t r = wrow0 + (int64_t)t * (kWaves * kTileRows) + r32;
+    r = r < rows ? r : rows - 1;  // rows past the end are computed from a clamped row, never stored
+#ifdef TT_HABL_ACOAL
+    r = (r - r32) / 32 * 32;  // timing ablation: instruction i reads row r + i/2.. contiguously
+    return reinterpret_cast<const f32x4*>(A + r * lda + lane * 4 - 4 * (hh * 8) / 4 * 0);
+#endif
+    return reinterpret_cast<const f32x4*>(A + r * lda + hh * 8);
+  };
+#ifdef TT_HABL_ACOAL
+  constexpr int kAStep = 2 * 64, kAHalf = 64;  // f32x4 units: rows of 256 floats
+#else
+  constexpr int kAStep = 4, kAHalf = 1;
+#endif
+  f32x4 areg[kSteps][2];
+  {
+    const f32x4* src = a_src(0);
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j) {
+      areg[j][0] = *(src + j * kAStep);
+      areg[j][1] = *(src + j * kAStep + kAHalf);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces (and A tile 0) landed
+  __syncthreads();                                   // B slice resident
+
+  // B operand of column tile ct, plane p, step j: local column n = 32 ct + r32, chunk 2 j + hh
+  const lds_char_t* bbase = lds + r32 * 512;
+  auto rdb = [&](int ct, int p, int j) {  // (32 ct + r32) & 31 == r32 picks the swizzle
+#ifdef TT_HABL_NOLDS
+    bf16x8 z;
+    asm volatile("" : "=v"(z));
+    return z;
+#endif
+    return *reinterpret_cast<const lds_bf16x8_t*>(bbase + ct * 32 * 512 + p * kPlaneB + (((2 * j + hh) ^ r32) << 4));
+  };
+
+  // Software pipeline: while step j's twelve MFMAs run, the wave reads step j+1's B operands from
+  // LDS and splits step j+1's A chunk in twelve packed pieces of 2-4 VALU, one per MFMA gap
+  // (pinned by volatile register ties and sched_barrier fences).  Step 15 prepares step 0 of the
+  // next tile.  Split words: w[plane][pair] = bf16 pair (x_2i, x_2i+1) of that plane.
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  struct SplitState {
+    f32x2 r;         // running remainder of the pair
+    bf16x2 h;        // last rounded term
+  };
+  // piece k of the split of chunk ar: pair k/3, stage k%3
+  auto split_piece = [&](const f32x4 (&ar)[2], int k, SplitState (&st)[4], u32x4 (&w)[3]) {
+    const int i = k / 3, stage = k % 3;
+    if (stage == 0) {
+      const f32x2 x = i < 2 ? f32x2{ar[0][2 * i], ar[0][2 * i + 1]} : f32x2{ar[1][2 * i - 4], ar[1][2 * i - 3]};
+      st[i].h = __builtin_convertvector(x, bf16x2);
+      w[0][i] = __builtin_bit_cast(unsigned, st[i].h);
+      st[i].r = x - __builtin_convertvector(st[i].h, f32x2);
+      asm volatile("" : "+v"(st[i].r), "+v"(w[0][i]));
+    } else if (stage == 1) {
+      st[i].h = __builtin_convertvector(st[i].r, bf16x2);
+      w[1][i] = __builtin_bit_cast(unsigned, st[i].h);
+      st[i].r = st[i].r - __builtin_convertvector(st[i].h, f32x2);
+      asm volatile("" : "+v"(st[i].r), "+v"(w[1][i]));
+    } else {
+      w[2][i] = __builtin_bit_cast(unsigned, __builtin_convertvector(st[i].r, bf16x2));
+      asm volatile("" : "+v"(w[2][i]));
+    }
+  };
+#ifdef TT_HABL_NOSPLIT
+  auto split_all = [&](const f32x4 (&ar)[2], u32x4 (&w)[3]) {
+    w[0] = __builtin_bit_cast(u32x4, ar[0]);
+    w[1] = w[0];
+    w[2] = w[0];
+  };
+#endif
+  u32x4 ca[3];
+  bf16x8 cb[2][3];
+  {
+    SplitState st[4];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) split_piece(areg[0], k, st, ca);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) cb[ct][p] = rdb(ct, p, 0);
+
+  float bv[2] = {0.f, 0.f};  // this lane's two bias columns, loaded once
+  if constexpr (EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_L2) {
+    bv[0] = bias[c * kColsWG + r32];
+    bv[1] = bias[c * kColsWG + 32 + r32];
+  }
+  // ReLU mask words of a tile: lane L = 32 ct + 2 v + half owns word (row v/half, column block
+  // 2c + ct); rows are 8 words (256 columns) long.
+  auto mask_row = [&](int L) { return ((L >> 1) & 3) + 8 * ((L >> 3) & 3) + 4 * (L & 1); };
+  const int mask_ct = lane >> 5;
+
+  for (int t = 0; t < tiles; ++t) {
+    const int64_t trow0 = wrow0 + (int64_t)t * (kWaves * kTileRows);
+    if (__builtin_amdgcn_readfirstlane((int)(trow0 >= rows))) break;
+    const bool more = t + 1 < tiles && trow0 + kWaves * kTileRows < rows;
+    // unconditional refills keep each step one basic block; the last tile re-reads itself (L2)
+    const f32x4* nsrc = more ? a_src(t + 1) : a_src(t);
+    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    unsigned mword = 0;
+    if constexpr (EPI == EPI_RELU_MASK) {  // issued before the tile's A refills: no flush to wait on it
+      int64_t r = trow0 + mask_row(lane);
+      r = r < rows ? r : rows - 1;
+      mword = relu_mask[r * (kN / 32) + 2 * c + mask_ct];
+    }
+#pragma unroll
+    for (int j = 0; j < kSteps; ++j) {
+      const int jn = (j + 1) % kSteps;
+      u32x4 na[3];
+      bf16x8 nb[2][3];
+      SplitState st[4];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) nb[ct][p] = rdb(ct, p, jn);
+      // areg[j] was split during the previous step: refill it with the next tile
+#ifndef TT_HABL_NOALOAD
+      areg[j][0] = *(nsrc + j * kAStep);
+      areg[j][1] = *(nsrc + j * kAStep + kAHalf);
+#else
+      asm volatile("" : "+v"(areg[j][0]), "+v"(areg[j][1]));
+#endif
+#ifdef TT_HABL_NOSPLIT
+      split_all(areg[jn], na);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 a0 = __builtin_bit_cast(bf16x8, ca[0]), a1 = __builtin_bit_cast(bf16x8, ca[1]),
+                   a2 = __builtin_bit_cast(bf16x8, ca[2]);
+#pragma unroll
+      for (int m = 0; m < 12; ++m) {
+        const int ct = m / 6;
+        f32x16& C = acc[ct];
+        const bf16x8(&b)[3] = cb[ct];
+#ifdef TT_HABL_NOMFMA
+        asm volatile("" ::"v"(a0), "v"(a1), "v"(a2), "v"(b[0]), "v"(b[1]), "v"(b[2]));
+#else
+        switch (m % 6) {
+          case 0: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[0], C, 0, 0, 0); break;
+          case 1: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[1], C, 0, 0, 0); break;
+          case 2: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[2], C, 0, 0, 0); break;
+          case 3: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[0], C, 0, 0, 0); break;
+          case 4: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[1], C, 0, 0, 0); break;
+          default: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0], C, 0, 0, 0); break;
+        }
+#endif
+#ifndef TT_HABL_NOSPLIT
+        split_piece(areg[jn], m, st, na);
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        ca[p] = na[p];
+        cb[0][p] = nb[0][p];
+        cb[1][p] = nb[1][p];
+      }
+    }
+
+    // Epilogue.  acc[ct][v] is row trow0 + (v & 3) + 8 (v >> 2) + 4 hh, column
+    // 64 c + 32 ct + r32.  Rows past the end are never stored; full tiles store unguarded.
+    unsigned my_mask = 0;
+    float my_ss = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        float y = acc[ct][v];
+        if constexpr (EPI == EPI_BIAS_RELU) {
+          y = fmaxf(y + bv[ct], 0.f);
+          const uint64_t bal = __ballot(y > 0.f);  // bit l: lane l's column, row of its half
+          const int L = ct * 32 + v * 2;
+          my_mask = lane == L ? (unsigned)bal : (lane == L + 1 ? (unsigned)(bal >> 32) : my_mask);
+        }
+        if constexpr (EPI == EPI_BIAS_L2) y += bv[ct];
+        if constexpr (EPI == EPI_RELU_MASK) {
+          const unsigned w = (unsigned)__shfl((int)mword, ct * 32 + v * 2 + hh);
+          y = (w >> r32) & 1u ? y : 0.f;
+        }
+        acc[ct][v] = y;
+      }
+    }
+    if constexpr (EPI == EPI_BIAS_L2) {  // partial sum of squares of this slice's 64 columns
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        float ss = acc[0][v] * acc[0][v] + acc[1][v] * acc[1][v];
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) ss += __shfl_xor(ss, o);
+        my_ss = r32 == v ? ss : my_ss;  // lanes 0-15 / 32-47 keep rows v of their half
+      }
+    }
+    float* orow = out + trow0 * kN + c * kColsWG + r32;
+    if (__builtin_amdgcn_readfirstlane((int)(trow0 + kTileRows <= rows))) {
+#ifndef TT_HABL_NOSTORE
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) orow[((v & 3) + 8 * (v >> 2) + 4 * hh) * kN + ct * 32] = acc[ct][v];
+#endif
+    } else {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int rl = (v & 3) + 8 * (v >> 2) + 4 * hh;
+          if (trow0 + rl < rows) orow[rl * kN + ct * 32] = acc[ct][v];
+        }
+    }
+    if constexpr (EPI == EPI_BIAS_RELU) {
+      if (relu_mask && trow0 + mask_row(lane) < rows)
+        relu_mask[(trow0 + mask_row(lane)) * (kN / 32) + 2 * c + mask_ct] = my_mask;
+    }
+    if constexpr (EPI == EPI_BIAS_L2) {
+      const int64_t row = trow0 + (r32 & 3) + 8 * ((r32 >> 2) & 3) + 4 * hh;
+      if (r32 < 16 && row < rows) part[(int64_t)c * rows + row] = my_ss;
+    }
+  }
+}
+
+// Finishes F.normalize (ATen: x / max(|x|, 1e-12)) from the slices' partial sums of squares:
+// one 64-lane wave per row, 4 floats per lane.
+__global__ __launch_bounds__(256) void head_normalize_kernel(float* __restrict__ y, int64_t rows,
+                                                             const float* __restrict__ part,
+                                                             float* __restrict__ norms) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = lane_id();
+  float ss = 0.f;
+#pragma unroll
+  for (int s = 0; s < kSlices; ++s) ss += part[s * rows + row];
+  const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
+  f32x4* p = reinterpret_cast<f32x4*>(y + row * kN) + lane;
+  f32x4 v = *p;
+  v[0] *= inv;
+  v[1] *= inv;
+  v[2] *= inv;
+  v[3] *= inv;
+  *p = v;
+  if (lane == 0) norms[row] = nrm;
+}
+
+}  // namespace
+}  // namespace tt
+
+using namespace tt;
+
+extern "C" size_t tt_head_planes_bytes(int N, int K) { return (size_t)3 * N * K * 2; }
+
+extern "C" int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream) {
+  TT_REQUIRE(N == kN && K == kK, "tt_head_split: only %dx%d weights (got %dx%d)", kN, kK, N, K);
+  TT_REQUIRE(W && planes, "null pointer");
+  split_planes_kernel<<<dim3(kN * kK / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      W, transpose, static_cast<__bf16*>(planes));
+  TT_LAUNCH_CHECK("tt_head_split");
+  return TT_OK;
+}
+
+extern "C" size_t tt_head_gemm_ws_size(int64_t rows, int epi) {
+  return epi == EPI_BIAS_L2 && rows > 0 ? (size_t)kSlices * rows * sizeof(float) : 0;
+}
+
+extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,
+                            const float* bias, uint32_t* relu_mask, float* out, float* norms, void* ws,
+                            size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(N == kN && K == kK, "tt_head_gemm: only K = N = 256 (got K=%d N=%d)", K, N);
+  TT_REQUIRE(rows >= 0 && lda >= K, "bad shape rows=%lld lda=%lld", (long long)rows, (long long)lda);
+  if (rows == 0) return TT_OK;
+  TT_REQUIRE(rows < (int64_t(1) << 31), "rows=%lld too large", (long long)rows);
+  TT_REQUIRE(A && planes && out, "null pointer");
+  TT_REQUIRE(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(planes) |
+               reinterpret_cast<uintptr_t>(out)) & 15) == 0 && lda % 4 == 0,
+             "A / planes / out must be 16-byte aligned");
+  TT_REQUIRE(epi >= EPI_BIAS_RELU && epi <= EPI_PLAIN, "epi=%d", epi);
+  TT_REQUIRE((epi != EPI_BIAS_RELU && epi != EPI_BIAS_L2) || bias, "epilogue needs bias");
+  TT_REQUIRE(epi != EPI_RELU_MASK || relu_mask, "epilogue needs the ReLU mask of the forward");
+  TT_REQUIRE(epi != EPI_BIAS_L2 || norms, "epilogue needs norms");
+  TT_REQUIRE(ws_bytes >= tt_head_gemm_ws_size(rows, epi) && (ws || !tt_head_gemm_ws_size(rows, epi)),
+             "workspace too small (%zu < %zu)", ws_bytes, tt_head_gemm_ws_size(rows, epi));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // tiles per wave: enough row groups to give every CU one workgroup of the four slices
+  const int64_t tile_rows = kWaves * kTileRows;
+  const int64_t tiles = std::max<int64_t>(1, (rows + tile_rows * 64 - 1) / (tile_rows * 64));
+  const int64_t groups = (rows + tiles * tile_rows - 1) / (tiles * tile_rows);
+  const int64_t padded = (groups + 7) / 8 * 8;  // head_block: 8 groups per 32 blocks
+  const dim3 grid((unsigned)(padded * kSlices)), block(256);
+  const __bf16* P = static_cast<const __bf16*>(planes);
+  float* part = static_cast<float*>(ws);
+  const int G = (int)groups, T = (int)tiles;
+  switch (epi) {
+    case EPI_BIAS_RELU:
+      head_gemm_kernel<EPI_BIAS_RELU><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
+      break;
+    case EPI_BIAS_L2:
+      head_gemm_kernel<EPI_BIAS_L2><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
+      break;
+    case EPI_RELU_MASK:
+      head_gemm_kernel<EPI_RELU_MASK><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
+      break;
+    default:
+      head_gemm_kernel<EPI_PLAIN><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
+      break;
+  }
+  TT_LAUNCH_CHECK("tt_head_gemm");
+  if (epi == EPI_BIAS_L2) {
+    head_normalize_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
+    TT_LAUNCH_CHECK("tt_head_gemm normalize");
+  }
+  return TT_OK;
+}

@@ -297,6 +297,59 @@ def tower_ff(x, W1, b1, W2, b2):
     return TowerFF.apply(x, W1, b1, W2, b2)
 
 
+HEAD_WIDTH = 256  # the head GEMM kernels are specialised for E = H = 256
+
+
+def _planes(W: torch.Tensor, transpose: bool) -> torch.Tensor:
+    N, K = W.shape
+    buf = torch.empty(_lib.lib().tt_head_planes_bytes(N, K), dtype=torch.uint8, device=W.device)
+    call("tt_head_split", ptr(W.contiguous()), N, K, int(transpose), ptr(buf), stream_of(W))
+    return buf
+
+
+def _head_gemm(A: torch.Tensor, planes: torch.Tensor, epi: int, bias=None, mask=None, norms=None) -> torch.Tensor:
+    rows, K = A.shape
+    out = torch.empty(rows, HEAD_WIDTH, dtype=_FLOAT, device=A.device)
+    nws = _lib.lib().tt_head_gemm_ws_size(rows, epi)
+    ws = torch.empty(nws, dtype=torch.uint8, device=A.device) if nws else None
+    call("tt_head_gemm", ptr(A), rows, A.stride(0), K, ptr(planes), HEAD_WIDTH, epi, ptr(bias), ptr(mask), ptr(out),
+         ptr(norms), ptr(ws), nws, stream_of(A))
+    return out
+
+
+class TowerHead(torch.autograd.Function):
+    """F.normalize(Linear-ReLU-Linear(x)) for E = H = 256 (encoders.py:38-42,77) on the split-bf16
+    MFMA GEMMs with fused epilogues: bias + ReLU (+ the ReLU bitmask), bias + row L2 normalise
+    (forward); the ReLU mask fused into dh = dy W2 (backward).  Weight gradients on K-split
+    library GEMMs, bias gradients on tt_colsum."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        require_gpu(x, W1, W2)
+        x = _contig_f32(x, "x")
+        rows = x.shape[0]
+        mask = torch.empty(rows, HEAD_WIDTH // 32, dtype=torch.int32, device=x.device)
+        h = _head_gemm(x, _planes(W1, False), 0, bias=b1, mask=mask)
+        norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
+        out = _head_gemm(h, _planes(W2, False), 1, bias=b2, norms=norm)
+        ctx.save_for_backward(x, h, mask, out, norm, W1, W2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, h, mask, out, norm, W1, W2 = ctx.saved_tensors
+        dout = _contig_f32(dout, "dout")
+        dy = torch.empty_like(out)
+        call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy), stream_of(out))
+        dh = _head_gemm(dy, _planes(W2, True), 2, mask=mask)
+        dx = _head_gemm(dh, _planes(W1, True), 3) if ctx.needs_input_grad[0] else None
+        return dx, _weight_grad(dh, x), colsum(dh), _weight_grad(dy, h), colsum(dy)
+
+
+def tower_head(x, W1, b1, W2, b2):
+    return TowerHead.apply(x, W1, b1, W2, b2)
+
+
 # --------------------------------------------------------------------------------------------
 # contrastive_triplet_loss   (twotower/losses.py:9-44)
 def _triplet_fwd(q, p, n, margin):
