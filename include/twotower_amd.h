@@ -218,12 +218,23 @@ int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const 
  *   (tt_head_planes_bytes bytes);
  * tt_head_gemm: out[r, n] = epi(sum_k A[r, k] W[n, k]) for the planes of W, with
  *   epi 0: relu(. + bias)            (Linear + ReLU forward); relu_mask, if not null, receives
- *          the (out > 0) bits: word r * N/32 + n/32, bit n % 32
+ *          the (out > 0) bits in an opaque tile-private layout of tt_head_relu_mask_bytes(rows)
  *   epi 1: (. + bias) / max(|row|, 1e-12), norms[r] = |row|   (Linear + F.normalize forward)
- *   epi 2: . * mask(r, n)            (ReLU backward fused into dh = dy W2; relu_mask from epi 0)
+ *   epi 2: . * mask(r, n)            (ReLU backward fused into dh = dy W2; relu_mask written by
+ *                                     epi 0 for the same rows)
  *   epi 3: .                         (dx = dh W1). */
 size_t tt_head_planes_bytes(int N, int K);
 int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream);
+/* the four plane sets of one Linear-ReLU-Linear head in one launch, each tt_head_planes_bytes(256,
+ * 256) long, in the order W1, W2, W1^T, W2^T (forward operands, then backward operands) */
+int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t stream);
+/* tt_head_wgrad: dW = G^T X (N x N) and, if db is not null, db = column sums of G, for G, X
+ * (rows x N fp32): the weight and bias gradients of a head Linear (encoders.py:38-42; autograd's
+ * grad_W = grad_out^T input, grad_b = grad_out.sum(0)).  Deterministic (fixed-order slab sums). */
+size_t tt_head_wgrad_ws_size(int64_t rows, int N);
+int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
+                  size_t ws_bytes, tt_stream_t stream);
+size_t tt_head_relu_mask_bytes(int64_t rows);
 size_t tt_head_gemm_ws_size(int64_t rows, int epi); /* epi 1: per-slice row sums of squares */
 int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,
                  const float* bias, uint32_t* relu_mask, float* out, float* norms, void* ws, size_t ws_bytes,

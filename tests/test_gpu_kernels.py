@@ -591,12 +591,39 @@ def test_tower_head_vs_oracle(rows):
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows", [1, 45, 1000])
 def test_head_relu_mask_bits(rows):
-    """The forward's ReLU bitmask (word r*8 + n/32, bit n%32) is exactly (h > 0)."""
+    """The forward's ReLU bitmask is exactly (h > 0): decoded with its tile-private layout (word
+    ((r // 32) * 4 + n // 64) * 64 + lane, lane = n % 32 + 32 hh, bit 16 ((n // 32) % 2) + v, for
+    r % 32 = (v & 3) + 8 (v >> 2) + 4 hh)."""
     rng = np.random.default_rng(7 + rows)
     x = cuda(rng.standard_normal((rows, 256)).astype(np.float32))
     W = cuda((rng.standard_normal((256, 256)) / 16).astype(np.float32))
     b = cuda((rng.standard_normal(256) / 16).astype(np.float32))
-    mask = torch.full((rows, 8), -1, dtype=torch.int32, device="cuda")
+    nwords = _lib.lib().tt_head_relu_mask_bytes(rows) // 4
+    mask = torch.zeros(nwords, dtype=torch.int32, device="cuda")
     h = ops._head_gemm(x, ops._planes(W, False), 0, bias=b, mask=mask)
-    bits = (mask.cpu().numpy().view(np.uint32)[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1
-    assert np.array_equal(bits.reshape(rows, 256).astype(bool), h.cpu().numpy() > 0)
+    words = mask.cpu().numpy().view(np.uint32)
+    r = np.arange(rows)[:, None]
+    n = np.arange(256)[None, :]
+    rr = r % 32
+    hh = (rr >> 2) & 1
+    v = (rr & 3) + 4 * (rr >> 3)
+    idx = ((r // 32) * 4 + n // 64) * 64 + (n % 32) + 32 * hh
+    bits = (words[idx] >> (16 * ((n // 32) % 2) + v)) & 1
+    assert np.array_equal(bits.astype(bool), h.cpu().numpy() > 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [0, 1, 17, 1000, 24576 + 5])
+def test_head_wgrad_vs_fp64(rows):
+    """dW = G^T X and db = colsum(G) (autograd's Linear weight / bias gradients) vs float64."""
+    rng = np.random.default_rng(11 + rows)
+    g = rng.standard_normal((rows, 256)).astype(np.float32)
+    x = rng.standard_normal((rows, 256)).astype(np.float32)
+    dW, db = ops.head_wgrad(cuda(g), cuda(x))
+    if rows == 0:
+        assert float(dW.abs().max()) == 0.0 and float(db.abs().max()) == 0.0
+        return
+    assert rel(dW, g.astype(np.float64).T @ x.astype(np.float64)) < 1e-5
+    assert rel(db, g.astype(np.float64).sum(0)) < 1e-5
+    dW2, db2 = ops.head_wgrad(cuda(g), cuda(x))
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)  # deterministic

@@ -44,3 +44,6 @@ for epi in range(4):
 print(f"split planes: {t(lambda: ops._planes(W, True)):.1f} us")
 print(f"torch addmm: {t(lambda: torch.addmm(b, x, W.t())):.1f} us")
 print(f"torch addmm+relu: {t(lambda: torch._addmm_activation(b, x, W.t())):.1f} us")
+g2 = torch.randn(N, 256, device="cuda")
+print(f"head_wgrad (dW + db): {t(lambda: ops.head_wgrad(g2, x)):.1f} us")
+print(f"K-split library wgrad + colsum: {t(lambda: (ops._weight_grad(g2, x), ops.colsum(g2))):.1f} us")

@@ -43,12 +43,20 @@ __device__ __forceinline__ void split3(float x, __bf16& a0, __bf16& a1, __bf16& 
   a2 = (__bf16)(r1 - (float)a1);
 }
 
-__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ W, int transpose,
-                                                           __bf16* __restrict__ planes) {
+// blockIdx.y selects one of up to 4 (weight, transpose) jobs; job j writes planes + j * 3 N K.
+struct SplitJobs {
+  const float* W[4];
+  int transpose[4];
+};
+
+__global__ __launch_bounds__(256) void split_planes_kernel(SplitJobs jobs, __bf16* __restrict__ planes_base) {
   const int i = blockIdx.x * 256 + threadIdx.x;  // output index n * kK + k
   if (i >= kN * kK) return;
+  const int job = blockIdx.y;
+  const float* W = jobs.W[job];
+  __bf16* planes = planes_base + (size_t)job * 3 * kN * kK;
   const int n = i / kK, k = i % kK;
-  const float x = transpose ? W[k * kN + n] : W[n * kK + k];
+  const float x = jobs.transpose[job] ? W[k * kN + n] : W[n * kK + k];
   __bf16 a0, a1, a2;
   split3(x, a0, a1, a2);
   planes[i] = a0;
@@ -193,10 +201,9 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     bv[0] = bias[c * kColsWG + r32];
     bv[1] = bias[c * kColsWG + 32 + r32];
   }
-  // ReLU mask words of a tile: lane L = 32 ct + 2 v + half owns word (row v/half, column block
-  // 2c + ct); rows are 8 words (256 columns) long.
-  auto mask_row = [&](int L) { return ((L >> 1) & 3) + 8 * ((L >> 3) & 3) + 4 * (L & 1); };
-  const int mask_ct = lane >> 5;
+  // ReLU mask: tile-private words.  The forward and the backward launch the same tiling for the
+  // same rows, so lane l of the tile (row tile trow0 / 32, slice c) keeps its own 32 bits
+  // (bit 16 ct + v = element acc[ct][v] > 0) in word ((trow0 / 32) * 4 + c) * 64 + l.
 
   for (int t = 0; t < tiles; ++t) {
     const int64_t trow0 = wrow0 + (int64_t)t * (kWaves * kTileRows);
@@ -205,12 +212,10 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     // unconditional refills keep each step one basic block; the last tile re-reads itself (L2)
     const f32x4* nsrc = more ? a_src(t + 1) : a_src(t);
     f32x16 acc[2] = {f32x16{}, f32x16{}};
+    const int64_t mask_idx = ((trow0 / kTileRows) * kSlices + c) * 64 + lane;
     unsigned mword = 0;
-    if constexpr (EPI == EPI_RELU_MASK) {  // issued before the tile's A refills: no flush to wait on it
-      int64_t r = trow0 + mask_row(lane);
-      r = r < rows ? r : rows - 1;
-      mword = relu_mask[r * (kN / 32) + 2 * c + mask_ct];
-    }
+    if constexpr (EPI == EPI_RELU_MASK)  // issued before the tile's A refills: no flush to wait on it
+      mword = relu_mask[mask_idx];
 #pragma unroll
     for (int j = 0; j < kSteps; ++j) {
       const int jn = (j + 1) % kSteps;
@@ -275,15 +280,10 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         float y = acc[ct][v];
         if constexpr (EPI == EPI_BIAS_RELU) {
           y = fmaxf(y + bv[ct], 0.f);
-          const uint64_t bal = __ballot(y > 0.f);  // bit l: lane l's column, row of its half
-          const int L = ct * 32 + v * 2;
-          my_mask = lane == L ? (unsigned)bal : (lane == L + 1 ? (unsigned)(bal >> 32) : my_mask);
+          my_mask |= (y > 0.f ? 1u : 0u) << (16 * ct + v);
         }
         if constexpr (EPI == EPI_BIAS_L2) y += bv[ct];
-        if constexpr (EPI == EPI_RELU_MASK) {
-          const unsigned w = (unsigned)__shfl((int)mword, ct * 32 + v * 2 + hh);
-          y = (w >> r32) & 1u ? y : 0.f;
-        }
+        if constexpr (EPI == EPI_RELU_MASK) y = (mword >> (16 * ct + v)) & 1u ? y : 0.f;
         acc[ct][v] = y;
       }
     }
@@ -314,8 +314,7 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         }
     }
     if constexpr (EPI == EPI_BIAS_RELU) {
-      if (relu_mask && trow0 + mask_row(lane) < rows)
-        relu_mask[(trow0 + mask_row(lane)) * (kN / 32) + 2 * c + mask_ct] = my_mask;
+      if (relu_mask) relu_mask[mask_idx] = my_mask;
     }
     if constexpr (EPI == EPI_BIAS_L2) {
       const int64_t row = trow0 + (r32 & 3) + 8 * ((r32 >> 2) & 3) + 4 * hh;
@@ -346,6 +345,211 @@ __global__ __launch_bounds__(256) void head_normalize_kernel(float* __restrict__
   if (lane == 0) norms[row] = nrm;
 }
 
+// ------------------------------------------------------------------------------------------
+// Weight and bias gradients of a head Linear: dW = G^T X (256 x 256), db = colsum(G), for tall
+// G, X (rows x 256 fp32; G = dh / dy, X = x / h).  K (= rows) is split over 64 slabs: a
+// workgroup owns one 128 x 128 output block of one slab (grid = 4 blocks x slabs), its four waves
+// 2 x 2 tiles of 32 x 32 each.  Rows stream in chunks of 16: every thread loads 4 floats of G and
+// 4 of X for two rows (raw loads run three chunks ahead in registers), splits them into bf16
+// terms and writes the three planes row-major into LDS (XOR-swizzled by row & 3 in 64-B units);
+// the MFMA operands, which need 8 consecutive ROWS of one column per lane, come back with
+// ds_read_b64_tr_b16.  One barrier per chunk (double-buffered planes).  The loader threads of the
+// j-block-0 workgroups also sum their G columns (db).  Slab partials are reduced in fixed order
+// by head_wgrad_reduce_kernel: deterministic.
+constexpr int kWgChunk = 16;                              // rows per chunk
+constexpr int kWgBlk = 128;                               // output block edge
+constexpr int kWgPlane = kWgChunk * kWgBlk * 2;           // 4 KiB: one bf16 plane of a chunk
+constexpr int kWgBuf = 2 * 3 * kWgPlane;                  // G and X planes: 24 KiB
+constexpr int kWgSlabs = 64;  // a multiple of 8 (XCD-aware block mapping)
+
+__device__ __forceinline__ int wg_off(int row, int col) {  // byte offset in a plane
+  return row * (kWgBlk * 2) + ((col * 2) ^ ((row & 3) << 6));
+}
+
+__global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ X,
+                                                            int64_t rows, int64_t slab_rows,
+                                                            float* __restrict__ part_w, float* __restrict__ part_b) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+  typedef __attribute__((address_space(3))) char lds_char_t;
+  typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
+  lds_char_t* lds = (lds_char_t*)smem;
+  // blocks b, b+8, b+16, b+24 share an XCD (round-robin dispatch): they take the four output
+  // blocks of one slab, so its G / X rows come from HBM once and from that XCD's L2 after
+  const int blk = (blockIdx.x >> 3) & 3, slab = (blockIdx.x >> 5) * 8 + (blockIdx.x & 7);
+  const int bi = blk & 1, bj = blk >> 1;  // output block rows i in [128 bi, +128), cols j in [128 bj, +128)
+  const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
+  const int64_t r_begin = (int64_t)slab * slab_rows;
+  const int64_t r_end = r_begin + slab_rows < rows ? r_begin + slab_rows : rows;
+  // every slab runs slab_rows / 16 chunks (a multiple of the ring depth): no tail branches;
+  // rows past r_end load a clamped row and are zeroed when staged
+  const int nchunks = (int)(slab_rows / kWgChunk);
+
+  // loader: float4 column group lc (4 columns) of rows lr and lr + 8 of each chunk
+  const int lc = tid & 31, lr = tid >> 5;
+  const float* gsrc = G + 128 * bi + 4 * lc;
+  const float* xsrc = X + 128 * bj + 4 * lc;
+  constexpr int kRing = 3;  // chunks in flight (registers); the loop is unrolled by it
+  f32x4 raw[kRing][4];     // per chunk: G row lr, G row lr+8, X row lr, X row lr+8
+  auto load_chunk = [&](int ch, f32x4 (&r)[4]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int64_t row = r_begin + (int64_t)ch * kWgChunk + lr + 8 * h;
+      row = row < rows ? row : 0;
+      r[h] = *reinterpret_cast<const f32x4*>(gsrc + row * kN);  // rows past the end: zeroed when staged
+      r[2 + h] = *reinterpret_cast<const f32x4*>(xsrc + row * kN);
+    }
+  };
+  f32x4 colsum = {0.f, 0.f, 0.f, 0.f};
+  auto stage_chunk = [&](const f32x4 (&r)[4], int ch, int buf) {
+    const int64_t row0 = r_begin + (int64_t)ch * kWgChunk + lr;
+    const bool ok[2] = {row0 < r_end, row0 + 8 < r_end};
+    f32x4 rv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      rv[q] = r[q];
+      asm volatile("" : "+v"(rv[q]));  // keeps the use (and its vmcnt wait) here, not hoisted
+      rv[q] = ok[q & 1] ? rv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // q: 0,1 = G rows lr, lr+8; 2,3 = X rows lr, lr+8
+      const int row = lr + 8 * (q & 1);
+      lds_char_t* base = lds + buf * kWgBuf + (q >> 1) * 3 * kWgPlane + wg_off(row, 4 * lc);
+      bf16x4 t0, t1, t2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 u0, u1, u2;
+        split3(rv[q][e], u0, u1, u2);
+        t0[e] = u0;
+        t1[e] = u1;
+        t2[e] = u2;
+      }
+      *reinterpret_cast<lds_u64_t*>(base) = __builtin_bit_cast(uint64_t, t0);
+      *reinterpret_cast<lds_u64_t*>(base + kWgPlane) = __builtin_bit_cast(uint64_t, t1);
+      *reinterpret_cast<lds_u64_t*>(base + 2 * kWgPlane) = __builtin_bit_cast(uint64_t, t2);
+    }
+    if (bj == 0) colsum += rv[0] + rv[1];
+  };
+
+  // transposed operand reads: lane (kh, gh, q, p) reads rows 8 kh + q (+4), columns 16 gh + 4 p of
+  // the 32-column tile; it receives column (lane & 31) of rows 8 kh + 0..7
+  const int kh = lane >> 5, gh = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+  auto rd = [&](int buf, int mat, int plane, int tile) {
+    const lds_char_t* b = lds + buf * kWgBuf + mat * 3 * kWgPlane + plane * kWgPlane;
+    const int col = 32 * tile + 16 * gh + 4 * pp;
+#ifdef TT_WABL_NOREAD
+    bf16x8 z;
+    asm volatile("" : "=v"(z) : "v"(b), "v"(col));
+    return z;
+#endif
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(b + wg_off(8 * kh + q, col)));
+    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(b + wg_off(8 * kh + 4 + q, col)));
+    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  };
+  const int wi = wid & 1, wj = wid >> 1;  // wave tiles: i tiles 2 wi, 2 wi + 1; j tiles 2 wj, 2 wj + 1
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) acc[a][0] = acc[a][1] = f32x16{};
+
+#pragma unroll
+  for (int k = 0; k < kRing; ++k) load_chunk(k, raw[k]);
+  stage_chunk(raw[0], 0, 0);
+  // one chunk: its planes are in buffer ch & 1; raw[S] held chunk ch (staged last step) and is
+  // refilled with chunk ch + kRing; raw[(S + 1) % kRing] holds chunk ch + 1, staged now
+  auto step = [&](int ch, f32x4 (&refill)[4], const f32x4 (&next)[4]) {
+    __syncthreads();  // planes of chunk ch visible; everyone is done with chunk ch-1's buffer
+    const int buf = ch & 1;
+    load_chunk(ch + kRing < nchunks ? ch + kRing : ch, refill);  // past the end: a harmless reload
+    bf16x8 ga[2][3], xb[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        ga[t][p] = rd(buf, 0, p, 2 * wi + t);
+        xb[t][p] = rd(buf, 1, p, 2 * wj + t);
+      }
+#ifndef TT_WABL_NOSTAGE
+    stage_chunk(next, ch + 1, buf ^ 1);  // past the end: zeros into the unused buffer
+#else
+    asm volatile("" ::"v"(next[0]), "v"(next[1]), "v"(next[2]), "v"(next[3]));
+#endif
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj) {
+        f32x16& C = acc[ti][tj];
+#ifdef TT_WABL_NOMFMA
+        asm volatile("" ::"v"(ga[ti][0]), "v"(ga[ti][1]), "v"(ga[ti][2]), "v"(xb[tj][0]), "v"(xb[tj][1]), "v"(xb[tj][2]));
+        continue;
+#endif
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][2], xb[tj][0], C, 0, 0, 0);
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][1], xb[tj][1], C, 0, 0, 0);
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][0], xb[tj][2], C, 0, 0, 0);
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][1], xb[tj][0], C, 0, 0, 0);
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][0], xb[tj][1], C, 0, 0, 0);
+        C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][0], xb[tj][0], C, 0, 0, 0);
+      }
+  };
+  for (int ch = 0; ch < nchunks; ch += kRing) {  // unrolled by the ring depth: static ring slots
+#pragma unroll
+    for (int k = 0; k < kRing; ++k) step(ch + k, raw[k], raw[(k + 1) % kRing]);
+  }
+
+  // partial dW of this slab: acc[ti][tj][v] = (i, j) with i = 128 bi + 32 (2 wi + ti) + (v & 3) +
+  // 8 (v >> 2) + 4 kh, j = 128 bj + 32 (2 wj + tj) + (lane & 31)
+  float* pw = part_w + (size_t)slab * kN * kN;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int i = 128 * bi + 32 * (2 * wi + ti) + (v & 3) + 8 * (v >> 2) + 4 * kh;
+        const int j = 128 * bj + 32 * (2 * wj + tj) + (lane & 31);
+#ifdef TT_WABL_NOSTORE
+        if (acc[ti][tj][v] == 12345.678f)
+#endif
+        pw[i * kN + j] = acc[ti][tj][v];
+      }
+  if (bj == 0 && part_b) {  // fold the 8 row groups (lr) of each column group in LDS, fixed order
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem);
+    red[tid] = colsum;
+    __syncthreads();
+    if (tid < 32) {
+      f32x4 t = red[tid];
+#pragma unroll
+      for (int g = 1; g < 8; ++g) t += red[g * 32 + tid];
+      *reinterpret_cast<f32x4*>(part_b + (size_t)slab * kN + 128 * bi + 4 * tid) = t;
+    }
+  }
+}
+
+// dW[i, j] = sum over slabs of the partials, db likewise: 8 loads in flight per thread (slab
+// s goes to partial s % 8), folded in a fixed tree -- deterministic.
+__device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t stride4, int slabs) {
+  f32x4 a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < slabs; s0 += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = s0 + u < slabs ? p[(size_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += v[u];
+  }
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+__global__ __launch_bounds__(64) void head_wgrad_reduce_kernel(const float* __restrict__ part_w,
+                                                               const float* __restrict__ part_b, int slabs,
+                                                               float* __restrict__ dW, float* __restrict__ db) {
+  const int i = blockIdx.x * 64 + threadIdx.x;  // f32x4 index over 256 x 256
+  reinterpret_cast<f32x4*>(dW)[i] = sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, kN * kN / 4, slabs);
+  if (db && i < kN / 4)
+    reinterpret_cast<f32x4*>(db)[i] = sum_slabs(reinterpret_cast<const f32x4*>(part_b) + i, kN / 4, slabs);
+}
+
 }  // namespace
 }  // namespace tt
 
@@ -356,10 +560,26 @@ extern "C" size_t tt_head_planes_bytes(int N, int K) { return (size_t)3 * N * K 
 extern "C" int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream) {
   TT_REQUIRE(N == kN && K == kK, "tt_head_split: only %dx%d weights (got %dx%d)", kN, kK, N, K);
   TT_REQUIRE(W && planes, "null pointer");
-  split_planes_kernel<<<dim3(kN * kK / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
-      W, transpose, static_cast<__bf16*>(planes));
+  SplitJobs jobs{};
+  jobs.W[0] = W;
+  jobs.transpose[0] = transpose;
+  split_planes_kernel<<<dim3(kN * kK / 256, 1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      jobs, static_cast<__bf16*>(planes));
   TT_LAUNCH_CHECK("tt_head_split");
   return TT_OK;
+}
+
+extern "C" int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t stream) {
+  TT_REQUIRE(W1 && W2 && planes, "null pointer");
+  const SplitJobs jobs{{W1, W2, W1, W2}, {0, 0, 1, 1}};
+  split_planes_kernel<<<dim3(kN * kK / 256, 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      jobs, static_cast<__bf16*>(planes));
+  TT_LAUNCH_CHECK("tt_head_split_ff");
+  return TT_OK;
+}
+
+extern "C" size_t tt_head_relu_mask_bytes(int64_t rows) {
+  return (size_t)((rows + kTileRows - 1) / kTileRows) * kSlices * 64 * sizeof(uint32_t);
 }
 
 extern "C" size_t tt_head_gemm_ws_size(int64_t rows, int epi) {
@@ -412,5 +632,39 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
     head_normalize_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
     TT_LAUNCH_CHECK("tt_head_gemm normalize");
   }
+  return TT_OK;
+}
+
+extern "C" size_t tt_head_wgrad_ws_size(int64_t rows, int N) {
+  (void)rows;
+  return (size_t)kWgSlabs * N * (N + 1) * sizeof(float);
+}
+
+extern "C" int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
+                             size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(N == kN, "tt_head_wgrad: only N = %d (got %d)", kN, N);
+  TT_REQUIRE(rows >= 0, "bad rows %lld", (long long)rows);
+  TT_REQUIRE(dW && (rows == 0 || (G && X)), "null pointer");
+  TT_REQUIRE(ws && ws_bytes >= tt_head_wgrad_ws_size(rows, N), "workspace too small (%zu < %zu)", ws_bytes,
+             tt_head_wgrad_ws_size(rows, N));
+  TT_REQUIRE(((reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(dW) |
+               reinterpret_cast<uintptr_t>(db) | reinterpret_cast<uintptr_t>(ws)) & 15) == 0,
+             "buffers must be 16-byte aligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {  // the kernel's clamped loads need row 0 to exist
+    TT_HIP(hipMemsetAsync(dW, 0, (size_t)N * N * sizeof(float), s), "memset dW");
+    if (db) TT_HIP(hipMemsetAsync(db, 0, (size_t)N * sizeof(float), s), "memset db");
+    return TT_OK;
+  }
+  float* part_w = static_cast<float*>(ws);
+  float* part_b = part_w + (size_t)kWgSlabs * kN * kN;
+  // slab rows: a multiple of the chunk, every slab launched (empty slabs write zero partials)
+  constexpr int64_t kQuant = 3 * kWgChunk;  // whole ring turns (kRing chunks) per slab
+  const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + kWgSlabs * kQuant - 1) / (kWgSlabs * kQuant) * kQuant);
+  head_wgrad_kernel<<<dim3(4 * kWgSlabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
+                                                                      db ? part_b : nullptr);
+  TT_LAUNCH_CHECK("tt_head_wgrad");
+  head_wgrad_reduce_kernel<<<dim3(kN * kN / 4 / 64), dim3(64), 0, s>>>(part_w, part_b, kWgSlabs, dW, db);
+  TT_LAUNCH_CHECK("tt_head_wgrad reduce");
   return TT_OK;
 }

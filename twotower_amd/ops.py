@@ -5,6 +5,8 @@ Reference call sites each op replaces are cited per function (paths inside k0r1g
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -88,7 +90,8 @@ class BagPlan:
         dev = ids.device
         self.V, self.E = V, E
         main = torch.cuda.current_stream(dev)
-        side = _lib.side_stream(dev)
+        # TT_PLAN_ON_MAIN=1 (diagnostic): serialise the plan on the main stream
+        side = main if os.environ.get("TT_PLAN_ON_MAIN") == "1" else _lib.side_stream(dev)
         side.wait_stream(main)
         pad = -1 if padding_idx is None else int(padding_idx)
         with torch.cuda.stream(side):
@@ -328,22 +331,39 @@ class TowerHead(torch.autograd.Function):
         require_gpu(x, W1, W2)
         x = _contig_f32(x, "x")
         rows = x.shape[0]
-        mask = torch.empty(rows, HEAD_WIDTH // 32, dtype=torch.int32, device=x.device)
-        h = _head_gemm(x, _planes(W1, False), 0, bias=b1, mask=mask)
+        nb = _lib.lib().tt_head_planes_bytes(HEAD_WIDTH, HEAD_WIDTH)
+        planes = torch.empty(4 * nb, dtype=torch.uint8, device=x.device)  # W1, W2, W1^T, W2^T
+        call("tt_head_split_ff", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), ptr(planes), stream_of(x))
+        mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
+        h = _head_gemm(x, planes[:nb], 0, bias=b1, mask=mask)
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
-        out = _head_gemm(h, _planes(W2, False), 1, bias=b2, norms=norm)
-        ctx.save_for_backward(x, h, mask, out, norm, W1, W2)
+        out = _head_gemm(h, planes[nb:2 * nb], 1, bias=b2, norms=norm)
+        ctx.save_for_backward(x, h, mask, out, norm, planes)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, h, mask, out, norm, W1, W2 = ctx.saved_tensors
+        x, h, mask, out, norm, planes = ctx.saved_tensors
+        nb = planes.numel() // 4
         dout = _contig_f32(dout, "dout")
         dy = torch.empty_like(out)
         call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy), stream_of(out))
-        dh = _head_gemm(dy, _planes(W2, True), 2, mask=mask)
-        dx = _head_gemm(dh, _planes(W1, True), 3) if ctx.needs_input_grad[0] else None
-        return dx, _weight_grad(dh, x), colsum(dh), _weight_grad(dy, h), colsum(dy)
+        dh = _head_gemm(dy, planes[3 * nb:], 2, mask=mask)
+        dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3) if ctx.needs_input_grad[0] else None
+        dW1, db1 = head_wgrad(dh, x)
+        dW2, db2 = head_wgrad(dy, h)
+        return dx, dW1, db1, dW2, db2
+
+
+def head_wgrad(G: torch.Tensor, X: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """(G^T X, G.sum(0)) for (rows, 256) fp32 G, X on the split-bf16 MFMA kernel (tt_head_wgrad)."""
+    rows, N = G.shape
+    dW = torch.empty(N, N, dtype=_FLOAT, device=G.device)
+    db = torch.empty(N, dtype=_FLOAT, device=G.device)
+    nws = _lib.lib().tt_head_wgrad_ws_size(rows, N)
+    ws = torch.empty(nws, dtype=torch.uint8, device=G.device)
+    call("tt_head_wgrad", ptr(G), ptr(X), rows, N, ptr(dW), ptr(db), ptr(ws), nws, stream_of(G))
+    return dW, db
 
 
 def tower_head(x, W1, b1, W2, b2):
