@@ -525,29 +525,45 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
   }
 }
 
-// dW[i, j] = sum over slabs of the partials, db likewise: 8 loads in flight per thread (slab
-// s goes to partial s % 8), folded in a fixed tree -- deterministic.
-__device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t stride4, int slabs) {
+// dW[i, j] = sum over slabs of the partials, db likewise.  Four threads per output float4 take
+// a quarter of the slabs each (8 loads in flight, slab s to partial s % 8, folded in a fixed
+// tree); the quarters are added in a fixed order through LDS -- deterministic.
+constexpr int kRedQ = 4;
+__device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t stride4, int s_begin, int s_end) {
   f32x4 a[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s0 = 0; s0 < slabs; s0 += 8) {
+  for (int s0 = s_begin; s0 < s_end; s0 += 8) {
     f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = s0 + u < slabs ? p[(size_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 8; ++u) v[u] = s0 + u < s_end ? p[(size_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 8; ++u) a[u] += v[u];
   }
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
-__global__ __launch_bounds__(64) void head_wgrad_reduce_kernel(const float* __restrict__ part_w,
-                                                               const float* __restrict__ part_b, int slabs,
-                                                               float* __restrict__ dW, float* __restrict__ db) {
-  const int i = blockIdx.x * 64 + threadIdx.x;  // f32x4 index over 256 x 256
-  reinterpret_cast<f32x4*>(dW)[i] = sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, kN * kN / 4, slabs);
-  if (db && i < kN / 4)
-    reinterpret_cast<f32x4*>(db)[i] = sum_slabs(reinterpret_cast<const f32x4*>(part_b) + i, kN / 4, slabs);
+__global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part_w,
+                                                                const float* __restrict__ part_b, int slabs,
+                                                                float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ f32x4 red[kRedQ][64];
+  const int o = threadIdx.x & 63, qq = threadIdx.x >> 6;  // output float4 of the block, slab quarter
+  const int i = blockIdx.x * 64 + o;
+  const int per = (slabs + kRedQ - 1) / kRedQ;
+  const int s0 = qq * per, s1 = min(slabs, s0 + per);
+  const bool is_b = blockIdx.x == gridDim.x - 1;  // the last block folds db (64 float4 = 256 columns)
+  const f32x4 t = is_b ? (db ? sum_slabs(reinterpret_cast<const f32x4*>(part_b) + o, kN / 4, s0, s1)
+                             : f32x4{0.f, 0.f, 0.f, 0.f})
+                       : sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, kN * kN / 4, s0, s1);
+  red[qq][o] = t;
+  __syncthreads();
+  if (qq == 0) {
+    const f32x4 r = (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
+    if (!is_b)
+      reinterpret_cast<f32x4*>(dW)[i] = r;
+    else if (db)
+      reinterpret_cast<f32x4*>(db)[o] = r;
+  }
 }
 
 }  // namespace
@@ -664,7 +680,7 @@ extern "C" int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N
   head_wgrad_kernel<<<dim3(4 * kWgSlabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
                                                                       db ? part_b : nullptr);
   TT_LAUNCH_CHECK("tt_head_wgrad");
-  head_wgrad_reduce_kernel<<<dim3(kN * kN / 4 / 64), dim3(64), 0, s>>>(part_w, part_b, kWgSlabs, dW, db);
+  head_wgrad_reduce_kernel<<<dim3(kN * kN / 4 / 64 + 1), dim3(256), 0, s>>>(part_w, part_b, kWgSlabs, dW, db);
   TT_LAUNCH_CHECK("tt_head_wgrad reduce");
   return TT_OK;
 }

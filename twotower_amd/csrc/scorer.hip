@@ -685,6 +685,37 @@ constexpr int kTailRows = 64;  // >= the bf16 engine's BJ
 __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t rows, int H, __bf16* __restrict__ xb,
                                           float* __restrict__ norms, int64_t b0, int64_t nb, float& mx) {
   const int lane = lane_id(), wid = threadIdx.x >> 6;
+  if (H == 4 * kWave) {  // one float4 per lane per row: four rows' loads in flight per wave
+    constexpr int U = 4;
+    const int64_t step = nb * 4;
+    for (int64_t r0 = b0 * 4 + wid; r0 < rows; r0 += U * step) {
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + u * step;
+        v[u] = r < rows ? reinterpret_cast<const f32x4*>(x + r * H)[lane] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      float ss[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + u * step;
+        ss[u] = v[u][0] * v[u][0] + v[u][1] * v[u][1] + v[u][2] * v[u][2] + v[u][3] * v[u][3];
+        if (xb && r < rows)
+          reinterpret_cast<bf16x4*>(xb + r * H)[lane] =
+              bf16x4{(__bf16)v[u][0], (__bf16)v[u][1], (__bf16)v[u][2], (__bf16)v[u][3]};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + u * step;
+        const float n = sqrtf(wave_sum(ss[u]));
+        if (r < rows) {
+          if (lane == 0 && norms) norms[r] = n;
+          mx = fmaxf(mx, n);
+        }
+      }
+    }
+    return;
+  }
   for (int64_t r = b0 * 4 + wid; r < rows; r += nb * 4) {
     const f32x4* src = reinterpret_cast<const f32x4*>(x + r * H);
     float ss = 0.f;
@@ -731,6 +762,25 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
 }
 
 
+__device__ __forceinline__ f32x4 load4(const float* p, int lane) { return reinterpret_cast<const f32x4*>(p)[lane]; }
+__device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
+  const bf16x4 v = reinterpret_cast<const bf16x4*>(p)[lane];
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+// sum over s < S of p[s * stride4], in split order (the same order as the generic path), with up
+// to four splits' loads in flight
+__device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t stride4, int S) {
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o += v[u];
+  }
+  return o;
+}
+
 // Merge forward split partials, one wave per query row:
 //   l_i    = sum_s l_s,i - n_pad 2^-shift_i             (pad rows: X = 0 exactly)
 //   lse_i  = (shift_i + log2 l_i) ln 2
@@ -755,6 +805,21 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   const float lse_i = lse2_i * kLn2;
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
+  if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
+    const f32x4 qv = load4(qr, lane), dv = load4(dl, lane);
+    float dot = wave_sum(qv[0] * dv[0] + qv[1] * dv[1] + qv[2] * dv[2] + qv[3] * dv[3]);
+    if (lane == 0) {
+      lse[i] = lse_i;
+      lse2[i] = lse2_i;
+      loss_rows[i] = lse_i - dot * inv_tau;
+    }
+    if (dqu) {
+      const float inv_l = ok ? 1.f / l : NAN;
+      const f32x4 o = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane, B * (H / 4), S);
+      reinterpret_cast<f32x4*>(dqu + i * H)[lane] = o * inv_l - dv;
+    }
+    return;
+  }
   float dot = 0.f;
   for (int h = lane; h < H; h += kWave) dot += (float)qr[h] * (float)dl[h];
   dot = wave_sum(dot);
@@ -785,6 +850,16 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = lane_id();
   const float scale = grad_loss[0] * grad_scale * inv_tau;
+  if (H == 4 * kWave) {
+    if (r < M) {
+      const int64_t qi = r - label_off;
+      f32x4 a = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + r * (H / 4) + lane, M * (H / 4), S);
+      if (qi >= 0 && qi < B) a -= load4(Qmat + qi * H, lane);
+      reinterpret_cast<f32x4*>(dd + r * H)[lane] = a * scale;
+    }
+    if (r < B) reinterpret_cast<f32x4*>(dq + r * H)[lane] = reinterpret_cast<const f32x4*>(dqu + r * H)[lane] * scale;
+    return;
+  }
   if (r < M) {
     const int64_t qi = r - label_off;
     const bool lab = qi >= 0 && qi < B;
