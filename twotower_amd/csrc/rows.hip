@@ -39,6 +39,17 @@ __global__ __launch_bounds__(kBlock) void l2norm_bwd_kernel(const float* __restr
   const int lane = lane_id();
   const float nrm = norm[r];
   const float den = fmaxf(nrm, 1e-12f);
+  if (H == 4 * kWave) {  // one float4 per lane, both rows kept in registers
+    const f32x4 g = reinterpret_cast<const f32x4*>(dout + r * H)[lane];
+    const f32x4 o = reinterpret_cast<const f32x4*>(out + r * H)[lane];
+    const float sx4 = wave_sum(g[0] * o[0] + g[1] * o[1] + g[2] * o[2] + g[3] * o[3]) * den;
+    const float coef4 = (nrm >= 1e-12f && nrm > 0.f) ? sx4 / (den * den * nrm) : 0.f;
+    f32x4 y;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y[k] = g[k] / den - coef4 * (o[k] * den);
+    reinterpret_cast<f32x4*>(dx + r * H)[lane] = y;
+    return;
+  }
   // x = out * den; s_x = sum(dout * x)
   float sx = 0.f;
   for (int c = lane; c < H; c += kWave) sx += dout[r * H + c] * out[r * H + c];
