@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--timing-steps", type=int, default=10, help="eager steps timed per op after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=1024)
+    ap.add_argument("--zipf", type=float, default=None,
+                    help="token ids ~ Zipf(s) over the vocabulary (text-like hot rows); default uniform")
     return ap.parse_args()
 
 
@@ -105,7 +107,8 @@ def main():
     opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
     step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
-    batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev) for k in range(4)]
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev, zipf_s=args.zipf)
+               for k in range(4)]
     nnz = sum(int((t > 0).sum()) for b in batches for t in b) / len(batches)  # tokens per step
 
     for k in range(args.warmup):

@@ -104,6 +104,28 @@ def test_bag_backward_sorted_is_deterministic_and_hot_rows():
     assert rel(g1, ref) < 1e-5
 
 
+@pytest.mark.parametrize("E", [64, 96, 256])
+def test_bag_backward_zipf_long_rows_in_pieces(E):
+    """Zipf(1.1) ids: rows past 128 tokens are summed in pieces (one wave per piece, partials
+    folded in piece order) -- still deterministic and equal to the oracle."""
+    rng = np.random.default_rng(12)
+    V, N, L = 5000, 6000, 64
+    ranks = np.arange(1, V)
+    p = ranks ** -1.1
+    ids_np = rng.choice(ranks, size=(N, L), p=p / p.sum())
+    ids_np[:, 50:] = 0  # padding tail
+    ids = cuda(ids_np)
+    counts = np.bincount(ids_np[ids_np > 0], minlength=V)
+    assert counts.max() > 128 * 256  # the hottest row takes the long-piece length
+    d_pooled = cuda(rng.standard_normal((N, E)).astype(np.float32))
+    _, denom = ops.bag_mean_forward(cuda(rng.standard_normal((V, E)).astype(np.float32)), ids)
+    g1 = ops.bag_mean_backward(d_pooled, denom, ids, V, 0, _lib.TT_SCATTER_SORTED)
+    g2 = ops.bag_mean_backward(d_pooled, denom, ids, V, 0, _lib.TT_SCATTER_SORTED)
+    assert torch.equal(g1, g2)
+    ref = O.bag_mean_bwd(d_pooled.double().cpu().numpy(), denom.double().cpu().numpy(), ids_np, V, 0)
+    assert rel(g1, ref) < 1e-5
+
+
 def test_bag_backward_padding_idx_nonzero():
     rng = np.random.default_rng(4)
     V, N, L, E = 300, 64, 16, 64

@@ -193,6 +193,109 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_mark_kernel(const uint32_t* __
   if (i == n - 1 || keys[i + 1] != k) seg_end[k] = (int32_t)(i + 1);
 }
 
+// Long rows (Zipf-hot ids) are split so no wave walks tens of thousands of tokens: a row with
+// more than kPieceT tokens is cut into pieces of max(kPieceT, ceil(len / kMaxPieces)) tokens;
+// one wave per piece sums its gs rows (token order) into a partial, and the row's reduce wave
+// sums the <= kMaxPieces partials in piece order instead of the tokens.  Deterministic.
+constexpr int kPieceT = 128;
+constexpr int kMaxPieces = 256;
+
+__device__ __forceinline__ int piece_len(int len) {
+  const int t = (len + kMaxPieces - 1) / kMaxPieces;
+  return t > kPieceT ? t : kPieceT;
+}
+
+__global__ __launch_bounds__(kBlock) void bag_piece_count_kernel(const int32_t* __restrict__ seg_start,
+                                                                 const int32_t* __restrict__ seg_end, int64_t V,
+                                                                 int32_t* __restrict__ nch) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r > V) return;
+  if (r == V) {
+    nch[V] = 0;
+    return;
+  }
+  const int len = seg_end[r] - seg_start[r];
+  nch[r] = len > kPieceT ? (len + piece_len(len) - 1) / piece_len(len) : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void bag_piece_list_kernel(const int32_t* __restrict__ seg_start,
+                                                                const int32_t* __restrict__ seg_end,
+                                                                const int32_t* __restrict__ nch,
+                                                                const int32_t* __restrict__ piece_off, int64_t V,
+                                                                int32_t* __restrict__ piece_beg,
+                                                                int32_t* __restrict__ piece_end) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= V) return;
+  const int np = nch[r];
+  if (np == 0) return;
+  const int st = seg_start[r], en = seg_end[r], t = piece_len(en - st), k0 = piece_off[r];
+  for (int k = 0; k < np; ++k) {
+    piece_beg[k0 + k] = st + k * t;
+    piece_end[k0 + k] = min(st + (k + 1) * t, en);
+  }
+}
+
+// One wave per piece (LPR lanes x NV float4 per row, RPI pieces per wave): partial = sum of its
+// tokens' gs rows in token order (U interleaved partial sums folded in a fixed order).
+template <int LPR, int NV, int U>
+__global__ __launch_bounds__(kBlock) void bag_piece_sum_kernel(const int32_t* __restrict__ piece_off, int64_t V,
+                                                               const int32_t* __restrict__ piece_beg,
+                                                               const int32_t* __restrict__ piece_end,
+                                                               const int32_t* __restrict__ vals,
+                                                               const float* __restrict__ gs, int E,
+                                                               float* __restrict__ partial) {
+  constexpr int RPI = kWave / LPR;
+  const int lane = lane_id();
+  const int sub = lane / LPR, c = lane % LPR;
+  const int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  if (pc >= piece_off[V]) return;
+  const int st = piece_beg[pc], en = piece_end[pc];
+  f32x4 part[U][NV];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) part[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = st; e < en; e += U) {
+    int sq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) sq[u] = (e + u < en) ? vals[e + u] : -1;
+    f32x4 v[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const f32x4* rp = reinterpret_cast<const f32x4*>(gs + (int64_t)(sq[u] < 0 ? 0 : sq[u]) * E);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[u][k] = (sq[u] >= 0) ? rp[k * LPR + c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) part[u][k] += v[u][k];
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    f32x4 a = part[0][k];
+#pragma unroll
+    for (int u = 1; u < U; ++u) a += part[u][k];
+    reinterpret_cast<f32x4*>(partial + pc * E)[k * LPR + c] = a;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void bag_piece_sum_generic_kernel(const int32_t* __restrict__ piece_off,
+                                                                       int64_t V, const int32_t* __restrict__ piece_beg,
+                                                                       const int32_t* __restrict__ piece_end,
+                                                                       const int32_t* __restrict__ vals,
+                                                                       const float* __restrict__ gs, int E,
+                                                                       float* __restrict__ partial) {
+  const int64_t pc = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (pc >= piece_off[V]) return;
+  const int st = piece_beg[pc], en = piece_end[pc];
+  for (int c = lane_id(); c < E; c += kWave) {
+    float acc = 0.f;
+    for (int e = st; e < en; ++e) acc += gs[(int64_t)vals[e] * E + c];
+    partial[pc * E + c] = acc;
+  }
+}
+
 // Row reduce: wave owns RPI rows (LPR lanes x NV float4 each); sums gs[seq] over the
 // row's sorted entries (ascending seq => fixed order) and either writes the gradient row or
 // applies AdamW to (table, exp_avg, exp_avg_sq) in place.
@@ -201,13 +304,18 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
     const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
-    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev) {
+    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev,
+    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial) {
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
   const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   if (row >= V) return;
-  const int st = seg_start[row], en = seg_end[row];
+  // a long row sums its piece partials (in piece order) instead of its tokens
+  const int np = nch[row];
+  const bool pieces = np > 0;
+  const int st = pieces ? piece_off[row] : seg_start[row], en = pieces ? st + np : seg_end[row];
+  const float* src = pieces ? partial : gs;
   // AdamW operands first: independent of the segment, so their HBM reads overlap the gather chain.
   f32x4 pv[NV], mv[NV], vv[NV];
   if constexpr (FUSED) {
@@ -230,11 +338,11 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
   for (int e = st; e < en; e += U) {
     int s[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) s[u] = (e + u < en) ? vals[e + u] : -1;
+    for (int u = 0; u < U; ++u) s[u] = (e + u < en) ? (pieces ? e + u : vals[e + u]) : -1;
     f32x4 v[U][NV];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const f32x4* rp = reinterpret_cast<const f32x4*>(gs + (int64_t)(s[u] < 0 ? 0 : s[u]) * E);
+      const f32x4* rp = reinterpret_cast<const f32x4*>(src + (int64_t)(s[u] < 0 ? 0 : s[u]) * E);
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[u][k] = (s[u] >= 0) ? rp[k * LPR + c] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -280,15 +388,18 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_generic_kernel(
     const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
-    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev) {
+    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev,
+    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial) {
   const int lane = lane_id();
   const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (row >= V) return;
   if (FUSED && aa_dev) aa = *aa_dev;
-  const int st = seg_start[row], en = seg_end[row];
+  const int np = nch[row];
+  const bool pieces = np > 0;
+  const int st = pieces ? piece_off[row] : seg_start[row], en = pieces ? st + np : seg_end[row];
   for (int c = lane; c < E; c += kWave) {
     float acc = 0.f;
-    for (int e = st; e < en; ++e) acc += gs[(int64_t)vals[e] * E + c];
+    for (int e = st; e < en; ++e) acc += pieces ? partial[(int64_t)e * E + c] : gs[(int64_t)vals[e] * E + c];
     if constexpr (!FUSED) {
       grad[row * E + c] = acc;
     } else {
@@ -349,10 +460,21 @@ struct BwdWs {
   int32_t* seg_end;
   void* sort_tmp;
   size_t sort_bytes;
+  int32_t* nch;        // V + 1 piece counts (0 = short row)
+  int32_t* piece_off;  // V + 1 exclusive scan of nch (piece_off[V] = number of pieces)
+  int32_t* piece_beg;  // max_pieces token ranges
+  int32_t* piece_end;
+  float* partial;      // max_pieces x E
+  void* scan_tmp;
+  size_t scan_bytes;
+  int64_t max_pieces;
   size_t total;
 };
 
-BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes) {
+// sum over long rows of ceil(len / piece_len) <= sum (len / kPieceT + 1) < 2 n / kPieceT
+int64_t max_pieces_for(int64_t n) { return 2 * ((n + kPieceT - 1) / kPieceT) + 1; }
+
+BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes, size_t scan_bytes) {
   BwdWs w{};
   const size_t n = (size_t)nseq * L;
   size_t off = 0;
@@ -366,7 +488,19 @@ BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes
   const size_t o_gs = take((size_t)nseq * E * 4);
   const size_t o_ss = take((size_t)V * 4), o_se = take((size_t)V * 4);
   const size_t o_tmp = take(sort_bytes);
+  const int64_t mp = max_pieces_for((int64_t)n);
+  const size_t o_nch = take((size_t)(V + 1) * 4), o_po = take((size_t)(V + 1) * 4);
+  const size_t o_pb = take((size_t)mp * 4), o_pe = take((size_t)mp * 4), o_pp = take((size_t)mp * E * 4);
+  const size_t o_stmp = take(scan_bytes);
+  w.max_pieces = mp;
+  w.scan_bytes = scan_bytes;
   if (b) {
+    w.nch = reinterpret_cast<int32_t*>(b + o_nch);
+    w.piece_off = reinterpret_cast<int32_t*>(b + o_po);
+    w.piece_beg = reinterpret_cast<int32_t*>(b + o_pb);
+    w.piece_end = reinterpret_cast<int32_t*>(b + o_pe);
+    w.partial = reinterpret_cast<float*>(b + o_pp);
+    w.scan_tmp = b + o_stmp;
     w.keys_in = reinterpret_cast<uint32_t*>(b + o_ki);
     w.keys_out = reinterpret_cast<uint32_t*>(b + o_ko);
     w.vals_in = reinterpret_cast<int32_t*>(b + o_vi);
@@ -379,6 +513,17 @@ BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes
   w.sort_bytes = sort_bytes;
   w.total = off;
   return w;
+}
+
+size_t scan_tmp_bytes(int64_t V) {
+  size_t bytes = 0;
+  hipError_t e = rocprim::exclusive_scan(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, 0,
+                                         (size_t)(V + 1), rocprim::plus<int32_t>(), (hipStream_t)0, false);
+  if (e != hipSuccess) {
+    set_error("rocprim::exclusive_scan size query: %s", hipGetErrorString(e));
+    return 0;
+  }
+  return bytes;
 }
 
 size_t sort_tmp_bytes(int64_t n, int64_t V) {
@@ -418,18 +563,37 @@ int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, f
   };
   const dim3 block(kBlock);
   switch (E) {
-    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
-    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
-    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
-    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
-    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
-    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev); break;
+    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
+    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
+    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
+    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
+    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
+    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
   }
   TT_LAUNCH_CHECK("bag_bwd_reduce");
   return TT_OK;
 }
 
-// plan: keys/vals -> stable radix sort (key = row id, value = seq) -> segment bounds.
+int launch_piece_sum(const BwdWs& w, int64_t V, int E, hipStream_t s) {
+  auto grid_for = [&](int rpi) {
+    const int64_t waves = (w.max_pieces + rpi - 1) / rpi;
+    return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+  };
+  const dim3 block(kBlock);
+  switch (E) {
+    case 64: bag_piece_sum_kernel<16, 1, 4><<<grid_for(4), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 128: bag_piece_sum_kernel<32, 1, 4><<<grid_for(2), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 256: bag_piece_sum_kernel<64, 1, 4><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 512: bag_piece_sum_kernel<64, 2, 4><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 1024: bag_piece_sum_kernel<64, 4, 2><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    default: bag_piece_sum_generic_kernel<<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+  }
+  TT_LAUNCH_CHECK("bag_piece_sum");
+  return TT_OK;
+}
+
+// plan: keys/vals -> stable radix sort (key = row id, value = seq) -> segment bounds -> the
+// pieces of long rows.
 template <typename IdT>
 int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, const BwdWs& w,
                hipStream_t s) {
@@ -437,7 +601,11 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   const dim3 block(kBlock);
   TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
   TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
-  if (n == 0) return TT_OK;
+  if (n == 0) {  // no pieces: nch = 0 and piece_off = 0 everywhere
+    TT_HIP(hipMemsetAsync(w.nch, 0, (size_t)(V + 1) * 4, s), "memset nch");
+    TT_HIP(hipMemsetAsync(w.piece_off, 0, (size_t)(V + 1) * 4, s), "memset piece_off");
+    return TT_OK;
+  }
   bag_plan_keys_kernel<IdT><<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
       ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in);
   TT_LAUNCH_CHECK("bag_plan_keys");
@@ -448,6 +616,16 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   bag_bwd_mark_kernel<<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
       w.keys_out, n, (uint32_t)V, w.seg_start, w.seg_end);
   TT_LAUNCH_CHECK("bag_bwd_mark");
+  const dim3 rgrid((unsigned)((V + 1 + kBlock - 1) / kBlock));
+  bag_piece_count_kernel<<<rgrid, block, 0, s>>>(w.seg_start, w.seg_end, V, w.nch);
+  TT_LAUNCH_CHECK("bag_piece_count");
+  size_t stmp = w.scan_bytes;
+  TT_HIP(rocprim::exclusive_scan(w.scan_tmp, stmp, w.nch, w.piece_off, 0, (size_t)(V + 1), rocprim::plus<int32_t>(),
+                                 s, false),
+         "rocprim::exclusive_scan");
+  bag_piece_list_kernel<<<rgrid, block, 0, s>>>(w.seg_start, w.seg_end, w.nch, w.piece_off, V, w.piece_beg,
+                                                w.piece_end);
+  TT_LAUNCH_CHECK("bag_piece_list");
   return TT_OK;
 }
 
@@ -460,6 +638,8 @@ int apply_plan(const float* dpooled, const float* denom, int64_t nseq, int64_t V
     bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
         dpooled, denom, nseq, E, w.gs);
     TT_LAUNCH_CHECK("bag_scale_rows");
+    int rc = launch_piece_sum(w, V, E, s);
+    if (rc) return rc;
   }
   return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, aa_dev, s);
 }
@@ -494,14 +674,14 @@ extern "C" int tt_bag_mean_fwd(const float* table, int64_t V, int E, const void*
 
 extern "C" size_t tt_bag_mean_bwd_ws_size(int64_t nseq, int L, int64_t V, int E) {
   const size_t sb = sort_tmp_bytes(nseq * (int64_t)L, V);
-  return carve(nullptr, nseq, L, V, E, sb).total + 256;
+  return carve(nullptr, nseq, L, V, E, sb, scan_tmp_bytes(V)).total + 256;
 }
 
 static BwdWs plan_layout(void* ws, int64_t nseq, int L, int64_t V, int E) {
   if (nseq == 0 || L == 0) nseq = 0, L = 0;
   const size_t sb = nseq > 0 ? sort_tmp_bytes(nseq * (int64_t)L, V) : 0;
   void* base = ws ? reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256)) : nullptr;
-  return carve(base, nseq, L, V, E, sb);
+  return carve(base, nseq, L, V, E, sb, scan_tmp_bytes(V));
 }
 
 static int plan_impl(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld, int64_t V, int E,
