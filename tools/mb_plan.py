@@ -6,9 +6,10 @@ import twotower_amd as tt
 from twotower_amd import ops
 
 B, L, V, E = 8192, 64, 200_000, 256
-q, p, n = tt.data.synthetic_triplets(B, L, V, seed=0, device="cuda")
-ids = torch.cat([q, p, n]).to(torch.int32).contiguous()
-print("tokens", int((ids > 0).sum()), "slots", ids.numel())
+idsets = {}
+for name, z in (("uniform", None), ("zipf1.0", 1.0)):
+    q, p, n = tt.data.synthetic_triplets(B, L, V, seed=0, device="cuda", zipf_s=z)
+    idsets[name] = torch.cat([q, p, n]).to(torch.int32).contiguous()
 
 
 def t(fn, it=10, reps=10):
@@ -34,9 +35,8 @@ def t(fn, it=10, reps=10):
     return e0.elapsed_time(e1) / (it * reps) * 1e3
 
 
-def plan():
-    pl = ops.BagPlan(ids, V, E, 0)
-    pl.wait()
-
-
-print(f"tt_bag_plan: {t(plan):.1f} us")
+for name, ids in idsets.items():
+    def plan():
+        pl = ops.BagPlan(ids, V, E, 0)
+        pl.wait()
+    print(f"tt_bag_plan {name}: {t(plan):.1f} us")
