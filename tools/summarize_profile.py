@@ -19,8 +19,9 @@ from collections import defaultdict
 # kernel-name pattern -> the C-ABI op (bench.py 'abi') it belongs to
 OPS = [
     (r"bag_fwd", "tt_bag_mean_fwd"),
-    (r"bag_plan_keys|bag_bwd_mark|radix_sort|onesweep|rocprim", "tt_bag_plan"),
-    (r"bag_scale_rows|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>", "tt_bag_mean_bwd_adamw_planned"),
+    (r"bag_plan_keys|bag_bwd_mark|bag_piece_count|bag_piece_list|radix_sort|onesweep|rocprim", "tt_bag_plan"),
+    (r"bag_scale_rows|bag_piece_sum|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>",
+     "tt_bag_mean_bwd_adamw_planned"),
     (r"bag_bwd_reduce", "tt_bag_mean_bwd_planned"),
     (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
     (r"score_bf16_kernel<1|score_f32_kernel<1|to_log2|bwd_combine", "tt_inbatch_bwd"),
@@ -30,6 +31,9 @@ OPS = [
     (r"l2norm_bwd", "tt_l2norm_bwd"),
     (r"colsum", "tt_colsum"),
     (r"relu_bwd", "tt_relu_bwd"),
+    (r"head_gemm|head_normalize", "tt_head_gemm"),
+    (r"head_wgrad", "tt_head_wgrad"),
+    (r"split_planes", "tt_head_split_ff"),
     (r"Cijk_", "hipBLASLt GEMM (tower FF)"),
 ]
 
