@@ -466,6 +466,70 @@ def test_graph_step_equals_eager(loss_name):
         assert torch.equal(p1, p2), n_
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_step_side_stream_wgrad_equals_serial(graph):
+    """E = H = 256 (TowerHead): TrainStep computes the head weight gradients on a side stream
+    beside the fused table update; the result equals a plain backward + step (all serial)."""
+    V, E, B, L = 7000, 256, 160, 24
+
+    def build():
+        torch.manual_seed(9)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        return model, opt, tt.losses.build("in_batch", temperature=0.1)
+
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=40 + k, device=DEV) for k in range(4)]
+    m1, o1, l1 = build()
+    m2, o2, l2 = build()
+    s2 = tt.TrainStep(m2, l2, o2, graph=graph, eager_steps=1)
+    for b in batches:
+        loss1 = l1(*m1(*b))
+        o1.zero_grad(set_to_none=True)
+        loss1.backward()
+        assert not o1._side_grads.events  # no owner active: gradients on the current stream
+        o1.step()
+        loss2 = s2(*b)
+        assert torch.equal(loss1.detach(), loss2)
+    assert not o2._side_grads.events and not o2._side_grads.active
+    for (n_, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), n_
+
+
+def test_step_side_stream_wgrad_multi_use_head():
+    """A head applied three times in one step (towers called one by one): autograd sums its
+    weight gradients as they arrive, so they stay on the current stream; still == serial."""
+    V, E, B, L = 5000, 256, 96, 16
+
+    class Separate(torch.nn.Module):
+        def __init__(self, tower):
+            super().__init__()
+            self.tower = tower
+
+        def forward(self, q, p, n):
+            return self.tower(q), self.tower(p), self.tower(n)
+
+    def build():
+        torch.manual_seed(11)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = Separate(tt.encoders.build_tower("mean", emb, hidden_dim=E)).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        return model, opt, tt.losses.build("triplet", margin=0.2)
+
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=60 + k, device=DEV) for k in range(3)]
+    m1, o1, l1 = build()
+    m2, o2, l2 = build()
+    s2 = tt.TrainStep(m2, l2, o2)
+    for b in batches:
+        loss1 = l1(*m1(*b))
+        o1.zero_grad(set_to_none=True)
+        loss1.backward()
+        o1.step()
+        assert torch.equal(loss1.detach(), s2(*b))
+    for (n_, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), n_
+
+
 @pytest.mark.parametrize("tag,H", [("proj", 24), ("noproj", 16)])
 def test_avg_pool_tower_golden(golden, tag, H):
     """AveragePoolingTower (encoders.py:84-155), eval mode, against the reference's output and

@@ -97,16 +97,71 @@ def header_symbols(path: str = HEADER_PATH) -> list[str]:
     return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(tt_\w+)\s*\(", text, flags=re.M)))
 
 
-def side_stream(device: torch.device) -> torch.cuda.Stream:
-    """A per-device auxiliary stream (id-only work that can run beside the forward)."""
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+def side_stream(device: torch.device, role: str = "plan") -> torch.cuda.Stream:
+    """A per-device auxiliary stream.  role "plan": id-only work that runs beside the forward
+    (the bag backward's sort plan); role "wgrad": the tower weight gradients, which run beside
+    the fused table update (see SideGrads)."""
+    dev = torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), role)
     st = _SIDE.get(key)
     if st is None:
-        st = _SIDE[key] = torch.cuda.Stream(device=key)
+        st = _SIDE[key] = torch.cuda.Stream(device=key[0])
     return st
 
 
-_SIDE: dict[int, torch.cuda.Stream] = {}
+_SIDE: dict[tuple, torch.cuda.Stream] = {}
+
+
+class SideGrads:
+    """Gradients produced on a side stream, joined by whoever consumes them.
+
+    An optimizer that can order its own work (optim.AdamW) attaches one SideGrads to each of its
+    dense parameters (``param._tt_side_grads``).  While it is ``active`` -- set by a caller that
+    runs backward and the optimizer step back to back (train_step.TrainStep), so no one reads
+    ``.grad`` in between -- a backward that finds it there computes that parameter's gradient
+    on the "wgrad" side stream and registers the completion event; the optimizer launches work
+    that does not read those gradients first (the fused table scatter + AdamW) and calls
+    ``join()`` on the current stream before reading them.  Otherwise the backward computes on
+    the current stream as usual."""
+
+    def __init__(self):
+        self.events: list[torch.cuda.Event] = []
+        self.grads: list[tuple] = []  # (param, gradient storage) pairs produced on the side
+        self.uses: dict[int, int] = {}  # forward uses per parameter since the last join
+        self.active = False
+
+    def use(self, param: torch.Tensor) -> None:
+        self.uses[id(param)] = self.uses.get(id(param), 0) + 1
+
+    def single_use(self, params) -> bool:
+        """Every parameter entered the graph once (several uses get their gradients summed by
+        autograd as they arrive, before any join)."""
+        return all(self.uses.get(id(p), 0) == 1 for p in params)
+
+    def add(self, event: torch.cuda.Event, grads=()) -> None:
+        self.events.append(event)
+        self.grads.extend((p, g.data_ptr()) for p, g in grads)
+
+    def join(self, stream: torch.cuda.Stream | None = None) -> None:
+        for ev in self.events:
+            (stream or torch.cuda.current_stream()).wait_event(ev)
+        self.events.clear()
+        self.uses.clear()
+        grads, self.grads = self.grads, []
+        for p, at in grads:  # autograd must have handed the side-stream buffer to .grad as is
+            if p.grad is None or p.grad.data_ptr() != at:
+                raise RuntimeError("twotower_amd: a side-stream gradient was copied or accumulated before "
+                                   "its kernel ran (SideGrads needs .grad set to None before backward)")
+
+
+def join_side_grads(params) -> None:
+    """Make the current stream wait for every side-stream gradient of ``params``."""
+    seen = set()
+    for p in params:
+        sg = getattr(p, "_tt_side_grads", None)
+        if sg is not None and id(sg) not in seen:
+            seen.add(id(sg))
+            sg.join()
 
 
 def lib() -> ctypes.CDLL:

@@ -161,6 +161,9 @@ class GradSync:
     def sync(self) -> None:
         if not is_active(self.group):
             return
+        from ._lib import join_side_grads
+
+        join_side_grads(self.params)  # gradients computed on a side stream (ops.TowerHead)
         small = [p for p in self.params if p.grad is not None and p.numel() <= self.bucket_cap]
         large = [p for p in self.params if p.grad is not None and p.numel() > self.bucket_cap]
         works = []

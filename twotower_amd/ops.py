@@ -93,6 +93,8 @@ class BagPlan:
         # TT_PLAN_ON_MAIN=1 (diagnostic): serialise the plan on the main stream
         side = main if os.environ.get("TT_PLAN_ON_MAIN") == "1" else _lib.side_stream(dev)
         side.wait_stream(main)
+        if side is not main:
+            ids.record_stream(side)  # allocated on the current stream, read on the side stream
         pad = -1 if padding_idx is None else int(padding_idx)
         with torch.cuda.stream(side):
             if gather_group is not None:
@@ -108,14 +110,13 @@ class BagPlan:
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
             call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, pad,
                  ptr(self.buf), self.buf.numel(), side.cuda_stream)
-        if not torch.cuda.is_current_stream_capturing():
-            self.buf.record_stream(side)
-            ids.record_stream(side)
         self.ready = torch.cuda.Event()
         self.ready.record(side)
 
     def wait(self) -> None:
-        torch.cuda.current_stream(self.buf.device).wait_event(self.ready)
+        cur = torch.cuda.current_stream(self.buf.device)
+        cur.wait_event(self.ready)
+        self.buf.record_stream(cur)  # allocated on the side stream, read here
 
 
 def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan: BagPlan,
@@ -149,18 +150,22 @@ class BagMeanPool(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, weight, ids, padding_idx, scatter_mode, want_plan=False):
-        pooled, denom = bag_mean_forward(weight, ids)
+        require_gpu(weight, ids)
+        if ids.dim() != 2:
+            raise ValueError(f"ids must be (batch, seq_len), got shape {tuple(ids.shape)}")
         ids = ids.contiguous()
+        pooled, denom = bag_mean_forward(weight, ids)
+        ctx.plan = None
+        if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
+            # forked after the gather: the sort runs beside the towers and the scorer
+            deferred = getattr(weight, "_tt_deferred", None)
+            group = deferred.gather_group if deferred is not None else None
+            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
         ctx.save_for_backward(ids, denom)
         ctx.V = weight.shape[0]
         ctx.padding_idx = padding_idx
         ctx.scatter_mode = scatter_mode
         ctx.weight_ref = weight
-        ctx.plan = None
-        if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
-            deferred = getattr(weight, "_tt_deferred", None)
-            group = deferred.gather_group if deferred is not None else None
-            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
         return pooled
 
     @staticmethod
@@ -339,6 +344,12 @@ class TowerHead(torch.autograd.Function):
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
         out = _head_gemm(h, planes[nb:2 * nb], 1, bias=b2, norms=norm)
         ctx.save_for_backward(x, h, mask, out, norm, planes)
+        sides = {id(getattr(w, "_tt_side_grads", None)) for w in (W1, b1, W2, b2)}
+        ctx.side_grads = W1._tt_side_grads if len(sides) == 1 and hasattr(W1, "_tt_side_grads") else None
+        ctx.params = (W1, b1, W2, b2) if ctx.side_grads is not None else None
+        if ctx.side_grads is not None and ctx.side_grads.active:
+            for w in ctx.params:
+                ctx.side_grads.use(w)
         return out
 
     @staticmethod
@@ -350,16 +361,41 @@ class TowerHead(torch.autograd.Function):
         call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy), stream_of(out))
         dh = _head_gemm(dy, planes[3 * nb:], 2, mask=mask)
         dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3) if ctx.needs_input_grad[0] else None
-        dW1, db1 = head_wgrad(dh, x)
-        dW2, db2 = head_wgrad(dy, h)
+        side = ctx.side_grads
+        N = out.shape[1]
+        dW1, dW2 = (torch.empty(N, N, dtype=_FLOAT, device=dy.device) for _ in range(2))
+        db1, db2 = (torch.empty(N, dtype=_FLOAT, device=dy.device) for _ in range(2))
+        if (side is None or not side.active or not all(ctx.needs_input_grad[1:5]) or not side.single_use(ctx.params)
+                or any(p.grad is not None for p in ctx.params)):  # (an existing .grad accumulates now)
+            head_wgrad(dh, x, dW1, db1)
+            head_wgrad(dy, h, dW2, db2)
+            return dx, dW1, db1, dW2, db2
+        # The optimizer joins these (optim.AdamW), so the weight gradients run on a side stream
+        # beside what follows on this one: dx feeds the fused table scatter + AdamW, an
+        # HBM-bound pass the MFMA-bound weight-gradient kernels overlap.  Autograd must hand the
+        # returned buffers to .grad as they are (checked at the join): no extra references.
+        main = torch.cuda.current_stream(dy.device)
+        aux = _lib.side_stream(dy.device, "wgrad")
+        aux.wait_stream(main)
+        # cross-stream lifetimes (also during capture, where the allocator then defers the
+        # blocks' reuse to the end of the capture instead of handing them to a later node)
+        for t in (dh, dy, x, h, dW1, db1, dW2, db2):
+            t.record_stream(aux)
+        with torch.cuda.stream(aux):
+            head_wgrad(dh, x, dW1, db1)
+            head_wgrad(dy, h, dW2, db2)
+        done = torch.cuda.Event()
+        done.record(aux)
+        side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)))
         return dx, dW1, db1, dW2, db2
 
 
-def head_wgrad(G: torch.Tensor, X: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+def head_wgrad(G: torch.Tensor, X: torch.Tensor, dW: torch.Tensor | None = None,
+               db: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """(G^T X, G.sum(0)) for (rows, 256) fp32 G, X on the split-bf16 MFMA kernel (tt_head_wgrad)."""
     rows, N = G.shape
-    dW = torch.empty(N, N, dtype=_FLOAT, device=G.device)
-    db = torch.empty(N, dtype=_FLOAT, device=G.device)
+    dW = torch.empty(N, N, dtype=_FLOAT, device=G.device) if dW is None else dW
+    db = torch.empty(N, dtype=_FLOAT, device=G.device) if db is None else db
     nws = _lib.lib().tt_head_wgrad_ws_size(rows, N)
     ws = torch.empty(nws, dtype=torch.uint8, device=G.device)
     call("tt_head_wgrad", ptr(G), ptr(X), rows, N, ptr(dW), ptr(db), ptr(ws), nws, stream_of(G))

@@ -33,6 +33,7 @@ class AdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                                       capturable=bool(capturable)))
         self._tables: list[torch.Tensor] = []
+        self._side_grads = _lib.SideGrads()
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
         if fused_tables:
@@ -50,13 +51,25 @@ class AdamW(torch.optim.Optimizer):
                 self._tables.append(w)
                 if mode == "shard":
                     self._shards[id(w)] = distributed.ShardedRows(w, group)
+            # the dense parameters' gradients may then be computed on a side stream beside the
+            # fused table update (ops.TowerHead); step() joins them after launching that update
+            tabs = {id(w) for w in self._tables}
+            for g in self.param_groups:
+                for p in g["params"]:
+                    if id(p) not in tabs:
+                        p._tt_side_grads = self._side_grads
 
     def release_tables(self) -> None:
-        """Return the tables to ordinary dense gradients."""
+        """Return the tables to ordinary dense gradients (and every gradient to the current stream)."""
         for w in self._tables:
             if hasattr(w, "_tt_deferred"):
                 del w._tt_deferred
         self._tables = []
+        for g in self.param_groups:
+            for p in g["params"]:
+                if getattr(p, "_tt_side_grads", None) is self._side_grads:
+                    del p._tt_side_grads
+        self._side_grads.join()
 
     def _state(self, p: torch.Tensor, capturable: bool) -> dict:
         st = self.state[p]
@@ -127,6 +140,7 @@ class AdamW(torch.optim.Optimizer):
     def _step_host(self, group: dict) -> None:
         """torch's default (non-capturable) form: step counters on the host."""
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+        self._side_grads.join()
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
             if deferred is not None and deferred.parts:
@@ -190,10 +204,13 @@ class AdamW(torch.optim.Optimizer):
             dense.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], a))
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
         ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd)
-        ops.adamw_multi(dense)
+        # the fused table updates first: they read no dense gradient, so side-stream gradients
+        # (ops.TowerHead's weight gradients) are still being computed beside them
         for p, st, (ids, dp, den, plan) in fused:
             ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
                                                 self._adam_args(p))
+        self._side_grads.join()
+        ops.adamw_multi(dense)
         for sh in gathers:
             sh.all_gather_params()
 

@@ -33,19 +33,30 @@ class TrainStep:
         self._seed: dict[torch.device, torch.Tensor] = {}  # d(loss) seed of backward, kept on device
 
     def eager(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
-        q, p, n = self.model(queries, positive_docs, negative_docs)
-        loss = self.loss_fn(q, p, n)
-        self.optimizer.zero_grad(set_to_none=True)
-        # backward seeded with the (1/world pre-scaled) unit gradient from a resident tensor:
-        # no fill / scale kernels per step
-        seed = self._seed.get(loss.device)
-        if seed is None:
-            scale = self.sync.loss_scale() if self.sync is not None else 1.0
-            seed = self._seed[loss.device] = torch.full((), scale, dtype=loss.dtype, device=loss.device)
-        loss.backward(seed)
-        if self.sync is not None:
-            self.sync.sync()
-        self.optimizer.step()
+        # forward, backward and step back to back: the optimizer may take gradients computed on
+        # a side stream and join them itself (_lib.SideGrads)
+        side = getattr(self.optimizer, "_side_grads", None)
+        if side is not None:
+            side.join()
+            side.active = True
+        try:
+            q, p, n = self.model(queries, positive_docs, negative_docs)
+            loss = self.loss_fn(q, p, n)
+            self.optimizer.zero_grad(set_to_none=True)
+            # backward seeded with the (1/world pre-scaled) unit gradient from a resident tensor:
+            # no fill / scale kernels per step
+            seed = self._seed.get(loss.device)
+            if seed is None:
+                scale = self.sync.loss_scale() if self.sync is not None else 1.0
+                seed = self._seed[loss.device] = torch.full((), scale, dtype=loss.dtype, device=loss.device)
+            loss.backward(seed)
+            if self.sync is not None:
+                self.sync.sync()
+            self.optimizer.step()
+        finally:
+            if side is not None:
+                side.active = False
+                side.join()  # no-op after the optimizer's own join
         return loss.detach()
 
     def __call__(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
