@@ -195,6 +195,39 @@ int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, 
                    const float* grad_loss, float grad_scale, float* dq, float* dd,
                    void* ws, size_t ws_bytes, tt_stream_t stream);
 
+/* ---- the same loss from explicit, prepared operands (bf16 / bf16_split only), for data
+ * parallelism with candidate-owner gradients (cross-device negatives without a gradient
+ * reduce-scatter): each rank prepares its queries and candidates, the caller all-gathers the
+ * candidate copies and norm maxima (forward) and the query copies and lse2 (backward), and the
+ * backward computes dd for the rank's OWN candidates over every rank's queries.  Replaces the
+ * reference's single-device torch.matmul + F.cross_entropy (twotower/losses.py:107-116) when
+ * the batch is split over ranks.
+ * tt_inbatch_prep_rows: xb (optional) = bf16 copy of x with TT_INBATCH_TAIL_ROWS zero rows after
+ *   the last row ((rows + 64) x H storage); norms (optional, rows) = fp32 row L2 norms;
+ *   max_parts (optional, TT_INBATCH_MAX_PARTS floats) = per-block max norms, unused entries 0.
+ * tt_inbatch_fwd_ex: Qb (B rows) and qnorm of this rank's queries; Db_all (M_all rows + zero
+ *   tail) every rank's candidates; dmax_parts (n_parts) every rank's max_parts; labels i +
+ *   label_off.  Writes lse, lse2 (log2 units), loss_rows, loss (mean over B), dq_unscaled.
+ * tt_inbatch_bwd_ex: Qb_all (nQ_all rows + zero tail) and lse2_all (nQ_all + 64 floats, the
+ *   tail +inf) of every rank's queries; Db (M rows) this rank's candidates; the label of
+ *   candidate j (0 <= j - label_off < B) is query row q_row0 + j - label_off of Qb_all.
+ *   dd[j] = scale sum_i (P_ij - [label]) q~_i over all nQ_all queries, scale =
+ *   grad_loss[0] * grad_scale * inv_tau (every rank's loss seeded alike); dq = scale * dq_unscaled.
+ * ws: tt_inbatch_ex_ws_size(B, M_all, nQ_all, M) bytes serve both passes (partials only). */
+#define TT_INBATCH_TAIL_ROWS 64
+#define TT_INBATCH_MAX_PARTS 512
+int tt_inbatch_prep_rows(const float* x, int64_t rows, int H, void* xb, float* norms, float* max_parts,
+                         tt_stream_t stream);
+size_t tt_inbatch_ex_ws_size(int64_t B, int64_t M_all, int64_t nQ_all, int64_t M, int H, int dtype);
+int tt_inbatch_fwd_ex(const void* Qb, const float* qnorm, int64_t B, const void* Db_all,
+                      const float* dmax_parts, int n_parts, int64_t M_all, int H, int dtype, float inv_tau,
+                      int64_t label_off, int want_grad, float* lse, float* lse2, float* loss_rows,
+                      float* loss, float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream);
+int tt_inbatch_bwd_ex(const void* Qb_all, const float* lse2_all, int64_t nQ_all, int64_t q_row0,
+                      const void* Db, int64_t M, int64_t B, int64_t label_off, int H, int dtype,
+                      float inv_tau, const float* dq_unscaled, const float* grad_loss, float grad_scale,
+                      float* dq, float* dd, void* ws, size_t ws_bytes, tt_stream_t stream);
+
 /* ---- search over indexed documents (inference/search/two_tower.py:72-115, evaluate.py:159-199)
  * tt_cosine_scores: scores[i*nd + j] = F.cosine_similarity(q_i, d_j) with eps 1e-8 (each side
  *   divided by max(|x|, eps), then summed products); q (nq x H), docs (nd x H) fp32, H % 4 == 0.

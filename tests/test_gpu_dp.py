@@ -37,10 +37,15 @@ def _build(loss_name, world, table_sync="auto"):
     torch.manual_seed(7)
     emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
     model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to("cuda:0")
-    kw = {"temperature": 0.1, "cross_device_negatives": world > 1} if loss_name == "in_batch" else {"margin": 0.2}
+    if loss_name.startswith("in_batch"):
+        kw = {"temperature": 0.1, "cross_device_negatives": world > 1,
+              "compute_dtype": "bf16" if loss_name.endswith("bf16") else "fp32"}
+    else:
+        kw = {"margin": 0.2}
     opt = tt.optim.AdamW(model.parameters(), lr=LR, eps=1.0, weight_decay=0.0, fused_tables=True, tables=[emb],
                          capturable=True, table_sync=table_sync)
-    return model, tt.TrainStep(model, tt.losses.build(loss_name, **kw), opt)
+    name = "in_batch" if loss_name.startswith("in_batch") else loss_name
+    return model, tt.TrainStep(model, tt.losses.build(name, **kw), opt)
 
 
 def _batch():
@@ -49,8 +54,8 @@ def _batch():
     return tt.data.synthetic_triplets(WORLD * B, L, V, seed=3, device="cuda:0")
 
 
-def _worker(rank, port, loss_name, table_sync, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TT_INBATCH_DP=inbatch_dp)
     try:
         torch.cuda.set_device(0)
         if rank >= 0:
@@ -60,6 +65,7 @@ def _worker(rank, port, loss_name, table_sync, q):
         full = _batch()
         b = full if rank < 0 else tuple(t[rank * B:(rank + 1) * B] for t in full)
         loss = step(*b).clone()
+        torch.cuda.synchronize()
         if rank >= 0:
             dist.all_reduce(loss)
             loss /= WORLD
@@ -115,3 +121,41 @@ def test_dp_step_equals_global_batch(loss_name, table_sync):
             g = u / (1.0 - abs(u))
             err = abs(g - o_grads[k]).max() / abs(o_grads[k]).max()
             assert err < 1e-5, (name, k, float(err))
+
+
+@pytest.mark.parametrize("inbatch_dp", ["owner", "allgather"])
+def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp):
+    """bf16 scorer with cross-device negatives: candidate-owner gradients (bf16 copies gathered,
+    no gradient reduce-scatter) and the fp32-row all-gather + reduce-scatter form both give the
+    single process's bf16 gradients on the global batch (same bf16 products, other fp32 sum
+    orders), recovered from the parameter change as above."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ref = ctx.Process(target=_worker, args=(-1, 0, "in_batch_bf16", "gather", q))
+    ref.start()
+    _, r_loss, init, r_delta, _ = q.get(timeout=300)
+    ref.join(timeout=60)
+    assert init is not None, r_loss
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, "in_batch_bf16", "gather", q, inbatch_dp)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+
+    def grads(delta):
+        out = {}
+        for k, key in KEYS.items():
+            u = -delta[key].astype("float64") / LR
+            out[k] = u / (1.0 - abs(u))
+        return out
+
+    want = grads(r_delta)
+    for r, loss, _, delta, _ in out:
+        assert delta is not None, loss
+        assert abs(loss - r_loss) < 1e-5, (r, loss, r_loss)
+        got = grads(delta)
+        for k in KEYS:
+            err = abs(got[k] - want[k]).max() / abs(want[k]).max()
+            assert err < 1e-5, (inbatch_dp, r, k, float(err))

@@ -261,6 +261,87 @@ def test_in_batch_vs_oracle(H, B, M, off, dt):
     assert rel(Q.grad, rdq) < tol and rel(D.grad, rdd) < tol
 
 
+def _ex_rank(q, d, qb_all, lse2_all, db_all, parts_all, world, rank, inv_tau, dt, g):
+    """One rank of the candidate-owner data-parallel loss through the explicit-operand ABI,
+    with the 'all-gathered' buffers given (tt_inbatch_prep_rows / _fwd_ex / _bwd_ex)."""
+    B, H = q.shape
+    M = d.shape[0]
+    code = _lib.compute_dtype_code(dt)
+    st = torch.cuda.current_stream().cuda_stream
+    qb = torch.empty(B + 64, H, dtype=torch.bfloat16, device=DEV)
+    qn = torch.empty(B, device=DEV)
+    _lib.call("tt_inbatch_prep_rows", q.data_ptr(), B, H, qb.data_ptr(), qn.data_ptr(), None, st)
+    db = torch.empty(M + 64, H, dtype=torch.bfloat16, device=DEV)
+    ws = torch.empty(_lib.lib().tt_inbatch_ex_ws_size(B, world * M, world * B, M, H, code), dtype=torch.uint8,
+                     device=DEV)
+    lse, lse2, rows = (torch.empty(B, device=DEV) for _ in range(3))
+    loss = torch.empty((), device=DEV)
+    dqu, dq, dd = torch.empty(B, H, device=DEV), torch.empty(B, H, device=DEV), torch.empty(M, H, device=DEV)
+    _lib.call("tt_inbatch_fwd_ex", qb.data_ptr(), qn.data_ptr(), B, db_all.data_ptr(), parts_all.data_ptr(),
+              parts_all.numel(), world * M, H, code, inv_tau, rank * M, 1, lse.data_ptr(), lse2.data_ptr(),
+              rows.data_ptr(), loss.data_ptr(), dqu.data_ptr(), ws.data_ptr(), ws.numel(), st)
+    _lib.call("tt_inbatch_prep_rows", d.data_ptr(), M, H, db.data_ptr(), None, None, st)
+    gl = torch.tensor([g], device=DEV)
+    _lib.call("tt_inbatch_bwd_ex", qb_all.data_ptr(), lse2_all.data_ptr(), world * B, rank * B, db.data_ptr(), M, B,
+              0, H, code, inv_tau, dqu.data_ptr(), gl.data_ptr(), 1.0 / B, dq.data_ptr(), dd.data_ptr(),
+              ws.data_ptr(), ws.numel(), st)
+    return loss, lse2, dq, dd
+
+
+@pytest.mark.parametrize("H,world,B", [(256, 2, 192), (128, 3, 100), (64, 4, 64)])
+@pytest.mark.parametrize("dt", ["bf16", "bf16_split"])
+def test_in_batch_candidate_owner_ranks_equal_global_batch(H, world, B, dt):
+    """Cross-device negatives with candidate-owner gradients, every rank simulated in one
+    process: rank r scores its B queries against all world * 2B candidates (labels offset by
+    r * 2B) and computes the gradient of its own 2B candidates over all world * B queries.
+    Together they must give the single-process loss on the global batch [q_r], [p_r; n_r]
+    rank-major, with each rank's loss seeded by g = 1/world and the loss mean per rank."""
+    rng = np.random.default_rng(H + world)
+    M = 2 * B
+    q = [cuda(_unit(rng, B, H)) for _ in range(world)]
+    d = [cuda(_unit(rng, M, H)) for _ in range(world)]
+    st = torch.cuda.current_stream().cuda_stream
+    # the all-gathered buffers
+    db_all = torch.zeros(world * M + 64, H, dtype=torch.bfloat16, device=DEV)
+    parts_all = torch.empty(world * 512, device=DEV)
+    qb_all = torch.zeros(world * B + 64, H, dtype=torch.bfloat16, device=DEV)
+    for r in range(world):
+        tmp = torch.empty(M + 64, H, dtype=torch.bfloat16, device=DEV)
+        _lib.call("tt_inbatch_prep_rows", d[r].data_ptr(), M, H, tmp.data_ptr(), None,
+                  parts_all[r * 512:].data_ptr(), st)
+        db_all[r * M:(r + 1) * M] = tmp[:M]
+        qb_all[r * B:(r + 1) * B] = q[r].bfloat16()
+    lse2_all = torch.full((world * B + 64,), float("inf"), device=DEV)
+    fwd = []
+    for r in range(world):  # forward of every rank first: lse2 is gathered before any backward
+        out = _ex_rank(q[r], d[r], qb_all, lse2_all, db_all, parts_all, world, r, 10.0, dt, 1.0 / world)
+        fwd.append(out)
+    # lse2 of the _ex_rank call above was computed before lse2_all was filled: redo the
+    # backward half with the gathered lse2 (forward results are deterministic)
+    for r in range(world):
+        lse2_all[r * B:(r + 1) * B] = fwd[r][1]
+    res = [_ex_rank(q[r], d[r], qb_all, lse2_all, db_all, parts_all, world, r, 10.0, dt, 1.0 / world)
+           for r in range(world)]
+    # single process on the global batch: queries [q_0..], candidates [d_0..] rank-major,
+    # query r*B + i labelled with candidate r*M + i (the local label i of rank r)
+    Q = torch.cat(q).requires_grad_(True)
+    D = torch.cat(d).requires_grad_(True)
+    losses, dQ, dD = [], torch.zeros_like(Q), torch.zeros_like(D)
+    for r in range(world):
+        qr = Q.detach()[r * B:(r + 1) * B].clone().requires_grad_(True)
+        Dr = D.detach().clone().requires_grad_(True)
+        lr_ = ops.InBatchSoftmaxLoss.apply(qr, Dr, 10.0, r * M, dt, None)
+        lr_.backward(torch.tensor(1.0 / world, device=DEV))
+        losses.append(lr_.detach())
+        dQ[r * B:(r + 1) * B] += qr.grad
+        dD += Dr.grad
+    for r in range(world):
+        loss, _, dq, dd = res[r]
+        assert abs(loss.item() - losses[r].item()) < 1e-5 * max(1.0, abs(losses[r].item()))
+        assert rel(dq, dQ[r * B:(r + 1) * B].double().cpu().numpy()) < 1e-5
+        assert rel(dd, dD[r * M:(r + 1) * M].double().cpu().numpy()) < 1e-5
+
+
 def test_in_batch_three_tensor_form_and_zero_copy_candidates():
     rng = np.random.default_rng(11)
     B, H = 96, 128

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwotower
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "twotower_amd.h")
 
 TT_IDS_I32, TT_IDS_I64 = 0, 1
+TT_INBATCH_TAIL_ROWS, TT_INBATCH_MAX_PARTS = 64, 512  # twotower_amd.h
 TT_F32, TT_BF16, TT_BF16_SPLIT = 0, 1, 2
 TT_SCATTER_SORTED, TT_SCATTER_ATOMIC = 0, 1
 
@@ -85,6 +86,12 @@ _SIGNATURES = {
                                 _vp, _c_sz, _vp]),
     "tt_inbatch_bwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
                                 _vp, _vp, _c_sz, _vp]),
+    "tt_inbatch_prep_rows": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
+    "tt_inbatch_ex_ws_size": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int]),
+    "tt_inbatch_fwd_ex": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_int, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "tt_inbatch_bwd_ex": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp,
+                                   _vp, _c_f32, _vp, _vp, _vp, _c_sz, _vp]),
 }
 
 _lock = threading.Lock()

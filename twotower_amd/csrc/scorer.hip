@@ -681,6 +681,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
 // rows (kPadBytes - 16 zero bytes, then +inf for the backward lse2).
 constexpr int kMaxPrepBlocks = 512;
 constexpr int kTailRows = 64;  // >= the bf16 engine's BJ
+static_assert(kTailRows == TT_INBATCH_TAIL_ROWS && kMaxPrepBlocks == TT_INBATCH_MAX_PARTS, "ABI constants");
 
 __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t rows, int H, __bf16* __restrict__ xb,
                                           float* __restrict__ norms, int64_t b0, int64_t nb, float& mx) {
@@ -761,6 +762,28 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) dmax_part[b] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
 }
 
+
+// One matrix: optional bf16 copy (with a kTailRows zero tail written by block 0), optional row
+// norms, optional per-block max norm (max_parts[b], gridDim.x <= kMaxPrepBlocks values).
+__global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ x, int64_t rows, int H,
+                                                        __bf16* __restrict__ xb, float* __restrict__ norms,
+                                                        float* __restrict__ max_parts) {
+  __shared__ float wmax[4];
+  if (blockIdx.x == 0 && xb)
+    for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x) xb[rows * H + i] = (__bf16)0.f;
+  float mx = 0.f;
+  prep_rows(x, rows, H, xb, norms, blockIdx.x, gridDim.x, mx);
+  if (!max_parts) return;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  if (lane == 0) wmax[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) max_parts[blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+}
+
+// lse2 tail of the backward engine's R rows: +inf (G = 0 on the zero rows).
+__global__ void fill_inf_kernel(float* __restrict__ p, int n) {
+  if ((int)threadIdx.x < n) p[threadIdx.x] = INFINITY;
+}
 
 __device__ __forceinline__ f32x4 load4(const float* p, int lane) { return reinterpret_cast<const f32x4*>(p)[lane]; }
 __device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
@@ -1009,6 +1032,100 @@ extern "C" size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype) {
   return carve(nullptr, B, M, H, dtype).total + 256;
 }
 
+namespace tt {
+namespace {
+
+// Forward from prepared operands: Rm = candidates (M rows; bf16 copies carry the zero tail),
+// Cm = queries (B rows), qnorm (B), dmax_part (n_dmax per-block maxima of the candidate norms).
+// Writes lse, lse2 (log2 units, B), loss_rows, the mean loss and (want_grad) dq_unscaled.
+int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, int H, const float* qnorm,
+             const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
+             float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
+             hipStream_t s) {
+  const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
+  const float c2 = inv_tau * kLog2e;
+  Ws w{};
+  w.qnorm = const_cast<float*>(qnorm);
+  w.dmax_part = const_cast<float*>(dmax_part);
+  w.pad = const_cast<char*>(pad);
+  w.l_part = l_part;
+  w.acc_part = acc_part;
+  int rc;
+  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
+  const dim3 grid((unsigned)((B + 3) / 4)), block(256);
+  if (dtype == TT_F32)
+    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
+                                                    acc_part, inv_tau, label_off, static_cast<const float*>(Cm),
+                                                    static_cast<const float*>(Rm), lse, lse2, loss_rows, dqu);
+  else
+    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
+                                                     acc_part, inv_tau, label_off, static_cast<const __bf16*>(Cm),
+                                                     static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu);
+  TT_LAUNCH_CHECK("score_fwd_combine");
+  return launch_mean(loss_rows, B, loss, s);
+}
+
+// Backward from prepared operands: Rm = queries (nQ rows + zero tail for bf16), lse2_R (nQ rows
+// + a +inf tail), Cm = candidates (M rows).  The label of candidate j is query row q_label of
+// Qlab (j - label_off in [0, B)); dq = scale * dq_unscaled (B rows).
+int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const void* Cm, int64_t M, const void* Qlab,
+             int64_t B, int64_t label_off, int H, float inv_tau, const float* dqu, const float* grad_loss,
+             float grad_scale, float* dq, float* dd, const char* pad, float* acc_part, hipStream_t s) {
+  const Plan p = plan_for(nQ, M, bj_for(dtype), wg_per_cu(H));
+  const float c2 = inv_tau * kLog2e;
+  Ws w{};
+  w.pad = const_cast<char*>(pad);
+  w.acc_part = acc_part;
+  int rc;
+  if ((rc = dispatch_engine<DD>(H, dtype, Rm, nQ, Cm, M, p, c2, lse2_R, w, 0, s))) return rc;
+  const int64_t rows = std::max(B, M);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  if (dtype == TT_F32)
+    bwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, acc_part,
+                                                    static_cast<const float*>(Qlab), dqu, grad_loss, grad_scale,
+                                                    inv_tau, dq, dd);
+  else
+    bwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, acc_part,
+                                                     static_cast<const __bf16*>(Qlab), dqu, grad_loss, grad_scale,
+                                                     inv_tau, dq, dd);
+  TT_LAUNCH_CHECK("score_bwd_combine");
+  return TT_OK;
+}
+
+int launch_prep_rows(const float* x, int64_t rows, int H, __bf16* xb, float* norms, float* max_parts,
+                     hipStream_t s) {
+  const int g = (int)std::max<int64_t>(1, std::min<int64_t>((rows + 3) / 4, kMaxPrepBlocks));
+  if (max_parts && g < kMaxPrepBlocks) TT_HIP(hipMemsetAsync(max_parts + g, 0, (kMaxPrepBlocks - g) * 4, s), "memset max_parts");
+  prep_rows_kernel<<<dim3((unsigned)g), dim3(256), 0, s>>>(x, rows, H, xb, norms, max_parts);
+  TT_LAUNCH_CHECK("score_prep_rows");
+  return TT_OK;
+}
+
+// partial buffers of the explicit-operand passes
+struct ExWs {
+  float* l_part;
+  float* acc_part;
+  size_t total;
+};
+ExWs carve_ex(void* base, int64_t B, int64_t M_all, int64_t nQ_all, int64_t M, int H, int dtype) {
+  const int BJ = bj_for(dtype);
+  const Plan pf = plan_for(M_all, B, BJ, wg_per_cu(H)), pd = plan_for(nQ_all, M, BJ, wg_per_cu(H));
+  const size_t ol = 0;
+  const size_t oa = align_up((size_t)pf.S * B * 4, 256);
+  const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
+  ExWs w{};
+  if (base) {
+    char* b = reinterpret_cast<char*>(align_up(reinterpret_cast<size_t>(base), 256));
+    w.l_part = reinterpret_cast<float*>(b + ol);
+    w.acc_part = reinterpret_cast<float*>(b + oa);
+  }
+  w.total = oa + parts + 256;
+  return w;
+}
+
+}  // namespace
+}  // namespace tt
+
 extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
                               int64_t label_off, int want_grad, float* lse, float* loss_rows, float* loss,
                               float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream) {
@@ -1020,8 +1137,6 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
-  const float c2 = inv_tau * kLog2e;
   const bool bf = dtype != TT_F32;
   const int gq = (int)std::min<int64_t>((B + 3) / 4, 512);
   const int gd = (int)std::min<int64_t>((M + 3) / 4, kMaxPrepBlocks);
@@ -1031,18 +1146,8 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
-  if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, gd, s))) return rc;
-  const dim3 grid((unsigned)((B + 3) / 4)), block(256);
-  float* dqu = want_grad ? dq_unscaled : nullptr;
-  if (!bf)
-    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, w.qnorm, w.dmax_part, gd, w.l_part,
-                                                    w.acc_part, inv_tau, label_off, q, d, lse, w.lse2, loss_rows, dqu);
-  else
-    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, w.qnorm, w.dmax_part, gd, w.l_part,
-                                                     w.acc_part, inv_tau, label_off, w.Qb, w.Db, lse, w.lse2,
-                                                     loss_rows, dqu);
-  TT_LAUNCH_CHECK("score_fwd_combine");
-  return launch_mean(loss_rows, B, loss, s);
+  return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
+                  want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s);
 }
 
 extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
@@ -1054,23 +1159,63 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const Plan p = plan_for(B, M, bj_for(dtype), wg_per_cu(H));
-  const float c2 = inv_tau * kLog2e;
   const bool bf = dtype != TT_F32;
   // lse in log2 units (ws.lse2) and the pad rows were left in the workspace by the forward
   const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
   const void* Cm = bf ? (const void*)w.Db : (const void*)d;
-  if ((rc = dispatch_engine<DD>(H, dtype, Rm, B, Cm, M, p, c2, w.lse2, w, 0, s))) return rc;
-  const int64_t rows = std::max(B, M);
-  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
-  if (!bf)
-    bwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, w.acc_part, q, dq_unscaled, grad_loss,
-                                                    grad_scale, inv_tau, dq, dd);
-  else
-    bwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, w.acc_part, w.Qb, dq_unscaled,
-                                                     grad_loss, grad_scale, inv_tau, dq, dd);
-  TT_LAUNCH_CHECK("score_bwd_combine");
-  return TT_OK;
+  return bwd_core(dtype, Rm, B, w.lse2, Cm, M, Rm, B, label_off, H, inv_tau, dq_unscaled, grad_loss, grad_scale, dq,
+                  dd, w.pad, w.acc_part, s);
+}
+
+// ---- explicit operands (data parallel with candidate-owner gradients; see twotower_amd.h)
+extern "C" int tt_inbatch_prep_rows(const float* x, int64_t rows, int H, void* xb, float* norms, float* max_parts,
+                                    tt_stream_t stream) {
+  TT_REQUIRE(x && rows >= 0, "bad rows/pointer");
+  TT_REQUIRE(H % 4 == 0 && H >= 4, "H=%d must be a positive multiple of 4", H);
+  TT_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "x must be 16-byte aligned");
+  if (rows == 0 && !max_parts && !xb) return TT_OK;
+  return launch_prep_rows(x, rows, H, static_cast<__bf16*>(xb), norms, max_parts,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" size_t tt_inbatch_ex_ws_size(int64_t B, int64_t M_all, int64_t nQ_all, int64_t M, int H, int dtype) {
+  return carve_ex(nullptr, B, M_all, nQ_all, M, H, dtype).total;
+}
+
+extern "C" int tt_inbatch_fwd_ex(const void* Qb, const float* qnorm, int64_t B, const void* Db_all,
+                                 const float* dmax_parts, int n_parts, int64_t M_all, int H, int dtype, float inv_tau,
+                                 int64_t label_off, int want_grad, float* lse, float* lse2, float* loss_rows,
+                                 float* loss, float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_args(B, M_all, H, dtype, label_off);
+  if (rc) return rc;
+  TT_REQUIRE(dtype != TT_F32, "explicit-operand passes take bf16 operand copies (dtype bf16 / bf16_split)");
+  TT_REQUIRE(Qb && qnorm && Db_all && dmax_parts && lse && lse2 && loss_rows && loss && ws, "null pointer");
+  TT_REQUIRE(n_parts > 0, "n_parts=%d", n_parts);
+  TT_REQUIRE(!want_grad || dq_unscaled, "want_grad needs dq_unscaled");
+  const size_t need = tt_inbatch_ex_ws_size(B, M_all, B, 1, H, dtype);
+  TT_REQUIRE(need <= ws_bytes, "workspace too small: need %zu have %zu", need, ws_bytes);
+  const ExWs w = carve_ex(ws, B, M_all, B, 1, H, dtype);
+  return fwd_core(dtype, Db_all, M_all, Qb, B, H, qnorm, dmax_parts, n_parts, inv_tau, label_off, lse, lse2,
+                  loss_rows, loss, want_grad ? dq_unscaled : nullptr, nullptr, w.l_part, w.acc_part,
+                  reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_inbatch_bwd_ex(const void* Qb_all, const float* lse2_all, int64_t nQ_all, int64_t q_row0,
+                                 const void* Db, int64_t M, int64_t B, int64_t label_off, int H, int dtype,
+                                 float inv_tau, const float* dq_unscaled, const float* grad_loss, float grad_scale,
+                                 float* dq, float* dd, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_args(B, M, H, dtype, label_off);
+  if (rc) return rc;
+  TT_REQUIRE(dtype != TT_F32, "explicit-operand passes take bf16 operand copies (dtype bf16 / bf16_split)");
+  TT_REQUIRE(Qb_all && lse2_all && Db && dq_unscaled && grad_loss && dq && dd && ws, "null pointer");
+  TT_REQUIRE(q_row0 >= 0 && q_row0 + B <= nQ_all, "query rows [%lld, %lld) outside the %lld gathered rows",
+             (long long)q_row0, (long long)(q_row0 + B), (long long)nQ_all);
+  const size_t need = tt_inbatch_ex_ws_size(1, 1, nQ_all, M, H, dtype);
+  TT_REQUIRE(need <= ws_bytes, "workspace too small: need %zu have %zu", need, ws_bytes);
+  const ExWs w = carve_ex(ws, 1, 1, nQ_all, M, H, dtype);
+  const void* Qlab = static_cast<const __bf16*>(Qb_all) + q_row0 * H;
+  return bwd_core(dtype, Qb_all, nQ_all, lse2_all, Db, M, Qlab, B, label_off, H, inv_tau, dq_unscaled, grad_loss,
+                  grad_scale, dq, dd, nullptr, w.acc_part, reinterpret_cast<hipStream_t>(stream));
 }
 
 #ifdef TT_SCORER_TRACE

@@ -57,13 +57,13 @@ def reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> Non
     dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
 
 
-def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
-    """out = cat over ranks of inp (rank-major); inp may be this rank's slab of out."""
+def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
+    """out = cat over ranks of inp (rank-major); inp may be this rank's slab of out.  With
+    async_op the work handle is returned (wait() before reading out), else None."""
     if _is_gloo(group):
         parts = list(out.chunk(dist.get_world_size(group)))
-        dist.all_gather(parts, inp.contiguous(), group=group)  # writes the chunks (views of out) in place
-        return
-    dist.all_gather_into_tensor(out, inp, group=group)
+        return dist.all_gather(parts, inp.contiguous(), group=group, async_op=async_op)  # chunks are views of out
+    return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
 class ShardedRows:

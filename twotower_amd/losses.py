@@ -76,8 +76,9 @@ def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *arg
                                   group=None) -> torch.Tensor:
     """CE over S = q d^T / temperature with labels arange(B) (losses.py:88-118), on the fused
     MFMA scorer.  Third positional argument: a negatives tensor (train.py:133 call) or the
-    reference's positional temperature.  ``cross_device_negatives`` all-gathers the candidates
-    of every data-parallel rank (RCCL) and offsets the labels by this rank's slot."""
+    reference's positional temperature.  ``cross_device_negatives`` scores every data-parallel
+    rank's candidates (RCCL all-gather, labels offset by this rank's slot); at bf16 each rank
+    then computes the gradient of its own candidates (ops.InBatchSoftmaxLossOwned)."""
     if args:
         if isinstance(args[0], torch.Tensor):
             if len(args) > 1:
@@ -91,10 +92,22 @@ def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *arg
             temperature = args[0]
     label_off = 0
     if cross_device_negatives:
-        from .distributed import gather_candidates
+        from . import distributed
 
-        d_emb, label_off = gather_candidates(d_emb, group=group)
+        if (distributed.is_active(group) and compute_dtype != "fp32" and _owner_gradients()):
+            # bf16 candidate copies all-gathered, candidate gradients computed by their owners
+            return ops.InBatchSoftmaxLossOwned.apply(q_emb, d_emb, 1.0 / float(temperature), compute_dtype, None,
+                                                     group)
+        d_emb, label_off = distributed.gather_candidates(d_emb, group=group)
     return ops.in_batch_softmax_loss(q_emb, d_emb, temperature, label_off=label_off, compute_dtype=compute_dtype)
+
+
+def _owner_gradients() -> bool:
+    """Cross-device negatives at bf16: candidate-owner gradients (default) or TT_INBATCH_DP=
+    allgather for the fp32-row all-gather + gradient reduce-scatter form (the fp32 path)."""
+    import os
+
+    return os.environ.get("TT_INBATCH_DP", "owner") != "allgather"
 
 
 LOSS_REGISTRY = {

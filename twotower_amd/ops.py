@@ -561,6 +561,85 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         return grad, None, None, None, None
 
 
+class InBatchSoftmaxLossOwned(torch.autograd.Function):
+    """Data-parallel in-batch loss with cross-device negatives and candidate-owner gradients
+    (bf16 / bf16_split).  Forward: every rank's bf16 candidate copies and norm maxima are
+    all-gathered (half the bytes of fp32 rows) and this rank's queries are scored against all
+    of them.  The bf16 query copies and lse2 are all-gathered asynchronously (overlapping the
+    forward scorer); the backward computes the gradient of this rank's OWN candidates over every
+    rank's queries, so no candidate gradient is reduce-scattered.  Every rank's loss must be
+    seeded alike (TrainStep: 1/world), as the remote queries' terms take this rank's seed."""
+
+    @staticmethod
+    def forward(ctx, q, d, inv_tau, compute_dtype, grad_scale, group):
+        from .distributed import all_gather_rows
+
+        require_gpu(q, d)
+        q, d = _contig_f32(q, "q"), _contig_f32(d, "d")
+        B, H = q.shape
+        M = d.shape[0]
+        if d.shape[1] != H:
+            raise ValueError(f"q is (B, {H}) but d is {tuple(d.shape)}")
+        dt = _lib.compute_dtype_code(compute_dtype)
+        if dt == _lib.TT_F32:
+            raise ValueError("candidate-owner gradients need a bf16 compute dtype")
+        world, rank = torch.distributed.get_world_size(group), torch.distributed.get_rank(group)
+        dev, T, P = q.device, _lib.TT_INBATCH_TAIL_ROWS, _lib.TT_INBATCH_MAX_PARTS
+        st = stream_of(q)
+        bf = torch.bfloat16
+        qb = torch.empty(B + T, H, dtype=bf, device=dev)
+        qnorm = torch.empty(B, dtype=_FLOAT, device=dev)
+        call("tt_inbatch_prep_rows", ptr(q), B, H, ptr(qb), ptr(qnorm), None, st)
+        db = torch.empty(M + T, H, dtype=bf, device=dev)
+        parts = torch.empty(P, dtype=_FLOAT, device=dev)
+        call("tt_inbatch_prep_rows", ptr(d), M, H, ptr(db), None, ptr(parts), st)
+        # bf16 rows travel as bytes (any backend), rank-major; the zero tail stays local
+        db_all = torch.empty(world * M + T, H, dtype=bf, device=dev)
+        db_all[world * M:].zero_()
+        all_gather_rows(db_all[:world * M].view(torch.uint8), db[:M].view(torch.uint8), group)
+        parts_all = torch.empty(world * P, dtype=_FLOAT, device=dev)
+        all_gather_rows(parts_all, parts, group)
+        qb_all = torch.empty(world * B + T, H, dtype=bf, device=dev)
+        qb_all[world * B:].zero_()
+        w_q = all_gather_rows(qb_all[:world * B].view(torch.uint8), qb[:B].view(torch.uint8), group, async_op=True)
+        want_grad = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        ws = torch.empty(_lib.lib().tt_inbatch_ex_ws_size(B, world * M, world * B, M, H, dt), dtype=torch.uint8,
+                         device=dev)
+        lse = torch.empty(B, dtype=_FLOAT, device=dev)
+        lse2 = torch.empty(B, dtype=_FLOAT, device=dev)
+        rows = torch.empty(B, dtype=_FLOAT, device=dev)
+        loss = torch.empty((), dtype=_FLOAT, device=dev)
+        dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
+        call("tt_inbatch_fwd_ex", ptr(qb), ptr(qnorm), B, ptr(db_all), ptr(parts_all), world * P, world * M, H, dt,
+             float(inv_tau), rank * M, int(want_grad), ptr(lse), ptr(lse2), ptr(rows), ptr(loss), ptr(dqu), ptr(ws),
+             ws.numel(), st)
+        lse2_all = torch.empty(world * B + T, dtype=_FLOAT, device=dev)
+        lse2_all[world * B:].fill_(float("inf"))
+        w_l = all_gather_rows(lse2_all[:world * B], lse2, group, async_op=True)
+        ctx.works = (w_q, w_l)
+        # internal buffers (not inputs or outputs), some still being filled by the async
+        # all-gathers: kept on ctx rather than version-checked by save_for_backward
+        ctx.bufs = (qb_all, lse2_all, db, dqu, ws) if want_grad else None
+        ctx.meta = (B, M, H, dt, float(inv_tau), world, rank, float(1.0 / B) if grad_scale is None else float(grad_scale))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        qb_all, lse2_all, db, dqu, ws = ctx.bufs
+        ctx.bufs = None
+        B, M, H, dt, inv_tau, world, rank, grad_scale = ctx.meta
+        for w in ctx.works:
+            if w is not None:
+                w.wait()
+        ctx.works = ()
+        g = g.to(_FLOAT).contiguous().reshape(1)
+        dq = torch.empty(B, H, dtype=_FLOAT, device=db.device)
+        dd = torch.empty(M, H, dtype=_FLOAT, device=db.device)
+        call("tt_inbatch_bwd_ex", ptr(qb_all), ptr(lse2_all), world * B, rank * B, ptr(db), M, B, 0, H, dt, inv_tau,
+             ptr(dqu), ptr(g), grad_scale, ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(db))
+        return dq, dd, None, None, None, None
+
+
 def in_batch_softmax_loss(q: torch.Tensor, d: torch.Tensor, temperature: float = 0.1, label_off: int = 0,
                           compute_dtype="fp32", grad_scale: float | None = None) -> torch.Tensor:
     return InBatchSoftmaxLoss.apply(q, d, 1.0 / float(temperature), label_off, compute_dtype, grad_scale)
