@@ -65,6 +65,9 @@ def parse():
                     help="replay the step as one HIP graph (auto: on for a single GPU)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard"],
+                    help="N ranks: table update from gathered ids + row grads (gather) or row-sharded AdamW "
+                         "(shard); auto picks gather up to 4 ranks")
     ap.add_argument("--timing-steps", type=int, default=10, help="eager steps timed per op after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=1024)
@@ -104,7 +107,8 @@ def main():
     use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
     # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
     # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
-    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
+                         table_sync=args.table_sync)
     step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
     batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev, zipf_s=args.zipf)
@@ -226,6 +230,7 @@ def main():
         "config": {"workload": cfg["workload"] + ("; candidates all-gathered over ranks" if world > 1 else ""),
                    "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
                    "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
+                   "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if world > 1 else "local"),
                    "hip_graph": use_graph},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "roofline": roofline,
