@@ -28,11 +28,17 @@ import twotower_amd as tt  # noqa: E402
 from twotower_amd import _lib  # noqa: E402
 
 CONFIGS = {
-    # name: V, E(=H), L, B, scorer dtype
-    "c3": dict(V=200_000, d=256, L=64, B=8192, dtype="bf16", workload="C3: vocab 200k, d 256, seq 64, batch 8192, "
-               "in-batch negatives (M = 2B), bf16 MFMA scorer, fp32 embedding grad"),
-    "c2": dict(V=50_000, d=128, L=32, B=4096, dtype="fp32", workload="C2: vocab 50k, d 128, seq 32, batch 4096, "
-               "in-batch negatives (M = 2B), fp32"),
+    # name: V, E(=H), L, B (queries per GPU), scorer dtype, loss, negatives per query
+    "c3": dict(V=200_000, d=256, L=64, B=8192, dtype="bf16", loss="in_batch", negatives=1,
+               workload="C3: vocab 200k, d 256, seq 64, batch 8192, in-batch negatives (M = 2B), bf16 MFMA scorer, "
+               "fp32 embedding grad"),
+    "c2": dict(V=50_000, d=128, L=32, B=4096, dtype="fp32", loss="in_batch", negatives=1,
+               workload="C2: vocab 50k, d 128, seq 32, batch 4096, in-batch negatives (M = 2B), fp32"),
+    # BASELINE.json configs[4] per GPU: presets/multi_pos_multi_neg.yml shape (1 positive + 4 negatives
+    # per query = 6 sequences per query), vocab 1M; per-sample loss, so ranks exchange gradients only
+    "c5": dict(V=1_000_000, d=256, L=64, B=8192, dtype="fp32", loss="multiple_negatives", negatives=4,
+               workload="C5: vocab 1M, d 256, seq 64, batch 8192 queries x (1 positive + 4 negatives), "
+               "multiple_negatives InfoNCE (cosine / 0.1, fp32), sorted scatter-add embedding grad fused with AdamW"),
 }
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
@@ -102,8 +108,15 @@ def main():
     torch.manual_seed(1234)  # identical initial weights on every rank
     emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=d)
     model = tt.build_two_tower("mean", emb, hidden_dim=d, tied_weights=True).to(dev)
-    loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
-                              cross_device_negatives=world > 1)
+    K = cfg["negatives"]
+    if cfg["loss"] == "in_batch":
+        loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
+                                  cross_device_negatives=world > 1)
+    else:  # multiple_negatives over (q, p, n viewed as (B, K, H)); per-sample, no cross-rank exchange
+        mn = tt.losses.build("multiple_negatives", temperature=0.1)
+
+        def loss_fn(q, p, n):
+            return mn(q, p, n.view(q.shape[0], K, q.shape[1]))
     use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
     # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
     # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
@@ -111,7 +124,8 @@ def main():
                          table_sync=args.table_sync)
     step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
-    batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev, zipf_s=args.zipf)
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev, zipf_s=args.zipf,
+                                          negatives=K)
                for k in range(4)]
     nnz = sum(int((t > 0).sum()) for b in batches for t in b) / len(batches)  # tokens per step
 
@@ -156,8 +170,8 @@ def main():
         return
 
     # ---- per-op device times (HIP events on the launch stream) -> rooflines
-    nseq = 3 * B
-    M = 2 * B * world
+    nseq = (2 + K) * B
+    M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1
     kernels = []
 
     def add(name, key, algo, unit, peak, bound, per_launch_note, side_stream=False):
@@ -191,6 +205,10 @@ def main():
         "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ")
     add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
         "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q)")
+    add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
+        HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
+    add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
+        "q, p, negatives read + their gradients written 2*(2 + K)*B*H*4 bytes")
     add("dense AdamW (tower FF, multi-tensor)", "tt_adamw_multi", 28 * sum(p.numel() for n_, p in model.named_parameters()
                                                       if "embedding" not in n_), "GB/s", HBM_PEAK_GBS, "hbm",
         "28 bytes per parameter")
@@ -209,10 +227,13 @@ def main():
 
         cb = args.cpu_batch
         cpu_batches = [tuple(t[:cb].to("cpu", torch.int64) for t in b) for b in batches[:2]]
-        r = time_cpu_step(V, d, d, cpu_batches, loss="in_batch", min_seconds=args.cpu_seconds)
+        if K > 1:
+            cpu_batches = [tuple(t.to("cpu", torch.int64) for t in (b[0][:cb], b[1][:cb], b[2][:cb * K]))
+                           for b in batches[:2]]
+        r = time_cpu_step(V, d, d, cpu_batches, loss=cfg["loss"], min_seconds=args.cpu_seconds)
         cpu = {"value": round(r["pairs_per_s"], 1), "unit": "pairs/s", "cores": r["threads"], "kind": "port",
                "sample": f"torch-CPU restatement of the reference step (oracle/cpu_step.py), same V/d/L, batch "
-                         f"{cb} instead of {B}, in-batch loss fp32, {r['steps']} steps in {r['seconds']:.1f}s"}
+                         f"{cb} instead of {B}, {cfg['loss']} loss fp32, {r['steps']} steps in {r['seconds']:.1f}s"}
 
     line = {
         "metric": "(query,doc) pairs/sec whole node at B=8192 d=256; HBM GB/s on embed gather",

@@ -35,6 +35,10 @@ def ref_loss(name: str, q, p, n, temperature=0.1, margin=0.2):
         d = torch.cat([p, n])
         logits = (q @ d.T) / temperature
         return F.cross_entropy(logits, torch.arange(q.shape[0]))
+    if name == "multiple_negatives":                                     # losses.py:47-85, n (B*K, H)
+        d = torch.cat([p.unsqueeze(1), n.view(q.shape[0], -1, q.shape[1])], dim=1)
+        logits = F.cosine_similarity(q.unsqueeze(1).expand_as(d), d, dim=2) / temperature
+        return F.cross_entropy(logits, torch.zeros(q.shape[0], dtype=torch.long))
     raise ValueError(name)
 
 

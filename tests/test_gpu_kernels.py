@@ -794,3 +794,50 @@ def test_head_wgrad_vs_fp64(rows):
     assert rel(db, g.astype(np.float64).sum(0)) < 1e-5
     dW2, db2 = ops.head_wgrad(cuda(g), cuda(x))
     assert torch.equal(dW, dW2) and torch.equal(db, db2)  # deterministic
+
+
+def test_c5_shaped_step_matches_cpu_oracle():
+    """The bench's C5 step shape (1 positive + 4 negatives per query, multiple_negatives loss,
+    E = H = 256 TowerHead, fused table AdamW, graph replay) against the CPU restatement of the
+    reference step (oracle/cpu_step.py: nn.Embedding + masked mean + FF + F.normalize, the
+    reference's multiple_negatives_loss, torch.optim.AdamW): per-step losses 1e-5 and the
+    parameter change over three steps within 1e-5 of its scale (+ 4 fp32 ulp of the parameter).  eps = 1 on both sides keeps
+    AdamW's update smooth in the gradient (with eps = 1e-8 an element whose gradient is near
+    eps flips its ~lr-sized update on rounding noise, as between any two fp32 orders)."""
+    from oracle.cpu_step import RefTower, ref_loss
+
+    V, E, B, L, K = 3000, 256, 48, 24, 4
+    torch.manual_seed(11)
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+    ref = RefTower(V, E, E).double()
+    sd = {k.split("query_tower.")[1].replace("embedding.embedding", "embedding"): v.detach().cpu().double()
+          for k, v in model.state_dict().items() if k.startswith("query_tower.")}
+    ref.load_state_dict(sd)
+    init = {k: v.clone() for k, v in sd.items()}
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, eps=1.0, fused_tables=True, tables=[emb], capturable=True)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-3, eps=1.0)
+    mn = tt.losses.build("multiple_negatives", temperature=0.1)
+    step = tt.TrainStep(model, lambda q, p, n: mn(q, p, n.view(q.shape[0], K, q.shape[1])), opt, graph=True,
+                        eager_steps=1)
+    for k in range(3):
+        b = tt.data.synthetic_triplets(B, L, V, seed=70 + k, device=DEV, negatives=K)
+        assert b[2].shape == (K * B, L)
+        got = float(step(*b).item())
+        q, p, n = (t.cpu().long() for t in b)
+        rl = ref_loss("multiple_negatives", ref(q), ref(p), ref(n))
+        ropt.zero_grad()
+        rl.backward()
+        ropt.step()
+        assert abs(got - float(rl)) < 1e-5 * max(1.0, abs(float(rl))), (k, got, float(rl))
+    rsd = ref.state_dict()
+    for k, v in model.state_dict().items():
+        if not k.startswith("query_tower."):
+            continue
+        key = k.split("query_tower.")[1].replace("embedding.embedding", "embedding")
+        want = rsd[key] - init[key]
+        # 1e-5 of the change, plus the fp32 storage of the parameter itself (a few ulp of |p|:
+        # the embedding rows move by ~3e-5 |p| of weight decay, below fp32 resolution of p)
+        diff = (v.double().cpu() - init[key] - want).abs()
+        tol = 1e-5 * want.abs().max() + 4 * 2.0 ** -24 * rsd[key].abs()
+        assert bool((diff <= tol).all()), (k, float((diff / tol).max()))

@@ -28,8 +28,10 @@ def _ids(gen, B, L, V, lengths, dtype, device, zipf_s=None):
 
 
 def synthetic_triplets(B: int, L: int, V: int, *, seed: int = 0, device="cuda", dtype=torch.int32,
-                       query_len=(3, 12), doc_len=None, zipf_s=None):
-    """One batch (q, p, n), each (B, L) ids with trailing PAD = 0."""
+                       query_len=(3, 12), doc_len=None, zipf_s=None, negatives: int = 1):
+    """One batch (q, p, n) of ids with trailing PAD = 0: q and p (B, L), n (negatives * B, L)
+    with the negatives of query b in rows b * negatives + k (multi_pos_multi_neg shape when
+    negatives > 1, viewed as (B, negatives, L) by the multiple_negatives loss)."""
     doc_len = doc_len or (max(1, L // 2), L)
     gens = []
     for k in range(3):
@@ -38,10 +40,11 @@ def synthetic_triplets(B: int, L: int, V: int, *, seed: int = 0, device="cuda", 
         gens.append(g)
     ql = _lengths(gens[0], B, min(query_len[0], L), min(query_len[1], L), device)
     pl = _lengths(gens[1], B, doc_len[0], doc_len[1], device)
-    nl = _lengths(gens[2], B, doc_len[0], doc_len[1], device)
+    nb = B * int(negatives)
+    nl = _lengths(gens[2], nb, doc_len[0], doc_len[1], device)
     return (_ids(gens[0], B, L, V, ql, dtype, device, zipf_s),
             _ids(gens[1], B, L, V, pl, dtype, device, zipf_s),
-            _ids(gens[2], B, L, V, nl, dtype, device, zipf_s))
+            _ids(gens[2], nb, L, V, nl, dtype, device, zipf_s))
 
 
 def tokens_per_triplet(L: int, query_len=(3, 12), doc_len=None) -> float:
