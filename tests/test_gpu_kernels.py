@@ -225,6 +225,27 @@ def test_multiple_negatives_golden(golden):
     assert rel(q.grad, g["mn_dq"]) < 1e-5 and rel(p.grad, g["mn_dp"]) < 1e-5 and rel(negs.grad, g["mn_dnegs"]) < 1e-5
 
 
+@pytest.mark.parametrize("H,N", [(256, 1), (256, 4), (256, 7), (256, 15), (256, 16), (128, 4)])
+def test_multiple_negatives_vs_oracle(H, N):
+    """multiple_negatives_loss against the fp64 oracle: the H = 256 float4 paths (N <= 4 and
+    N <= 15) and the generic kernel (N = 16, H = 128), with an all-zero query and an all-zero
+    negative (cosine eps clamp, zero norm gradient)."""
+    rng = np.random.default_rng(H * 100 + N)
+    B = 300
+    q = rng.standard_normal((B, H)).astype(np.float32)
+    p = rng.standard_normal((B, H)).astype(np.float32)
+    negs = rng.standard_normal((B, N, H)).astype(np.float32)
+    q[5] = 0.0
+    negs[7, N - 1] = 0.0
+    Q, P, Nn = (cuda(x).requires_grad_(True) for x in (q, p, negs))
+    loss = tt.losses.multiple_negatives_loss(Q, P, Nn, temperature=0.1)
+    loss.backward()
+    rl, (rdq, rdp, rdn) = O.multi_neg_fwd_bwd(q.astype(np.float64), p.astype(np.float64), negs.astype(np.float64),
+                                              temperature=0.1)
+    assert abs(loss.item() - rl) < 1e-5 * max(1.0, abs(rl))
+    assert rel(Q.grad, rdq) < 1e-5 and rel(P.grad, rdp) < 1e-5 and rel(Nn.grad, rdn) < 1e-5
+
+
 # ---------------------------------------------------------------------------------------------
 # in-batch scorer
 def test_in_batch_golden(golden):

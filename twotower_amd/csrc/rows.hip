@@ -253,6 +253,107 @@ __global__ __launch_bounds__(kBlock) void multi_neg_bwd_kernel(const float* __re
   }
 }
 
+// H = 256 fast path (C5: B x (1 + N) documents of 1 KiB): one float4 per lane, the query and all
+// 1 + N document rows loaded up front (register arrays indexed by unrolled constants, NMAX
+// documents at most), every partial dot / squared norm reduced in one batch of wave sums, and
+// each gradient row written once (no read-modify-write of dq).  Same formulas as the generic
+// kernels above; the column sum order differs (4 consecutive columns per lane).
+__device__ __forceinline__ float dot4(const f32x4& a, const f32x4& b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+}
+
+template <int NMAX>
+struct MnRows {
+  f32x4 q, d[NMAX + 1];
+  CosStats st[NMAX + 1];
+};
+
+template <int NMAX>
+__device__ __forceinline__ void mn_load_stats(const float* __restrict__ q, const float* __restrict__ p,
+                                              const float* __restrict__ negs, int64_t r, int N, MnRows<NMAX>& m) {
+  const int lane = lane_id();
+  m.q = reinterpret_cast<const f32x4*>(q + r * 256)[lane];
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) m.d[k] = reinterpret_cast<const f32x4*>(mn_doc(p, negs, r, k, N, 256))[lane];
+  const float qq = wave_sum(dot4(m.q, m.q));
+  const float n1 = sqrtf(qq);
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) {
+      m.st[k].dot = wave_sum(dot4(m.q, m.d[k]));
+      m.st[k].n1 = n1;
+      m.st[k].n2 = sqrtf(wave_sum(dot4(m.d[k], m.d[k])));
+    }
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(kBlock) void multi_neg_fwd_h256_kernel(const float* __restrict__ q,
+                                                                    const float* __restrict__ p,
+                                                                    const float* __restrict__ negs, int64_t B, int N,
+                                                                    float inv_tau, float* __restrict__ loss_rows) {
+  const int64_t r = wave_row();
+  if (r >= B) return;
+  MnRows<NMAX> m;
+  mn_load_stats<NMAX>(q, p, negs, r, N, m);
+  float z[NMAX + 1], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) {
+      z[k] = cos_value(m.st[k]) * inv_tau;
+      mx = fmaxf(mx, z[k]);
+    }
+  float se = 0.f;
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) se += expf(z[k] - mx);
+  if (lane_id() == 0) loss_rows[r] = mx + logf(se) - z[0];
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(kBlock) void multi_neg_bwd_h256_kernel(const float* __restrict__ q,
+                                                                    const float* __restrict__ p,
+                                                                    const float* __restrict__ negs, int64_t B, int N,
+                                                                    float inv_tau, const float* __restrict__ grad_loss,
+                                                                    float* __restrict__ dq, float* __restrict__ dp,
+                                                                    float* __restrict__ dnegs) {
+  const int64_t r = wave_row();
+  if (r >= B) return;
+  const int lane = lane_id();
+  MnRows<NMAX> m;
+  mn_load_stats<NMAX>(q, p, negs, r, N, m);
+  float cs[NMAX + 1], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) {
+      cs[k] = cos_value(m.st[k]);
+      mx = fmaxf(mx, cs[k] * inv_tau);
+    }
+  float se = 0.f;
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) se += expf(cs[k] * inv_tau - mx);
+  const float g = grad_loss[0] / (float)B;
+  f32x4 gq = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k <= NMAX; ++k)
+    if (k <= N) {
+      const float pk = expf(cs[k] * inv_tau - mx) / se;
+      const float gcos = g * (pk - (k == 0 ? 1.f : 0.f)) * inv_tau;
+      float a_other, a_q, a_d;
+      cos_grad_coefs(m.st[k], cs[k], a_other, a_q, a_d);
+      f32x4 gd;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gq[j] += gcos * (m.d[k][j] * a_other - a_q * m.q[j]);
+        gd[j] = gcos * (m.q[j] * a_other - a_d * m.d[k][j]);
+      }
+      float* ddr = (k == 0) ? dp + r * 256 : dnegs + (r * N + (k - 1)) * (int64_t)256;
+      reinterpret_cast<f32x4*>(ddr)[lane] = gd;
+    }
+  reinterpret_cast<f32x4*>(dq + r * 256)[lane] = gq;
+}
+
 // One workgroup: fixed-order strided partial sums then a fixed tree => bitwise reproducible.
 __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
   __shared__ float part[1024];
@@ -332,6 +433,15 @@ int launch_mean(const float* x, int64_t n, float* out, hipStream_t s) {
 }  // namespace tt
 
 using namespace tt;
+
+namespace tt {
+namespace {
+// 16-byte alignment of every non-null pointer (the float4 fast paths)
+inline bool aligned16(const void* a, const void* b, const void* c) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) == 0;
+}
+}  // namespace
+}  // namespace tt
 
 extern "C" int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, tt_stream_t stream) {
   TT_REQUIRE(rows >= 0 && H > 0, "bad shape rows=%lld H=%d", (long long)rows, H);
@@ -461,7 +571,12 @@ extern "C" int tt_multi_neg_fwd(const float* q, const float* p, const float* neg
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (B > 0) {
     TT_REQUIRE(q && p && loss_rows && (N == 0 || negs), "null pointer");
-    multi_neg_fwd_kernel<<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, H, inv_tau, loss_rows);
+    if (H == 256 && N <= 4 && aligned16(q, p, negs))
+      multi_neg_fwd_h256_kernel<4><<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, inv_tau, loss_rows);
+    else if (H == 256 && N <= 15 && aligned16(q, p, negs))
+      multi_neg_fwd_h256_kernel<15><<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, inv_tau, loss_rows);
+    else
+      multi_neg_fwd_kernel<<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, H, inv_tau, loss_rows);
     TT_LAUNCH_CHECK("tt_multi_neg_fwd");
   }
   return launch_mean(loss_rows, B, loss, s);
@@ -473,8 +588,16 @@ extern "C" int tt_multi_neg_bwd(const float* q, const float* p, const float* neg
   TT_REQUIRE(B >= 0 && H > 0 && N >= 0 && N <= kMaxNeg, "bad shape B=%lld N=%d H=%d", (long long)B, N, H);
   if (B == 0) return TT_OK;
   TT_REQUIRE(q && p && grad_loss && dq && dp && (N == 0 || (negs && dnegs)), "null pointer");
-  multi_neg_bwd_kernel<<<rows_grid(B), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(
-      q, p, negs, B, N, H, inv_tau, grad_loss, dq, dp, dnegs);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (H == 256 && N <= 4 && aligned16(q, p, negs) && aligned16(dq, dp, dnegs))
+    multi_neg_bwd_h256_kernel<4><<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, inv_tau, grad_loss, dq, dp,
+                                                                       dnegs);
+  else if (H == 256 && N <= 15 && aligned16(q, p, negs) && aligned16(dq, dp, dnegs))
+    multi_neg_bwd_h256_kernel<15><<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, inv_tau, grad_loss, dq, dp,
+                                                                        dnegs);
+  else
+    multi_neg_bwd_kernel<<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, H, inv_tau, grad_loss, dq, dp,
+                                                               dnegs);
   TT_LAUNCH_CHECK("tt_multi_neg_bwd");
   return TT_OK;
 }
