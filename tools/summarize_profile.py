@@ -23,10 +23,14 @@ OPS = [
     (r"bag_scale_rows|bag_piece_sum|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>",
      "tt_bag_mean_bwd_adamw_planned"),
     (r"bag_bwd_reduce", "tt_bag_mean_bwd_planned"),
-    (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
+    (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|prep_qd|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
     (r"score_bf16_kernel<1|score_f32_kernel<1|to_log2|bwd_combine", "tt_inbatch_bwd"),
     (r"adamw_(vec4|scalar)", "tt_adamw"),
     (r"adamw_multi|adam_prepare", "tt_adamw_multi"),
+    (r"multi_neg_fwd", "tt_multi_neg_fwd"),
+    (r"multi_neg_bwd", "tt_multi_neg_bwd"),
+    (r"triplet_fwd", "tt_triplet_fwd"),
+    (r"triplet_bwd", "tt_triplet_bwd"),
     (r"l2norm_fwd", "tt_l2norm_fwd"),
     (r"l2norm_bwd", "tt_l2norm_bwd"),
     (r"colsum", "tt_colsum"),
