@@ -174,7 +174,7 @@ def main():
     M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1
     kernels = []
 
-    def add(name, key, algo, unit, peak, bound, per_launch_note, side_stream=False):
+    def add(name, key, algo, unit, peak, bound, per_launch_note, side_stream=False, executed=None):
         if key not in ops_t:
             return
         ms = ops_t[key]["mean_ms"]
@@ -183,6 +183,9 @@ def main():
              "calls_per_step": ops_t[key]["calls"] / timing_steps, "achieved": round(achieved, 2),
              "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "algorithmic": algo,
              "per_launch": per_launch_note}
+        if executed is not None:  # work the kernels do beyond the algorithmic count (e.g. P.D in the forward)
+            k["executed"] = executed
+            k["executed_rate"] = round(executed / (ms * 1e-3) / 1e12, 2)
         if side_stream:  # its event span covers the overlap with the forward, not its kernels alone
             k["stream"] = "side (overlapped)"
         kernels.append(k)
@@ -201,10 +204,12 @@ def main():
     add("embedding bag backward (dense grad, apply half)", "tt_bag_mean_bwd_planned",
         nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
     pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
+    mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
     add("in-batch scorer forward (S=QD^T, lse, P.D)", "tt_inbatch_fwd", 2.0 * B * M * d, "TFLOP/s", pk, "mfma",
-        "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ")
+        "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ",
+        executed=(2.0 + 2.0 * mult) * B * M * d)
     add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
-        "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q)")
+        "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q)", executed=(2.0 + 2.0 * mult) * B * M * d)
     add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
         HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
     add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
