@@ -92,3 +92,22 @@ if os.environ.get("MB_REFS", "1") == "1":
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 20 * 1e3
         print(f"{name} over V x E: {us:.1f} us  {nbytes / us / 1e3:.0f} GB/s")
+
+# ---- the dense-gradient apply (data parallel 'shard' mode writes the V x E gradient)
+if os.environ.get("MB_DENSE", "1") == "1":
+    gout = torch.empty(V, E, device="cuda")
+
+    def dense_apply():
+        ops.bag_mean_backward_planned(d_pooled, denom, plan, out=gout)
+
+    for _ in range(3):
+        dense_apply()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(20):
+        dense_apply()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 20 * 1e3
+    print(f"bag bwd dense-grad apply ({os.environ.get('TT_BAG_REDUCE', 'default')}): {us:.1f} us  "
+          f"{(N * E * 4 + N * 4 + V * E * 4) / us / 1e3:.0f} GB/s algorithmic")

@@ -12,6 +12,7 @@
 // Layout: the table is V x E fp32 row-major (1 KiB rows at E = 256).  A wavefront owns a
 // sequence (forward) or a table row (backward).  Each lane moves 16 B per row-load so a
 // wave-instruction reads 64 x 16 B = 1 KiB: one E=256 row, two E=128 rows or four E=64 rows.
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -382,6 +383,87 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
   }
 }
 
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const float* p, int64_t i) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i);
+  else return reinterpret_cast<const f32x4*>(p)[i];
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, int64_t i, f32x4 x) {
+  if constexpr (NT) __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p) + i);
+  else reinterpret_cast<f32x4*>(p)[i] = x;
+}
+
+// Column-sliced row reduce, XCD-aware: the row is cut into NS column slices of 4 * LPR floats
+// and the blocks that share an XCD under round-robin placement (equal blockIdx % 8) work on one
+// slice (8 / NS XCDs per slice), so an XCD gathers only its slice of the gs rows (at C3, NS = 4:
+// 6.3 MB per XCD instead of 25 MB).  Placement is a speed choice only: any block -> XCD map
+// computes the same (slice, rows) work.  With NT the streamed table / moment (or gradient) bytes
+// carry the non-temporal hint so they do not push the gathered gs slice out of L2: at C3 the
+// pair cut the update from 300 to 261 us (NS = 2: 277, NS = 8: 296 -- 128-B pieces of each row
+// stream worse; without NT no gain).  RPI = 64 / LPR rows per wave, one slice each; the
+// per-element sums are bag_bwd_reduce_kernel's, in the same order.
+template <int LPR, int U, bool FUSED, bool NT>
+__global__ __launch_bounds__(kBlock) void bag_bwd_reduce_sliced_kernel(
+    const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
+    const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E, int NS,
+    float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
+    float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev,
+    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial) {
+  constexpr int RPI = kWave / LPR;
+  const int lane = lane_id();
+  const int sub = lane / LPR, c = lane % LPR;
+  const int xg = blockIdx.x & 7, gps = 8 / NS;
+  const int slice = xg % NS;
+  const int64_t rb = (int64_t)(blockIdx.x >> 3) * gps + xg / NS;
+  const int64_t row = (rb * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  if (row >= V) return;
+  const int col = slice * LPR + c;  // float4 index inside the row
+  const int np = nch[row];
+  const bool pieces = np > 0;
+  const int st = pieces ? piece_off[row] : seg_start[row], en = pieces ? st + np : seg_end[row];
+  const float* src = pieces ? partial : gs;
+  f32x4 pv, mv, vv;
+  if constexpr (FUSED) {
+    if (aa_dev) aa = *aa_dev;
+    pv = ld4<NT>(param + row * E, col);
+    mv = ld4<NT>(exp_avg + row * E, col);
+    vv = ld4<NT>(exp_avg_sq + row * E, col);
+  }
+  f32x4 part[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = st; e < en; e += U) {
+    int sq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) sq[u] = (e + u < en) ? (pieces ? e + u : vals[e + u]) : -1;
+    f32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      x[u] = (sq[u] >= 0) ? reinterpret_cast<const f32x4*>(src + (int64_t)sq[u] * E)[col] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U; ++u) part[u] += x[u];
+  }
+  f32x4 acc = part[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) acc += part[u];
+  if constexpr (!FUSED) {
+    st4<NT>(grad + row * E, col, acc);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float pj = pv[j], mj = mv[j], vj = vv[j];
+      adam_update(pj, acc[j], mj, vj, aa);
+      pv[j] = pj;
+      mv[j] = mj;
+      vv[j] = vj;
+    }
+    st4<NT>(param + row * E, col, pv);
+    st4<NT>(exp_avg + row * E, col, mv);
+    st4<NT>(exp_avg_sq + row * E, col, vv);
+  }
+}
+
 // Generic-E row reduce (scalar columns).
 template <bool FUSED>
 __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_generic_kernel(
@@ -573,6 +655,17 @@ int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nse
   return TT_OK;
 }
 
+// E in {256, 512, 1024}: the XCD-sliced reduce with non-temporal table/moment traffic (C3:
+// 261 us against 300 us for the whole-row kernel, tools/mb_bag_bwd.py).  TT_BAG_REDUCE=rows
+// selects the whole-row kernel (same sums in the same order) for comparison.
+bool use_sliced_reduce(int E) {
+  static const bool rows = [] {
+    const char* e = std::getenv("TT_BAG_REDUCE");
+    return e && std::strcmp(e, "rows") == 0;
+  }();
+  return !rows && (E == 256 || E == 512 || E == 1024);
+}
+
 template <bool FUSED>
 int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, float* m, float* v,
                   const AdamArgs& aa, const AdamArgs* aa_dev, hipStream_t s) {
@@ -581,6 +674,21 @@ int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, f
     return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   };
   const dim3 block(kBlock);
+  if (use_sliced_reduce(E)) {
+    // NS = 4 column slices of LPR = E / 16 float4 (256 B at E = 256); the row blocks of a slice
+    // are dealt to 8 / NS = 2 block groups, the grid padded to whole groups of 8 blocks
+    constexpr int NS = 4;
+    const int LPR = E / (4 * NS);
+    const int64_t rpb = kWavesPerBlock * (kWave / LPR), rbs = (V + rpb - 1) / rpb, gps = 8 / NS;
+    const dim3 grid((unsigned)(((rbs + gps - 1) / gps) * 8));
+#define TT_SL(L) bag_bwd_reduce_sliced_kernel<L, 4, FUSED, true><<<grid, block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, NS, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial)
+    if (LPR == 16) TT_SL(16);
+    else if (LPR == 32) TT_SL(32);
+    else TT_SL(64);
+#undef TT_SL
+    TT_LAUNCH_CHECK("bag_bwd_reduce_sliced");
+    return TT_OK;
+  }
   switch (E) {
     case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
     case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
