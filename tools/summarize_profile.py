@@ -20,8 +20,8 @@ from collections import defaultdict
 OPS = [
     (r"bag_fwd", "tt_bag_mean_fwd"),
     (r"bag_plan_keys|bag_bwd_mark|bag_piece_count|bag_piece_list|radix_sort|onesweep|rocprim", "tt_bag_plan"),
-    (r"bag_scale_rows|bag_piece_sum|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>",
-     "tt_bag_mean_bwd_adamw_planned"),
+    (r"bag_scale_rows|bag_piece_sum|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>"
+     r"|bag_bwd_reduce_sliced_kernel<\d+, \d+, true", "tt_bag_mean_bwd_adamw_planned"),
     (r"bag_bwd_reduce", "tt_bag_mean_bwd_planned"),
     (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|prep_qd|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
     (r"score_bf16_kernel<1|score_f32_kernel<1|to_log2|bwd_combine", "tt_inbatch_bwd"),
