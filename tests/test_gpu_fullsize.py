@@ -1,0 +1,126 @@
+"""GPU parity at the bench's full sizes (BASELINE.json configs[2], C3: V 200k, E = H 256, L 64,
+B 8192 queries + their positive and negative documents), through checks that do not need the
+oracle to process the whole batch: exact identities (denominators, single-token bags, the fused
+update against the unfused path bit for bit, graph replay against eager), the float64 oracle on
+sampled rows, and the bf16 scorer against a plain PyTorch fp32 computation on the same
+bf16-rounded operands.  Each test runs in a few seconds."""
+import numpy as np
+import pytest
+import torch
+
+import twotower_amd as tt
+from twotower_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+V, E, L, B = 200_000, 256, 64, 8192
+
+
+def _ids(seed=0):
+    q, p, n = tt.data.synthetic_triplets(B, L, V, seed=seed, device=DEV)
+    ids = torch.cat([q, p, n]).contiguous()
+    ids[5] = 0                    # an all-pad sequence
+    ids[6, 1:] = 0                # single-token sequences
+    ids[7, 1:] = 0
+    ids[7, 0] = V - 1             # ... of the last row
+    ids[8, 3] = 0                 # an interior pad
+    return ids
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_c3_bag_forward_full_size():
+    torch.manual_seed(0)
+    table = torch.randn(V, E, device=DEV)
+    ids = _ids()
+    pooled, denom = ops.bag_mean_forward(table, ids)
+    cnt = (ids > 0).sum(1).float()
+    assert torch.equal(denom, cnt + 1e-9)                                 # encoders.py:72, fp32
+    assert torch.count_nonzero(pooled[5]) == 0
+    assert torch.equal(pooled[6], table[ids[6, 0]]) and torch.equal(pooled[7], table[V - 1])  # bit-exact
+    rows = np.random.default_rng(1).choice(ids.shape[0], 256, replace=False)
+    ids_h = ids[rows].cpu().numpy()
+    tab = table.double().cpu().numpy()
+    want = np.stack([tab[r[r > 0]].sum(0) / max((r > 0).sum(), 1e-9) for r in ids_h])
+    assert _rel(pooled[rows].double().cpu().numpy(), want) < 1e-6
+
+
+def test_c3_fused_update_full_size_equals_unfused_and_oracle():
+    """The fused scatter + AdamW (XCD-sliced reduce) equals the dense-gradient path + AdamW
+    bit for bit over two steps at C3 size; the dense gradient matches the float64 oracle on
+    sampled rows (hot and cold)."""
+    torch.manual_seed(1)
+    ids = _ids(seed=2)
+    t0 = torch.randn(V, E, device=DEV)
+    d_pooled = torch.randn(ids.shape[0], E, device=DEV)
+    _, denom = ops.bag_mean_forward(t0, ids)
+    A, Bt = t0.clone(), t0.clone()
+    mA, vA, mB, vB = (torch.zeros_like(t0) for _ in range(4))
+    hp = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01)
+    for step in (1, 2):
+        grad = ops.bag_mean_backward(d_pooled, denom, ids, V, 0)
+        ops.adamw_step(A, grad, mA, vA, step=step, **hp)
+        ops.bag_mean_backward_adamw(d_pooled, denom, ids, Bt, mB, vB, 0, step=step, **hp)
+    assert torch.equal(A, Bt) and torch.equal(mA, mB) and torch.equal(vA, vB)
+    # oracle on sampled rows: G[r] = sum over tokens t with id r of d_pooled[seq(t)] / denom[seq(t)]
+    ids_h = ids.cpu().numpy()
+    counts = np.bincount(ids_h.ravel(), minlength=V)
+    hot = np.argsort(counts[1:])[-4:] + 1
+    rows = np.concatenate([hot, np.random.default_rng(3).choice(np.arange(1, V), 60, replace=False), [0]])
+    gs = (d_pooled.double() / denom.double()[:, None]).cpu().numpy()
+    want = np.zeros((len(rows), E))
+    for k, r in enumerate(rows):
+        if r == 0:
+            continue                                                     # padding row: no gradient
+        seqs, _ = np.nonzero(ids_h == r)
+        want[k] = gs[seqs].sum(0)
+    got = grad[torch.as_tensor(rows, device=DEV)].double().cpu().numpy()
+    assert _rel(got, want) < 1e-5
+    assert not got[-1].any()
+
+
+def test_c3_scorer_full_size_vs_torch_fp32():
+    """bf16 scorer at B 8192 x M 16384 x H 256 against torch fp32 on the same bf16-rounded q, d:
+    loss to 1e-4, gradients to 2e-2 (P is rounded to bf16 once, as the standard form does)."""
+    g = torch.Generator(device=DEV).manual_seed(4)
+    q = torch.nn.functional.normalize(torch.randn(B, E, device=DEV, generator=g), dim=-1)
+    d = torch.nn.functional.normalize(torch.randn(2 * B, E, device=DEV, generator=g), dim=-1)
+    Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
+    loss = ops.in_batch_softmax_loss(Q, D, 0.1, compute_dtype="bf16")
+    loss.backward()
+    qr = q.bfloat16().float().requires_grad_(True)
+    dr = d.bfloat16().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(qr @ dr.T / 0.1, torch.arange(B, device=DEV))
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-4 * abs(ref.item())
+    assert _rel(Q.grad.double().cpu().numpy(), qr.grad.double().cpu().numpy()) < 2e-2
+    assert _rel(D.grad.double().cpu().numpy(), dr.grad.double().cpu().numpy()) < 2e-2
+
+
+def test_c3_step_graph_equals_eager_full_size():
+    """Two C3 training steps (fused towers, bf16 in-batch loss over 2B candidates, fused table
+    AdamW, side-stream plan and weight gradients): graph replay equals eager bit for bit."""
+
+    def build():
+        torch.manual_seed(5)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        return model, opt, tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16")
+
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=10 + k, device=DEV) for k in range(3)]
+    m1, o1, l1 = build()
+    s1 = tt.TrainStep(m1, l1, o1)
+    losses = [s1(*b).item() for b in batches]
+    p1 = [p.detach().clone() for p in m1.parameters()]
+    del s1, o1, m1
+    m2, o2, l2 = build()
+    s2 = tt.TrainStep(m2, l2, o2, graph=True, eager_steps=1)
+    for b, want in zip(batches, losses):
+        assert s2(*b).item() == want
+    assert len(s2._graphs) == 1
+    for a, b_ in zip(p1, m2.parameters()):
+        assert torch.equal(a, b_)
+    assert np.isfinite(losses).all() and losses[0] > losses[-1] - 1.0
