@@ -124,3 +124,39 @@ def test_c3_step_graph_equals_eager_full_size():
     for a, b_ in zip(p1, m2.parameters()):
         assert torch.equal(a, b_)
     assert np.isfinite(losses).all() and losses[0] > losses[-1] - 1.0
+
+
+def test_c5_full_size_update_and_multi_negative_loss():
+    """C5 shape (configs[4] per GPU: V 1M, 8192 queries x (1 positive + 4 negatives)): the fused
+    update equals the unfused path bit for bit, and multiple_negatives matches a plain PyTorch
+    fp32/fp64 restatement of losses.py:47-85 (loss and gradients 1e-5)."""
+    Vc, K = 1_000_000, 4
+    q, p, n = tt.data.synthetic_triplets(B, L, Vc, seed=6, device=DEV, negatives=K)
+    ids = torch.cat([q, p, n]).contiguous()
+    assert ids.shape == ((2 + K) * B, L)
+    torch.manual_seed(7)
+    t0 = torch.randn(Vc, E, device=DEV)
+    d_pooled = torch.randn(ids.shape[0], E, device=DEV)
+    _, denom = ops.bag_mean_forward(t0, ids)
+    A, Bt = t0.clone(), t0.clone()
+    mA, vA, mB, vB = (torch.zeros_like(t0) for _ in range(4))
+    hp = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01)
+    grad = ops.bag_mean_backward(d_pooled, denom, ids, Vc, 0)
+    ops.adamw_step(A, grad, mA, vA, step=1, **hp)
+    ops.bag_mean_backward_adamw(d_pooled, denom, ids, Bt, mB, vB, 0, step=1, **hp)
+    assert torch.equal(A, Bt) and torch.equal(mA, mB) and torch.equal(vA, vB)
+    del A, Bt, mA, vA, mB, vB, grad, t0
+
+    g = torch.Generator(device=DEV).manual_seed(8)
+    qv, pv, nv = (torch.randn(r, E, device=DEV, generator=g) for r in (B, B, K * B))
+    Q, P, N = (x.clone().requires_grad_(True) for x in (qv, pv, nv))
+    loss = tt.losses.multiple_negatives_loss(Q, P, N.view(B, K, E), temperature=0.1)
+    loss.backward()
+    Qr, Pr, Nr = (x.double().requires_grad_(True) for x in (qv, pv, nv))
+    docs = torch.cat([Pr.unsqueeze(1), Nr.view(B, K, E)], 1)
+    logits = torch.nn.functional.cosine_similarity(Qr.unsqueeze(1).expand_as(docs), docs, dim=2) / 0.1
+    ref = torch.nn.functional.cross_entropy(logits, torch.zeros(B, dtype=torch.long, device=DEV))
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
+    for got, want in ((Q.grad, Qr.grad), (P.grad, Pr.grad), (N.grad, Nr.grad)):
+        assert _rel(got.double().cpu().numpy(), want.cpu().numpy()) < 1e-5
