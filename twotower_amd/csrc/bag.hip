@@ -237,14 +237,17 @@ __global__ __launch_bounds__(kBlock) void bag_piece_list_kernel(const int32_t* _
 }
 
 // One wave per piece (LPR lanes x NV float4 per row, RPI pieces per wave): partial = sum of its
-// tokens' gs rows in token order (U interleaved partial sums folded in a fixed order).
-template <int LPR, int NV, int U>
+// tokens' gs rows in token order (U interleaved partial sums folded in a fixed order).  LD >= U
+// rows are loaded per iteration (LD / U per partial sum, added in token order), so a piece of
+// 128-256 tokens takes LD-fold fewer dependent load round trips; the sums are the LD = U sums.
+template <int LPR, int NV, int U, int LD>
 __global__ __launch_bounds__(kBlock) void bag_piece_sum_kernel(const int32_t* __restrict__ piece_off, int64_t V,
                                                                const int32_t* __restrict__ piece_beg,
                                                                const int32_t* __restrict__ piece_end,
                                                                const int32_t* __restrict__ vals,
                                                                const float* __restrict__ gs, int E,
                                                                float* __restrict__ partial) {
+  static_assert(LD % U == 0, "LD must be a multiple of U");
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
@@ -256,21 +259,21 @@ __global__ __launch_bounds__(kBlock) void bag_piece_sum_kernel(const int32_t* __
   for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int k = 0; k < NV; ++k) part[u][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int e = st; e < en; e += U) {
-    int sq[U];
+  for (int e = st; e < en; e += LD) {
+    int sq[LD];
 #pragma unroll
-    for (int u = 0; u < U; ++u) sq[u] = (e + u < en) ? vals[e + u] : -1;
-    f32x4 v[U][NV];
+    for (int u = 0; u < LD; ++u) sq[u] = (e + u < en) ? vals[e + u] : -1;
+    f32x4 v[LD][NV];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < LD; ++u) {
       const f32x4* rp = reinterpret_cast<const f32x4*>(gs + (int64_t)(sq[u] < 0 ? 0 : sq[u]) * E);
 #pragma unroll
       for (int k = 0; k < NV; ++k) v[u][k] = (sq[u] >= 0) ? rp[k * LPR + c] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < LD; ++u)  // entry e + u goes to partial (e + u - st) % U: e - st is a multiple of U
 #pragma unroll
-      for (int k = 0; k < NV; ++k) part[u][k] += v[u][k];
+      for (int k = 0; k < NV; ++k) part[u % U][k] += v[u][k];
   }
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
@@ -708,11 +711,11 @@ int launch_piece_sum(const BwdWs& w, int64_t V, int E, hipStream_t s) {
   };
   const dim3 block(kBlock);
   switch (E) {
-    case 64: bag_piece_sum_kernel<16, 1, 4><<<grid_for(4), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
-    case 128: bag_piece_sum_kernel<32, 1, 4><<<grid_for(2), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
-    case 256: bag_piece_sum_kernel<64, 1, 4><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
-    case 512: bag_piece_sum_kernel<64, 2, 4><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
-    case 1024: bag_piece_sum_kernel<64, 4, 2><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 64: bag_piece_sum_kernel<16, 1, 4, 16><<<grid_for(4), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 128: bag_piece_sum_kernel<32, 1, 4, 16><<<grid_for(2), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 256: bag_piece_sum_kernel<64, 1, 4, 16><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 512: bag_piece_sum_kernel<64, 2, 4, 8><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
+    case 1024: bag_piece_sum_kernel<64, 4, 2, 8><<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
     default: bag_piece_sum_generic_kernel<<<grid_for(1), block, 0, s>>>(w.piece_off, V, w.piece_beg, w.piece_end, w.vals_out, w.gs, E, w.partial); break;
   }
   TT_LAUNCH_CHECK("bag_piece_sum");
