@@ -17,8 +17,8 @@
 // soon as the current one is consumed -- a full tile (~3 us) of latency cover with no barrier in
 // the main loop.  The four column slices of a row group run on the same XCD (blockIdx % 8), so
 // A is fetched from HBM once and served to the other three from that XCD's L2.
-// The L2-normalise epilogue needs whole rows: each slice writes its rows' partial sums of
-// squares and head_normalize_kernel finishes the rows in place.
+// The L2-normalise epilogue needs whole rows: the slices write the biased rows and
+// head_normalize_kernel (one wave per row) forms each row's norm and scales it in place.
 #include "common.hpp"
 
 namespace tt {
@@ -272,7 +272,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     // Epilogue.  acc[ct][v] is row trow0 + (v & 3) + 8 (v >> 2) + 4 hh, column
     // 64 c + 32 ct + r32.  Rows past the end are never stored; full tiles store unguarded.
     unsigned my_mask = 0;
-    float my_ss = 0.f;
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
 #pragma unroll
@@ -285,15 +284,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         if constexpr (EPI == EPI_BIAS_L2) y += bv[ct];
         if constexpr (EPI == EPI_RELU_MASK) y = (mword >> (16 * ct + v)) & 1u ? y : 0.f;
         acc[ct][v] = y;
-      }
-    }
-    if constexpr (EPI == EPI_BIAS_L2) {  // partial sum of squares of this slice's 64 columns
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        float ss = acc[0][v] * acc[0][v] + acc[1][v] * acc[1][v];
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) ss += __shfl_xor(ss, o);
-        my_ss = r32 == v ? ss : my_ss;  // lanes 0-15 / 32-47 keep rows v of their half
       }
     }
     float* orow = out + trow0 * kN + c * kColsWG + r32;
@@ -316,10 +306,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     if constexpr (EPI == EPI_BIAS_RELU) {
       if (relu_mask) relu_mask[mask_idx] = my_mask;
     }
-    if constexpr (EPI == EPI_BIAS_L2) {
-      const int64_t row = trow0 + (r32 & 3) + 8 * ((r32 >> 2) & 3) + 4 * hh;
-      if (r32 < 16 && row < rows) part[(int64_t)c * rows + row] = my_ss;
-    }
   }
 }
 
@@ -331,12 +317,10 @@ __global__ __launch_bounds__(256) void head_normalize_kernel(float* __restrict__
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = lane_id();
-  float ss = 0.f;
-#pragma unroll
-  for (int s = 0; s < kSlices; ++s) ss += part[s * rows + row];
-  const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
   f32x4* p = reinterpret_cast<f32x4*>(y + row * kN) + lane;
   f32x4 v = *p;
+  const float ss = wave_sum(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
+  const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
   v[0] *= inv;
   v[1] *= inv;
   v[2] *= inv;
@@ -599,7 +583,9 @@ extern "C" size_t tt_head_relu_mask_bytes(int64_t rows) {
 }
 
 extern "C" size_t tt_head_gemm_ws_size(int64_t rows, int epi) {
-  return epi == EPI_BIAS_L2 && rows > 0 ? (size_t)kSlices * rows * sizeof(float) : 0;
+  (void)rows;
+  (void)epi;
+  return 0;  // the L2 epilogue's row norms are formed by head_normalize_kernel from the rows
 }
 
 extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,
