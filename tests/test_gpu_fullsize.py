@@ -99,6 +99,31 @@ def test_c3_scorer_full_size_vs_torch_fp32():
     assert _rel(D.grad.double().cpu().numpy(), dr.grad.double().cpu().numpy()) < 2e-2
 
 
+def test_c4_rank_scorer_at_eight_gpu_shape_vs_torch_fp32():
+    """One rank of the 8-GPU cross-device step (BASELINE.json configs[3], C4): its B 8192 queries
+    against all 8 x 2B = 131072 gathered candidates, labels offset to rank 5's block, H 256, on
+    the bf16 scorer; against torch fp32 on the same bf16-rounded operands (the largest scorer
+    shape the driver's scaling run reaches).  Loss to 1e-4, gradients to 2e-2."""
+    world, rank = 8, 5
+    M = world * 2 * B
+    g = torch.Generator(device=DEV).manual_seed(9)
+    q = torch.nn.functional.normalize(torch.randn(B, E, device=DEV, generator=g), dim=-1)
+    d = torch.nn.functional.normalize(torch.randn(M, E, device=DEV, generator=g), dim=-1)
+    Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
+    loss = ops.in_batch_softmax_loss(Q, D, 0.1, label_off=rank * 2 * B, compute_dtype="bf16")
+    loss.backward()
+    qr = q.bfloat16().float().requires_grad_(True)
+    dr = d.bfloat16().float().requires_grad_(True)
+    labels = torch.arange(B, device=DEV) + rank * 2 * B
+    ref = torch.nn.functional.cross_entropy(qr @ dr.T / 0.1, labels)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-4 * abs(ref.item())
+    assert _rel(Q.grad.double().cpu().numpy(), qr.grad.double().cpu().numpy()) < 2e-2
+    assert _rel(D.grad.double().cpu().numpy(), dr.grad.double().cpu().numpy()) < 2e-2
+    # candidates of other ranks' blocks receive only softmax mass: no label term there
+    assert float(D.grad[:rank * 2 * B].abs().max()) < float(D.grad[rank * 2 * B:(rank * 2 + 1) * B].abs().max())
+
+
 def test_c3_step_graph_equals_eager_full_size():
     """Two C3 training steps (fused towers, bf16 in-batch loss over 2B candidates, fused table
     AdamW, side-stream plan and weight gradients): graph replay equals eager bit for bit."""
