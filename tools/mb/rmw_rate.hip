@@ -7,6 +7,9 @@
 //   rmwnt     : rmw1 with non-temporal stores
 //   rmwpers   : persistent grid (2048 blocks), each wave strides over rows with the next row's
 //               loads issued before the current row's stores
+//   il<K>     : the three arrays interleaved by row ([p_r | m_r | v_r], 3 KiB per row, one
+//               buffer): one wave per K rows, one contiguous read and write stream
+//   ilsl4     : il with the XCD-sliced placement of the fused kernel (4 column slices)
 // Prints us and GB/s (bytes = 24 per element for the RMW variants, 8 for copy).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -107,6 +110,48 @@ __global__ __launch_bounds__(256) void rmw_sliced_k(f32x4* __restrict__ p, f32x4
   v[i] = c;
 }
 
+template <int K>
+__global__ __launch_bounds__(256) void rmw_il_k(f32x4* __restrict__ t, long rows) {
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const long r0 = w * K;
+  if (r0 >= rows) return;
+  f32x4 a[K], b[K], c[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (r0 + k < rows) {
+      const long i = (r0 + k) * 3 * E4 + lane;
+      a[k] = t[i];
+      b[k] = t[i + E4];
+      c[k] = t[i + 2 * E4];
+    }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (r0 + k < rows) {
+      const long i = (r0 + k) * 3 * E4 + lane;
+      upd(a[k], b[k], c[k]);
+      t[i] = a[k];
+      t[i + E4] = b[k];
+      t[i + 2 * E4] = c[k];
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void rmw_il_sliced_k(f32x4* __restrict__ t, long rows) {
+  constexpr int LPR = E4 / S, RPW = 64 / LPR;
+  const int xg = blockIdx.x & 7, gps = 8 / S, slice = xg % S;
+  const long rb = (long)(blockIdx.x >> 3) * gps + xg / S;
+  const int lane = threadIdx.x & 63;
+  const long r = (rb * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  if (r >= rows) return;
+  const long i = r * 3 * E4 + slice * LPR + lane % LPR;
+  f32x4 a = t[i], b = t[i + E4], c = t[i + 2 * E4];
+  upd(a, b, c);
+  t[i] = a;
+  t[i + E4] = b;
+  t[i + 2 * E4] = c;
+}
+
 int main() {
   const long rows = 200000, n4 = rows * E4;
   f32x4 *p, *m, *v, *d;
@@ -149,6 +194,14 @@ int main() {
   run("sliced2", rmw_bytes, [&] { rmw_sliced_k<2><<<sl(0, 2), 256>>>(p, m, v, rows); });
   run("sliced4", rmw_bytes, [&] { rmw_sliced_k<4><<<sl(0, 4), 256>>>(p, m, v, rows); });
   run("sliced8", rmw_bytes, [&] { rmw_sliced_k<8><<<sl(0, 8), 256>>>(p, m, v, rows); });
+  f32x4* t;
+  hipMalloc(&t, 3 * n4 * 16);
+  hipMemset(t, 0, 3 * n4 * 16);
+  run("il1", rmw_bytes, [&] { rmw_il_k<1><<<(unsigned)((rows + 3) / 4), 256>>>(t, rows); });
+  run("il2", rmw_bytes, [&] { rmw_il_k<2><<<(unsigned)((rows / 2 + 3) / 4), 256>>>(t, rows); });
+  run("ilsl4", rmw_bytes, [&] { rmw_il_sliced_k<4><<<sl(0, 4), 256>>>(t, rows); });
+  run("ilsl2", rmw_bytes, [&] { rmw_il_sliced_k<2><<<sl(0, 2), 256>>>(t, rows); });
+  run("rmwK4", rmw_bytes, [&] { rmw_k<4, false><<<(unsigned)((rows / 4 + 3) / 4), 256>>>(p, m, v, rows); });
   run("copy", copy_bytes, [&] { copy_k<<<(unsigned)((n4 + 255) / 256), 256>>>(p, d, n4); });
   return 0;
 }
