@@ -265,7 +265,7 @@ def _unit(rng, n, H):
     return (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
 
 
-@pytest.mark.parametrize("H", [64, 128, 256])
+@pytest.mark.parametrize("H", [32, 64, 128, 256])
 @pytest.mark.parametrize("B,M,off", [(300, 700, 0), (129, 129, 0), (64, 256, 128), (1000, 2000, 1000)])
 @pytest.mark.parametrize("dt", ["fp32", "bf16_split", "bf16"])
 def test_in_batch_vs_oracle(H, B, M, off, dt):
@@ -358,11 +358,15 @@ def test_in_batch_candidate_owner_ranks_equal_global_batch(H, world, B, dt):
         losses.append(lr_.detach())
         dQ[r * B:(r + 1) * B] += qr.grad
         dD += Dr.grad
+    # dd: the single-process bf16 backward takes G from the forward's stored bf16 probabilities
+    # times a per-query factor folded into q~ (one rounding more than the owner form's recomputed
+    # G: ~1e-4); bf16_split recomputes in both forms
+    tol_dd = 1e-3 if dt == "bf16" else 1e-5
     for r in range(world):
         loss, _, dq, dd = res[r]
         assert abs(loss.item() - losses[r].item()) < 1e-5 * max(1.0, abs(losses[r].item()))
         assert rel(dq, dQ[r * B:(r + 1) * B].double().cpu().numpy()) < 1e-5
-        assert rel(dd, dD[r * M:(r + 1) * M].double().cpu().numpy()) < 1e-5
+        assert rel(dd, dD[r * M:(r + 1) * M].double().cpu().numpy()) < tol_dd
 
 
 def test_in_batch_three_tensor_form_and_zero_copy_candidates():

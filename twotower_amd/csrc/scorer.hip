@@ -17,6 +17,9 @@
 // logit, the -q_i contribution to dD) are applied by the combine kernels.
 // The streamed dimension is split over workgroups (blockIdx % S == split: one split per XCD
 // when S == 8); split partials are merged by the combine kernels.
+#include <cstdlib>
+#include <cstring>
+
 #include "common.hpp"
 
 namespace tt {
@@ -470,12 +473,44 @@ __device__ long long g_tt_trace[8 * 64];
   } while (0)
 #endif
 
-template <int MODE, bool PRECISE, int H>
+// Stored probabilities (forward, bf16 engine): the backward can take G from the forward instead of
+// recomputing S = R C^T.  P is a grid of 2 KiB blocks, block (ct, qt) = candidates [32 ct, +32) x
+// queries [32 qt, +32), at byte ((ct * nqt) + qt) * 2048: 32 candidate rows of 64 B, each row's 32
+// queries permuted so that the 8 of one backward B-operand lane are contiguous (position
+// 16 (q >> 4) + 8 ((q >> 2) & 1) + 4 ((q >> 3) & 1) + (q & 3)).  The values are this wave's bf16
+// G = 2^(x c2 - shift_q); the backward folds 2^(shift_q - lse2_q) into its query rows.
+// In the forward a lane holds one query and 16 candidates; adjacent query lanes swap halves (one
+// DPP move and one v_perm per register) so each lane stores 4-byte query pairs: 8 stores per tile,
+// each writing 4 whole 64-B rows.
+__device__ __forceinline__ unsigned p_pos(int q) { return 16 * (q >> 4) + 8 * ((q >> 2) & 1) + 4 * ((q >> 3) & 1) + (q & 3); }
+
+// Store k (0..7) of a tile: register k & 3 of bh[k >> 2].  The engine issues them one per
+// acc-chain step (k * NS / 8), bh[1]'s after the map has finished it.
+__device__ __forceinline__ void store_p_piece(char* __restrict__ blk, unsigned lane_off, bool odd, const bf16x8 (&bh)[2],
+                                              int k) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const unsigned sel = odd ? 0x03020706u : 0x05040100u;
+  const unsigned x = __builtin_bit_cast(u32x4, bh[k >> 2])[k & 3];
+  const unsigned y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);  // lane ^ 1
+  const unsigned v = __builtin_amdgcn_perm(y, x, sel);
+  const int row = 16 * (k >> 2) + 8 * ((k >> 1) & 1) + 2 * (k & 1);  // + 4 hh + odd (in lane_off)
+#ifdef TT_ABLATE_PSTORE  // timing ablation (never in a real build): no P stores
+  asm volatile("" ::"v"(v), "v"(blk + lane_off + row * 64));
+  return;
+#endif
+  // default cache policy: the backward, right after, finds part of P still in the Infinity Cache
+  // (measured: non-temporal stores and loads cost the backward 10 us at C3)
+  *reinterpret_cast<unsigned*>(blk + lane_off + row * 64) = v;
+}
+
+template <int MODE, bool PRECISE, int H, bool STOREP = false>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
     const float* __restrict__ dmax_part, int n_dmax,
-    const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part) {
+    const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part,
+    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0) {
+  static_assert(!STOREP || (MODE == FWD && !PRECISE), "stored probabilities: forward, single-rounded G");
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
   constexpr int NHT = H / 32;
@@ -506,6 +541,17 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const FillOffs<__bf16, H> fo = make_fill_offs<__bf16, H>();
   LdsOffs<H> lo;
   lo.init(lane);
+  // stored probabilities: this wave's query tile qt, candidate tile of (stage t, tile jt)
+  const int64_t p_qt = cb * NW + wid;
+  const bool hh_odd = (r32 & 1) != 0;
+  const unsigned p_lane = 64u * (4 * hh + (r32 & 1)) + 2u * p_pos(r32 & ~1);
+  auto pblk = [&](int64_t t, int jt) {
+    const int64_t ct = (row_begin + t * T::BJ) / 32 + jt;
+    return pstore + (ct * p_nqt + p_qt) * 2048;
+  };
+  (void)pblk;
+  (void)p_lane;
+  (void)hh_odd;
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // scalar per wave
   auto piece = [&](int c, int b, int64_t r0) {  // piece c of the stage at row r0 into buffer b
@@ -568,11 +614,36 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
         ms.init(c2, shift, lse4 + jt * 8, hh);
         xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32, lo, cf, xa, ms, bh, bl);
         TT_TRACE(jt * 4 + 3);
-        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run);
+        if constexpr (STOREP) {
+          char* blk = pblk(t, jt);
+          auto hook_p = [&](int st) {
+#ifdef TT_ABLATE_PSTORE4  // timing ablation: two contiguous 16-B stores per lane per tile
+            if (st == 0 || st == NHT)
+              __builtin_nontemporal_store(__builtin_bit_cast(f32x4, bh[st ? 1 : 0]),
+                                          reinterpret_cast<f32x4*>(blk + (st ? 1024 : 0) + lane * 16));
+#else
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (k * (2 * NHT) / 8 == st) store_p_piece(blk, p_lane, hh_odd, bh, k);
+#endif
+          };
+          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_p);
+        } else {
+          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run);
+        }
       } else {
         // stage t+1 landed: all but this wave's two newest fills (t+2, t+3's predecessor t+2 is
         // newest; t+1 is the third newest) have retired
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
+        if constexpr (STOREP) {
+          // vmcnt counts the P stores too (8 per tile): after fills(t+1) come at least the stores
+          // of tiles (t-1, 0), (t-1, 1), (t, 0) and fills(t+2); at t = 0 only fills(2) and (0, 0)'s
+          if (t == 0)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + 8) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + 24) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
+        }
         TT_TRACE(jt * 4 + 1);
 #ifndef TT_ABLATE_BARRIER  // timing ablations (tools/ablate_scorer.sh); never defined in a real build
         __syncthreads();  // ... in every wave, and every wave is past stage t-1
@@ -583,13 +654,186 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
         ms.init(c2, shift, lse4 + jt * 8, hh);
         xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, 0, lo, cf, xa, ms, bh, bl, hook_s);
         TT_TRACE(jt * 4 + 3);
-        acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_a);
+        if constexpr (STOREP) {
+          char* blk = pblk(t, jt);
+          auto hook_ap = [&](int st) {
+            hook_a(st);
+#ifdef TT_ABLATE_PSTORE4
+            if (st == 0 || st == NHT)
+              __builtin_nontemporal_store(__builtin_bit_cast(f32x4, bh[st ? 1 : 0]),
+                                          reinterpret_cast<f32x4*>(blk + (st ? 1024 : 0) + lane * 16));
+#else
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (k * (2 * NHT) / 8 == st) store_p_piece(blk, p_lane, hh_odd, bh, k);
+#endif
+          };
+          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_ap);
+        } else {
+          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_a);
+        }
       }
       xa = xb;
     }
   }
   drain_dma();  // no LDS-DMA may outlive the workgroup
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 backward from stored probabilities (single-rounded G): Acc^T = Qs^T P_tile for every
+// 32-row query tile, with Qs = q~ scaled per row by 2^(shift_q - lse2_q) (fwd_combine), so that
+// Qs^T P = q~^T G exactly as the recompute engine forms it, minus its S chain and softmax map.
+// The Qs tiles stream through the same four-stage LDS ring (stage fills by LDS-DMA, transposed
+// A-operand reads); the P fragments (two 16-B loads per lane per tile, one contiguous 1 KiB per
+// wave-instruction) go straight to registers three stages ahead.  Both are issued by inline asm
+// so the compiler inserts no vmcnt waits of its own: per stage t the order is [P(t+3),
+// fills(t+3)], and the barrier that opens stage t+1 waits until at most the P loads and fills of
+// stages t+2 and t+3 are in flight, i.e. vmcnt(2 NPC + 8).  Rows past the last query are the
+// zero tail of Qs.
+template <int s2, int imm_extra = 0>
+__device__ __forceinline__ bf16x8 p_load(const char* sbase, unsigned voff) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  i32x4 r;
+#ifdef TT_ABLATE_PLOAD  // timing ablation (never in a real build): no P loads
+  r = i32x4{(int)voff, s2, imm_extra, (int)(uintptr_t)sbase};
+  return __builtin_bit_cast(bf16x8, r);
+#endif
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "n"(32 * s2 + imm_extra)
+               : "memory");
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <int H, class Hook>
+__device__ __forceinline__ void acc_chain_p(const lds_char_t* tile, int jt, const LdsOffs<H>& lo, const bf16x8 (&g)[2],
+                                            f32x16 (&acc)[H / 32], Hook hook) {
+  using T = Tile<__bf16, H>;
+  constexpr int NHT = H / 32;
+  constexpr int NS = 2 * NHT;
+  const lds_char_t* tb = tile + jt * 32 * T::ROWB;
+  auto load = [&](int st) {
+    const int s2 = st / NHT, ht = st % NHT;
+    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
+    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
+    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  };
+  bf16x8 op[3];
+  op[0] = load(0);
+  if (NS > 1) op[1] = load(1);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    if (st + 2 < NS) op[(st + 2) % 3] = load(st + 2);
+    const int s2 = st / NHT, ht = st % NHT;
+    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], g[s2], acc[ht], 0, 0, 0);
+    hook(jt * NS + st);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
+    const __bf16* __restrict__ R, int64_t nR, int64_t nC, int S, int64_t rows_per_split, const char* __restrict__ P,
+    int64_t p_nqt, float* __restrict__ acc_part) {
+  using T = Tile<__bf16, H>;
+  constexpr int NHT = H / 32;
+  constexpr int NJ = T::BJ / 32;
+  static_assert(NJ == 2 && T::NSTAGE == 4, "two 32-row tiles per stage, four-stage ring");
+  constexpr int NPC = T::NI;                // fill pieces per stage per wave
+  constexpr int NSTEP = NJ * 2 * NHT;       // MFMA steps per stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;
+
+  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
+
+  const FillOffs<__bf16, H> fo = make_fill_offs<__bf16, H>();
+  LdsOffs<H> lo;
+  lo.init(lane);
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
+  auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
+  auto fill = [&](int c, int b, int64_t r0) { glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024); };
+  // this wave's candidate tile; a lane's fragment of a P block: candidate row r32, positions
+  // (2 s2 + hh) * 8 .. + 8
+  const char* pcol = P + (cb * NW + wid) * p_nqt * 2048;
+#ifdef TT_ABLATE_PCONTIG  // timing ablation: fragment-order addresses (1 KiB contiguous per load)
+  const unsigned pvo = (unsigned)(lane * 16);
+#else
+  const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
+#endif
+  bf16x8 pf[4][NJ][2];  // P fragments of stages t .. t+3 (index t % 4)
+  auto pissue = [&](bf16x8 (&dst)[NJ][2], int64_t t) {
+    const char* b = pcol + (stage_row(t) / 32) * 2048;
+#pragma unroll
+    for (int jt = 0; jt < NJ; ++jt) {
+#ifdef TT_ABLATE_PCONTIG
+      dst[jt][0] = p_load<0>(b + jt * 2048, pvo);
+      dst[jt][1] = p_load<0, 1024>(b + jt * 2048, pvo);
+#else
+      dst[jt][0] = p_load<0>(b + jt * 2048, pvo);
+      dst[jt][1] = p_load<1>(b + jt * 2048, pvo);
+#endif
+    }
+  };
+  auto tie = [&](bf16x8 (&x)[NJ][2]) {
+#pragma unroll
+    for (int jt = 0; jt < NJ; ++jt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) asm volatile("" : "+v"(x[jt][s2]));
+  };
+#ifdef TT_ABLATE_PLOAD
+  constexpr int kInFlight = 2 * NPC;
+#else
+  constexpr int kInFlight = 2 * (NPC + 2 * NJ);  // P loads + fills of the two newest stages
+#endif
+  // prologue in steady-state order: [P(k), fills(k)] for k = 0, 1, 2
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    pissue(pf[k], k);
+#pragma unroll
+    for (int c = 0; c < NPC; ++c) fill(c, k, stage_row(k));
+  }
+
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  // stage 0 and P(0) landed
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kInFlight) : "memory");
+  __syncthreads();
+  tie(pf[0]);
+
+  auto stage = [&](int64_t t, bf16x8 (&cur)[NJ][2], bf16x8 (&ahead)[NJ][2], bf16x8 (&next)[NJ][2]) {
+    const int buf = (int)(t & 3), fbuf = (buf + 3) & 3;
+    const int64_t frow = stage_row(t + 3);
+    pissue(ahead, t + 3);
+    auto hook = [&](int step) {
+#pragma unroll
+      for (int c = 0; c < NPC; ++c)
+        if (c * NSTEP / NPC == step) fill(c, fbuf, frow);
+    };
+    const lds_char_t* tile = lds + buf * T::STAGE_B;
+#pragma unroll
+    for (int jt = 0; jt < NJ; ++jt) acc_chain_p<H>(tile, jt, lo, cur[jt], acc, hook);
+    // stage t+1 and P(t+1) landed in this wave; then every wave is past stage t
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kInFlight) : "memory");
+    __syncthreads();
+    tie(next);
+  };
+  for (int64_t t = 0; t < ntiles; t += 4) {
+    stage(t, pf[0], pf[3], pf[1]);
+    if (t + 1 < ntiles) stage(t + 1, pf[1], pf[0], pf[2]);
+    if (t + 2 < ntiles) stage(t + 2, pf[2], pf[1], pf[3]);
+    if (t + 3 < ntiles) stage(t + 3, pf[3], pf[2], pf[0]);
+  }
+  drain_dma();  // no load may outlive the workgroup
+  write_partials<DD, H>(acc, 0.f, split, nC, my_col, hh, acc_part, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -815,10 +1059,14 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     int64_t B, int H, int S, int n_pad, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part,
     int n_dmax, const float* __restrict__ l_part, const float* __restrict__ acc_part, float inv_tau, int64_t label_off,
     const DT* __restrict__ Qmat, const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2,
-    float* __restrict__ loss_rows, float* __restrict__ dqu) {
+    float* __restrict__ loss_rows, float* __restrict__ dqu, __bf16* __restrict__ qs = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= B) return;
   const int lane = lane_id();
+  if (i >= B) {  // the zero tail of the scaled query copy (the stored-P backward's R rows)
+    if (qs && i < B + kTailRows)
+      for (int h = lane; h < H; h += kWave) qs[i * H + h] = (__bf16)0.f;
+    return;
+  }
   const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
   float l = 0.f;
   for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
@@ -831,6 +1079,11 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
     const f32x4 qv = load4(qr, lane), dv = load4(dl, lane);
     float dot = wave_sum(qv[0] * dv[0] + qv[1] * dv[1] + qv[2] * dv[2] + qv[3] * dv[3]);
+    if (qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
+      const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
+      reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
+          bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
+    }
     if (lane == 0) {
       lse[i] = lse_i;
       lse2[i] = lse2_i;
@@ -846,6 +1099,10 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   float dot = 0.f;
   for (int h = lane; h < H; h += kWave) dot += (float)qr[h] * (float)dl[h];
   dot = wave_sum(dot);
+  if (qs) {
+    const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
+    for (int h = lane; h < H; h += kWave) qs[i * H + h] = (__bf16)((float)qr[h] * f);
+  }
   if (lane == 0) {
     lse[i] = lse_i;
     lse2[i] = lse2_i;
@@ -933,6 +1190,9 @@ int wg_per_cu(int H) { return H <= 128 ? 2 : 1; }
 struct Ws {
   __bf16* Qb;
   __bf16* Db;
+  __bf16* Qs;   // stored-P backward: q~ scaled by 2^(shift - lse2) (+ zero tail)
+  char* P;      // stored-P backward: bf16 probabilities, p_nct x p_nqt blocks of 2 KiB
+  int64_t p_nqt;
   float* qnorm;
   float* lse2;
   float* dmax_part;
@@ -942,7 +1202,23 @@ struct Ws {
   size_t total;
 };
 
-// Layout: [Qb | Db] persist from forward to backward (the backward's MFMA operands);
+// The backward takes G from the forward's stored probabilities (bf16, single-rounded G) unless
+// TT_INBATCH_BWD=recompute (then it recomputes S = Q D^T, the reference-order form; measurement
+// switch, read once).
+bool stored_p(int dtype) {
+  static const bool recompute = [] {
+    const char* e = std::getenv("TT_INBATCH_BWD");
+    return e && std::strcmp(e, "recompute") == 0;
+  }();
+  return dtype == TT_BF16 && !recompute;
+}
+
+// P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
+// backward's 128-column blocks (every tile either engine touches exists)
+int64_t p_nqt_for(int64_t B) { return (B + 127) / 128 * 4; }
+int64_t p_nct_for(int64_t M) { return (M + 127) / 128 * 4; }
+
+// Layout: [Qb | Db | Qs | P] persist from forward to backward (the backward's MFMA operands);
 // everything else is scratch reused by both passes.
 Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const int BJ = bj_for(dtype);
@@ -957,6 +1233,9 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   // bf16 operand copies and lse2 carry a kTailRows tail (zeros / +inf): the engine's stage fills
   // never need per-lane redirection past the last row
   const size_t oq = take(bf ? (size_t)(B + kTailRows) * H * 2 : 0), od = take(bf ? (size_t)(M + kTailRows) * H * 2 : 0);
+  const bool sp = stored_p(dtype);
+  const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * 2 : 0);
+  const size_t op = take(sp ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : 0);
   const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
@@ -966,6 +1245,9 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   if (b) {
     w.Qb = reinterpret_cast<__bf16*>(b + oq);
     w.Db = reinterpret_cast<__bf16*>(b + od);
+    w.Qs = sp ? reinterpret_cast<__bf16*>(b + oqs) : nullptr;
+    w.P = sp ? b + op : nullptr;
+    w.p_nqt = p_nqt_for(B);
     w.qnorm = reinterpret_cast<float*>(b + oqn);
     w.lse2 = reinterpret_cast<float*>(b + ol2);
     w.dmax_part = reinterpret_cast<float*>(b + omx);
@@ -988,6 +1270,10 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
+  } else if (MODE == FWD && w.P) {
+    score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
+        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, w.P, w.p_nqt);
   } else {
     score_bf16_kernel<MODE, false, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -1041,7 +1327,7 @@ namespace {
 int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, int H, const float* qnorm,
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
-             hipStream_t s) {
+             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr) {
   const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
@@ -1050,9 +1336,11 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   w.pad = const_cast<char*>(pad);
   w.l_part = l_part;
   w.acc_part = acc_part;
+  w.P = P;
+  w.p_nqt = p_nqt;
   int rc;
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
-  const dim3 grid((unsigned)((B + 3) / 4)), block(256);
+  const dim3 grid((unsigned)((B + (Qs ? kTailRows : 0) + 3) / 4)), block(256);
   if (dtype == TT_F32)
     fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                     acc_part, inv_tau, label_off, static_cast<const float*>(Cm),
@@ -1060,7 +1348,7 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   else
     fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                      acc_part, inv_tau, label_off, static_cast<const __bf16*>(Cm),
-                                                     static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu);
+                                                     static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu, Qs);
   TT_LAUNCH_CHECK("score_fwd_combine");
   return launch_mean(loss_rows, B, loss, s);
 }
@@ -1088,6 +1376,33 @@ int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const v
     bwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, acc_part,
                                                      static_cast<const __bf16*>(Qlab), dqu, grad_loss, grad_scale,
                                                      inv_tau, dq, dd);
+  TT_LAUNCH_CHECK("score_bwd_combine");
+  return TT_OK;
+}
+
+// Backward from the forward's stored probabilities (bf16): score_ddp_kernel over Qs (B rows +
+// zero tail) and P, then the same combine (label terms from the unscaled q~).
+int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, const __bf16* Qs, const char* P,
+               int64_t p_nqt, const __bf16* Qlab, const float* dqu, const float* grad_loss, float grad_scale,
+               float* dq, float* dd, float* acc_part, hipStream_t s) {
+  const Plan p = plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H));
+  switch (H) {
+#define TT_DDP(HH)                                                                                                   \
+  case HH:                                                                                                           \
+    score_ddp_kernel<HH><<<dim3(p.grid), dim3(NT), Tile<__bf16, HH>::LDS_BYTES, s>>>(Qs, B, M, p.S, p.rows_per_split, \
+                                                                                    P, p_nqt, acc_part);            \
+    break;
+    TT_DDP(32)
+    TT_DDP(64)
+    TT_DDP(128)
+    TT_DDP(256)
+#undef TT_DDP
+    default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
+  }
+  TT_LAUNCH_CHECK("score_ddp");
+  const int64_t rows = std::max(B, M);
+  bwd_combine_kernel<__bf16><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(
+      B, M, H, p.S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, dq, dd);
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
@@ -1146,8 +1461,10 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
+  const bool sp = want_grad && w.P;
   return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
-                  want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s);
+                  want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s, sp ? w.P : nullptr, w.p_nqt,
+                  sp ? w.Qs : nullptr);
 }
 
 extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
@@ -1163,6 +1480,8 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   // lse in log2 units (ws.lse2) and the pad rows were left in the workspace by the forward
   const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
   const void* Cm = bf ? (const void*)w.Db : (const void*)d;
+  if (w.P) return bwd_core_p(B, M, H, label_off, inv_tau, w.Qs, w.P, w.p_nqt, w.Qb, dq_unscaled, grad_loss, grad_scale,
+                             dq, dd, w.acc_part, s);
   return bwd_core(dtype, Rm, B, w.lse2, Cm, M, Rm, B, label_off, H, inv_tau, dq_unscaled, grad_loss, grad_scale, dq,
                   dd, w.pad, w.acc_part, s);
 }
