@@ -617,15 +617,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
         if constexpr (STOREP) {
           char* blk = pblk(t, jt);
           auto hook_p = [&](int st) {
-#ifdef TT_ABLATE_PSTORE4  // timing ablation: two contiguous 16-B stores per lane per tile
-            if (st == 0 || st == NHT)
-              __builtin_nontemporal_store(__builtin_bit_cast(f32x4, bh[st ? 1 : 0]),
-                                          reinterpret_cast<f32x4*>(blk + (st ? 1024 : 0) + lane * 16));
-#else
 #pragma unroll
             for (int k = 0; k < 8; ++k)
               if (k * (2 * NHT) / 8 == st) store_p_piece(blk, p_lane, hh_odd, bh, k);
-#endif
           };
           acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_p);
         } else {
@@ -658,15 +652,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
           char* blk = pblk(t, jt);
           auto hook_ap = [&](int st) {
             hook_a(st);
-#ifdef TT_ABLATE_PSTORE4
-            if (st == 0 || st == NHT)
-              __builtin_nontemporal_store(__builtin_bit_cast(f32x4, bh[st ? 1 : 0]),
-                                          reinterpret_cast<f32x4*>(blk + (st ? 1024 : 0) + lane * 16));
-#else
 #pragma unroll
             for (int k = 0; k < 8; ++k)
               if (k * (2 * NHT) / 8 == st) store_p_piece(blk, p_lane, hh_odd, bh, k);
-#endif
           };
           acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_ap);
         } else {
@@ -763,23 +751,14 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   // this wave's candidate tile; a lane's fragment of a P block: candidate row r32, positions
   // (2 s2 + hh) * 8 .. + 8
   const char* pcol = P + (cb * NW + wid) * p_nqt * 2048;
-#ifdef TT_ABLATE_PCONTIG  // timing ablation: fragment-order addresses (1 KiB contiguous per load)
-  const unsigned pvo = (unsigned)(lane * 16);
-#else
   const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
-#endif
   bf16x8 pf[4][NJ][2];  // P fragments of stages t .. t+3 (index t % 4)
   auto pissue = [&](bf16x8 (&dst)[NJ][2], int64_t t) {
     const char* b = pcol + (stage_row(t) / 32) * 2048;
 #pragma unroll
     for (int jt = 0; jt < NJ; ++jt) {
-#ifdef TT_ABLATE_PCONTIG
-      dst[jt][0] = p_load<0>(b + jt * 2048, pvo);
-      dst[jt][1] = p_load<0, 1024>(b + jt * 2048, pvo);
-#else
       dst[jt][0] = p_load<0>(b + jt * 2048, pvo);
       dst[jt][1] = p_load<1>(b + jt * 2048, pvo);
-#endif
     }
   };
   auto tie = [&](bf16x8 (&x)[NJ][2]) {
