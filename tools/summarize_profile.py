@@ -24,7 +24,7 @@ OPS = [
      r"|bag_bwd_reduce_sliced_kernel<\d+, \d+, true", "tt_bag_mean_bwd_adamw_planned"),
     (r"bag_bwd_reduce", "tt_bag_mean_bwd_planned"),
     (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|prep_qd|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
-    (r"score_bf16_kernel<1|score_f32_kernel<1|to_log2|bwd_combine", "tt_inbatch_bwd"),
+    (r"score_bf16_kernel<1|score_f32_kernel<1|score_ddp_kernel|to_log2|bwd_combine", "tt_inbatch_bwd"),
     (r"adamw_(vec4|scalar)", "tt_adamw"),
     (r"adamw_multi|adam_prepare", "tt_adamw_multi"),
     (r"multi_neg_fwd", "tt_multi_neg_fwd"),
