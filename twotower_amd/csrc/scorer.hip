@@ -1184,12 +1184,14 @@ struct Ws {
 // The backward takes G from the forward's stored probabilities (bf16, single-rounded G) unless
 // TT_INBATCH_BWD=recompute (then it recomputes S = Q D^T, the reference-order form; measurement
 // switch, read once).
-bool stored_p(int dtype) {
+// P is kept only up to 2^31 entries (4 GiB of bf16): beyond that the backward recomputes rather
+// than hold the workspace that large.
+bool stored_p(int dtype, int64_t B, int64_t M) {
   static const bool recompute = [] {
     const char* e = std::getenv("TT_INBATCH_BWD");
     return e && std::strcmp(e, "recompute") == 0;
   }();
-  return dtype == TT_BF16 && !recompute;
+  return dtype == TT_BF16 && !recompute && B * M <= (int64_t(1) << 31);
 }
 
 // P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
@@ -1212,7 +1214,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   // bf16 operand copies and lse2 carry a kTailRows tail (zeros / +inf): the engine's stage fills
   // never need per-lane redirection past the last row
   const size_t oq = take(bf ? (size_t)(B + kTailRows) * H * 2 : 0), od = take(bf ? (size_t)(M + kTailRows) * H * 2 : 0);
-  const bool sp = stored_p(dtype);
+  const bool sp = stored_p(dtype, B, M);
   const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * 2 : 0);
   const size_t op = take(sp ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : 0);
   const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
