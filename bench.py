@@ -210,8 +210,13 @@ def main():
     add("in-batch scorer forward (S=QD^T, lse, P.D)", "tt_inbatch_fwd", 2.0 * B * M * d, "TFLOP/s", pk, "mfma",
         "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ",
         executed=(2.0 + 2.0 * mult) * B * M * d)
+    # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
+    stored_p = (scorer_dtype == "bf16" and world == 1 and os.environ.get("TT_INBATCH_BWD") != "recompute"
+                and B * M <= 2 ** 31)
     add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
-        "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q)", executed=(2.0 + 2.0 * mult) * B * M * d)
+        "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q); dQ's product runs in the forward"
+        + ("; G read from the forward's stored bf16 probabilities" if stored_p else ""),
+        executed=(2.0 if stored_p else 2.0 + 2.0 * mult) * B * M * d)
     add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
         HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
     add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
