@@ -55,12 +55,10 @@ def _batch():
 
 
 def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner"):
-    # bf16: every process recomputes G in the backward (TT_INBATCH_BWD=recompute), the form the
-    # candidate-owner passes use; the default single-process backward takes G from the forward's
-    # stored bf16 probabilities times a per-query factor rounded into q~, whose roundings follow
-    # the per-process split sums (parity of that path: the oracle / torch tests)
+    # every process recomputes G in the backward (the default; the candidate-owner passes always
+    # do), so single process and ranks form the same bf16 products
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TT_INBATCH_DP=inbatch_dp,
-                      TT_INBATCH_BWD="recompute" if loss_name.endswith("bf16") else "")
+                      TT_INBATCH_BWD="recompute")
     try:
         torch.cuda.set_device(0)
         if rank >= 0:

@@ -3,6 +3,8 @@ oracle and the reference's golden vectors.  Tolerances: token-id indexing bit-ex
 rows / pooled values of single-token bags), fp32 loss and gradients within 1e-5 relative
 (max-abs normalised), bf16 scorer against the oracle on bf16-rounded inputs: 1e-4 for the
 hi/lo split of P (bf16_split) and 2e-2 for the standard single-rounding bf16 form."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -358,10 +360,9 @@ def test_in_batch_candidate_owner_ranks_equal_global_batch(H, world, B, dt):
         losses.append(lr_.detach())
         dQ[r * B:(r + 1) * B] += qr.grad
         dD += Dr.grad
-    # dd: the single-process bf16 backward takes G from the forward's stored bf16 probabilities
-    # times a per-query factor folded into q~ (one rounding more than the owner form's recomputed
-    # G: ~1e-4); bf16_split recomputes in both forms
-    tol_dd = 1e-3 if dt == "bf16" else 1e-5
+    # dd: with TT_INBATCH_BWD=stored the single-process bf16 backward takes G from the forward's
+    # stored probabilities (one rounding more than the owner form's recomputed G: ~1e-4)
+    tol_dd = 1e-3 if dt == "bf16" and os.environ.get("TT_INBATCH_BWD") == "stored" else 1e-5
     for r in range(world):
         loss, _, dq, dd = res[r]
         assert abs(loss.item() - losses[r].item()) < 1e-5 * max(1.0, abs(losses[r].item()))

@@ -752,7 +752,10 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   // (2 s2 + hh) * 8 .. + 8
   const char* pcol = P + (cb * NW + wid) * p_nqt * 2048;
   const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
-  bf16x8 pf[4][NJ][2];  // P fragments of stages t .. t+3 (index t % 4)
+  // P fragments of stages t .. t+3 in five register sets (index t % 5): the loads of stage t+3
+  // go into the set stage t-2 read, so no load is in flight into registers an MFMA of the
+  // previous stage may still be reading (the asm loads are outside the compiler's hazard checks)
+  bf16x8 pf[5][NJ][2];
   auto pissue = [&](bf16x8 (&dst)[NJ][2], int64_t t) {
     const char* b = pcol + (stage_row(t) / 32) * 2048;
 #pragma unroll
@@ -805,11 +808,12 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
     __syncthreads();
     tie(next);
   };
-  for (int64_t t = 0; t < ntiles; t += 4) {
+  for (int64_t t = 0; t < ntiles; t += 5) {
     stage(t, pf[0], pf[3], pf[1]);
-    if (t + 1 < ntiles) stage(t + 1, pf[1], pf[0], pf[2]);
-    if (t + 2 < ntiles) stage(t + 2, pf[2], pf[1], pf[3]);
-    if (t + 3 < ntiles) stage(t + 3, pf[3], pf[2], pf[0]);
+    if (t + 1 < ntiles) stage(t + 1, pf[1], pf[4], pf[2]);
+    if (t + 2 < ntiles) stage(t + 2, pf[2], pf[0], pf[3]);
+    if (t + 3 < ntiles) stage(t + 3, pf[3], pf[1], pf[4]);
+    if (t + 4 < ntiles) stage(t + 4, pf[4], pf[2], pf[0]);
   }
   drain_dma();  // no load may outlive the workgroup
   write_partials<DD, H>(acc, 0.f, split, nC, my_col, hh, acc_part, nullptr);
@@ -1181,17 +1185,16 @@ struct Ws {
   size_t total;
 };
 
-// The backward takes G from the forward's stored probabilities (bf16, single-rounded G) unless
-// TT_INBATCH_BWD=recompute (then it recomputes S = Q D^T, the reference-order form; measurement
-// switch, read once).
-// P is kept only up to 2^31 entries (4 GiB of bf16): beyond that the backward recomputes rather
-// than hold the workspace that large.
+// TT_INBATCH_BWD=stored (read once): the bf16 backward takes G from the forward's stored
+// probabilities instead of recomputing S = Q D^T.  Opt-in: at H <= 64 it gave wrong dD in a few
+// runs (B 300, M 700; not reproduced in isolation, never seen at H = 256), cause not yet found
+// (DESIGN.md §9).  P is kept only up to 2^31 entries (4 GiB of bf16).
 bool stored_p(int dtype, int64_t B, int64_t M) {
-  static const bool recompute = [] {
+  static const bool stored = [] {
     const char* e = std::getenv("TT_INBATCH_BWD");
-    return e && std::strcmp(e, "recompute") == 0;
+    return e && std::strcmp(e, "stored") == 0;
   }();
-  return dtype == TT_BF16 && !recompute && B * M <= (int64_t(1) << 31);
+  return dtype == TT_BF16 && stored && B * M <= (int64_t(1) << 31);
 }
 
 // P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
