@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import twotower_amd as tt  # noqa: E402
-from twotower_amd import _lib  # noqa: E402
+from twotower_amd import _lib, ops as tt_ops  # noqa: E402
 
 CONFIGS = {
     # name: V, E(=H), L, B (queries per GPU), scorer dtype, loss, negatives per query
@@ -211,7 +211,7 @@ def main():
         "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ",
         executed=(2.0 + 2.0 * mult) * B * M * d)
     # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
-    stored_p = (scorer_dtype == "bf16" and world == 1 and os.environ.get("TT_INBATCH_BWD") == "stored"
+    stored_p = (scorer_dtype == "bf16" and world == 1 and tt_ops.get_inbatch_backward() == "stored"
                 and B * M <= 2 ** 31)
     add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
         "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q); dQ's product runs in the forward"

@@ -181,10 +181,17 @@ int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t 
  * fwd (want_grad != 0) also leaves dq_unscaled = sum_j P_ij d~_j - d~_label (B x H) so the
  * backward needs only the dD pass.  ws must stay untouched between fwd and bwd: it carries the
  * bf16 operands, the pad rows and lse in log2 units, which the backward engine reads (the lse
- * argument of tt_inbatch_bwd is the same quantity, validated but not re-read).  With the
- * environment TT_INBATCH_BWD=stored (read once per process; opt-in) the TT_BF16 workspace also
- * carries the forward's bf16 probabilities (about B * M * 2 bytes) and a rescaled bf16 copy of q,
- * from which the backward forms P without recomputing S. */
+ * argument of tt_inbatch_bwd is the same quantity, validated but not re-read).  In the default
+ * backward form (TT_INBATCH_BWD_STORED) the TT_BF16 workspace also carries the forward's bf16
+ * probabilities (about B * M * 2 bytes, kept while B * M <= 2^31) and a rescaled bf16 copy of q,
+ * from which the backward forms P without recomputing S.
+ * tt_inbatch_set_backward(mode) selects the form process-wide and returns the previous one (an
+ * unknown mode only reads it); the initial form is STORED unless the environment sets
+ * TT_INBATCH_BWD=recompute.  The workspace size depends on the form: size it after selecting, and
+ * do not switch between a forward and its backward. */
+#define TT_INBATCH_BWD_RECOMPUTE 0
+#define TT_INBATCH_BWD_STORED 1
+int tt_inbatch_set_backward(int mode);
 size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype);
 int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
                    float inv_tau, int64_t label_off, int want_grad,

@@ -2,7 +2,7 @@
 B 8192 queries + their positive and negative documents), through checks that do not need the
 oracle to process the whole batch: exact identities (denominators, single-token bags, the fused
 update against the unfused path bit for bit, graph replay against eager), the float64 oracle on
-sampled rows, and the bf16 scorer against a plain PyTorch fp32 computation on the same
+sampled rows, and the bf16 scorer against a plain PyTorch float64 computation on the same
 bf16-rounded operands.  Each test runs in a few seconds."""
 import numpy as np
 import pytest
@@ -81,29 +81,49 @@ def test_c3_fused_update_full_size_equals_unfused_and_oracle():
     assert not got[-1].any()
 
 
-def test_c3_scorer_full_size_vs_torch_fp32():
-    """bf16 scorer at B 8192 x M 16384 x H 256 against torch fp32 on the same bf16-rounded q, d:
-    loss to 1e-4, gradients to 2e-2 (P is rounded to bf16 once, as the standard form does)."""
+def _ref64_in_batch(q, d, tau, off, g=1.0):
+    """in_batch_sampled_softmax_loss (twotower/losses.py:88-118) in float64 on the GPU (plain
+    PyTorch: the oracle's formula at a size the host would take minutes for)."""
+    z = (q.double() @ d.double().T) / tau
+    B = q.shape[0]
+    rows = torch.arange(B, device=DEV)
+    lse = torch.logsumexp(z, 1)
+    loss = (lse - z[rows, rows + off]).mean()
+    P = torch.exp(z - lse[:, None])
+    del z
+    P[rows, rows + off] -= 1.0
+    P *= g / B
+    return loss.item(), (P @ d.double()) / tau, (P.T @ q.double()) / tau
+
+
+def _rel_t(a, b):
+    return float((a.double() - b).abs().max() / b.abs().max())
+
+
+# Measured errors (tools/scorer_error_table.py --big, profiles/r02_scorer_error.md) against float64
+# on the bf16-rounded operands; the bars below are about 1.5-2x those:
+#   C3 (B 8192, M 16384): stored bf16 dq 1.64e-5 dd 1.54e-5; bf16_split dq 7.9e-8 dd 7.1e-8
+#   C4 rank (M 131072):   stored bf16 dq 5.5e-6  dd 2.0e-6;  bf16_split dq 9.3e-8 dd 7.1e-8
+@pytest.mark.parametrize("form,tol", [("bf16", 3e-5), ("bf16_split", 1.5e-7)])
+def test_c3_scorer_full_size_vs_fp64(form, tol):
+    """The bf16 scorer forms at B 8192 x M 16384 x H 256 (C3, M = 2B) against float64 on the same
+    bf16-rounded q, d: loss to 1e-6, gradients to about 1.5-2x the measured error."""
     g = torch.Generator(device=DEV).manual_seed(4)
     q = torch.nn.functional.normalize(torch.randn(B, E, device=DEV, generator=g), dim=-1)
     d = torch.nn.functional.normalize(torch.randn(2 * B, E, device=DEV, generator=g), dim=-1)
     Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
-    loss = ops.in_batch_softmax_loss(Q, D, 0.1, compute_dtype="bf16")
+    loss = ops.in_batch_softmax_loss(Q, D, 0.1, compute_dtype=form)
     loss.backward()
-    qr = q.bfloat16().float().requires_grad_(True)
-    dr = d.bfloat16().float().requires_grad_(True)
-    ref = torch.nn.functional.cross_entropy(qr @ dr.T / 0.1, torch.arange(B, device=DEV))
-    ref.backward()
-    assert abs(loss.item() - ref.item()) < 1e-4 * abs(ref.item())
-    assert _rel(Q.grad.double().cpu().numpy(), qr.grad.double().cpu().numpy()) < 2e-2
-    assert _rel(D.grad.double().cpu().numpy(), dr.grad.double().cpu().numpy()) < 2e-2
+    rl, rdq, rdd = _ref64_in_batch(q.bfloat16().float(), d.bfloat16().float(), 0.1, 0)
+    assert abs(loss.item() - rl) < 1e-6 * abs(rl)
+    assert _rel_t(Q.grad, rdq) < tol and _rel_t(D.grad, rdd) < tol
 
 
-def test_c4_rank_scorer_at_eight_gpu_shape_vs_torch_fp32():
+def test_c4_rank_scorer_at_eight_gpu_shape_vs_fp64():
     """One rank of the 8-GPU cross-device step (BASELINE.json configs[3], C4): its B 8192 queries
     against all 8 x 2B = 131072 gathered candidates, labels offset to rank 5's block, H 256, on
-    the bf16 scorer; against torch fp32 on the same bf16-rounded operands (the largest scorer
-    shape the driver's scaling run reaches).  Loss to 1e-4, gradients to 2e-2."""
+    the bf16 scorer (stored probabilities: 2 GiB of P), against float64 on the same bf16-rounded
+    operands: loss to 1e-6, gradients to 1e-5 (measured 5.5e-6 / 2.0e-6)."""
     world, rank = 8, 5
     M = world * 2 * B
     g = torch.Generator(device=DEV).manual_seed(9)
@@ -112,14 +132,9 @@ def test_c4_rank_scorer_at_eight_gpu_shape_vs_torch_fp32():
     Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
     loss = ops.in_batch_softmax_loss(Q, D, 0.1, label_off=rank * 2 * B, compute_dtype="bf16")
     loss.backward()
-    qr = q.bfloat16().float().requires_grad_(True)
-    dr = d.bfloat16().float().requires_grad_(True)
-    labels = torch.arange(B, device=DEV) + rank * 2 * B
-    ref = torch.nn.functional.cross_entropy(qr @ dr.T / 0.1, labels)
-    ref.backward()
-    assert abs(loss.item() - ref.item()) < 1e-4 * abs(ref.item())
-    assert _rel(Q.grad.double().cpu().numpy(), qr.grad.double().cpu().numpy()) < 2e-2
-    assert _rel(D.grad.double().cpu().numpy(), dr.grad.double().cpu().numpy()) < 2e-2
+    rl, rdq, rdd = _ref64_in_batch(q.bfloat16().float(), d.bfloat16().float(), 0.1, rank * 2 * B)
+    assert abs(loss.item() - rl) < 1e-6 * abs(rl)
+    assert _rel_t(Q.grad, rdq) < 1e-5 and _rel_t(D.grad, rdd) < 1e-5
     # candidates of other ranks' blocks receive only softmax mass: no label term there
     assert float(D.grad[:rank * 2 * B].abs().max()) < float(D.grad[rank * 2 * B:(rank * 2 + 1) * B].abs().max())
 
@@ -185,3 +200,68 @@ def test_c5_full_size_update_and_multi_negative_loss():
     assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
     for got, want in ((Q.grad, Qr.grad), (P.grad, Pr.grad), (N.grad, Nr.grad)):
         assert _rel(got.double().cpu().numpy(), want.cpu().numpy()) < 1e-5
+
+
+# ---------------------------------------------------------------------------------------------
+# C2 (BASELINE.json configs[1]): V 50k, d 128, L 32, B 4096, in-batch negatives over M = 2B, fp32
+V2, E2, L2, B2 = 50_000, 128, 32, 4096
+
+
+def test_c2_scorer_full_size_vs_fp64_oracle():
+    """The fp32 in-batch scorer at the C2 shape (B 4096 queries x M 8192 candidates, H 128)
+    against the float64 oracle restatement of losses.py:88-118 (oracle/reference_math.py) on the
+    whole batch: loss, dq and dd within 1e-5 (max-abs normalised)."""
+    from oracle import reference_math as O
+
+    g = torch.Generator(device=DEV).manual_seed(21)
+    q = torch.nn.functional.normalize(torch.randn(B2, E2, device=DEV, generator=g), dim=-1)
+    d = torch.nn.functional.normalize(torch.randn(2 * B2, E2, device=DEV, generator=g), dim=-1)
+    Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
+    loss = tt.losses.in_batch_sampled_softmax_loss(Q, D, temperature=0.1, compute_dtype="fp32")
+    loss.backward()
+    rl, (rdq, rdd), _ = O.in_batch_fwd_bwd(q.double().cpu().numpy(), d.double().cpu().numpy(), 0.1)
+    assert abs(loss.item() - rl) < 1e-5 * abs(rl)
+    assert _rel(Q.grad.double().cpu().numpy(), rdq) < 1e-5
+    assert _rel(D.grad.double().cpu().numpy(), rdd) < 1e-5
+
+
+def test_c2_step_full_size_matches_cpu_oracle():
+    """Two whole C2 training steps (3 x 4096 sequences of 32 ids over a 50k x 128 table, tied
+    Linear-ReLU-Linear tower, fp32 in-batch loss over cat[p, n], fused table AdamW, graph
+    replay) against the CPU restatement of the reference step in float64 (oracle/cpu_step.py:
+    nn.Embedding + masked mean + FF + F.normalize, F.cross_entropy, torch.optim.AdamW): losses
+    within 1e-5, and every parameter's change within 1e-5 of its scale (+ 4 fp32 ulp of the
+    parameter).  eps = 1 on both sides keeps AdamW's update smooth in the gradient (see
+    test_c5_shaped_step_matches_cpu_oracle)."""
+    from oracle.cpu_step import RefTower, ref_loss
+
+    torch.manual_seed(22)
+    emb = tt.embeddings.build("lookup", vocab_size=V2, embedding_dim=E2)
+    model = tt.build_two_tower("mean", emb, hidden_dim=E2, tied_weights=True).to(DEV)
+    ref = RefTower(V2, E2, E2).double()
+    sd = {k.split("query_tower.")[1].replace("embedding.embedding", "embedding"): v.detach().cpu().double()
+          for k, v in model.state_dict().items() if k.startswith("query_tower.")}
+    ref.load_state_dict(sd)
+    init = {k: v.clone() for k, v in sd.items()}
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, eps=1.0, fused_tables=True, tables=[emb], capturable=True)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-3, eps=1.0)
+    loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype="fp32")
+    step = tt.TrainStep(model, loss_fn, opt, graph=True, eager_steps=1)
+    for k in range(2):
+        b = tt.data.synthetic_triplets(B2, L2, V2, seed=90 + k, device=DEV)
+        got = float(step(*b).item())
+        q, p, n = (t.cpu().long() for t in b)
+        rl = ref_loss("in_batch", ref(q), ref(p), ref(n))
+        ropt.zero_grad()
+        rl.backward()
+        ropt.step()
+        assert abs(got - float(rl)) < 1e-5 * max(1.0, abs(float(rl))), (k, got, float(rl))
+    rsd = ref.state_dict()
+    for k, v in model.state_dict().items():
+        if not k.startswith("query_tower."):
+            continue
+        key = k.split("query_tower.")[1].replace("embedding.embedding", "embedding")
+        want = rsd[key] - init[key]
+        diff = (v.double().cpu() - init[key] - want).abs()
+        tol = 1e-5 * want.abs().max() + 4 * 2.0 ** -24 * rsd[key].abs()
+        assert bool((diff <= tol).all()), (k, float((diff / tol).max()))

@@ -2,7 +2,8 @@
 oracle and the reference's golden vectors.  Tolerances: token-id indexing bit-exact (gathered
 rows / pooled values of single-token bags), fp32 loss and gradients within 1e-5 relative
 (max-abs normalised), bf16 scorer against the oracle on bf16-rounded inputs: 1e-4 for the
-hi/lo split of P (bf16_split) and 2e-2 for the standard single-rounding bf16 form."""
+hi/lo split of P (bf16_split) and the standard single-rounding bf16 form at about 1.5x their
+measured errors (BF16_SPLIT_GRAD_TOL, BF16_GRAD_TOL below)."""
 import os
 
 import numpy as np
@@ -15,6 +16,12 @@ from oracle import reference_math as O
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+# bf16 scorer gradient bars against the float64 oracle on the bf16-rounded operands (max-abs
+# normalised), at about 1.5x the largest error `tools/scorer_error_table.py --tests` measured
+# over every shape below, three seeds each (profiles/r02_scorer_error.md): stored-P bf16 1.40e-3
+# (recompute 0.95e-3; B 129, M 129, H 32: few terms per sum), bf16_split 1.54e-6
+BF16_GRAD_TOL = 2e-3
+BF16_SPLIT_GRAD_TOL = 2.5e-6
 
 
 def rel(a, b):
@@ -281,9 +288,75 @@ def test_in_batch_vs_oracle(H, B, M, off, dt):
     g = 0.7
     loss.backward(torch.tensor(g, device=DEV))
     rl, (rdq, rdd), _ = O.in_batch_fwd_bwd(q.astype(np.float64), d.astype(np.float64), 0.1, g=g, label_off=off)
-    tol = {"fp32": 1e-5, "bf16_split": 1e-4, "bf16": 2e-2}[dt]
+    tol = {"fp32": 1e-5, "bf16_split": BF16_SPLIT_GRAD_TOL, "bf16": BF16_GRAD_TOL}[dt]
     assert abs(loss.item() - rl) < 1e-5 * max(1.0, abs(rl))
     assert rel(Q.grad, rdq) < tol and rel(D.grad, rdd) < tol
+
+
+@pytest.mark.parametrize("H", [32, 64, 128, 256])
+@pytest.mark.parametrize("B,M,off", [(300, 700, 0), (129, 129, 0), (64, 256, 128), (1000, 2000, 1000),
+                                     (1, 64, 0), (320, 330, 10), (448, 900, 0), (2500, 2600, 100)])
+def test_in_batch_stored_backward_vs_oracle_and_recompute(H, B, M, off):
+    """The default bf16 backward (G from the forward's stored bf16 probabilities,
+    score_ddp_kernel) against the float64 oracle on the bf16-rounded operands, and against the
+    recompute backward.  The B values give every remainder of the kernel's five-stage rotation
+    (query tiles of 64 per split), the exits round 1's wrong-dD race lived on."""
+    rng = np.random.default_rng(7 * H + B + M)
+    q = torch.as_tensor(_unit(rng, B, H)).bfloat16().float().numpy()
+    d = torch.as_tensor(_unit(rng, M, H)).bfloat16().float().numpy()
+    g = 0.7
+    grads = {}
+    prev = ops.get_inbatch_backward()
+    try:
+        for form in ("stored", "recompute"):
+            ops.set_inbatch_backward(form)
+            Q, D = cuda(q).requires_grad_(True), cuda(d).requires_grad_(True)
+            loss = ops.InBatchSoftmaxLoss.apply(Q, D, 10.0, off, "bf16", None)
+            loss.backward(torch.tensor(g, device=DEV))
+            grads[form] = (loss.item(), Q.grad.clone(), D.grad.clone())
+    finally:
+        ops.set_inbatch_backward(prev)
+    rl, (rdq, rdd), _ = O.in_batch_fwd_bwd(q.astype(np.float64), d.astype(np.float64), 0.1, g=g, label_off=off)
+    loss, dq, dd = grads["stored"]
+    assert abs(loss - rl) < 1e-5 * max(1.0, abs(rl))
+    assert rel(dq, rdq) < BF16_GRAD_TOL and rel(dd, rdd) < BF16_GRAD_TOL
+    # the two backward forms differ only by the rounding of q~ * 2^(shift - lse2) to bf16 (one
+    # bf16 rounding, 2^-9, per summed term: largest where few queries contribute)
+    assert rel(dd, grads["recompute"][2]) < 4e-3 and torch.equal(dq, grads["recompute"][1])
+
+
+def test_in_batch_stored_backward_first_call_of_fresh_process():
+    """Round 1's failure showed on the first (cold) call of a process only: run the first bf16
+    in-batch forward + backward of a fresh process, with no host sync between the passes, at
+    H 32, 64 and 256 (each a first launch of its kernels), against the float64 oracle."""
+    import subprocess
+    import sys
+
+    code = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %r)
+from oracle import reference_math as O
+from twotower_amd import ops
+assert ops.get_inbatch_backward() == "stored"
+worst = 0.0
+for H in (32, 64, 256):
+    rng = np.random.default_rng(H)
+    q = rng.standard_normal((300, H)); d = rng.standard_normal((700, H))
+    q = torch.as_tensor(q / np.linalg.norm(q, axis=1, keepdims=True)).float().bfloat16().float()
+    d = torch.as_tensor(d / np.linalg.norm(d, axis=1, keepdims=True)).float().bfloat16().float()
+    Q, D = q.cuda().requires_grad_(True), d.cuda().requires_grad_(True)
+    ops.InBatchSoftmaxLoss.apply(Q, D, 10.0, 0, "bf16", None).backward()
+    _, (rdq, rdd), _ = O.in_batch_fwd_bwd(q.double().numpy(), d.double().numpy(), 0.1, g=1.0, label_off=0)
+    for got, want in ((Q.grad, rdq), (D.grad, rdd)):
+        e = float(np.nan_to_num(np.abs(got.double().cpu().numpy() - want).max(), nan=1e9) / np.abs(want).max())
+        worst = max(worst, e)
+print("WORST", worst)
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "TT_INBATCH_BWD"}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    worst = float(r.stdout.split("WORST")[1])
+    assert worst < BF16_GRAD_TOL, worst
 
 
 def _ex_rank(q, d, qb_all, lse2_all, db_all, parts_all, world, rank, inv_tau, dt, g):
@@ -352,6 +425,7 @@ def test_in_batch_candidate_owner_ranks_equal_global_batch(H, world, B, dt):
     Q = torch.cat(q).requires_grad_(True)
     D = torch.cat(d).requires_grad_(True)
     losses, dQ, dD = [], torch.zeros_like(Q), torch.zeros_like(D)
+    prev = ops.set_inbatch_backward("recompute")  # the owner passes recompute G: so does the reference
     for r in range(world):
         qr = Q.detach()[r * B:(r + 1) * B].clone().requires_grad_(True)
         Dr = D.detach().clone().requires_grad_(True)
@@ -360,9 +434,8 @@ def test_in_batch_candidate_owner_ranks_equal_global_batch(H, world, B, dt):
         losses.append(lr_.detach())
         dQ[r * B:(r + 1) * B] += qr.grad
         dD += Dr.grad
-    # dd: with TT_INBATCH_BWD=stored the single-process bf16 backward takes G from the forward's
-    # stored probabilities (one rounding more than the owner form's recomputed G: ~1e-4)
-    tol_dd = 1e-3 if dt == "bf16" and os.environ.get("TT_INBATCH_BWD") == "stored" else 1e-5
+    ops.set_inbatch_backward(prev)
+    tol_dd = 1e-5
     for r in range(world):
         loss, _, dq, dd = res[r]
         assert abs(loss.item() - losses[r].item()) < 1e-5 * max(1.0, abs(losses[r].item()))

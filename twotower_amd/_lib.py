@@ -19,6 +19,7 @@ TT_IDS_I32, TT_IDS_I64 = 0, 1
 TT_INBATCH_TAIL_ROWS, TT_INBATCH_MAX_PARTS = 64, 512  # twotower_amd.h
 TT_F32, TT_BF16, TT_BF16_SPLIT = 0, 1, 2
 TT_SCATTER_SORTED, TT_SCATTER_ATOMIC = 0, 1
+TT_INBATCH_BWD_RECOMPUTE, TT_INBATCH_BWD_STORED = 0, 1
 
 COMPUTE_DTYPES = {"fp32": TT_F32, "float32": TT_F32, "bf16": TT_BF16, "bfloat16": TT_BF16,
                   "bf16_split": TT_BF16_SPLIT}
@@ -81,6 +82,7 @@ _SIGNATURES = {
     "tt_triplet_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
     "tt_multi_neg_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp]),
     "tt_multi_neg_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
+    "tt_inbatch_set_backward": (_c_int, [_c_int]),
     "tt_inbatch_ws_size": (_c_sz, [_c_i64, _c_i64, _c_int, _c_int]),
     "tt_inbatch_fwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp, _vp, _vp,
                                 _vp, _c_sz, _vp]),

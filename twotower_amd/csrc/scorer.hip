@@ -17,6 +17,7 @@
 // logit, the -q_i contribution to dD) are applied by the combine kernels.
 // The streamed dimension is split over workgroups (blockIdx % S == split: one split per XCD
 // when S == 8); split partials are merged by the combine kernels.
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
@@ -808,14 +809,36 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
     __syncthreads();
     tie(next);
   };
-  for (int64_t t = 0; t < ntiles; t += 5) {
+  // Full rounds of five stages, then the remaining 0-4 stages as nested conditionals: no path
+  // through the code reaches a stage whose predecessor was skipped, and every register set is
+  // named again after the final drain.  The P loads of the last three stages are still in flight
+  // when the stages end; a set that were dead on some path (round 1: the sets of stages t+3/t+4
+  // when the loop ended after stage t or t+1, leaving through the latch) is free for the compiler
+  // to reuse while its load lands.  Round 1 found exactly that: the latch's loop-bound compare was
+  // allocated into the in-flight set of stage t+3, so a cold (slow) P load overwrote the bound and
+  // the wave ran on past its last tile (wrong dD for that wave's 32 candidates).
+  // tools/isa_audit.py checks the emitted ISA for any such use (tests/test_isa_audit.py).
+  int64_t t = 0;
+  for (; t + 5 <= ntiles; t += 5) {
     stage(t, pf[0], pf[3], pf[1]);
-    if (t + 1 < ntiles) stage(t + 1, pf[1], pf[4], pf[2]);
-    if (t + 2 < ntiles) stage(t + 2, pf[2], pf[0], pf[3]);
-    if (t + 3 < ntiles) stage(t + 3, pf[3], pf[1], pf[4]);
-    if (t + 4 < ntiles) stage(t + 4, pf[4], pf[2], pf[0]);
+    stage(t + 1, pf[1], pf[4], pf[2]);
+    stage(t + 2, pf[2], pf[0], pf[3]);
+    stage(t + 3, pf[3], pf[1], pf[4]);
+    stage(t + 4, pf[4], pf[2], pf[0]);
+  }
+  if (t < ntiles) {
+    stage(t, pf[0], pf[3], pf[1]);
+    if (t + 1 < ntiles) {
+      stage(t + 1, pf[1], pf[4], pf[2]);
+      if (t + 2 < ntiles) {
+        stage(t + 2, pf[2], pf[0], pf[3]);
+        if (t + 3 < ntiles) stage(t + 3, pf[3], pf[1], pf[4]);
+      }
+    }
   }
   drain_dma();  // no load may outlive the workgroup
+#pragma unroll
+  for (int k = 0; k < 5; ++k) tie(pf[k]);
   write_partials<DD, H>(acc, 0.f, split, nC, my_col, hh, acc_part, nullptr);
 }
 
@@ -1185,16 +1208,19 @@ struct Ws {
   size_t total;
 };
 
-// TT_INBATCH_BWD=stored (read once): the bf16 backward takes G from the forward's stored
-// probabilities instead of recomputing S = Q D^T.  Opt-in: at H <= 64 it gave wrong dD in a few
-// runs (B 300, M 700; not reproduced in isolation, never seen at H = 256), cause not yet found
-// (DESIGN.md §9).  P is kept only up to 2^31 entries (4 GiB of bf16).
-bool stored_p(int dtype, int64_t B, int64_t M) {
-  static const bool stored = [] {
+// Backward form of the single-process bf16 loss.  Default: stored probabilities (the backward
+// takes G from the forward's bf16 P instead of recomputing S = Q D^T; executed flops 6BMH instead
+// of 8BMH).  TT_INBATCH_BWD=recompute (read at load) or tt_inbatch_set_backward(0) selects the
+// recompute engine.  P is kept only up to 2^31 entries (4 GiB of bf16); larger batches recompute.
+std::atomic<int>& bwd_mode() {
+  static std::atomic<int> m{[] {
     const char* e = std::getenv("TT_INBATCH_BWD");
-    return e && std::strcmp(e, "stored") == 0;
-  }();
-  return dtype == TT_BF16 && stored && B * M <= (int64_t(1) << 31);
+    return (e && std::strcmp(e, "recompute") == 0) ? 0 : 1;
+  }()};
+  return m;
+}
+bool stored_p(int dtype, int64_t B, int64_t M) {
+  return dtype == TT_BF16 && bwd_mode().load(std::memory_order_relaxed) == 1 && B * M <= (int64_t(1) << 31);
 }
 
 // P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
@@ -1297,6 +1323,11 @@ Ws carve_user(void* ws, int64_t B, int64_t M, int H, int dtype) {
 }  // namespace tt
 
 using namespace tt;
+
+extern "C" int tt_inbatch_set_backward(int mode) {
+  if (mode != TT_INBATCH_BWD_RECOMPUTE && mode != TT_INBATCH_BWD_STORED) return bwd_mode().load();
+  return bwd_mode().exchange(mode);
+}
 
 extern "C" size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype) {
   return carve(nullptr, B, M, H, dtype).total + 256;

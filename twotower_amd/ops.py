@@ -491,6 +491,22 @@ class MultiNegLoss(torch.autograd.Function):
 
 # --------------------------------------------------------------------------------------------
 # in_batch_sampled_softmax_loss   (twotower/losses.py:88-118), fused MFMA scorer
+_BWD_FORMS = {"recompute": _lib.TT_INBATCH_BWD_RECOMPUTE, "stored": _lib.TT_INBATCH_BWD_STORED}
+
+
+def set_inbatch_backward(form: str) -> str:
+    """Select the single-process bf16 in-batch backward process-wide ("stored": G from the
+    forward's stored bf16 probabilities, the default; "recompute": recompute S = Q D^T) and return
+    the previous form.  Switch only between steps, never between a forward and its backward."""
+    prev = _lib.lib().tt_inbatch_set_backward(_BWD_FORMS[form])
+    return {v: k for k, v in _BWD_FORMS.items()}[prev]
+
+
+def get_inbatch_backward() -> str:
+    """The current single-process bf16 in-batch backward form ("stored" or "recompute")."""
+    return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
+
+
 def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad):
     B, H = q.shape
     M = d.shape[0]
