@@ -986,9 +986,11 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ d, int64_t M, int H, int gq,
                                                       __bf16* __restrict__ qb, __bf16* __restrict__ db,
                                                       float* __restrict__ qnorm, float* __restrict__ dmax_part,
-                                                      char* __restrict__ pad, float* __restrict__ lse2) {
+                                                      char* __restrict__ pad, float* __restrict__ lse2,
+                                                      int* __restrict__ xrows) {
   __shared__ float wmax[4];
   if (blockIdx.x == 0) {
+    if (xrows && threadIdx.x == 0) xrows[0] = 0;
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
@@ -1054,18 +1056,52 @@ __device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t
   return o;
 }
 
+// Exact row of the loss for a query whose shift bound overshot (l < 2^-100 would lose the row):
+// two passes over all M candidates with the true row max, as F.cross_entropy does
+// (twotower/losses.py:116).  One wave, fp32 dot products of the same operands the engine scores;
+// lane owns elements h = lane + 64 u.  Returns the row max m2 (log2 units), l = sum 2^(x c2 - m2)
+// and o = sum 2^(x c2 - m2) d~_j (the lane's elements).  A correctness net for pathological inputs
+// (small tau with large or weakly aligned rows): M dot products per row, far slower than the
+// engine, and never taken when the bound is within 100 log2 units of the row max.
+template <typename DT>
+__device__ float exact_row_dot(const DT* __restrict__ qr, const DT* __restrict__ dj, int H, int lane) {
+  float acc = 0.f;
+  for (int h = lane; h < H; h += kWave) acc += (float)qr[h] * (float)dj[h];
+  return wave_sum(acc);
+}
+
+template <typename DT>
+__device__ void exact_row(const DT* __restrict__ qr, const DT* __restrict__ Dm, int64_t M, int H, float c2, int lane,
+                          float& m2, float& l, float (&o)[4]) {
+  m2 = -INFINITY;
+  for (int64_t j = 0; j < M; ++j) m2 = fmaxf(m2, exact_row_dot(qr, Dm + j * H, H, lane) * c2);
+  l = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) o[u] = 0.f;
+  for (int64_t j = 0; j < M; ++j) {
+    const DT* dj = Dm + j * H;
+    const float p = __builtin_amdgcn_exp2f(exact_row_dot(qr, dj, H, lane) * c2 - m2);
+    l += p;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + kWave * u < H) o[u] += p * (float)dj[lane + kWave * u];
+  }
+}
+
 // Merge forward split partials, one wave per query row:
 //   l_i    = sum_s l_s,i - n_pad 2^-shift_i             (pad rows: X = 0 exactly)
 //   lse_i  = (shift_i + log2 l_i) ln 2
 //   loss_i = lse_i - (q~_i . d~_label) inv_tau           (diagonal logit, fp32 dot of the operands)
 //   dqu_i  = O_i / l_i - d~_label,   O_i = sum_s Acc_s,i
-// Rows whose bound sits so far above the true max that l underflows (l < 2^-100) report NaN.
+// Rows whose bound sits so far above the true max that l underflows (l < 2^-100) are redone
+// exactly (exact_row); with a stored-P backward they are listed in xrows for the backward combine.
 template <typename DT>
 __global__ __launch_bounds__(256) void fwd_combine_kernel(
-    int64_t B, int H, int S, int n_pad, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part,
-    int n_dmax, const float* __restrict__ l_part, const float* __restrict__ acc_part, float inv_tau, int64_t label_off,
-    const DT* __restrict__ Qmat, const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2,
-    float* __restrict__ loss_rows, float* __restrict__ dqu, __bf16* __restrict__ qs = nullptr) {
+    int64_t B, int64_t M, int H, int S, int n_pad, float c2, const float* __restrict__ qnorm,
+    const float* __restrict__ dmax_part, int n_dmax, const float* __restrict__ l_part,
+    const float* __restrict__ acc_part, float inv_tau, int64_t label_off, const DT* __restrict__ Qmat,
+    const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2, float* __restrict__ loss_rows,
+    float* __restrict__ dqu, __bf16* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = lane_id();
   if (i >= B) {  // the zero tail of the scaled query copy (the stored-P backward's R rows)
@@ -1077,11 +1113,31 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   float l = 0.f;
   for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
   l -= (float)n_pad * __builtin_amdgcn_exp2f(-sh);
-  const bool ok = l >= 7.888609052210118e-31f;  // 2^-100
-  const float lse2_i = ok ? sh + log2f(l) : NAN;  // log2 units, for the backward engine
-  const float lse_i = lse2_i * kLn2;
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
+  if (!(l >= 7.888609052210118e-31f)) {  // l < 2^-100 (or NaN): the bound overshot, redo the row exactly
+    float m2, lx, o[4];
+    exact_row(qr, Dmat, M, H, c2, lane, m2, lx, o);
+    const float lse2_i = m2 + log2f(lx);
+    const float dot = exact_row_dot(qr, dl, H, lane);
+    if (lane == 0) {
+      lse[i] = lse2_i * kLn2;
+      lse2[i] = lse2_i;
+      loss_rows[i] = lse2_i * kLn2 - dot * inv_tau;
+    }
+    const float inv_l = 1.f / lx;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = lane + kWave * u;
+      if (h >= H) break;
+      if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
+      if (qs) qs[i * H + h] = (__bf16)0.f;  // its stored P underflowed: the backward combine adds the row
+    }
+    if (qs && xrows && lane == 0) xrows[1 + atomicAdd(xrows, 1)] = (int)i;
+    return;
+  }
+  const float lse2_i = sh + log2f(l);  // log2 units, for the backward engine
+  const float lse_i = lse2_i * kLn2;
   if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
     const f32x4 qv = load4(qr, lane), dv = load4(dl, lane);
     float dot = wave_sum(qv[0] * dv[0] + qv[1] * dv[1] + qv[2] * dv[2] + qv[3] * dv[3]);
@@ -1096,7 +1152,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
       loss_rows[i] = lse_i - dot * inv_tau;
     }
     if (dqu) {
-      const float inv_l = ok ? 1.f / l : NAN;
+      const float inv_l = 1.f / l;
       const f32x4 o = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane, B * (H / 4), S);
       reinterpret_cast<f32x4*>(dqu + i * H)[lane] = o * inv_l - dv;
     }
@@ -1115,7 +1171,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     loss_rows[i] = lse_i - dot * inv_tau;
   }
   if (dqu) {
-    const float inv_l = ok ? 1.f / l : NAN;
+    const float inv_l = 1.f / l;
     for (int h = lane; h < H; h += kWave) {
       float o = 0.f;
       for (int s = 0; s < S; ++s) o += acc_part[((int64_t)s * B + i) * H + h];
@@ -1126,13 +1182,30 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
 
 // dd_j = scale (sum_s Acc_s,j - [0 <= j - off < B] q~_{j-off});  dq = scale * dqu;
 // scale = grad_loss * grad_scale * inv_tau.
+// Stored-P backward only (xrows non-null): query rows the forward redid exactly (their stored P
+// underflowed, their scaled-query rows are zero) add sum_i 2^(x_ij c2 - lse2_i) q~_i here.
+template <typename DT>
+__device__ __forceinline__ void add_exact_rows(f32x4& a, const int* __restrict__ xrows, const DT* __restrict__ Qmat,
+                                               const DT* __restrict__ dr, const float* __restrict__ lse2, float c2,
+                                               int H, int lane) {
+  const int n = xrows[0];
+  for (int k = 0; k < n; ++k) {
+    const int i = xrows[1 + k];
+    const DT* qr = Qmat + (int64_t)i * H;
+    const float g = __builtin_amdgcn_exp2f(exact_row_dot(qr, dr, H, lane) * c2 - lse2[i]);
+    a += g * load4(qr, lane);
+  }
+}
+
 template <typename DT>
 __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, int H, int S, int64_t label_off,
                                                           const float* __restrict__ acc_part,
                                                           const DT* __restrict__ Qmat, const float* __restrict__ dqu,
                                                           const float* __restrict__ grad_loss, float grad_scale,
                                                           float inv_tau, float* __restrict__ dq,
-                                                          float* __restrict__ dd) {
+                                                          float* __restrict__ dd, const int* __restrict__ xrows = nullptr,
+                                                          const DT* __restrict__ Dmat = nullptr,
+                                                          const float* __restrict__ lse2 = nullptr, float c2 = 0.f) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = lane_id();
   const float scale = grad_loss[0] * grad_scale * inv_tau;
@@ -1140,6 +1213,7 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
     if (r < M) {
       const int64_t qi = r - label_off;
       f32x4 a = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + r * (H / 4) + lane, M * (H / 4), S);
+      if (xrows) add_exact_rows(a, xrows, Qmat, Dmat + r * H, lse2, c2, H, lane);
       if (qi >= 0 && qi < B) a -= load4(Qmat + qi * H, lane);
       reinterpret_cast<f32x4*>(dd + r * H)[lane] = a * scale;
     }
@@ -1149,11 +1223,21 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
   if (r < M) {
     const int64_t qi = r - label_off;
     const bool lab = qi >= 0 && qi < B;
-    for (int h = lane; h < H; h += kWave) {
+    const int nx = xrows ? xrows[0] : 0;
+    for (int h0 = 0; h0 < H; h0 += kWave) {
+      const int h = h0 + lane;
       float a = 0.f;
-      for (int s = 0; s < S; ++s) a += acc_part[((int64_t)s * M + r) * H + h];
-      if (lab) a -= (float)Qmat[qi * H + h];
-      dd[r * H + h] = a * scale;
+      if (h < H)
+        for (int s = 0; s < S; ++s) a += acc_part[((int64_t)s * M + r) * H + h];
+      for (int k = 0; k < nx; ++k) {  // exact rows (stored-P backward; see add_exact_rows)
+        const int i = xrows[1 + k];
+        const float g = __builtin_amdgcn_exp2f(exact_row_dot(Qmat + (int64_t)i * H, Dmat + r * H, H, lane) * c2 - lse2[i]);
+        if (h < H) a += g * (float)Qmat[(int64_t)i * H + h];
+      }
+      if (h < H) {
+        if (lab) a -= (float)Qmat[qi * H + h];
+        dd[r * H + h] = a * scale;
+      }
     }
   }
   if (r < B) {
@@ -1198,6 +1282,7 @@ struct Ws {
   __bf16* Db;
   __bf16* Qs;   // stored-P backward: q~ scaled by 2^(shift - lse2) (+ zero tail)
   char* P;      // stored-P backward: bf16 probabilities, p_nct x p_nqt blocks of 2 KiB
+  int* xrows;   // stored-P backward: [count, rows...] of queries the forward redid exactly
   int64_t p_nqt;
   float* qnorm;
   float* lse2;
@@ -1246,6 +1331,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const bool sp = stored_p(dtype, B, M);
   const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * 2 : 0);
   const size_t op = take(sp ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : 0);
+  const size_t ox = take(sp ? (size_t)(B + 1) * 4 : 0);
   const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
@@ -1257,6 +1343,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.Db = reinterpret_cast<__bf16*>(b + od);
     w.Qs = sp ? reinterpret_cast<__bf16*>(b + oqs) : nullptr;
     w.P = sp ? b + op : nullptr;
+    w.xrows = sp ? reinterpret_cast<int*>(b + ox) : nullptr;
     w.p_nqt = p_nqt_for(B);
     w.qnorm = reinterpret_cast<float*>(b + oqn);
     w.lse2 = reinterpret_cast<float*>(b + ol2);
@@ -1342,7 +1429,7 @@ namespace {
 int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, int H, const float* qnorm,
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
-             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr) {
+             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr) {
   const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
@@ -1357,13 +1444,14 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
   const dim3 grid((unsigned)((B + (Qs ? kTailRows : 0) + 3) / 4)), block(256);
   if (dtype == TT_F32)
-    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
+    fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                     acc_part, inv_tau, label_off, static_cast<const float*>(Cm),
                                                     static_cast<const float*>(Rm), lse, lse2, loss_rows, dqu);
   else
-    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
+    fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                      acc_part, inv_tau, label_off, static_cast<const __bf16*>(Cm),
-                                                     static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu, Qs);
+                                                     static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu, Qs,
+                                                     xrows);
   TT_LAUNCH_CHECK("score_fwd_combine");
   return launch_mean(loss_rows, B, loss, s);
 }
@@ -1399,7 +1487,8 @@ int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const v
 // zero tail) and P, then the same combine (label terms from the unscaled q~).
 int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, const __bf16* Qs, const char* P,
                int64_t p_nqt, const __bf16* Qlab, const float* dqu, const float* grad_loss, float grad_scale,
-               float* dq, float* dd, float* acc_part, hipStream_t s) {
+               float* dq, float* dd, float* acc_part, const int* xrows, const __bf16* Db, const float* lse2,
+               hipStream_t s) {
   const Plan p = plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H));
   switch (H) {
 #define TT_DDP(HH)                                                                                                   \
@@ -1417,7 +1506,8 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
   TT_LAUNCH_CHECK("score_ddp");
   const int64_t rows = std::max(B, M);
   bwd_combine_kernel<__bf16><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(
-      B, M, H, p.S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, dq, dd);
+      B, M, H, p.S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, dq, dd, xrows, Db, lse2,
+      inv_tau * kLog2e);
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
@@ -1472,14 +1562,14 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
   const int gd = (int)std::min<int64_t>((M + 3) / 4, kMaxPrepBlocks);
   prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
                                                                  bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad,
-                                                                 w.lse2);
+                                                                 w.lse2, w.xrows);
   TT_LAUNCH_CHECK("score_prep");
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
   const bool sp = want_grad && w.P;
   return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
                   want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s, sp ? w.P : nullptr, w.p_nqt,
-                  sp ? w.Qs : nullptr);
+                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr);
 }
 
 extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
@@ -1496,7 +1586,7 @@ extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t
   const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
   const void* Cm = bf ? (const void*)w.Db : (const void*)d;
   if (w.P) return bwd_core_p(B, M, H, label_off, inv_tau, w.Qs, w.P, w.p_nqt, w.Qb, dq_unscaled, grad_loss, grad_scale,
-                             dq, dd, w.acc_part, s);
+                             dq, dd, w.acc_part, w.xrows, w.Db, w.lse2, s);
   return bwd_core(dtype, Rm, B, w.lse2, Cm, M, Rm, B, label_off, H, inv_tau, dq_unscaled, grad_loss, grad_scale, dq,
                   dd, w.pad, w.acc_part, s);
 }
