@@ -235,7 +235,7 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        from oracle.cpu_step import time_cpu_step  # CPU baseline only: the measured GPU path never uses it
+        from oracle.cpu_step import host_cores, time_cpu_step  # CPU baseline only: the GPU path never uses it
 
         cb = args.cpu_batch
         cpu_batches = [tuple(t[:cb].to("cpu", torch.int64) for t in b) for b in batches[:2]]
@@ -243,10 +243,22 @@ def main():
             cpu_batches = [tuple(t.to("cpu", torch.int64) for t in (b[0][:cb], b[1][:cb], b[2][:cb * K]))
                            for b in batches[:2]]
         r = time_cpu_step(V, d, d, cpu_batches, loss=cfg["loss"], min_seconds=args.cpu_seconds)
+        hc = host_cores()
+        # C1 (BASELINE.json configs[0]: configs/char_tower.yml, char vocab 34, E 64, H 128, triplet,
+        # batch 64, L 64): the reference's own CPU configuration, a few seconds
+        c1_batches = [tuple(t.long() for t in tt.data.synthetic_triplets(64, 64, 34, seed=k, device="cpu"))
+                      for k in range(2)]
+        r1 = time_cpu_step(34, 64, 128, c1_batches, loss="triplet", min_seconds=3.0, max_steps=5000)
         cpu = {"value": round(r["pairs_per_s"], 1), "unit": "pairs/s", "cores": r["threads"], "kind": "port",
-               "sample": f"torch-CPU restatement of the reference step (oracle/cpu_step.py), same V/d/L, batch "
+               "physical_cores": hc["physical_cores"], "logical_cpus": hc["logical_cpus"],
+               "sample": f"torch-CPU restatement of the reference step (oracle/cpu_step.py: train.py's step "
+                         f"body incl. its per-batch monitors, within 1-8 % of the reference's own train_epoch "
+                         f"on the same cores, profiles/r02_cpu_baseline_validation.json), same V/d/L, batch "
                          f"{min(cb, B)}" + (f" instead of {B}" if cb < B else "") + f", {cfg['loss']} loss fp32, "
-                         f"{r['steps']} steps in {r['seconds']:.1f}s"}
+                         f"{r['steps']} steps in {r['seconds']:.1f}s on {r['threads']} threads",
+               "c1": {"value": round(r1["pairs_per_s"], 1), "unit": "pairs/s",
+                      "sample": f"C1 (configs/char_tower.yml shape, batch 64): {r1['steps']} steps in "
+                                f"{r1['seconds']:.1f}s"}}
 
     line = {
         "metric": "(query,doc) pairs/sec whole node at B=8192 d=256; HBM GB/s on embed gather",

@@ -42,9 +42,35 @@ def ref_loss(name: str, q, p, n, temperature=0.1, margin=0.2):
     raise ValueError(name)
 
 
+def host_cores() -> dict:
+    """Physical cores this process may run on (affinity mask x /proc/cpuinfo core ids), the logical
+    CPUs in the mask, and the threads torch will use."""
+    import os
+
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    phys, cur = {}, {}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if "processor" in cur:
+                    phys[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                cur = {}
+                continue
+            k, v = (x.strip() for x in line.split(":", 1))
+            cur[k] = v
+        if "processor" in cur:
+            phys[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+    except OSError:
+        pass
+    cores = len({phys.get(c, ("?", c)) for c in cpus})
+    return {"physical_cores": cores, "logical_cpus": len(cpus), "torch_threads": torch.get_num_threads()}
+
+
 def time_cpu_step(V: int, E: int, H: int, batches, loss: str = "in_batch", threads: int | None = None,
                   min_seconds: float = 10.0, max_steps: int = 20) -> dict:
-    """Pairs/s of the reference CPU step on `batches` (list of (q, p, n) int64 CPU tensors)."""
+    """Pairs/s of the reference CPU step on `batches` (list of (q, p, n) int64 CPU tensors): the
+    body of train_epoch (twotower/train.py:103-166) without its tqdm bar and W&B calls.  Runs at
+    least 2 and at most max_steps steps, stopping once min_seconds have passed."""
     if threads:
         torch.set_num_threads(threads)
     torch.manual_seed(0)
@@ -58,6 +84,10 @@ def time_cpu_step(V: int, E: int, H: int, batches, loss: str = "in_batch", threa
         opt.zero_grad()
         loss_v.backward()
         opt.step()
+        with torch.no_grad():  # the loop's per-batch monitors (train.py:143-156)
+            F.cosine_similarity(qv, pv).mean().item()
+            F.cosine_similarity(qv, nv[:qv.shape[0]]).mean().item()
+        loss_v.item()
         return loss_v
 
     step(batches[0])                                                     # warm-up
