@@ -40,6 +40,13 @@ CONFIGS = {
                workload="C5: vocab 1M, d 256, seq 64, batch 8192 queries x (1 positive + 4 negatives), "
                "multiple_negatives InfoNCE (cosine / 0.1, fp32), sorted scatter-add embedding grad fused with AdamW"),
 }
+# measured scorer gradient error at C3 (max over dq, dd; profiles/r02_scorer_error_table.jsonl)
+SCORER_GRAD_ERROR = {
+    ("bf16", True): {"vs_rounded_operands": 1.64e-5, "vs_fp32_operands": 3.11e-3},
+    ("bf16", False): {"vs_rounded_operands": 1.64e-5, "vs_fp32_operands": 3.11e-3},
+    ("bf16_split", False): {"vs_rounded_operands": 7.9e-8, "vs_fp32_operands": 3.11e-3},
+    ("fp32", False): {"vs_fp32_operands": 9.7e-8},
+}
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 
@@ -207,16 +214,34 @@ def main():
         nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
     pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
     mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
-    add("in-batch scorer forward (S=QD^T, lse, P.D)", "tt_inbatch_fwd", 2.0 * B * M * d, "TFLOP/s", pk, "mfma",
-        "2*B*M*H algorithmic flops (S); the kernel also computes P.D (another 2BMH) for dQ",
-        executed=(2.0 + 2.0 * mult) * B * M * d)
     # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
     stored_p = (scorer_dtype == "bf16" and world == 1 and tt_ops.get_inbatch_backward() == "stored"
                 and B * M <= 2 ** 31)
-    add("in-batch scorer backward (dQ, dD)", "tt_inbatch_bwd", 4.0 * B * M * d, "TFLOP/s", pk, "mfma",
-        "4*B*M*H algorithmic flops (dQ = dS.D, dD = dS^T.Q); dQ's product runs in the forward"
-        + ("; G read from the forward's stored bf16 probabilities" if stored_p else ""),
-        executed=(2.0 if stored_p else 2.0 + 2.0 * mult) * B * M * d)
+    if "tt_inbatch_fwd" in ops_t and "tt_inbatch_bwd" in ops_t:
+        # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
+        # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
+        fwd_ms, bwd_ms = ops_t["tt_inbatch_fwd"]["mean_ms"], ops_t["tt_inbatch_bwd"]["mean_ms"]
+        ms = fwd_ms + bwd_ms
+        algo = 6.0 * B * M * d
+        executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
+        achieved = algo / (ms * 1e-3) / 1e12
+        form = ("bf16, backward from stored bf16 probabilities" if stored_p else
+                {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
+                 "fp32": "fp32 MFMA"}[scorer_dtype])
+        kernels.append({
+            "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
+            "abi": "tt_inbatch_fwd+tt_inbatch_bwd", "bound": "mfma", "mean_ms": round(ms, 4),
+            "pass_ms": {"forward": round(fwd_ms, 4), "backward": round(bwd_ms, 4)},
+            "calls_per_step": ops_t["tt_inbatch_fwd"]["calls"] / timing_steps, "achieved": round(achieved, 2),
+            "peak": pk, "unit": "TFLOP/s", "frac": round(achieved / pk, 4), "algorithmic": algo,
+            "executed": executed, "executed_rate": round(executed / (ms * 1e-3) / 1e12, 2),
+            "per_launch": "6*B*M*H algorithmic flops (2BMH S + 4BMH dQ, dD) over both passes",
+            "form": form,
+            # measured max-abs-normalised gradient error at C3 (tools/scorer_error_table.py --big,
+            # profiles/r02_scorer_error_table.jsonl): against float64 on the same bf16-rounded
+            # operands, and against float64 on the fp32 operands (what the reference computes)
+            "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
+        })
     add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
         HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
     add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
