@@ -38,10 +38,10 @@ _LABEL = re.compile(r"^(\.LBB\d+_\d+):")
 _VMEM_PREFIX = ("global_", "buffer_", "scratch_", "tbuffer_")
 
 
-def compile_to_asm(src: str, out_dir: str) -> str:
+def compile_to_asm(src: str, out_dir: str, extra=()) -> str:
     out = os.path.join(out_dir, os.path.basename(src) + ".s")
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-           "-I" + os.path.join(ROOT, "include"), "--cuda-device-only", "-S", src, "-o", out]
+           "-I" + os.path.join(ROOT, "include"), *extra, "--cuda-device-only", "-S", src, "-o", out]
     subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     return out
 
@@ -213,15 +213,120 @@ def audit_kernel(kname, blocks):
     return sorted(set(findings))
 
 
-def audit_file(src: str, only: str | None = None):
+def audit_file(src: str, only: str | None = None, extra=()):
     with tempfile.TemporaryDirectory() as d:
-        s = compile_to_asm(src, d)
+        s = compile_to_asm(src, d, extra)
         funcs = parse_functions(s)
     return audit_functions(funcs, only)
 
 
 def audit_asm_text(text: str, only: str | None = None):
     return audit_functions(parse_functions("", text), only)
+
+
+_MFMA = re.compile(r"^v_mfma")
+_OPND = re.compile(r"([va])\[(\d+):(\d+)\]|([va])(\d+)\b")
+XDL_VALU_STATES = 12  # 8-pass XDL (v_mfma_f32_32x32x16_bf16) result -> any other access
+VALU_XDL_STATES = 2   # VALU write -> MFMA operand read
+
+
+def _operands(args: str):
+    """-> list of register sets, one per comma-separated operand (literals give an empty set)."""
+    return [_regs(a) for a in args.split(",")]
+
+
+def _states(inst) -> int:
+    if inst.op == "s_nop":
+        try:
+            return int(inst.args.strip(), 0) + 1
+        except ValueError:
+            return 1
+    return 1
+
+
+def _linear(blocks):
+    out = []
+    for label, insts in blocks:
+        for i in insts:
+            out.append((label, i))
+    return out
+
+
+def audit_asm_mfma(kname, blocks):
+    """Wait states hipcc cannot insert around an MFMA issued from inline asm (cdna_hip_programming.md
+    §5.7 item 2): (a) a VALU write of any of its operands in the VALU_XDL_STATES before it; (b) any
+    access to its destination in the XDL_VALU_STATES after it, except the next MFMA taking it whole as
+    srcC (an accumulation chain).  Scanned in program order and across every branch to a label."""
+    findings = []
+    lin = _linear(blocks)
+    pos = {}
+    for n, (label, _) in enumerate(lin):
+        pos.setdefault(label, n)
+    # predecessors by branch (fall-through is program order)
+    branch_in = {}
+    for n, (_, i) in enumerate(lin):
+        if i.op.startswith(("s_branch", "s_cbranch")):
+            branch_in.setdefault(i.args.strip(), []).append(n)
+
+    def back(n, need, seen=None):
+        """instructions within `need` wait states before lin[n] (all paths)."""
+        seen = seen or set()
+        out = []
+        k, left = n - 1, need
+        label = lin[n][0]
+        starts = [n]
+        while k >= 0 and left > 0:
+            out.append(lin[k][1])
+            left -= _states(lin[k][1])
+            if lin[k][0] != lin[k + 1][0] and lin[k + 1][0] in branch_in:
+                for b in branch_in[lin[k + 1][0]]:
+                    if (b, left) not in seen:
+                        seen.add((b, left))
+                        out += back(b + 1, left, seen)
+            k -= 1
+        del label, starts
+        return out
+
+    def fwd(n, need, seen=None):
+        seen = seen or set()
+        out = []
+        k, left = n + 1, need
+        while k < len(lin) and left > 0:
+            inst = lin[k][1]
+            out.append(inst)
+            left -= _states(inst)
+            if inst.op.startswith(("s_branch", "s_cbranch")):
+                tgt = inst.args.strip()
+                if tgt in pos and (tgt, left) not in seen:
+                    seen.add((tgt, left))
+                    out += fwd(pos[tgt] - 1, left, seen)
+                if inst.op == "s_branch":
+                    break
+            k += 1
+        return out
+
+    for n, (_, inst) in enumerate(lin):
+        if not (inst.in_asm and _MFMA.match(inst.op)):
+            continue
+        ops = _operands(inst.args)
+        dst, srcs = ops[0], set().union(*ops[1:])
+        for prev in back(n, VALU_XDL_STATES):
+            if prev.op.startswith("v_") and not _MFMA.match(prev.op) and not prev.op.startswith("v_cmp"):
+                w = _operands(prev.args)[0] if prev.args else set()
+                if w & srcs:
+                    findings.append(f"{kname}: line {inst.line}: asm MFMA reads {sorted(w & srcs)[:2]} written by "
+                                    f"`{prev.op}` (line {prev.line}) fewer than {VALU_XDL_STATES} wait states before")
+        for nxt in fwd(n, XDL_VALU_STATES):
+            touched = _regs(nxt.args)
+            if not (touched & dst):
+                continue
+            if _MFMA.match(nxt.op):
+                o = _operands(nxt.args)
+                if o[-1] == dst and not (set().union(*o[1:-1]) & dst):
+                    continue  # accumulation chain: the next MFMA takes it whole as srcC
+            findings.append(f"{kname}: line {nxt.line}: `{nxt.op}` touches {sorted(touched & dst)[:2]} fewer than "
+                            f"{XDL_VALU_STATES} wait states after the asm MFMA at line {inst.line}")
+    return findings
 
 
 def audit_functions(funcs, only=None):
@@ -236,6 +341,7 @@ def audit_functions(funcs, only=None):
         n_asm_loads += sum(1 for _, insts in blocks for i in insts
                            if i.in_asm and _is_vmem(i.op) and "load" in i.op and "_lds" not in i.op)
         findings += audit_kernel(name, blocks)
+        findings += audit_asm_mfma(name, blocks)
         for key in ("vgpr_spill_count", "private_segment_fixed_size"):
             if meta.get(key, 0):
                 findings.append(f"{name}: .{key} = {meta[key]}")

@@ -18,6 +18,7 @@
 // The streamed dimension is split over workgroups (blockIdx % S == split: one split per XCD
 // when S == 8); split partials are merged by the combine kernels.
 #include <atomic>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 
@@ -310,15 +311,15 @@ struct NoHook {
 // which needs them only from its second half: the vector work is split between both MFMA runs.
 template <int MODE, bool PRECISE>
 struct MapState {
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  f32x2 c2v, ls, yv;
+  // scalar f32 only: packed f32 VALU beside MFMAs costs +22-26 cycles per instruction
+  // (MI355X_MICROARCH.md, 'price of one filler'), so no f32x2 here
+  float c2, ls;
   float sub[16];
   float e[16];
 
-  __device__ __forceinline__ void init(float c2, float shift, const lds_f32x4_t* lse4, int hh) {
-    c2v = f32x2{c2, c2};
-    ls = f32x2{0.f, 0.f};
-    yv = f32x2{0.f, 0.f};
+  __device__ __forceinline__ void init(float c2_, float shift, const lds_f32x4_t* lse4, int hh) {
+    c2 = c2_;
+    ls = 0.f;
     if constexpr (MODE == FWD) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) sub[v] = shift;
@@ -332,25 +333,21 @@ struct MapState {
     }
   }
 
+  // slot v: element v's exponent and exp; odd slots also add the pair to the row sum and pack it
   __device__ __forceinline__ void slot(int v, const f32x16& xa, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
-    const int p = v & ~1;
-    if ((v & 1) == 0) {
-      const f32x2 xv = {xa[p], xa[p + 1]}, sv = {sub[p], sub[p + 1]};
-      yv = xv * c2v - sv;
+    const float y = __builtin_fmaf(xa[v], c2, -sub[v]);
 #ifdef TT_ABLATE_EXP
-      e[p] = yv[0];
+    e[v] = y;
 #else
-      e[p] = __builtin_amdgcn_exp2f(yv[0]);
+    e[v] = __builtin_amdgcn_exp2f(y);
 #endif
-      asm volatile("" : "+v"(e[p]));  // side-effecting use: keeps the exp inside this step
-    } else {
-#ifdef TT_ABLATE_EXP
-      e[p + 1] = yv[1];
-#else
-      e[p + 1] = __builtin_amdgcn_exp2f(yv[1]);
-#endif
-      asm volatile("" : "+v"(e[p + 1]));
-      if constexpr (MODE == FWD) ls += f32x2{e[p], e[p + 1]};
+    asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
+    if (v & 1) {
+      const int p = v & ~1;
+      if constexpr (MODE == FWD) {
+        ls += e[p] + e[p + 1];
+        asm volatile("" : "+v"(ls));  // keeps the sum in this step (not sunk to the unit's end)
+      }
 #pragma unroll
       for (int w = p; w <= p + 1; ++w) {
         const __bf16 h = (__bf16)e[w];
@@ -422,7 +419,11 @@ __device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int jrow, 
   return acc;
 }
 
-// Acc chain with the transposed operand reads of each step issued two steps ahead.
+// Acc chain with the transposed operand reads of each step issued kApf steps ahead.
+#ifndef TT_APF
+#define TT_APF 2
+#endif
+constexpr int kApf = TT_APF;
 template <int MODE, bool PRECISE, int H, class Hook = NoHook>
 __device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, const LdsOffs<H>& lo,
                                                     bf16x8 (&bh)[2], bf16x8 (&bl)[2], f32x16 (&acc)[H / 32],
@@ -442,16 +443,16 @@ __device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int 
     const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
     return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
   };
-  bf16x8 op[3];
-  op[0] = load(0);
-  if (NS > 1) op[1] = load(1);
+  bf16x8 op[kApf + 1];
+#pragma unroll
+  for (int k = 0; k < kApf && k < NS; ++k) op[k] = load(k);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
-    if (st + 2 < NS) op[(st + 2) % 3] = load(st + 2);
+    if (st + kApf < NS) op[(st + kApf) % (kApf + 1)] = load(st + kApf);
     const int s2 = st / NHT, ht = st % NHT;
-    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], bh[s2], acc[ht], 0, 0, 0);
-    if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], bl[s2], acc[ht], 0, 0, 0);
+    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % (kApf + 1)], bh[s2], acc[ht], 0, 0, 0);
+    if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % (kApf + 1)], bl[s2], acc[ht], 0, 0, 0);
     if (st < NHT) {  // map slots 8-15 (G rows 16-31, first used at step NHT)
 #pragma unroll
       for (int v = 8 + 8 * st / NHT; v < 8 + 8 * (st + 1) / NHT; ++v) ms.slot(v, xa, bh, bl);
@@ -459,7 +460,112 @@ __device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int 
     hook(st);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if constexpr (MODE == FWD) l_run += ms.ls[0] + ms.ls[1];
+  if constexpr (MODE == FWD) l_run += ms.ls;
+}
+
+// ------------------------------------------------------------------------------------------
+// Forward unit U(j) as ONE stream of MFMA steps with a uniform operand prefetch distance kSd:
+//   steps [0, NK):        S chain of X tile j+1 (xb = R_{j+1} C^T), one ds_read_b128 operand each,
+//                         beside map slots 0-7 of X tile j (xa);
+//   steps [NK, NK + NSA): Acc chain of tile j (Acc^T += R_j^T G_j), two ds_read_b64_tr_b16 each,
+//                         beside map slots 8-15 and the P stores.
+// The operand of step i is read kSd steps ahead, ACROSS the chain boundaries: the Acc chain's first
+// operands are read during the last S steps, and the next unit's first S operands (X tile j+2)
+// during the last Acc steps, so no chain starts by waiting out a full LDS latency (round 2: 100-
+// 180 cycles at each of the four chain starts per stage).  The S chain accumulates into VGPRs by
+// inline asm (hipcc puts every MFMA accumulator in AGPRs here, which cost 16 v_accvgpr_read per
+// tile before the map could read X); its result is first read kSd + NSA steps later by the map of
+// the next unit, far beyond the 8-pass MFMA's wait states.
+#ifndef TT_SD
+#define TT_SD 4
+#endif
+template <int H>
+constexpr int kSdFor = TT_SD < H / 8 ? TT_SD : H / 8;  // <= NSTEP: never past the next unit
+
+#ifdef TT_S_BUILTIN  // diagnostic: the S chain through the builtin (compiler-placed accumulators)
+__device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, f32x16{}, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, d, 0, 0, 0);
+}
+#else
+__device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+}
+#endif
+
+template <int H>
+struct UnitSrc {
+  const lds_char_t* s;  // S chain source: stage tile + 32-row X tile base (bytes)
+  const lds_char_t* a;  // Acc chain source: stage tile + 32-row tile base (bytes)
+  const lds_char_t* n;  // next unit's S chain source
+};
+
+// Operand i of the step stream that starts at this unit: i in [0, NSTEP) is this unit's, i >= NSTEP
+// the next unit's (whose S source is u.n and whose Acc tile is this unit's S tile, u.s).
+template <int H>
+__device__ __forceinline__ bf16x8 unit_operand(int i, const UnitSrc<H>& u, const LdsOffs<H>& lo) {
+  using T = Tile<__bf16, H>;
+  constexpr int NK = H / 16, NHT = H / 32, NSA = 2 * NHT, NSTEP = NK + NSA;
+  const bool nxt = i >= NSTEP;
+  const int w = nxt ? i - NSTEP : i;
+#ifdef TT_ABLATE_LDSREAD  // timing ablation (never in a real build): no operand reads
+  return bf16x8{(__bf16)(float)w, (__bf16)(float)(lo.s[0] & 7), 0, 0, 0, 0, 0, (__bf16)(float)nxt};
+#endif
+  if (w < NK) {
+    const lds_char_t* tb = nxt ? u.n : u.s;
+    return *reinterpret_cast<const lds_bf16x8_t*>(tb + lo.s[w & 7] + (w >= 8 ? 256 : 0));
+  }
+  const lds_char_t* ta = nxt ? u.s : u.a;
+  const int st = w - NK, s2 = st / NHT, ht = st % NHT;
+  const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+  const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(ta + lo.a0[ht & 3] + imm));
+  const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(ta + lo.a1[ht & 3] + imm));
+  return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+}
+
+// One unit.  ring[] holds the operands of steps 0..kSd-1 on entry and of the next unit's steps
+// 0..kSd-1 on exit.  hook(step) places fills and P stores.
+template <int MODE, bool PRECISE, int H, class Hook>
+__device__ __forceinline__ void fwd_unit(const UnitSrc<H>& u, const LdsOffs<H>& lo, const bf16x8 (&cf)[H / 16],
+                                         const f32x16& xa, f32x16& xb, MapState<MODE, PRECISE>& ms,
+                                         bf16x8 (&ring)[kSdFor<H>], f32x16 (&acc)[H / 32], float& l_run, Hook hook) {
+  constexpr int NK = H / 16, NHT = H / 32, NSA = 2 * NHT, NSTEP = NK + NSA;
+  constexpr int kSd = kSdFor<H>;
+  static_assert(kSd <= NSTEP, "the prefetch may not reach past the next unit (stage barrier)");
+  bf16x8 bh[2], bl[2];
+  // The map's first read of xa follows the previous unit's last S MFMA by that unit's NSA Acc
+  // steps.  A VALU read of an 8-pass XDL result needs 12 wait states, and hipcc does not count the
+  // asm MFMAs: at H <= 64 (NSA <= 4, fewer than 12 instructions in between) pad them here.
+  if constexpr (NSA <= 4) asm volatile("s_nop 7\n\ts_nop 4" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NSTEP; ++i) {
+    const bf16x8 op = ring[i % kSd];
+    if (i < NK) {
+      if (i == 0) mfma_v_first(xb, op, cf[0]);
+      else mfma_v(xb, op, cf[i]);
+    } else {
+      const int st = i - NK, s2 = st / NHT, ht = st % NHT;
+      acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op, bh[s2], acc[ht], 0, 0, 0);
+      if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op, bl[s2], acc[ht], 0, 0, 0);
+    }
+    ring[i % kSd] = unit_operand<H>(i + kSd, u, lo);
+    if (i < NK) {
+#pragma unroll
+      for (int v = 8 * i / NK; v < 8 * (i + 1) / NK; ++v) ms.slot(v, xa, bh, bl);
+    } else if (i - NK < NHT) {  // map slots 8-15 (G rows 16-31, first used at Acc step NHT)
+      const int st = i - NK;
+#pragma unroll
+      for (int v = 8 + 8 * st / NHT; v < 8 + 8 * (st + 1) / NHT; ++v) ms.slot(v, xa, bh, bl);
+    }
+    hook(i, bh);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (MODE == FWD) l_run += ms.ls;
 }
 
 #ifdef TT_SCORER_TRACE  // debug builds only (tools/trace_scorer.py): s_memtime at region boundaries
@@ -556,6 +662,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // scalar per wave
   auto piece = [&](int c, int b, int64_t r0) {  // piece c of the stage at row r0 into buffer b
+#ifdef TT_ABLATE_FILL  // timing ablation (never in a real build): stages after the prologue keep stale data
+    if (r0 != row_begin || b != 0) return;
+#endif
     if (c < T::NI) {
       glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024);
     } else if constexpr (MODE == DD) {  // every wave loads the lse row (same bytes): uniform vmcnt
@@ -587,6 +696,83 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPC) : "memory");
   __syncthreads();
 
+#ifndef TT_FWD_V1
+  // Stage t = units U(2t) (jt 0) and U(2t+1) (jt 1); each unit's S chain scores the NEXT 32-row
+  // X tile, so jt 1's reads tile 0 of stage t+1.  One barrier per stage, at the start of U(2t):
+  // after it stage t+1 is visible (the fills of this wave landed: vmcnt; in every wave: barrier),
+  // and every wave is past stage t-1, whose buffer then takes the fills of stage t+3, spread over
+  // both units.  The next unit's first operands are read ahead across that barrier only from
+  // buffers it already covers (tile 1 of stage t, read at the end of U(2t-1)).
+  static_assert(NJ % 2 == 0, "X tiles alternate between two register sets");
+  f32x16 xa, xb;
+  {  // X tile 0 (its operand reads exposed once), into VGPRs like every later X tile
+    const UnitSrc<H> u0{lds, lds, lds};
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const bf16x8 a = unit_operand<H>(k, u0, lo);
+      // cf was just formed by VALU (v_cndmask): a VALU write -> MFMA operand read needs 2 wait
+      // states, which hipcc does not insert ahead of an asm statement
+      asm volatile("s_nop 1" ::"v"(cf[k]), "v"(a));
+      if (k == 0) mfma_v_first(xa, a, cf[0]);
+      else mfma_v(xa, a, cf[k]);
+    }
+    // the first unit's map reads xa within a few instructions: 12+ wait states after the last
+    // asm MFMA (8-pass XDL write -> VALU read; hipcc pads nothing for an asm statement)
+    asm volatile("s_nop 7\n\ts_nop 7" : "+v"(xa));
+  }
+  bf16x8 ring[kSdFor<H>];
+  {
+    UnitSrc<H> u0{lds + 32 * T::ROWB, lds, lds};  // the first unit's S source: tile 1 of stage 0
+#pragma unroll
+    for (int k = 0; k < kSdFor<H>; ++k) ring[k] = unit_operand<H>(k, u0, lo);
+  }
+  constexpr int NSTEP = NK + 2 * NHT;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int buf = (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
+    const int64_t frow = stage_row(t + 3);
+    const lds_char_t* tile = lds + buf * T::STAGE_B;
+    const lds_char_t* ntl = lds + nbuf * T::STAGE_B;
+    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
+    TT_TRACE(0);
+    // every VMEM op of stage t-1 (NPC fills, 8 P stores per tile) may still be in flight; all older
+    // ones, among them the fills of stage t+1 (issued during stage t-2), have landed
+    if (t == 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + (STOREP ? 8 * NJ : 0)) : "memory");
+    TT_TRACE(1);
+#ifndef TT_ABLATE_BARRIER
+    asm volatile("s_barrier" ::: "memory");
+#endif
+    TT_TRACE(2);
+    auto unit = [&](auto jtc, const f32x16& xin, f32x16& xout) {
+      constexpr int jt = decltype(jtc)::value;
+      auto src = [&](int k) {  // 32-row tile k of stage t (k >= NJ: of stage t+1)
+        return k < NJ ? tile + k * 32 * T::ROWB : ntl + (k - NJ) * 32 * T::ROWB;
+      };
+      const UnitSrc<H> u{src(jt + 1), src(jt), src(jt + 2)};
+      MapState<MODE, PRECISE> ms;
+      ms.init(c2, shift, lse4 + jt * 8, hh);
+      char* blk = STOREP ? pblk(t, jt) : nullptr;
+      auto hook = [&](int i, const bf16x8 (&bh)[2]) {
+#pragma unroll
+        for (int c = 0; c < NPC; ++c)
+          if (c * (NJ * NSTEP) / NPC == jt * NSTEP + i) piece(c, fbuf, frow);
+        if constexpr (STOREP) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (NK + k * (2 * NHT) / 8 == i) store_p_piece(blk, p_lane, hh_odd, bh, k);
+        }
+      };
+      fwd_unit<MODE, PRECISE, H>(u, lo, cf, xin, xout, ms, ring, acc, l_run, hook);
+      TT_TRACE(3 + jt);
+    };
+    // the X tiles alternate between xa and xb: no copy between units
+    static_assert(NJ == 2, "two units per stage");
+    unit(std::integral_constant<int, 0>{}, xa, xb);
+    unit(std::integral_constant<int, 1>{}, xb, xa);
+  }
+#else
   f32x16 xa = ntiles > 0 ? s_chain<H>(lds, r32, hh, cf) : f32x16{};
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
@@ -665,6 +851,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
       xa = xb;
     }
   }
+#endif
   drain_dma();  // no LDS-DMA may outlive the workgroup
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 }
@@ -707,15 +894,15 @@ __device__ __forceinline__ void acc_chain_p(const lds_char_t* tile, int jt, cons
     const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
     return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
   };
-  bf16x8 op[3];
-  op[0] = load(0);
-  if (NS > 1) op[1] = load(1);
+  bf16x8 op[kApf + 1];
+#pragma unroll
+  for (int k = 0; k < kApf && k < NS; ++k) op[k] = load(k);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int st = 0; st < NS; ++st) {
-    if (st + 2 < NS) op[(st + 2) % 3] = load(st + 2);
+    if (st + kApf < NS) op[(st + kApf) % (kApf + 1)] = load(st + kApf);
     const int s2 = st / NHT, ht = st % NHT;
-    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % 3], g[s2], acc[ht], 0, 0, 0);
+    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % (kApf + 1)], g[s2], acc[ht], 0, 0, 0);
     hook(jt * NS + st);
     __builtin_amdgcn_sched_barrier(0);
   }
