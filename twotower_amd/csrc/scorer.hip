@@ -574,9 +574,29 @@ __device__ long long g_tt_trace[8 * 64];
   do {                                                                                               \
     if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace[t * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+__device__ long long g_tt_trace_b[8 * 64];
+__device__ long long g_tt_ktrace[2 * 1024 * 4];  // [bwd, fwd] per workgroup (wave 0): s_memrealtime at entry, loop start, loop end, exit
+#define TT_KTRACE(slot) TT_KTRACE_K(0, slot)
+#define TT_KTRACE_K(k, slot)                                                                        \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_tt_ktrace[(k) * 4096 + blockIdx.x * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define TT_TRACE_B(slot)                                                                             \
+  do {                                                                                               \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace_b[t * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define TT_TRACE(slot) \
   do {                 \
+  } while (0)
+#define TT_TRACE_B(slot) \
+  do {                   \
+  } while (0)
+#define TT_KTRACE(slot) \
+  do {                  \
+  } while (0)
+#define TT_KTRACE_K(k, slot) \
+  do {                       \
   } while (0)
 #endif
 
@@ -633,6 +653,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const int64_t row_begin = (int64_t)split * rows_per_split;
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
+  if (MODE == FWD) TT_KTRACE_K(1, 0);
   const float dmax = MODE == FWD ? fold_dmax(dmax_part, n_dmax) : 0.f;  // wave-uniform call
   const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
 
@@ -727,6 +748,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     for (int k = 0; k < kSdFor<H>; ++k) ring[k] = unit_operand<H>(k, u0, lo);
   }
   constexpr int NSTEP = NK + 2 * NHT;
+  if (MODE == FWD) TT_KTRACE_K(1, 1);
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
     const int64_t frow = stage_row(t + 3);
@@ -852,8 +874,13 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     }
   }
 #endif
+  if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+#ifdef TT_SCORER_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  if (MODE == FWD) TT_KTRACE_K(1, 3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -908,7 +935,12 @@ __device__ __forceinline__ void acc_chain_p(const lds_char_t* tile, int jt, cons
   }
 }
 
-template <int H>
+// CW = candidate tiles (of 32) per wave.  CW = 2 (H = 256): every transposed Qs operand read feeds
+// two MFMAs and every staged Qs byte twice the MFMAs, which halves the LDS-DMA fill pieces per
+// MFMA; the stage's vector-memory instructions (fills + P loads), issued while every wave of the
+// CU issues them too, were what bounded this kernel (round 2 trace: a 16-MFMA tile carrying 12
+// of them took 1488 cycles, the same tile without them 592).
+template <int H, int CW>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
     const __bf16* __restrict__ R, int64_t nR, int64_t nC, int S, int64_t rows_per_split, const char* __restrict__ P,
     int64_t p_nqt, float* __restrict__ acc_part) {
@@ -917,7 +949,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   constexpr int NJ = T::BJ / 32;
   static_assert(NJ == 2 && T::NSTAGE == 4, "two 32-row tiles per stage, four-stage ring");
   constexpr int NPC = T::NI;                // fill pieces per stage per wave
-  constexpr int NSTEP = NJ * 2 * NHT;       // MFMA steps per stage
+  constexpr int NS = 2 * NHT;               // operand steps per 32-row tile (CW MFMAs each)
+  constexpr int NSTEP = NJ * NS;            // operand steps per stage
+  constexpr int NPL = 2 * NJ * CW;          // P loads per stage per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const lds_char_t* lds = (const lds_char_t*)smem;
 
@@ -925,77 +959,139 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   const int r32 = lane & 31, hh = lane >> 5;
   const int split = blockIdx.x % S;
   const int64_t cb = blockIdx.x / S;
-  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
+  const int64_t ct0 = (cb * NW + wid) * CW;  // this wave's first 32-candidate tile
   const int64_t row_begin = (int64_t)split * rows_per_split;
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
 
+  TT_KTRACE(0);
   const FillOffs<__bf16, H> fo = make_fill_offs<__bf16, H>();
   LdsOffs<H> lo;
   lo.init(lane);
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
   auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
-  auto fill = [&](int c, int b, int64_t r0) { glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024); };
-  // this wave's candidate tile; a lane's fragment of a P block: candidate row r32, positions
-  // (2 s2 + hh) * 8 .. + 8
-  const char* pcol = P + (cb * NW + wid) * p_nqt * 2048;
+  auto fill = [&](int c, int b, int64_t r0) {
+#ifdef TT_ABLATE_FILL  // timing ablation (never in a real build): stages after the prologue keep stale data
+    if (r0 != row_begin || b > 2) return;
+#endif
+    glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024);
+  };
+  // a lane's fragment of a P block: candidate row r32, query positions (2 s2 + hh) * 8 .. + 8
+  const char* pcol = P + ct0 * p_nqt * 2048;
   const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
   // P fragments of stages t .. t+3 in five register sets (index t % 5): the loads of stage t+3
   // go into the set stage t-2 read, so no load is in flight into registers an MFMA of the
   // previous stage may still be reading (the asm loads are outside the compiler's hazard checks)
-  bf16x8 pf[5][NJ][2];
-  auto pissue = [&](bf16x8 (&dst)[NJ][2], int64_t t) {
-    const char* b = pcol + (stage_row(t) / 32) * 2048;
-#pragma unroll
-    for (int jt = 0; jt < NJ; ++jt) {
-      dst[jt][0] = p_load<0>(b + jt * 2048, pvo);
-      dst[jt][1] = p_load<1>(b + jt * 2048, pvo);
-    }
+  struct PSet {
+    bf16x8 v[NJ][CW][2];
   };
-  auto tie = [&](bf16x8 (&x)[NJ][2]) {
+  PSet pf[5];
+  auto pload = [&](PSet& dst, int64_t t, int k) {  // P load k (of NPL) of stage t
+    const int c = k / (2 * NJ), jt = (k / 2) % NJ;
+    const char* b = pcol + (c * p_nqt + stage_row(t) / 32 + jt) * 2048;
+    if (k % 2 == 0) dst.v[jt][c][0] = p_load<0>(b, pvo);
+    else dst.v[jt][c][1] = p_load<1>(b, pvo);
+  };
+  auto pissue = [&](PSet& dst, int64_t t) {
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) pload(dst, t, k);
+  };
+  auto tie = [&](PSet& x) {
 #pragma unroll
     for (int jt = 0; jt < NJ; ++jt)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) asm volatile("" : "+v"(x[jt][s2]));
+      for (int c = 0; c < CW; ++c)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) asm volatile("" : "+v"(x.v[jt][c][s2]));
   };
 #ifdef TT_ABLATE_PLOAD
-  constexpr int kInFlight = 2 * NPC;
+  constexpr int kPl = 0;
 #else
-  constexpr int kInFlight = 2 * (NPC + 2 * NJ);  // P loads + fills of the two newest stages
+  constexpr int kPl = NPL;
 #endif
-  // prologue in steady-state order: [P(k), fills(k)] for k = 0, 1, 2
+  // prologue in steady-state order: [P(k), fills(k)] for k = 0, 1, 2, but only the first half
+  // of fills(2): the second half of every stage's fills comes from the first tile of the stage
+  // two before it (below)
+  constexpr int NPC2 = NPC / 2, NPC1 = NPC - NPC2;  // pieces in the first / second half
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     pissue(pf[k], k);
 #pragma unroll
-    for (int c = 0; c < NPC; ++c) fill(c, k, stage_row(k));
+    for (int c = 0; c < (k < 2 ? NPC : NPC1); ++c) fill(c, k, stage_row(k));
   }
 
-  f32x16 acc[NHT];
+  f32x16 acc[CW][NHT];
 #pragma unroll
-  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  // stage 0 and P(0) landed
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kInFlight) : "memory");
+  for (int c = 0; c < CW; ++c)
+#pragma unroll
+    for (int t = 0; t < NHT; ++t) acc[c][t] = f32x16{};
+  // stage 0 and P(0) landed: only P(1), fills(1), P(2) and fills(2)'s first half may be in flight
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + NPC1 + 2 * kPl) : "memory");
   __syncthreads();
   tie(pf[0]);
 
-  auto stage = [&](int64_t t, bf16x8 (&cur)[NJ][2], bf16x8 (&ahead)[NJ][2], bf16x8 (&next)[NJ][2]) {
-    const int buf = (int)(t & 3), fbuf = (buf + 3) & 3;
-    const int64_t frow = stage_row(t + 3);
-    pissue(ahead, t + 3);
-    auto hook = [&](int step) {
-#pragma unroll
-      for (int c = 0; c < NPC; ++c)
-        if (c * NSTEP / NPC == step) fill(c, fbuf, frow);
-    };
-    const lds_char_t* tile = lds + buf * T::STAGE_B;
-#pragma unroll
-    for (int jt = 0; jt < NJ; ++jt) acc_chain_p<H>(tile, jt, lo, cur[jt], acc, hook);
-    // stage t+1 and P(t+1) landed in this wave; then every wave is past stage t
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kInFlight) : "memory");
-    __syncthreads();
-    tie(next);
+  // One stream of NSTEP operand steps per stage whose A operands (two transposed reads each) are
+  // read kDd steps ahead, across the tile boundary and into the next stage: the stage barrier sits
+  // in the MIDDLE of stage t (before tile 1) and waits for stage t+1 (its fills and P(t+1)), so
+  // the last steps of stage t may read stage t+1's first operands.  After that barrier every wave
+  // is past stage t-1, so the first half of fills(t+3) (into stage t-1's buffer) is issued over
+  // tile 1 and its second half over tile 0 of stage t+1; P(t+3) is loaded over tile 0 of stage t,
+  // after that tile's fill pieces.  The vector-memory instructions are spread over the whole
+  // stage: in bursts they cost each wave ~75 cycles apiece (round 2 trace).  At the barrier of stage t the VMEM ops younger than fills(t+1)'s last
+  // piece (tile 0 of stage t-1) are P(t+2), fills(t+2) and P(t+3): vmcnt(NPC + 2 NPL).
+  constexpr int kDd = kSdFor<H> < NS ? kSdFor<H> : NS;
+  auto opnd = [&](const lds_char_t* stile, int i) {  // A operand of step i of the stage at stile
+    const int jt = i / NS, st = i % NS, s2 = st / NHT, ht = st % NHT;
+    const lds_char_t* tb = stile + jt * 32 * T::ROWB;
+    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
+    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
+    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
   };
+  bf16x8 ring[kDd];
+#pragma unroll
+  for (int k = 0; k < kDd; ++k) ring[k] = opnd(lds, k);
+  auto stage = [&](int64_t t, PSet& cur, PSet& ahead, PSet& next) {
+    const int buf = (int)(t & 3), fbuf = (buf + 3) & 3, hbuf = (buf + 2) & 3;
+    const int64_t frow = stage_row(t + 3), hrow = stage_row(t + 2);
+    const lds_char_t* tile = lds + buf * T::STAGE_B;
+    const lds_char_t* ntile = lds + ((buf + 1) & 3) * T::STAGE_B;
+    TT_TRACE_B(0);
+#pragma unroll
+    for (int i = 0; i < NSTEP; ++i) {
+      if (i == NS) {
+        TT_TRACE_B(1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + 2 * kPl) : "memory");
+        TT_TRACE_B(2);
+#ifndef TT_ABLATE_BARRIER
+        asm volatile("s_barrier" ::: "memory");
+#endif
+        TT_TRACE_B(3);
+        tie(next);
+      }
+      const int jt = i / NS, st = i % NS, s2 = st / NHT, ht = st % NHT;
+#pragma unroll
+      for (int c = 0; c < CW; ++c)
+        acc[c][ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[i % kDd], cur.v[jt][c][s2], acc[c][ht], 0, 0, 0);
+      const int j = i + kDd;
+      ring[i % kDd] = j < NSTEP ? opnd(tile, j) : opnd(ntile, j - NSTEP);
+      // tile 0: the second half of fills(t+2) in its first half, then P(t+3) one load at a time
+      constexpr int F0 = NS / 2;
+#pragma unroll
+      for (int c = 0; c < NPC2; ++c)
+        if (c * F0 / NPC2 == i) fill(NPC1 + c, hbuf, hrow);
+#pragma unroll
+      for (int k = 0; k < NPL; ++k)
+        if (F0 + k * (NS - F0) / NPL == i) pload(ahead, t + 3, k);
+#pragma unroll
+      for (int c = 0; c < NPC1; ++c)
+        if (NS + c * NS / NPC1 == i) fill(c, fbuf, frow);    // tile 1: first half of fills(t+3)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    TT_TRACE_B(4);
+  };
+  static_assert(NJ == 2, "the stage barrier sits before tile 1");
+  TT_KTRACE(1);
   // Full rounds of five stages, then the remaining 0-4 stages as nested conditionals: no path
   // through the code reaches a stage whose predecessor was skipped, and every register set is
   // named again after the final drain.  The P loads of the last three stages are still in flight
@@ -1023,10 +1119,17 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
       }
     }
   }
+  TT_KTRACE(2);
   drain_dma();  // no load may outlive the workgroup
 #pragma unroll
   for (int k = 0; k < 5; ++k) tie(pf[k]);
-  write_partials<DD, H>(acc, 0.f, split, nC, my_col, hh, acc_part, nullptr);
+#pragma unroll
+  for (int c = 0; c < CW; ++c)
+    write_partials<DD, H>(acc[c], 0.f, split, nC, (ct0 + c) * 32 + r32, hh, acc_part, nullptr);
+#ifdef TT_SCORER_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  TT_KTRACE(3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1443,8 +1546,8 @@ struct Plan {
 
 // Split the streamed rows so the grid is one round of resident workgroups (256 CUs x wg_per_cu):
 // a second round would only add prologues/epilogues and twice the split partials.
-Plan plan_for(int64_t nR, int64_t nC, int BJ, int wg_per_cu) {
-  const int64_t ncb = (nC + 32 * NW - 1) / (32 * NW);
+Plan plan_for(int64_t nR, int64_t nC, int BJ, int wg_per_cu, int cols_per_block = 32 * NW) {
+  const int64_t ncb = (nC + cols_per_block - 1) / cols_per_block;
   const int64_t row_tiles = (nR + BJ - 1) / BJ;
   const int64_t target = 256 * wg_per_cu;
   int64_t S = (target + ncb - 1) / ncb;
@@ -1498,7 +1601,16 @@ bool stored_p(int dtype, int64_t B, int64_t M) {
 // P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
 // backward's 128-column blocks (every tile either engine touches exists)
 int64_t p_nqt_for(int64_t B) { return (B + 127) / 128 * 4; }
-int64_t p_nct_for(int64_t M) { return (M + 127) / 128 * 4; }
+int64_t p_nct_for(int64_t M) { return (M + 255) / 256 * 8; }  // also the 256-candidate backward blocks
+
+// candidate tiles per wave of the stored-P backward (score_ddp_kernel<H, CW>)
+#ifndef TT_DDP_CW256
+#define TT_DDP_CW256 1  // CW = 2 runs the loop ~15 % faster but doubles the split partials (S = 4): net slower (round 2)
+#endif
+int ddp_cw(int H) { return H == 256 ? TT_DDP_CW256 : 1; }
+Plan ddp_plan(int64_t B, int64_t M, int H) {
+  return plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H), 32 * NW * ddp_cw(H));
+}
 
 // Layout: [Qb | Db | Qs | P] persist from forward to backward (the backward's MFMA operands);
 // everything else is scratch reused by both passes.
@@ -1521,7 +1633,8 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const size_t ox = take(sp ? (size_t)(B + 1) * 4 : 0);
   const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
-  const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
+  size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
+  if (sp) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
   const size_t oa = take(parts);
   Ws w{};
   char* b = static_cast<char*>(base);
@@ -1676,17 +1789,17 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
                int64_t p_nqt, const __bf16* Qlab, const float* dqu, const float* grad_loss, float grad_scale,
                float* dq, float* dd, float* acc_part, const int* xrows, const __bf16* Db, const float* lse2,
                hipStream_t s) {
-  const Plan p = plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H));
+  const Plan p = ddp_plan(B, M, H);
   switch (H) {
-#define TT_DDP(HH)                                                                                                   \
+#define TT_DDP(HH, CW)                                                                                               \
   case HH:                                                                                                           \
-    score_ddp_kernel<HH><<<dim3(p.grid), dim3(NT), Tile<__bf16, HH>::LDS_BYTES, s>>>(Qs, B, M, p.S, p.rows_per_split, \
-                                                                                    P, p_nqt, acc_part);            \
+    score_ddp_kernel<HH, CW><<<dim3(p.grid), dim3(NT), Tile<__bf16, HH>::LDS_BYTES, s>>>(                           \
+        Qs, B, M, p.S, p.rows_per_split, P, p_nqt, acc_part);                                                        \
     break;
-    TT_DDP(32)
-    TT_DDP(64)
-    TT_DDP(128)
-    TT_DDP(256)
+    TT_DDP(32, 1)
+    TT_DDP(64, 1)
+    TT_DDP(128, 1)
+    TT_DDP(256, TT_DDP_CW256)
 #undef TT_DDP
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
@@ -1832,5 +1945,11 @@ extern "C" int tt_inbatch_bwd_ex(const void* Qb_all, const float* lse2_all, int6
 #ifdef TT_SCORER_TRACE
 extern "C" int tt_debug_scorer_trace(long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_trace), sizeof(long long) * 8 * 64);
+}
+extern "C" int tt_debug_scorer_ktrace(long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_ktrace), sizeof(long long) * 2 * 1024 * 4);
+}
+extern "C" int tt_debug_scorer_trace_bwd(long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_trace_b), sizeof(long long) * 8 * 64);
 }
 #endif
