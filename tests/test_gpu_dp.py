@@ -162,3 +162,65 @@ def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp):
         for k in KEYS:
             err = abs(got[k] - want[k]).max() / abs(want[k]).max()
             assert err < 1e-5, (inbatch_dp, r, k, float(err))
+
+
+def _seed_worker(rank, port, q, seeds, Bq, M, H):
+    import numpy as np
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        from twotower_amd import ops
+
+        rng = np.random.default_rng(11)
+        qa, da = rng.standard_normal((WORLD * Bq, H)), rng.standard_normal((WORLD * M, H))
+        qa = torch.as_tensor(qa / np.linalg.norm(qa, axis=1, keepdims=True), dtype=torch.float32).bfloat16().float()
+        da = torch.as_tensor(da / np.linalg.norm(da, axis=1, keepdims=True), dtype=torch.float32).bfloat16().float()
+        Q = qa[rank * Bq:(rank + 1) * Bq].to("cuda:0").requires_grad_(True)
+        D = da[rank * M:(rank + 1) * M].to("cuda:0").requires_grad_(True)
+        loss = ops.InBatchSoftmaxLossOwned.apply(Q, D, 10.0, "bf16", None, None)
+        loss.backward(torch.tensor(seeds[rank], device="cuda:0"))
+        torch.cuda.synchronize()
+        q.put((rank, Q.grad.cpu().numpy(), D.grad.cpu().numpy(), qa.numpy(), da.numpy()))
+    except Exception as e:
+        import traceback
+
+        q.put((rank, f"{e!r}\n{traceback.format_exc()}", None, None, None))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("seeds", [(0.5, 0.5), (0.3, 1.7), (0.0, 1.0)])
+def test_owner_backward_takes_each_ranks_seed(seeds):
+    """Candidate-owner gradients when the ranks seed their loss backward differently (ADVICE
+    round 1): the objective is sum_r seed_r * loss_r, and the gradient of each rank's candidates
+    must weigh every remote query's terms by that query's own rank seed.  Checked against float64
+    autograd on the bf16-rounded operands at the bf16 scorer's bar."""
+    import numpy as np
+
+    Bq, M, H = 96, 192, 64
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, port, q, seeds, Bq, M, H)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=300) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r, dq, dd, qa, da in out:
+        assert dd is not None, dq
+    qa, da = (torch.as_tensor(out[0][3], dtype=torch.float64).requires_grad_(True),
+              torch.as_tensor(out[0][4], dtype=torch.float64).requires_grad_(True))
+    logits = qa @ da.T * 10.0
+    labels = torch.cat([torch.arange(Bq) + r * M for r in range(WORLD)])
+    ce = torch.nn.functional.cross_entropy(logits, labels, reduction="none")
+    w = torch.cat([torch.full((Bq,), float(seeds[r]) / Bq, dtype=torch.float64) for r in range(WORLD)])
+    (ce * w).sum().backward()
+    for r, dq, dd, _, _ in out:
+        for got, want in ((dq, qa.grad[r * Bq:(r + 1) * Bq]), (dd, da.grad[r * M:(r + 1) * M])):
+            want = want.numpy()
+            err = np.abs(got.astype(np.float64) - want).max() / max(np.abs(want).max(), 1e-30)
+            assert err < 2e-3, (seeds, r, float(err))

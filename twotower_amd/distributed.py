@@ -144,12 +144,23 @@ def gather_candidates(d: torch.Tensor, group=None) -> tuple[torch.Tensor, int]:
 class GradSync:
     """Sum-all-reduce of every gradient after backward.  Small parameters travel in one flat
     bucket; large ones (the embedding table) are reduced in place.  With the loss pre-scaled
-    by 1/world the sums are the global-batch mean gradients."""
+    by 1/world the sums are the global-batch mean gradients.
+
+    Two ways to run it:
+      * ``sync()`` -- after backward, before the optimizer (any optimizer);
+      * ``launch(side)`` -- called by optim.AdamW inside ``step()`` once it has issued the table
+        exchange and launched the fused table update: the all-reduce runs on a communication
+        stream that waits only for the gradients' producers (the backward on the current stream
+        and the "wgrad" side stream of ops.TowerHead), so it overlaps the table update, and its
+        completion event joins the optimizer's SideGrads, which the dense AdamW waits for.
+        The table's collectives are issued before it, so they are not queued behind the tower
+        gradients on the communicator."""
 
     def __init__(self, params, group=None, bucket_cap: int = 1 << 22):
         self.group = group
         self.params = [p for p in params if p.requires_grad]
         self.bucket_cap = bucket_cap
+        self._streams: dict = {}
 
     @property
     def world(self) -> int:
@@ -158,14 +169,12 @@ class GradSync:
     def loss_scale(self) -> float:
         return 1.0 / self.world
 
-    def sync(self) -> None:
-        if not is_active(self.group):
-            return
-        from ._lib import join_side_grads
-
-        join_side_grads(self.params)  # gradients computed on a side stream (ops.TowerHead)
+    def _split(self):
         small = [p for p in self.params if p.grad is not None and p.numel() <= self.bucket_cap]
         large = [p for p in self.params if p.grad is not None and p.numel() > self.bucket_cap]
+        return small, large
+
+    def _reduce(self, small, large) -> None:
         works = []
         if small:
             flat = torch.cat([p.grad.reshape(-1) for p in small])
@@ -180,3 +189,37 @@ class GradSync:
                     n = p.numel()
                     p.grad.copy_(flat[off:off + n].view_as(p.grad))
                     off += n
+
+    def sync(self) -> None:
+        if not is_active(self.group):
+            return
+        from ._lib import join_side_grads
+
+        join_side_grads(self.params)  # gradients computed on a side stream (ops.TowerHead)
+        self._reduce(*self._split())
+
+    def launch(self, side) -> None:
+        """The all-reduce on a communication stream; its completion joins ``side`` (a
+        _lib.SideGrads the caller joins before reading the gradients).  CPU tensors (gloo tests)
+        or no side object: the plain synchronous ``sync()``."""
+        if not is_active(self.group):
+            return
+        small, large = self._split()
+        grads = [p.grad for p in small + large]
+        if side is None or not grads or not all(g.is_cuda for g in grads):
+            self.sync()
+            return
+        dev = grads[0].device
+        comm = self._streams.get(dev)
+        if comm is None:
+            comm = self._streams[dev] = torch.cuda.Stream(device=dev)
+        comm.wait_stream(torch.cuda.current_stream(dev))  # gradients written by the main-stream backward
+        for ev in side.events:  # ... and by the wgrad side stream
+            comm.wait_event(ev)
+        with torch.cuda.stream(comm):
+            self._reduce(small, large)
+            done = torch.cuda.Event()
+            done.record(comm)
+        for g in grads:
+            g.record_stream(comm)
+        side.events.append(done)

@@ -5,6 +5,8 @@ Reference call sites each op replaces are cited per function (paths inside k0r1g
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 
 import torch
@@ -577,6 +579,42 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         return grad, None, None, None, None
 
 
+_UNIFORM_SEED = [0]  # > 0 while a caller guarantees every rank seeds its loss backward alike
+
+
+@contextlib.contextmanager
+def uniform_loss_seed():
+    """Declare that every data-parallel rank seeds this backward with the same d(loss) (TrainStep:
+    1/world), so InBatchSoftmaxLossOwned skips the seed exchange.  A module-level count, not a
+    thread-local: autograd runs GPU backward functions on its own device threads."""
+    _UNIFORM_SEED[0] += 1
+    try:
+        yield
+    finally:
+        _UNIFORM_SEED[0] -= 1
+
+
+def _rank_seeds(lse2_all: torch.Tensor, g: torch.Tensor, B: int, world: int, group):
+    """Per-rank backward seeds for the candidate-owner backward: every rank's seed is gathered
+    and the reference seed g_ref = max_r g_r is what the kernel applies, with rank r's query
+    terms weighed by g_r / g_ref through their lse2 (the kernel forms 2^(x c2 - lse2_i), so
+    lse2_i -= log2(g_r / g_ref); a rank seeded 0 contributes nothing: lse2 = +inf).  The caller
+    rescales this rank's dq by g / g_ref and moves its label terms from g_ref to g.  Equal seeds
+    give shifts and corrections of exactly 0 (the same bits as without the exchange).  Negative
+    seeds cannot be folded and fail loudly (device assert).  -> (lse2_all, g_ref)"""
+    from .distributed import all_gather_rows
+
+    g_all = torch.empty(world, dtype=_FLOAT, device=g.device)
+    all_gather_rows(g_all, g.reshape(1), group)
+    torch._assert_async((g_all >= 0).all(), "in-batch loss: data-parallel backward seeds must be >= 0")
+    g_ref = g_all.max().reshape(1)
+    ratio = g_all / torch.where(g_ref > 0, g_ref, torch.ones_like(g_ref))
+    shift = torch.where(ratio > 0, torch.log2(ratio), torch.full_like(ratio, float("-inf")))
+    out = lse2_all.clone()
+    out[:world * B] -= shift.repeat_interleave(B)
+    return out, g_ref
+
+
 class InBatchSoftmaxLossOwned(torch.autograd.Function):
     """Data-parallel in-batch loss with cross-device negatives and candidate-owner gradients
     (bf16 / bf16_split).  Forward: every rank's bf16 candidate copies and norm maxima are
@@ -584,7 +622,9 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
     of them.  The bf16 query copies and lse2 are all-gathered asynchronously (overlapping the
     forward scorer); the backward computes the gradient of this rank's OWN candidates over every
     rank's queries, so no candidate gradient is reduce-scattered.  Every rank's loss must be
-    seeded alike (TrainStep: 1/world), as the remote queries' terms take this rank's seed."""
+    seeded alike (TrainStep: 1/world, declared by ops.uniform_loss_seed()); otherwise the ranks'
+    seeds are all-gathered in the backward and each remote query's terms take its own rank's seed
+    (_rank_seeds)."""
 
     @staticmethod
     def forward(ctx, q, d, inv_tau, compute_dtype, grad_scale, group):
@@ -637,6 +677,7 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
         # all-gathers: kept on ctx rather than version-checked by save_for_backward
         ctx.bufs = (qb_all, lse2_all, db, dqu, ws) if want_grad else None
         ctx.meta = (B, M, H, dt, float(inv_tau), world, rank, float(1.0 / B) if grad_scale is None else float(grad_scale))
+        ctx.group = group
         return loss
 
     @staticmethod
@@ -649,10 +690,17 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
                 w.wait()
         ctx.works = ()
         g = g.to(_FLOAT).contiguous().reshape(1)
+        g_kernel = g
+        if _UNIFORM_SEED[0] == 0:
+            lse2_all, g_kernel = _rank_seeds(lse2_all, g, B, world, ctx.group)
         dq = torch.empty(B, H, dtype=_FLOAT, device=db.device)
         dd = torch.empty(M, H, dtype=_FLOAT, device=db.device)
         call("tt_inbatch_bwd_ex", ptr(qb_all), ptr(lse2_all), world * B, rank * B, ptr(db), M, B, 0, H, dt, inv_tau,
-             ptr(dqu), ptr(g), grad_scale, ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(db))
+             ptr(dqu), ptr(g_kernel), grad_scale, ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(db))
+        if g_kernel is not g:  # this rank's own terms at its own seed (see _rank_seeds)
+            dq.mul_(g / torch.where(g_kernel > 0, g_kernel, torch.ones_like(g_kernel)))
+            lab = qb_all[rank * B:(rank + 1) * B].float()
+            dd[:B].add_(lab * ((g_kernel - g) * (grad_scale * inv_tau)))
         return dq, dd, None, None, None, None
 
 

@@ -34,6 +34,7 @@ class AdamW(torch.optim.Optimizer):
                                       capturable=bool(capturable)))
         self._tables: list[torch.Tensor] = []
         self._side_grads = _lib.SideGrads()
+        self._grad_sync = None  # distributed.GradSync set by train_step.TrainStep: launched inside step()
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
         if fused_tables:
@@ -140,6 +141,8 @@ class AdamW(torch.optim.Optimizer):
     def _step_host(self, group: dict) -> None:
         """torch's default (non-capturable) form: step counters on the host."""
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
+        if self._grad_sync is not None:
+            self._grad_sync.launch(self._side_grads)
         self._side_grads.join()
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
@@ -209,6 +212,10 @@ class AdamW(torch.optim.Optimizer):
         for p, st, (ids, dp, den, plan) in fused:
             ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
                                                 self._adam_args(p))
+        # data parallel: the tower-gradient all-reduce, issued after the table's collectives and
+        # the table update, overlaps that update on a communication stream; the join waits for it
+        if self._grad_sync is not None:
+            self._grad_sync.launch(self._side_grads)
         self._side_grads.join()
         ops.adamw_multi(dense)
         for sh in gathers:

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import torch
 
+from . import ops
 from .distributed import GradSync, is_active
 
 
@@ -25,6 +26,11 @@ class TrainStep:
         self.optimizer = optimizer
         self.group = group
         self.sync = GradSync(model.parameters(), group=group) if is_active(group) else None
+        # an optimizer that launches the gradient all-reduce itself, after its own table exchange
+        # (optim.AdamW): the all-reduce then overlaps the table update
+        self._sync_in_step = self.sync is not None and hasattr(optimizer, "_grad_sync")
+        if self._sync_in_step:
+            optimizer._grad_sync = self.sync
         self.graph = graph
         if graph and not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("TrainStep(graph=True) needs an optimizer built with capturable=True")
@@ -49,8 +55,9 @@ class TrainStep:
             if seed is None:
                 scale = self.sync.loss_scale() if self.sync is not None else 1.0
                 seed = self._seed[loss.device] = torch.full((), scale, dtype=loss.dtype, device=loss.device)
-            loss.backward(seed)
-            if self.sync is not None:
+            with ops.uniform_loss_seed():  # every rank seeds its loss alike (1/world)
+                loss.backward(seed)
+            if self.sync is not None and not self._sync_in_step:
                 self.sync.sync()
             self.optimizer.step()
         finally:
