@@ -1,7 +1,10 @@
 #!/bin/bash
-# round-2 GPU pass b: in-batch tests (no -x) + scorer error table + C2 full-size tests
+# Round-2 profiles after the scorer rework: C3 and C5 kernel traces + FETCH/WRITE PMC passes,
+# scorer SQ counters, and the default bench line.
+set -e
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-timeout -k 10 400 python -u tools/scorer_error_table.py --big > gpurun_out/r02b_err.log 2>&1 || exit 1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -k "in_batch" -v --timeout 120 --timeout-method thread > gpurun_out/r02b_ib.log 2>&1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fullsize.py -v --timeout 300 --timeout-method thread > gpurun_out/r02b_full.log 2>&1
+bash tools/profile_round.sh r02b_c3 --steps 10 --warmup 3 --no-cpu-baseline
+bash tools/profile_round.sh r02b_c5 --config c5 --steps 10 --warmup 3 --no-cpu-baseline
+bash tools/pmc_scorer.sh gpurun_out/r02b_scorer > /dev/null 2>&1
+python3 tools/pmc_report.py gpurun_out/r02b_scorer > gpurun_out/r02b_scorer/report.txt 2>&1
+timeout -k 10 300 python3 bench.py > gpurun_out/r02b_c3/bench.log 2>&1
