@@ -192,6 +192,11 @@ int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t 
 #define TT_INBATCH_BWD_RECOMPUTE 0
 #define TT_INBATCH_BWD_STORED 1
 int tt_inbatch_set_backward(int mode);
+/* tt_inbatch_set_fold(on): 1 runs the forward's combine and loss mean inside the bf16 stored-P
+ * engine at H = 256 (the gradients bit-identical to the separate combine and mean kernels, the loss
+ * within 1e-6); 0 (the initial state unless the environment sets TT_SCORER_FOLD=1) keeps the
+ * separate kernels.  Returns the previous state (another value only reads it). */
+int tt_inbatch_set_fold(int on);
 size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype);
 int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
                    float inv_tau, int64_t label_off, int want_grad,
@@ -224,6 +229,18 @@ int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, 
  *   dd[j] = scale sum_i (P_ij - [label]) q~_i over all nQ_all queries, scale =
  *   grad_loss[0] * grad_scale * inv_tau (every rank's loss seeded alike); dq = scale * dq_unscaled.
  * ws: tt_inbatch_ex_ws_size(B, M_all, nQ_all, M) bytes serve both passes (partials only). */
+/* tt_inbatch_l2_prep: F.normalize (encoders.py:77) of the B + M rows of y = [q; d] in place, as
+ *   tt_head_gemm epi 1 does it (norms[r] = |row|; y the epi 4 output, H = 256), fused with the
+ *   operand prep of tt_inbatch_fwd on the normalised rows, which it leaves in ws (dtype TT_BF16 or
+ *   TT_BF16_SPLIT; ws sized by tt_inbatch_ws_size(B, M, H, dtype)).
+ * tt_inbatch_fwd_prepped: tt_inbatch_fwd on q = y[:B], d = y[B:] with that workspace, without its
+ *   prep pass (bit-identical results). */
+int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dtype, float* norms, void* ws, size_t ws_bytes,
+                       tt_stream_t stream);
+int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+                           float inv_tau, int64_t label_off, int want_grad,
+                           float* lse, float* loss_rows, float* loss, float* dq_unscaled,
+                           void* ws, size_t ws_bytes, tt_stream_t stream);
 #define TT_INBATCH_TAIL_ROWS 64
 #define TT_INBATCH_MAX_PARTS 512
 int tt_inbatch_prep_rows(const float* x, int64_t rows, int H, void* xb, float* norms, float* max_parts,
@@ -265,7 +282,9 @@ int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const 
  *   epi 1: (. + bias) / max(|row|, 1e-12), norms[r] = |row|   (Linear + F.normalize forward)
  *   epi 2: . * mask(r, n)            (ReLU backward fused into dh = dy W2; relu_mask written by
  *                                     epi 0 for the same rows)
- *   epi 3: .                         (dx = dh W1). */
+ *   epi 3: .                         (dx = dh W1)
+ *   epi 4: . + bias                  (epi 1 before its normalise pass, which the caller runs:
+ *                                     tt_inbatch_l2_prep). */
 size_t tt_head_planes_bytes(int N, int K);
 int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream);
 /* the four plane sets of one Linear-ReLU-Linear head in one launch, each tt_head_planes_bytes(256,

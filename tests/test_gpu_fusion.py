@@ -1,0 +1,139 @@
+"""GPU: cross-kernel fusions must not change a bit.  Each fused path is compared with the unfused
+launches it replaces on the same inputs (torch.equal on every output and gradient), and the test
+checks that the fused entry point actually ran.
+
+* tower head normalise pass + in-batch scorer operand prep (tt_inbatch_l2_prep, then
+  tt_inbatch_fwd_prepped) against tt_head_gemm epi 1 + tt_inbatch_fwd's own prep pass."""
+import numpy as np
+import pytest
+import torch
+
+import twotower_amd as tt
+from twotower_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(V, seed):
+    torch.manual_seed(seed)
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
+    return tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
+
+
+def _ids(B, L, V, rng):
+    ids = rng.integers(1, V, size=(B, L))
+    lengths = rng.integers(1, L + 1, size=B)
+    ids[np.arange(L)[None, :] >= lengths[:, None]] = 0
+    return torch.as_tensor(ids, device=DEV)
+
+
+def _step(model, loss_fn, batch):
+    model.zero_grad(set_to_none=True)
+    q, p, n = model(*batch)
+    loss = loss_fn(q, p, n)
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {k: v.grad.clone() for k, v in model.named_parameters()}
+    return (q.detach().clone(), p.detach().clone(), n.detach().clone(), loss.detach().clone()), grads
+
+
+@pytest.mark.parametrize("B,L,dtype,bwd", [(8192, 64, "bf16", "stored"), (300, 12, "bf16", "stored"),
+                                           (129, 7, "bf16", "recompute"), (256, 16, "bf16_split", "stored")])
+def test_head_normalise_fused_with_scorer_prep_is_bit_identical(B, L, dtype, bwd, monkeypatch):
+    V = 5000
+    rng = np.random.default_rng(B + L)
+    batch = [_ids(B, L, V, rng) for _ in range(3)]
+    loss_fn = tt.losses.build("in_batch", temperature=0.05, compute_dtype=dtype)
+    assert tt.losses.scorer_prep_dtype(loss_fn) == dtype
+    prev = ops.set_inbatch_backward(bwd)
+    try:
+        model = _model(V, 7)
+        ref_out, ref_grads = _step(model, loss_fn, batch)
+
+        seen = []
+        real_call = ops.call
+
+        def spy(name, *args):
+            seen.append(name)
+            return real_call(name, *args)
+
+        monkeypatch.setattr(ops, "call", spy)
+        model.scorer_prep = dtype
+        out, grads = _step(model, loss_fn, batch)
+    finally:
+        ops.set_inbatch_backward(prev)
+    assert "tt_inbatch_l2_prep" in seen and "tt_inbatch_fwd_prepped" in seen and "tt_inbatch_fwd" not in seen
+    for a, b, name in zip(out, ref_out, ("q", "p", "n", "loss")):
+        assert torch.equal(a, b), name
+    for k in ref_grads:
+        assert torch.equal(grads[k], ref_grads[k]), k
+
+
+def test_scorer_prep_set_by_trainstep_and_ignored_by_other_losses():
+    model = _model(100, 0)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3)
+    tt.TrainStep(model, tt.losses.build("in_batch", compute_dtype="bf16"), opt)
+    assert model.scorer_prep == "bf16"
+    model2 = _model(100, 0)
+    tt.TrainStep(model2, tt.losses.build("in_batch", compute_dtype="fp32"), tt.optim.AdamW(model2.parameters()))
+    assert model2.scorer_prep is None
+    # a head output carrying prepared operands into a triplet loss: ignored, same loss
+    rng = np.random.default_rng(3)
+    batch = [_ids(64, 8, 100, rng) for _ in range(3)]
+    trip = tt.losses.build("triplet")
+    model.zero_grad(set_to_none=True)
+    a = trip(*model(*batch))
+    model.scorer_prep = None
+    b = trip(*model(*batch))
+    assert torch.equal(a, b)
+
+
+def _inbatch(q, d, inv_tau, label_off, fold):
+    """loss, dq, dd of the bf16 stored-P in-batch loss, forward combine folded or not."""
+    prev = ops.set_inbatch_fold(fold)
+    try:
+        Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
+        loss = ops.InBatchSoftmaxLoss.apply(Q, D, inv_tau, label_off, "bf16", None)
+        loss.backward(torch.tensor(0.75, device=DEV))
+        torch.cuda.synchronize()
+    finally:
+        ops.set_inbatch_fold(prev)
+    return loss.detach(), Q.grad, D.grad
+
+
+@pytest.mark.parametrize("B,M,H,label_off,case", [
+    (8192, 16384, 256, 0, "c3"), (8192, 8192, 256, 0, "square"), (300, 700, 256, 0, "ragged"),
+    (129, 129, 256, 0, "tiny"), (256, 1024, 256, 512, "label_off"), (96, 200, 256, 0, "exact_rows"),
+    (1000, 3000, 64, 0, "H64_unfolded")])
+def test_forward_combine_folded_into_engine_is_bit_identical(B, M, H, label_off, case):
+    """FwdFold (the split partials published sc1, the last split of each query block folds them
+    and runs the combine's row arithmetic lane-parallel, the last block forms the mean) against
+    fwd_combine_kernel + mean_kernel: the gradients (through lse2, dq_unscaled and the scaled query
+    copy) bit-identical; the loss within 1e-6 (the diagonal logit's dot product is summed in the
+    engine's lane layout, another fp32 order).  Three calls in a row each (counters reset between
+    launches); 'exact_rows' puts half the queries on the exact row path (tau 0.005, weakly aligned
+    rows); H 64 never folds (the switch must not change it)."""
+    rng = np.random.default_rng(B + M + label_off)
+    q = rng.standard_normal((B, H)).astype(np.float32)
+    d = rng.standard_normal((M, H)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    inv_tau = 10.0
+    if case == "exact_rows":
+        d[: B // 2] = q[: B // 2]
+        inv_tau = 200.0
+    q, d = torch.as_tensor(q, device=DEV), torch.as_tensor(d, device=DEV)
+    prev = ops.set_inbatch_backward("stored")
+    try:
+        ref = _inbatch(q, d, inv_tau, label_off, False)
+        for _ in range(3):
+            got = _inbatch(q, d, inv_tau, label_off, True)
+            for a, b, name in zip(got, ref, ("loss", "dq", "dd")):
+                assert torch.isfinite(a).all(), name
+                if name == "loss":
+                    assert abs(a.item() - b.item()) <= 1e-6 * abs(b.item()), (a.item(), b.item())
+                else:
+                    assert torch.equal(a, b), (name, (a - b).abs().max().item())
+    finally:
+        ops.set_inbatch_backward(prev)

@@ -2,6 +2,7 @@
 # Build measurement variants of libtwotower_amd.so (extra -D flags) into tools/variants/lib_<name>.so,
 # for A/B timing on the GPU box (tools/mb_variants.py).  Usage: tools/build_variants.sh name='-DX=1' ...
 set -e
+mkdir -p "$(cd "$(dirname "$0")" && pwd)/variants"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 for spec in "$@"; do
   name=${spec%%=*}; flags=${spec#*=}

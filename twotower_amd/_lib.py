@@ -83,11 +83,15 @@ _SIGNATURES = {
     "tt_multi_neg_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp]),
     "tt_multi_neg_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
     "tt_inbatch_set_backward": (_c_int, [_c_int]),
+    "tt_inbatch_set_fold": (_c_int, [_c_int]),
     "tt_inbatch_ws_size": (_c_sz, [_c_i64, _c_i64, _c_int, _c_int]),
     "tt_inbatch_fwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp, _vp, _vp,
                                 _vp, _c_sz, _vp]),
     "tt_inbatch_bwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
                                 _vp, _vp, _c_sz, _vp]),
+    "tt_inbatch_l2_prep": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp, _c_sz, _vp]),
+    "tt_inbatch_fwd_prepped": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp,
+                                        _vp, _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_prep_rows": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp, _vp]),
     "tt_inbatch_ex_ws_size": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int]),
     "tt_inbatch_fwd_ex": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_int, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int,

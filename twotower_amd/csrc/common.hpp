@@ -19,6 +19,13 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
+// v0^2 + v1^2 + v2^2 + v3^2 with its fma chain spelled out, so every kernel that forms a row
+// norm from the same float4 gets the same bits (contraction of the plain expression may pick
+// either product as the fma addend, differently per kernel).
+__device__ __forceinline__ float sumsq4(const f32x4& v) {
+  return __builtin_fmaf(v[3], v[3], __builtin_fmaf(v[2], v[2], __builtin_fmaf(v[1], v[1], v[0] * v[0])));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

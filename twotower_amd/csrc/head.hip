@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void head_normalize_kernel(float* __restrict__
   const int lane = lane_id();
   f32x4* p = reinterpret_cast<f32x4*>(y + row * kN) + lane;
   f32x4 v = *p;
-  const float ss = wave_sum(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
+  const float ss = wave_sum(sumsq4(v));
   const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
   v[0] *= inv;
   v[1] *= inv;
@@ -599,10 +599,13 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
   TT_REQUIRE(((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(planes) |
                reinterpret_cast<uintptr_t>(out)) & 15) == 0 && lda % 4 == 0,
              "A / planes / out must be 16-byte aligned");
+  // epi 4: the Linear of epi 1 without its normalise pass (tt_inbatch_l2_prep normalises)
+  const bool defer_l2 = epi == 4;
+  if (defer_l2) epi = EPI_BIAS_L2;
   TT_REQUIRE(epi >= EPI_BIAS_RELU && epi <= EPI_PLAIN, "epi=%d", epi);
   TT_REQUIRE((epi != EPI_BIAS_RELU && epi != EPI_BIAS_L2) || bias, "epilogue needs bias");
   TT_REQUIRE(epi != EPI_RELU_MASK || relu_mask, "epilogue needs the ReLU mask of the forward");
-  TT_REQUIRE(epi != EPI_BIAS_L2 || norms, "epilogue needs norms");
+  TT_REQUIRE(epi != EPI_BIAS_L2 || norms || defer_l2, "epilogue needs norms");
   TT_REQUIRE(ws_bytes >= tt_head_gemm_ws_size(rows, epi) && (ws || !tt_head_gemm_ws_size(rows, epi)),
              "workspace too small (%zu < %zu)", ws_bytes, tt_head_gemm_ws_size(rows, epi));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -630,7 +633,7 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
       break;
   }
   TT_LAUNCH_CHECK("tt_head_gemm");
-  if (epi == EPI_BIAS_L2) {
+  if (epi == EPI_BIAS_L2 && !defer_l2) {
     head_normalize_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
     TT_LAUNCH_CHECK("tt_head_gemm normalize");
   }

@@ -35,6 +35,9 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr int kPadBytes = 2048;  // zero row source (>= one 1 KiB row) + one +inf float after it
 enum Mode { FWD = 0, DD = 1 };
+constexpr int kMaxPrepBlocks = 512;  // per-block norm maxima of the prep (readers fold <= this many)
+constexpr int kTailRows = 64;         // zero rows after each bf16 operand copy (>= the bf16 engine's BJ)
+static_assert(kTailRows == TT_INBATCH_TAIL_ROWS && kMaxPrepBlocks == TT_INBATCH_MAX_PARTS, "ABI constants");
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) char lds_char_t;
@@ -581,6 +584,11 @@ __device__ long long g_tt_ktrace[2 * 1024 * 4];  // [bwd, fwd] per workgroup (wa
   do {                                                                                              \
     if (threadIdx.x == 0 && blockIdx.x < 1024) g_tt_ktrace[(k) * 4096 + blockIdx.x * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+__device__ long long g_tt_ftrace[1024 * 8];  // folded forward combine: s_memrealtime per workgroup at its stages
+#define TT_FTRACE(slot)                                                                              \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_tt_ftrace[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define TT_TRACE_B(slot)                                                                             \
   do {                                                                                               \
     if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace_b[t * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
@@ -593,6 +601,9 @@ __device__ long long g_tt_ktrace[2 * 1024 * 4];  // [bwd, fwd] per workgroup (wa
   do {                   \
   } while (0)
 #define TT_KTRACE(slot) \
+  do {                  \
+  } while (0)
+#define TT_FTRACE(slot) \
   do {                  \
   } while (0)
 #define TT_KTRACE_K(k, slot) \
@@ -630,14 +641,339 @@ __device__ __forceinline__ void store_p_piece(char* __restrict__ blk, unsigned l
   *reinterpret_cast<unsigned*>(blk + lane_off + row * 64) = v;
 }
 
-template <int MODE, bool PRECISE, int H, bool STOREP = false>
+__device__ __forceinline__ f32x4 load4(const float* p, int lane) { return reinterpret_cast<const f32x4*>(p)[lane]; }
+__device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
+  const bf16x4 v = reinterpret_cast<const bf16x4*>(p)[lane];
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+// sum over s < S of p[s * stride4], in split order (the same order as the generic path), with up
+// to four splits' loads in flight
+__device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t stride4, int S) {
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o += v[u];
+  }
+  return o;
+}
+
+// Exact row of the loss for a query whose shift bound overshot (l < 2^-100 would lose the row):
+// two passes over all M candidates with the true row max, as F.cross_entropy does
+// (twotower/losses.py:116).  One wave, fp32 dot products of the same operands the engine scores;
+// lane owns elements h = lane + 64 u.  Returns the row max m2 (log2 units), l = sum 2^(x c2 - m2)
+// and o = sum 2^(x c2 - m2) d~_j (the lane's elements).  A correctness net for pathological inputs
+// (small tau with large or weakly aligned rows): M dot products per row, far slower than the
+// engine, and never taken when the bound is within 100 log2 units of the row max.
+template <typename DT>
+__device__ float exact_row_dot(const DT* __restrict__ qr, const DT* __restrict__ dj, int H, int lane) {
+  float acc = 0.f;
+  for (int h = lane; h < H; h += kWave) acc += (float)qr[h] * (float)dj[h];
+  return wave_sum(acc);
+}
+
+template <typename DT>
+__device__ void exact_row(const DT* __restrict__ qr, const DT* __restrict__ Dm, int64_t M, int H, float c2, int lane,
+                          float& m2, float& l, float (&o)[4]) {
+  m2 = -INFINITY;
+  for (int64_t j = 0; j < M; ++j) m2 = fmaxf(m2, exact_row_dot(qr, Dm + j * H, H, lane) * c2);
+  l = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) o[u] = 0.f;
+  for (int64_t j = 0; j < M; ++j) {
+    const DT* dj = Dm + j * H;
+    const float p = __builtin_amdgcn_exp2f(exact_row_dot(qr, dj, H, lane) * c2 - m2);
+    l += p;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (lane + kWave * u < H) o[u] += p * (float)dj[lane + kWave * u];
+  }
+}
+
+// fwd_combine's row body at H = 256 (one float4 per lane), shared by fwd_combine_kernel and the
+// engine's folded combine so both produce the same bits: l = the split-summed row sum of query
+// row i (before the pad correction), get_o() = this lane's float4 of O_i = sum_s Acc_s,i.  Writes
+// lse, lse2, dqu and qs (and xrows for a row redone exactly); returns loss_i on every lane.  The
+// fma chains are spelled out so no kernel's contraction choice changes a bit.
+__device__ __forceinline__ float dot4(const f32x4& a, const f32x4& b) {
+  return __builtin_fmaf(a[3], b[3], __builtin_fmaf(a[2], b[2], __builtin_fmaf(a[1], b[1], a[0] * b[0])));
+}
+
+template <typename DT, class GetO>
+__device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, float sh, int n_pad, int64_t M,
+                                                float c2, float inv_tau, int64_t label_off,
+                                                const DT* __restrict__ Qmat, const DT* __restrict__ Dmat,
+                                                float* __restrict__ lse, float* __restrict__ lse2,
+                                                float* __restrict__ dqu, __bf16* __restrict__ qs,
+                                                int* __restrict__ xrows, int lane) {
+  constexpr int H = 4 * kWave;
+  l = __builtin_fmaf(-(float)n_pad, __builtin_amdgcn_exp2f(-sh), l);  // pad rows: X = 0 exactly
+  const DT* qr = Qmat + i * H;
+  const DT* dl = Dmat + (i + label_off) * H;
+  if (!(l >= 7.888609052210118e-31f)) {  // l < 2^-100 (or NaN): the bound overshot, redo the row exactly
+    float m2, lx, o[4];
+    exact_row(qr, Dmat, M, H, c2, lane, m2, lx, o);
+    const float lse2_i = m2 + log2f(lx);
+    const float dot = exact_row_dot(qr, dl, H, lane);
+    if (lane == 0) {
+      lse[i] = lse2_i * kLn2;
+      lse2[i] = lse2_i;
+    }
+    const float inv_l = 1.f / lx;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = lane + kWave * u;
+      if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
+      if (qs) qs[i * H + h] = (__bf16)0.f;  // its stored P underflowed: the backward combine adds the row
+    }
+    if (qs && xrows && lane == 0) {  // flagged for the backward combine (which adds flagged rows in row order)
+      xrows[1 + i] = 1;
+      atomicAdd(xrows, 1);
+    }
+    return __builtin_fmaf(-dot, inv_tau, lse2_i * kLn2);
+  }
+  const float lse2_i = sh + log2f(l);  // log2 units, for the backward engine
+  const float lse_i = lse2_i * kLn2;
+  const f32x4 qv = load4(qr, lane), dv = load4(dl, lane);
+  const float dot = wave_sum(dot4(qv, dv));
+  if (qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
+    const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
+    reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
+        bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
+  }
+  if (lane == 0) {
+    lse[i] = lse_i;
+    lse2[i] = lse2_i;
+  }
+  if (dqu) {
+    const float inv_l = 1.f / l;
+    const f32x4 o = get_o();
+    reinterpret_cast<f32x4*>(dqu + i * H)[lane] =
+        f32x4{__builtin_fmaf(o[0], inv_l, -dv[0]), __builtin_fmaf(o[1], inv_l, -dv[1]),
+              __builtin_fmaf(o[2], inv_l, -dv[2]), __builtin_fmaf(o[3], inv_l, -dv[3])};
+  }
+  return __builtin_fmaf(-dot, inv_tau, lse_i);
+}
+
+// Forward combine folded into the engine (score_bf16_kernel<..., FOLD = true>): what
+// fwd_combine_kernel and mean_kernel do after the engine, done by the workgroups themselves.
+// Every workgroup publishes its split partials (Acc^T, l) write-through (sc1 stores, drained by
+// every wave) and takes a ticket on its column block's counter; the last of the S splits to
+// arrive sums the partials in split order (the others' by sc1 loads), transposes the folded O^T
+// and l into LDS and runs fwd_combine_kernel's row body on them, one wave per query row (the same
+// arithmetic in the same order: bit-identical outputs).  The last column block to finish then
+// forms the mean loss from loss_rows in mean_kernel's order.  Hand-off form: MI355X_MICROARCH.md
+// § visibility, Valid forms, table row 1 (sc1 stores + agent atomic ticket + sc1 loads); no
+// workgroup waits on another, so nothing depends on residency or dispatch order.
+struct FwdFold {
+  int64_t label_off;
+  float inv_tau;
+  int n_pad;
+  float* lse;
+  float* lse2;
+  float* loss_rows;
+  float* loss;
+  float* dqu;
+  __bf16* qs;
+  int* xrows;
+  unsigned* tickets;  // [ncb] per column block, [ncb] the blocks' own counter; zeroed by the prep
+};
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBufRsrcFlags = 0x00020000;  // raw buffer, dword data (cdna_hip_programming.md T8)
+constexpr int kSc1 = 16;                   // buffer aux: sc1 (write-through store / L2 load)
+
+// The folded forward combine (see FwdFold) at the end of score_bf16_kernel<FWD, ..., FOLD>, in
+// the engine's own register layout: lane (r32, hh) of wave w holds query r32 of the wave's 32
+// (my_col), O^T elements h = 32 ht + 8 g4 + 4 hh + 0..3 (acc) and its operand chunks h = 8 (2 kk +
+// hh) .. + 7 (cf); l_run its half-row sums, shift its row's shift bound.
+__device__ __forceinline__ void fwd_fold(f32x16 (&acc)[8], const bf16x8 (&cf)[16], float l_run, float shift,
+                                         int split, int S, int64_t cb, int64_t ncb, int64_t M,
+                                         const __bf16* __restrict__ Q, int64_t B, const __bf16* __restrict__ D,
+                                         float c2, float* __restrict__ acc_part, float* __restrict__ l_part,
+                                         const FwdFold& fa, char* smem) {
+  constexpr int H = 4 * kWave, NHT = H / 32, NK = H / 16;
+  const int lane = lane_id(), wid = threadIdx.x >> 6, r32 = lane & 31, hh = lane >> 5;
+  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
+  const bool col_ok = my_col < B;
+  const int64_t src_col = col_ok ? my_col : 0;
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  int* flag = reinterpret_cast<int*>(smem);  // the engine's ring is free now
+  const auto ra = __builtin_amdgcn_make_buffer_rsrc(acc_part, 0, (int)((int64_t)S * B * H * 4), kBufRsrcFlags);
+  const auto rl = __builtin_amdgcn_make_buffer_rsrc(l_part, 0, (int)((int64_t)S * B * 4), kBufRsrcFlags);
+  const auto rr = __builtin_amdgcn_make_buffer_rsrc(fa.loss_rows, 0, (int)(B * 4), kBufRsrcFlags);
+  auto h_of = [&](int ht, int g4) { return ht * 32 + 8 * g4 + 4 * hh; };
+  TT_FTRACE(0);
+  // 1. publish this split's partial write-through; every wave drains its stores before the ticket
+  if (S > 1 && col_ok) {
+    const unsigned own = (unsigned)(((int64_t)split * B + my_col) * H * 4);
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2],
+                                            acc[ht][4 * g4 + 3]}),
+            ra, (int)(own + h_of(ht, g4) * 4), 0, kSc1);
+    if (hh == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, l_tot), rl,
+                                            (int)(((int64_t)split * B + my_col) * 4), 0, kSc1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TT_FTRACE(1);
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(fa.tickets + cb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(S - 1);
+    if (last) __hip_atomic_store(fa.tickets + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  const int is_last = *flag;
+  __syncthreads();  // the flag word is reused below
+  if (!is_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler fence: no load above the ticket
+  TT_FTRACE(2);
+  // 2. the last split folds O and l over the splits in fwd_combine's order (0 + s0 + s1 + ...), the
+  //    other splits' partials by sc1 loads (one split's 32 loads in flight at a time), in place
+  f32x4 o[NHT][4];
+#pragma unroll
+  for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) o[ht][g4] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float l = 0.f;
+  for (int s = 0; s < S; ++s) {
+    if (s == split) {
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          o[ht][g4] += f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
+      l += l_tot;
+    } else {
+      const unsigned base = (unsigned)(((int64_t)s * B + src_col) * H * 4);
+      f32x4 v[NHT][4];
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          v[ht][g4] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(base + h_of(ht, g4) * 4), 0, kSc1));
+      const float ls = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, (int)(((int64_t)s * B + src_col) * 4), 0, kSc1));
+#pragma unroll
+      for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) o[ht][g4] += v[ht][g4];
+      l += ls;
+    }
+  }
+  TT_FTRACE(3);
+  // 3. fwd_combine's row arithmetic (combine_row256), lane-parallel over the queries: the two lanes of
+  //    a query each hold half of its row (O elements as above, q~ chunks as in cf)
+  const float l_sum = l;
+  l = __builtin_fmaf(-(float)fa.n_pad, __builtin_amdgcn_exp2f(-shift), l);
+  const bool exact = !(l >= 7.888609052210118e-31f);  // l < 2^-100 (or NaN): the exact path below
+  const int64_t lab = src_col + fa.label_off;
+  const __bf16* dl = D + lab * H;
+  const float lse2_i = shift + log2f(l);
+  const float lse_i = lse2_i * kLn2;
+  float dot = 0.f;  // q~ . d~_label: this lane's 128 elements in chunk order, then the other half
+#pragma unroll
+  for (int kk = 0; kk < NK; ++kk) {
+    const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dl + (2 * kk + hh) * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dot = __builtin_fmaf((float)cf[kk][e], (float)dv[e], dot);
+  }
+  dot += __shfl_xor(dot, 32);
+  const float loss_i = __builtin_fmaf(-dot, fa.inv_tau, lse_i);
+  if (col_ok && !exact) {
+    if (hh == 0) {
+      fa.lse[my_col] = lse_i;
+      fa.lse2[my_col] = lse2_i;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, loss_i), rr, (int)(my_col * 4), 0, kSc1);
+    }
+    if (fa.qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
+      const float f = __builtin_amdgcn_exp2f(shift - lse2_i);
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        bf16x8 x;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = (__bf16)((float)cf[kk][e] * f);
+        *reinterpret_cast<bf16x8*>(fa.qs + my_col * H + (2 * kk + hh) * 8) = x;
+      }
+    }
+    const float inv_l = 1.f / l;
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int h0 = h_of(ht, g4);
+        const bf16x4 d4 = *reinterpret_cast<const bf16x4*>(dl + h0);
+        *reinterpret_cast<f32x4*>(fa.dqu + my_col * H + h0) =
+            f32x4{__builtin_fmaf(o[ht][g4][0], inv_l, -(float)d4[0]), __builtin_fmaf(o[ht][g4][1], inv_l, -(float)d4[1]),
+                  __builtin_fmaf(o[ht][g4][2], inv_l, -(float)d4[2]), __builtin_fmaf(o[ht][g4][3], inv_l, -(float)d4[3])};
+      }
+  }
+  // rows whose bound overshot: the whole wave redoes each one exactly (combine_row256's exact path)
+  unsigned long long xm = __ballot(col_ok && exact && hh == 0);
+  while (xm) {
+    const int j = __builtin_ctzll(xm);
+    xm &= xm - 1;
+    const int64_t i = cb * (32 * NW) + wid * 32 + j;
+    const float lx = __shfl(l_sum, j), shx = __shfl(shift, j);
+    const float loss_x = combine_row256<__bf16>(
+        i, lx, [&] { return f32x4{}; }, shx, fa.n_pad, M, c2,
+        fa.inv_tau, fa.label_off, Q, D, fa.lse, fa.lse2, fa.dqu, fa.qs, fa.xrows, lane);
+    if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, loss_x), rr, (int)(i * 4), 0, kSc1);
+  }
+  // 4. the last column block to get here forms the mean loss in mean_kernel's order
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  TT_FTRACE(4);
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(fa.tickets + ncb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(ncb - 1);
+    if (last) __hip_atomic_store(fa.tickets + ncb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  __syncthreads();  // every wave has read the flag before the LDS below is reused
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  TT_FTRACE(5);
+  // the zero tail of the scaled query copy (the stored-P backward streams BJ rows past B)
+  if (fa.qs)
+    for (int k = threadIdx.x; k < kTailRows * H / 8; k += NT)
+      reinterpret_cast<bf16x8*>(fa.qs + B * H)[k] = bf16x8{};
+  // mean_kernel: virtual thread t < 1024 sums x[t], x[t + 1024], ... from 0; then a fixed tree
+  float* part = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int k = 0; k < 1024 / NT; ++k) {
+    const int t = threadIdx.x + k * NT;
+    float sum = 0.f;
+    for (int64_t i = t; i < B; i += 1024)
+      sum += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(i * 4), 0, kSc1));
+    part[t] = sum;
+  }
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    for (int t = threadIdx.x; t < w; t += NT) part[t] += part[t + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) fa.loss[0] = part[0] / (float)B;
+  TT_FTRACE(6);
+}
+
+template <int MODE, bool PRECISE, int H, bool STOREP = false, bool FOLD = false>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
     const float* __restrict__ dmax_part, int n_dmax,
     const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part,
-    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0) {
+    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0, FwdFold fa = FwdFold{}) {
   static_assert(!STOREP || (MODE == FWD && !PRECISE), "stored probabilities: forward, single-rounded G");
+  static_assert(!FOLD || (MODE == FWD && !PRECISE && H == 4 * kWave), "folded combine: bf16 forward, H = 256");
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
   constexpr int NHT = H / 32;
@@ -876,6 +1212,11 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 #endif
   if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
+  if constexpr (FOLD) {
+    fwd_fold(acc, cf, l_run, shift, split, S, cb, (nC + 32 * NW - 1) / (32 * NW), nR, C, nC, R, c2, acc_part, l_part,
+             fa, smem);
+    return;
+  }
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 #ifdef TT_SCORER_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1219,9 +1560,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
 // norms of q, and for d one max norm per block (dmax_part[b]; readers fold the <= kMaxPrepBlocks
 // values themselves: no zero-initialised accumulator, no atomics).  Block 0 also writes the pad
 // rows (kPadBytes - 16 zero bytes, then +inf for the backward lse2).
-constexpr int kMaxPrepBlocks = 512;
-constexpr int kTailRows = 64;  // >= the bf16 engine's BJ
-static_assert(kTailRows == TT_INBATCH_TAIL_ROWS && kMaxPrepBlocks == TT_INBATCH_MAX_PARTS, "ABI constants");
 
 __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t rows, int H, __bf16* __restrict__ xb,
                                           float* __restrict__ norms, int64_t b0, int64_t nb, float& mx) {
@@ -1240,7 +1578,7 @@ __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t r
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t r = r0 + u * step;
-        ss[u] = v[u][0] * v[u][0] + v[u][1] * v[u][1] + v[u][2] * v[u][2] + v[u][3] * v[u][3];
+        ss[u] = sumsq4(v[u]);
         if (xb && r < rows)
           reinterpret_cast<bf16x4*>(xb + r * H)[lane] =
               bf16x4{(__bf16)v[u][0], (__bf16)v[u][1], (__bf16)v[u][2], (__bf16)v[u][3]};
@@ -1262,7 +1600,7 @@ __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t r
     float ss = 0.f;
     for (int c = lane; c < H / 4; c += kWave) {
       const f32x4 v = src[c];
-      ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      ss += sumsq4(v);
       if (xb)
         reinterpret_cast<bf16x4*>(xb + r * H)[c] = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
     }
@@ -1277,10 +1615,11 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
                                                       __bf16* __restrict__ qb, __bf16* __restrict__ db,
                                                       float* __restrict__ qnorm, float* __restrict__ dmax_part,
                                                       char* __restrict__ pad, float* __restrict__ lse2,
-                                                      int* __restrict__ xrows) {
+                                                      int* __restrict__ xrows, unsigned* __restrict__ tickets, int n_tickets) {
   __shared__ float wmax[4];
   if (blockIdx.x == 0) {
     if (xrows && threadIdx.x == 0) xrows[0] = 0;
+    for (int t = threadIdx.x; t < n_tickets; t += blockDim.x) tickets[t] = 0u;  // the folded combine's counters
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
@@ -1293,6 +1632,9 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
   }
   float mx = 0.f;
   if ((int)blockIdx.x < gq) {
+    if (xrows)  // no query row redone exactly yet (see combine_row256)
+      for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gq * blockDim.x)
+        xrows[1 + i] = 0;
     prep_rows(q, B, H, qb, qnorm, blockIdx.x, gq, mx);
     return;
   }
@@ -1304,6 +1646,94 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) dmax_part[b] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
 }
 
+
+// The tower head's F.normalize (encoders.py:77) fused with the prep above, for the fused
+// TwoTower output y = [q; d] (B + M rows, H = 256, one float4 per lane): each row is normalised
+// in place exactly as head_normalize_kernel does it (norms[r] = |row| for the L2 backward), and
+// the normalised row then takes prep_rows' path (bf16 copy, its norm, the per-block max) from the
+// registers, so the scorer's prep pass and its 25 MB re-read disappear.  Same block partition
+// and arithmetic as prep_qd_kernel + head_normalize_kernel: the workspace is bit-identical.
+__device__ __forceinline__ void l2_prep_rows(float* __restrict__ x, int64_t rows, __bf16* __restrict__ xb,
+                                             float* __restrict__ norms, float* __restrict__ pnorms, int64_t b0,
+                                             int64_t nb, float& mx) {
+  constexpr int H = 4 * kWave, U = 4;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int64_t step = nb * 4;
+  for (int64_t r0 = b0 * 4 + wid; r0 < rows; r0 += U * step) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + u * step;
+      v[u] = r < rows ? reinterpret_cast<const f32x4*>(x + r * H)[lane] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // head_normalize_kernel's arithmetic
+      const int64_t r = r0 + u * step;
+      const float ss = wave_sum(sumsq4(v[u]));
+      const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
+      v[u][0] *= inv;
+      v[u][1] *= inv;
+      v[u][2] *= inv;
+      v[u][3] *= inv;
+      if (r < rows) {
+        reinterpret_cast<f32x4*>(x + r * H)[lane] = v[u];
+        if (lane == 0) norms[r] = nrm;
+      }
+    }
+    float ss[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // prep_rows' arithmetic on the normalised row
+      const int64_t r = r0 + u * step;
+      ss[u] = sumsq4(v[u]);
+      if (r < rows)
+        reinterpret_cast<bf16x4*>(xb + r * H)[lane] =
+            bf16x4{(__bf16)v[u][0], (__bf16)v[u][1], (__bf16)v[u][2], (__bf16)v[u][3]};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + u * step;
+      const float n = sqrtf(wave_sum(ss[u]));
+      if (r < rows) {
+        if (lane == 0 && pnorms) pnorms[r] = n;
+        mx = fmaxf(mx, n);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void l2_prep_kernel(float* __restrict__ y, int64_t B, int64_t M, int gq,
+                                                      float* __restrict__ norms, __bf16* __restrict__ qb,
+                                                      __bf16* __restrict__ db, float* __restrict__ qnorm,
+                                                      float* __restrict__ dmax_part, char* __restrict__ pad,
+                                                      float* __restrict__ lse2, int* __restrict__ xrows, unsigned* __restrict__ tickets, int n_tickets) {
+  constexpr int H = 4 * kWave;
+  __shared__ float wmax[4];
+  if (blockIdx.x == 0) {  // prep_qd_kernel's block-0 set-up
+    if (xrows && threadIdx.x == 0) xrows[0] = 0;
+    for (int t = threadIdx.x; t < n_tickets; t += blockDim.x) tickets[t] = 0u;  // the folded combine's counters
+    for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
+      reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
+    for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
+    for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x) {
+      qb[B * H + i] = (__bf16)0.f;
+      db[M * H + i] = (__bf16)0.f;
+    }
+  }
+  float mx = 0.f;
+  if ((int)blockIdx.x < gq) {
+    if (xrows)  // no query row redone exactly yet (see combine_row256)
+      for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gq * blockDim.x)
+        xrows[1 + i] = 0;
+    l2_prep_rows(y, B, qb, norms, qnorm, blockIdx.x, gq, mx);
+    return;
+  }
+  const int b = blockIdx.x - gq, gd = gridDim.x - gq;
+  l2_prep_rows(y + B * H, M, db, norms + B, nullptr, b, gd, mx);
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  if (lane == 0) wmax[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) dmax_part[b] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+}
 
 // One matrix: optional bf16 copy (with a kTailRows zero tail written by block 0), optional row
 // norms, optional per-block max norm (max_parts[b], gridDim.x <= kMaxPrepBlocks values).
@@ -1325,57 +1755,6 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict_
 // lse2 tail of the backward engine's R rows: +inf (G = 0 on the zero rows).
 __global__ void fill_inf_kernel(float* __restrict__ p, int n) {
   if ((int)threadIdx.x < n) p[threadIdx.x] = INFINITY;
-}
-
-__device__ __forceinline__ f32x4 load4(const float* p, int lane) { return reinterpret_cast<const f32x4*>(p)[lane]; }
-__device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
-  const bf16x4 v = reinterpret_cast<const bf16x4*>(p)[lane];
-  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
-}
-// sum over s < S of p[s * stride4], in split order (the same order as the generic path), with up
-// to four splits' loads in flight
-__device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t stride4, int S) {
-  f32x4 o = {0.f, 0.f, 0.f, 0.f};
-  for (int s0 = 0; s0 < S; s0 += 4) {
-    f32x4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) o += v[u];
-  }
-  return o;
-}
-
-// Exact row of the loss for a query whose shift bound overshot (l < 2^-100 would lose the row):
-// two passes over all M candidates with the true row max, as F.cross_entropy does
-// (twotower/losses.py:116).  One wave, fp32 dot products of the same operands the engine scores;
-// lane owns elements h = lane + 64 u.  Returns the row max m2 (log2 units), l = sum 2^(x c2 - m2)
-// and o = sum 2^(x c2 - m2) d~_j (the lane's elements).  A correctness net for pathological inputs
-// (small tau with large or weakly aligned rows): M dot products per row, far slower than the
-// engine, and never taken when the bound is within 100 log2 units of the row max.
-template <typename DT>
-__device__ float exact_row_dot(const DT* __restrict__ qr, const DT* __restrict__ dj, int H, int lane) {
-  float acc = 0.f;
-  for (int h = lane; h < H; h += kWave) acc += (float)qr[h] * (float)dj[h];
-  return wave_sum(acc);
-}
-
-template <typename DT>
-__device__ void exact_row(const DT* __restrict__ qr, const DT* __restrict__ Dm, int64_t M, int H, float c2, int lane,
-                          float& m2, float& l, float (&o)[4]) {
-  m2 = -INFINITY;
-  for (int64_t j = 0; j < M; ++j) m2 = fmaxf(m2, exact_row_dot(qr, Dm + j * H, H, lane) * c2);
-  l = 0.f;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) o[u] = 0.f;
-  for (int64_t j = 0; j < M; ++j) {
-    const DT* dj = Dm + j * H;
-    const float p = __builtin_amdgcn_exp2f(exact_row_dot(qr, dj, H, lane) * c2 - m2);
-    l += p;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (lane + kWave * u < H) o[u] += p * (float)dj[lane + kWave * u];
-  }
 }
 
 // Merge forward split partials, one wave per query row:
@@ -1402,6 +1781,14 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
   float l = 0.f;
   for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
+  if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
+    const float loss_i = combine_row256<DT>(
+        i, l,
+        [&] { return sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane, B * (H / 4), S); },
+        sh, n_pad, M, c2, inv_tau, label_off, Qmat, Dmat, lse, lse2, dqu, qs, xrows, lane);
+    if (lane == 0) loss_rows[i] = loss_i;
+    return;
+  }
   l -= (float)n_pad * __builtin_amdgcn_exp2f(-sh);
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
@@ -1423,31 +1810,14 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
       if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
       if (qs) qs[i * H + h] = (__bf16)0.f;  // its stored P underflowed: the backward combine adds the row
     }
-    if (qs && xrows && lane == 0) xrows[1 + atomicAdd(xrows, 1)] = (int)i;
+    if (qs && xrows && lane == 0) {  // flagged for the backward combine (which adds flagged rows in row order)
+      xrows[1 + i] = 1;
+      atomicAdd(xrows, 1);
+    }
     return;
   }
   const float lse2_i = sh + log2f(l);  // log2 units, for the backward engine
   const float lse_i = lse2_i * kLn2;
-  if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
-    const f32x4 qv = load4(qr, lane), dv = load4(dl, lane);
-    float dot = wave_sum(qv[0] * dv[0] + qv[1] * dv[1] + qv[2] * dv[2] + qv[3] * dv[3]);
-    if (qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
-      const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
-      reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
-          bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
-    }
-    if (lane == 0) {
-      lse[i] = lse_i;
-      lse2[i] = lse2_i;
-      loss_rows[i] = lse_i - dot * inv_tau;
-    }
-    if (dqu) {
-      const float inv_l = 1.f / l;
-      const f32x4 o = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane, B * (H / 4), S);
-      reinterpret_cast<f32x4*>(dqu + i * H)[lane] = o * inv_l - dv;
-    }
-    return;
-  }
   float dot = 0.f;
   for (int h = lane; h < H; h += kWave) dot += (float)qr[h] * (float)dl[h];
   dot = wave_sum(dot);
@@ -1474,17 +1844,30 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
 // scale = grad_loss * grad_scale * inv_tau.
 // Stored-P backward only (xrows non-null): query rows the forward redid exactly (their stored P
 // underflowed, their scaled-query rows are zero) add sum_i 2^(x_ij c2 - lse2_i) q~_i here.
+// xrows = [count, flag of row 0, flag of row 1, ...]: the flagged rows are added in ascending row
+// order (a list filled by atomics would fix the order of these fp32 sums per run, not per input).
+template <class F>
+__device__ __forceinline__ void for_exact_rows(const int* __restrict__ xrows, int64_t B, int lane, F f) {
+  if (xrows[0] == 0) return;  // the usual case: one load per wave
+  for (int64_t base = 0; base < B; base += kWave) {
+    unsigned long long m = __ballot(base + lane < B && xrows[1 + base + lane] != 0);
+    while (m) {
+      const int k = __builtin_ctzll(m);
+      m &= m - 1;
+      f(base + k);
+    }
+  }
+}
+
 template <typename DT>
-__device__ __forceinline__ void add_exact_rows(f32x4& a, const int* __restrict__ xrows, const DT* __restrict__ Qmat,
-                                               const DT* __restrict__ dr, const float* __restrict__ lse2, float c2,
-                                               int H, int lane) {
-  const int n = xrows[0];
-  for (int k = 0; k < n; ++k) {
-    const int i = xrows[1 + k];
-    const DT* qr = Qmat + (int64_t)i * H;
+__device__ __forceinline__ void add_exact_rows(f32x4& a, const int* __restrict__ xrows, int64_t B,
+                                               const DT* __restrict__ Qmat, const DT* __restrict__ dr,
+                                               const float* __restrict__ lse2, float c2, int H, int lane) {
+  for_exact_rows(xrows, B, lane, [&](int64_t i) {
+    const DT* qr = Qmat + i * H;
     const float g = __builtin_amdgcn_exp2f(exact_row_dot(qr, dr, H, lane) * c2 - lse2[i]);
     a += g * load4(qr, lane);
-  }
+  });
 }
 
 template <typename DT>
@@ -1503,7 +1886,7 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
     if (r < M) {
       const int64_t qi = r - label_off;
       f32x4 a = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + r * (H / 4) + lane, M * (H / 4), S);
-      if (xrows) add_exact_rows(a, xrows, Qmat, Dmat + r * H, lse2, c2, H, lane);
+      if (xrows) add_exact_rows(a, xrows, B, Qmat, Dmat + r * H, lse2, c2, H, lane);
       if (qi >= 0 && qi < B) a -= load4(Qmat + qi * H, lane);
       reinterpret_cast<f32x4*>(dd + r * H)[lane] = a * scale;
     }
@@ -1513,17 +1896,16 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
   if (r < M) {
     const int64_t qi = r - label_off;
     const bool lab = qi >= 0 && qi < B;
-    const int nx = xrows ? xrows[0] : 0;
     for (int h0 = 0; h0 < H; h0 += kWave) {
       const int h = h0 + lane;
       float a = 0.f;
       if (h < H)
         for (int s = 0; s < S; ++s) a += acc_part[((int64_t)s * M + r) * H + h];
-      for (int k = 0; k < nx; ++k) {  // exact rows (stored-P backward; see add_exact_rows)
-        const int i = xrows[1 + k];
-        const float g = __builtin_amdgcn_exp2f(exact_row_dot(Qmat + (int64_t)i * H, Dmat + r * H, H, lane) * c2 - lse2[i]);
-        if (h < H) a += g * (float)Qmat[(int64_t)i * H + h];
-      }
+      if (xrows)  // exact rows (stored-P backward; see add_exact_rows)
+        for_exact_rows(xrows, B, lane, [&](int64_t i) {
+          const float g = __builtin_amdgcn_exp2f(exact_row_dot(Qmat + i * H, Dmat + r * H, H, lane) * c2 - lse2[i]);
+          if (h < H) a += g * (float)Qmat[i * H + h];
+        });
       if (h < H) {
         if (lab) a -= (float)Qmat[qi * H + h];
         dd[r * H + h] = a * scale;
@@ -1572,7 +1954,7 @@ struct Ws {
   __bf16* Db;
   __bf16* Qs;   // stored-P backward: q~ scaled by 2^(shift - lse2) (+ zero tail)
   char* P;      // stored-P backward: bf16 probabilities, p_nct x p_nqt blocks of 2 KiB
-  int* xrows;   // stored-P backward: [count, rows...] of queries the forward redid exactly
+  int* xrows;   // stored-P backward: [count, flag per query row] of queries the forward redid exactly
   int64_t p_nqt;
   float* qnorm;
   float* lse2;
@@ -1580,6 +1962,8 @@ struct Ws {
   char* pad;
   float* l_part;
   float* acc_part;
+  unsigned* tickets;  // folded forward combine: one counter per query column block + one overall
+  int n_tickets;
   size_t total;
 };
 
@@ -1594,6 +1978,17 @@ std::atomic<int>& bwd_mode() {
   }()};
   return m;
 }
+// Forward combine folded into the bf16 stored-P engine (FwdFold): off by default (measured slower
+// than the separate combine and mean kernels so far); TT_SCORER_FOLD=1 (read at load) or
+// tt_inbatch_set_fold(1) turns it on.
+std::atomic<int>& fold_flag() {
+  static std::atomic<int> m{[] {
+    const char* e = std::getenv("TT_SCORER_FOLD");
+    return (e && std::strcmp(e, "1") == 0) ? 1 : 0;
+  }()};
+  return m;
+}
+bool fold_mode() { return fold_flag().load(std::memory_order_relaxed) != 0; }
 bool stored_p(int dtype, int64_t B, int64_t M) {
   return dtype == TT_BF16 && bwd_mode().load(std::memory_order_relaxed) == 1 && B * M <= (int64_t(1) << 31);
 }
@@ -1636,7 +2031,10 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   if (sp) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
   const size_t oa = take(parts);
+  const int nt = sp ? (int)((B + 32 * NW - 1) / (32 * NW)) + 1 : 0;
+  const size_t ot = take((size_t)nt * 4);
   Ws w{};
+  w.n_tickets = nt;
   char* b = static_cast<char*>(base);
   if (b) {
     w.Qb = reinterpret_cast<__bf16*>(b + oq);
@@ -1651,6 +2049,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.pad = b + opad;
     w.l_part = reinterpret_cast<float*>(b + ol);
     w.acc_part = reinterpret_cast<float*>(b + oa);
+    w.tickets = nt ? reinterpret_cast<unsigned*>(b + ot) : nullptr;
   }
   w.total = off;
   return w;
@@ -1658,7 +2057,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
 
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
-                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
+                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const FwdFold* fold = nullptr) {
   if (dtype == TT_F32) {
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -1667,6 +2066,11 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
+  } else if (MODE == FWD && w.P && fold) {
+    if constexpr (H == 4 * kWave)
+      score_bf16_kernel<FWD, false, H, true, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
+          static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
+          w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, w.P, w.p_nqt, *fold);
   } else if (MODE == FWD && w.P) {
     score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -1682,12 +2086,13 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
 
 template <int MODE>
 int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
-                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
+                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s,
+                    const FwdFold* fold = nullptr) {
   switch (H) {
     case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
     case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
     case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
-    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
+    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s, fold);
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
 }
@@ -1716,6 +2121,11 @@ extern "C" int tt_inbatch_set_backward(int mode) {
   return bwd_mode().exchange(mode);
 }
 
+extern "C" int tt_inbatch_set_fold(int on) {
+  if (on != 0 && on != 1) return fold_flag().load();
+  return fold_flag().exchange(on);
+}
+
 extern "C" size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype) {
   return carve(nullptr, B, M, H, dtype).total + 256;
 }
@@ -1729,7 +2139,8 @@ namespace {
 int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, int H, const float* qnorm,
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
-             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr) {
+             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr,
+             unsigned* tickets = nullptr) {
   const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
@@ -1741,6 +2152,11 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   w.P = P;
   w.p_nqt = p_nqt;
   int rc;
+  if (tickets && P && dqu && dtype == TT_BF16 && H == 4 * kWave && fold_mode()) {
+    // the combine and the mean run inside the engine (FwdFold)
+    const FwdFold fold{label_off, inv_tau, p.n_pad, lse, lse2, loss_rows, loss, dqu, Qs, xrows, tickets};
+    return dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s, &fold);
+  }
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
   const dim3 grid((unsigned)((B + (Qs ? kTailRows : 0) + 3) / 4)), block(256);
   if (dtype == TT_F32)
@@ -1846,30 +2262,70 @@ ExWs carve_ex(void* base, int64_t B, int64_t M_all, int64_t nQ_all, int64_t M, i
 }  // namespace
 }  // namespace tt
 
-extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
-                              int64_t label_off, int want_grad, float* lse, float* loss_rows, float* loss,
-                              float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream) {
+namespace tt {
+namespace {
+int prep_blocks_q(int64_t B) { return (int)std::min<int64_t>((B + 3) / 4, 512); }
+int prep_blocks_d(int64_t M) { return (int)std::min<int64_t>((M + 3) / 4, kMaxPrepBlocks); }
+
+int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                int64_t label_off, int want_grad, float* lse, float* loss_rows, float* loss, float* dq_unscaled,
+                void* ws, size_t ws_bytes, hipStream_t s, bool prepped) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
   TT_REQUIRE(q && d && lse && loss_rows && loss && ws, "null pointer");
   TT_REQUIRE(!want_grad || dq_unscaled, "want_grad needs dq_unscaled");
   TT_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(d)) & 15) == 0, "q/d must be 16-byte aligned");
+  TT_REQUIRE(!prepped || dtype != TT_F32, "prepared operands are bf16 copies (dtype bf16 / bf16_split)");
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool bf = dtype != TT_F32;
-  const int gq = (int)std::min<int64_t>((B + 3) / 4, 512);
-  const int gd = (int)std::min<int64_t>((M + 3) / 4, kMaxPrepBlocks);
-  prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
-                                                                 bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad,
-                                                                 w.lse2, w.xrows);
-  TT_LAUNCH_CHECK("score_prep");
+  const int gd = prep_blocks_d(M);
+  if (!prepped) {
+    const int gq = prep_blocks_q(B);
+    prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
+                                                                   bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad,
+                                                                   w.lse2, w.xrows, w.tickets, w.n_tickets);
+    TT_LAUNCH_CHECK("score_prep");
+  }
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
   const void* Cm = bf ? (const void*)w.Qb : (const void*)q;
   const bool sp = want_grad && w.P;
   return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
                   want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s, sp ? w.P : nullptr, w.p_nqt,
-                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr);
+                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr, sp ? w.tickets : nullptr);
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                              int64_t label_off, int want_grad, float* lse, float* loss_rows, float* loss,
+                              float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  return inbatch_fwd(q, d, B, M, H, dtype, inv_tau, label_off, want_grad, lse, loss_rows, loss, dq_unscaled, ws,
+                     ws_bytes, reinterpret_cast<hipStream_t>(stream), false);
+}
+
+extern "C" int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dtype, float* norms, void* ws,
+                                  size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(B > 0 && M > 0, "B=%lld M=%lld must be positive", (long long)B, (long long)M);
+  TT_REQUIRE(H == 4 * kWave, "tt_inbatch_l2_prep: H = %d only (got %d)", 4 * kWave, H);
+  TT_REQUIRE(dtype == TT_BF16 || dtype == TT_BF16_SPLIT, "tt_inbatch_l2_prep: dtype bf16 / bf16_split (got %d)", dtype);
+  TT_REQUIRE(y && norms && ws, "null pointer");
+  TT_REQUIRE((reinterpret_cast<uintptr_t>(y) & 15) == 0, "y must be 16-byte aligned");
+  const Ws w = carve_user(ws, B, M, H, dtype);
+  TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
+  const int gq = prep_blocks_q(B), gd = prep_blocks_d(M);
+  l2_prep_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      y, B, M, gq, norms, w.Qb, w.Db, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows, w.tickets, w.n_tickets);
+  TT_LAUNCH_CHECK("score_l2_prep");
+  return TT_OK;
+}
+
+extern "C" int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+                                      float inv_tau, int64_t label_off, int want_grad, float* lse, float* loss_rows,
+                                      float* loss, float* dq_unscaled, void* ws, size_t ws_bytes,
+                                      tt_stream_t stream) {
+  return inbatch_fwd(q, d, B, M, H, dtype, inv_tau, label_off, want_grad, lse, loss_rows, loss, dq_unscaled, ws,
+                     ws_bytes, reinterpret_cast<hipStream_t>(stream), true);
 }
 
 extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
@@ -1948,6 +2404,9 @@ extern "C" int tt_debug_scorer_trace(long long* host_out) {
 }
 extern "C" int tt_debug_scorer_ktrace(long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_ktrace), sizeof(long long) * 2 * 1024 * 4);
+}
+extern "C" int tt_debug_scorer_ftrace(long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_ftrace), sizeof(long long) * 8 * 1024);
 }
 extern "C" int tt_debug_scorer_trace_bwd(long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_trace_b), sizeof(long long) * 8 * 64);

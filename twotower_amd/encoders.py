@@ -9,6 +9,7 @@ ONE launch over the shared table (the towers always share it, encoders.py:265,27
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 
 import torch
@@ -133,6 +134,9 @@ class TwoTower(nn.Module):
             self.document_tower = query_tower
         else:
             self.document_tower = document_tower if document_tower is not None else query_tower
+        # compute dtype of an in-batch loss whose operand prep the fused forward may fold into the
+        # tower head's normalise pass (ops.scorer_prep; TrainStep sets it); None: never
+        self.scorer_prep: str | None = None
         total = sum(p.numel() for p in self.parameters() if p.requires_grad)
         logger.info(f"Total trainable parameters: {total:,}")
 
@@ -164,7 +168,9 @@ class TwoTower(nn.Module):
         sizes = [t.shape[0] for t in inputs]
         nq = sizes[0]
         if self.query_tower is self.document_tower:
-            return list(torch.split(self.query_tower.encode_pooled(pooled), sizes, dim=0))
+            prep = ops.scorer_prep(nq, self.scorer_prep) if self.scorer_prep else contextlib.nullcontext()
+            with prep:  # one head over all rows: its normalise pass may also prep the in-batch scorer
+                return list(torch.split(self.query_tower.encode_pooled(pooled), sizes, dim=0))
         q = self.query_tower.encode_pooled(pooled[:nq])
         docs = self.document_tower.encode_pooled(pooled[nq:])
         return [q] + list(torch.split(docs, sizes[1:], dim=0))

@@ -102,6 +102,17 @@ def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *arg
     return ops.in_batch_softmax_loss(q_emb, d_emb, temperature, label_off=label_off, compute_dtype=compute_dtype)
 
 
+def scorer_prep_dtype(loss_fn) -> str | None:
+    """The compute dtype when ``loss_fn`` is a single-device bf16 in-batch loss (as built by
+    ``build("in_batch", compute_dtype="bf16" | "bf16_split", ...)``), whose operand prep a tied
+    TwoTower may fold into its head (ops.scorer_prep); else None."""
+    fn, kw = (loss_fn.func, loss_fn.keywords) if isinstance(loss_fn, partial) else (loss_fn, {})
+    if fn is not in_batch_sampled_softmax_loss or kw.get("cross_device_negatives"):
+        return None
+    dt = kw.get("compute_dtype", "fp32")
+    return dt if dt in ("bf16", "bf16_split") else None
+
+
 def _owner_gradients() -> bool:
     """Cross-device negatives at bf16: candidate-owner gradients (default) or TT_INBATCH_DP=
     allgather for the fp32-row all-gather + gradient reduce-scatter form (the fp32 path)."""

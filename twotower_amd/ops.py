@@ -159,7 +159,8 @@ class BagMeanPool(torch.autograd.Function):
         pooled, denom = bag_mean_forward(weight, ids)
         ctx.plan = None
         if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
-            # forked after the gather: the sort runs beside the towers and the scorer
+            # forked after the gather: the sort runs beside the towers and the scorer (forked
+            # before it, beside the gather, the step took 22 us longer: 0.887 vs 0.864 ms)
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
             ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
@@ -327,6 +328,24 @@ def _head_gemm(A: torch.Tensor, planes: torch.Tensor, epi: int, bias=None, mask=
     return out
 
 
+_SCORER_PREP: list[tuple[int, int]] = []  # (query rows, compute dtype code) of an open scorer_prep()
+
+
+@contextlib.contextmanager
+def scorer_prep(nq: int, compute_dtype: str):
+    """While open, a TowerHead over rows [q (nq rows); candidates] also prepares the in-batch
+    scorer's operands in its normalise pass (tt_inbatch_l2_prep): the bf16 copies and norms the
+    loss would otherwise form in a pass of its own.  They ride on the head's output tensor
+    (``_tt_inbatch_prep``) to InBatchSoftmaxLossPacked, which takes them once; any other consumer
+    ignores them.  TwoTower opens it for its one-head fused forward when asked
+    (``TwoTower.scorer_prep``, set by TrainStep for a bf16 in-batch loss)."""
+    _SCORER_PREP.append((int(nq), _lib.compute_dtype_code(compute_dtype)))
+    try:
+        yield
+    finally:
+        _SCORER_PREP.pop()
+
+
 class TowerHead(torch.autograd.Function):
     """F.normalize(Linear-ReLU-Linear(x)) for E = H = 256 (encoders.py:38-42,77) on the split-bf16
     MFMA GEMMs with fused epilogues: bias + ReLU (+ the ReLU bitmask), bias + row L2 normalise
@@ -344,7 +363,17 @@ class TowerHead(torch.autograd.Function):
         mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
         h = _head_gemm(x, planes[:nb], 0, bias=b1, mask=mask)
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
-        out = _head_gemm(h, planes[nb:2 * nb], 1, bias=b2, norms=norm)
+        req = _SCORER_PREP[-1] if _SCORER_PREP else None
+        if req is not None and 0 < req[0] < rows:
+            nq, dt = req  # normalise pass fused with the in-batch scorer's operand prep
+            out = _head_gemm(h, planes[nb:2 * nb], 4, bias=b2)
+            ws = torch.empty(_lib.lib().tt_inbatch_ws_size(nq, rows - nq, HEAD_WIDTH, dt), dtype=torch.uint8,
+                             device=x.device)
+            call("tt_inbatch_l2_prep", ptr(out), nq, rows - nq, HEAD_WIDTH, dt, ptr(norm), ptr(ws), ws.numel(),
+                 stream_of(x))
+            out._tt_inbatch_prep = (nq, rows - nq, dt, ws)
+        else:
+            out = _head_gemm(h, planes[nb:2 * nb], 1, bias=b2, norms=norm)
         ctx.save_for_backward(x, h, mask, out, norm, planes)
         sides = {id(getattr(w, "_tt_side_grads", None)) for w in (W1, b1, W2, b2)}
         ctx.side_grads = W1._tt_side_grads if len(sides) == 1 and hasattr(W1, "_tt_side_grads") else None
@@ -504,12 +533,18 @@ def set_inbatch_backward(form: str) -> str:
     return {v: k for k, v in _BWD_FORMS.items()}[prev]
 
 
+def set_inbatch_fold(on: bool) -> bool:
+    """Run the bf16 stored-P forward's combine and loss mean inside its engine (True) or as
+    separate kernels (False, the default; same gradient bits).  Returns the previous setting."""
+    return bool(_lib.lib().tt_inbatch_set_fold(1 if on else 0))
+
+
 def get_inbatch_backward() -> str:
     """The current single-process bf16 in-batch backward form ("stored" or "recompute")."""
     return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
 
 
-def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad):
+def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad, prep=None):
     B, H = q.shape
     M = d.shape[0]
     if d.shape[1] != H:
@@ -517,12 +552,16 @@ def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_
     dt = _lib.compute_dtype_code(compute_dtype)
     dev = q.device
     nbytes = _lib.lib().tt_inbatch_ws_size(B, M, H, dt)
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)  # carries the bf16 operands to backward
+    if prep is not None and prep[:3] == (B, M, dt) and prep[3].numel() >= nbytes:
+        ws, entry = prep[3], "tt_inbatch_fwd_prepped"  # operands prepared by the head's normalise pass
+    else:
+        ws, entry = torch.empty(nbytes, dtype=torch.uint8, device=dev), "tt_inbatch_fwd"
+    # ws carries the bf16 operands to backward
     lse = torch.empty(B, dtype=_FLOAT, device=dev)
     rows = torch.empty(B, dtype=_FLOAT, device=dev)
     loss = torch.empty((), dtype=_FLOAT, device=dev)
     dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
-    call("tt_inbatch_fwd", ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
+    call(entry, ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
          ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
     ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off), float(1.0 / B) if grad_scale is None else float(grad_scale))
     return loss, lse, dqu, ws
@@ -561,10 +600,11 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qd, nq, inv_tau, compute_dtype, grad_scale):
         require_gpu(qd)
+        prep = qd.__dict__.pop("_tt_inbatch_prep", None)  # taken once (TowerHead under scorer_prep)
         qd = _contig_f32(qd, "qd")
         q, d = qd[:nq], qd[nq:]
         want_grad = bool(ctx.needs_input_grad[0])
-        loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad)
+        loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad, prep)
         if want_grad:
             ctx.save_for_backward(qd, lse, dqu, ws)
         ctx.nq = nq

@@ -12,10 +12,13 @@ optimizer (optim.AdamW(capturable=True)); a new input shape is captured anew.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
 from .distributed import GradSync, is_active
+from .losses import scorer_prep_dtype
 
 
 class TrainStep:
@@ -31,6 +34,12 @@ class TrainStep:
         self._sync_in_step = self.sync is not None and hasattr(optimizer, "_grad_sync")
         if self._sync_in_step:
             optimizer._grad_sync = self.sync
+        # a single-device bf16 in-batch loss: the tied towers' head prepares its operands
+        # (TT_SCORER_PREP=0: the loss's own prep pass, for comparison)
+        dt = scorer_prep_dtype(loss_fn)
+        if (dt is not None and hasattr(model, "scorer_prep") and not is_active(group)
+                and os.environ.get("TT_SCORER_PREP", "1") != "0"):
+            model.scorer_prep = dt
         self.graph = graph
         if graph and not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("TrainStep(graph=True) needs an optimizer built with capturable=True")
