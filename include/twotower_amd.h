@@ -192,11 +192,6 @@ int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t 
 #define TT_INBATCH_BWD_RECOMPUTE 0
 #define TT_INBATCH_BWD_STORED 1
 int tt_inbatch_set_backward(int mode);
-/* tt_inbatch_set_fold(on): 1 runs the forward's combine and loss mean inside the bf16 stored-P
- * engine at H = 256 (the gradients bit-identical to the separate combine and mean kernels, the loss
- * within 1e-6); 0 (the initial state unless the environment sets TT_SCORER_FOLD=1) keeps the
- * separate kernels.  Returns the previous state (another value only reads it). */
-int tt_inbatch_set_fold(int on);
 size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype);
 int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
                    float inv_tau, int64_t label_off, int want_grad,

@@ -88,52 +88,3 @@ def test_scorer_prep_set_by_trainstep_and_ignored_by_other_losses():
     b = trip(*model(*batch))
     assert torch.equal(a, b)
 
-
-def _inbatch(q, d, inv_tau, label_off, fold):
-    """loss, dq, dd of the bf16 stored-P in-batch loss, forward combine folded or not."""
-    prev = ops.set_inbatch_fold(fold)
-    try:
-        Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
-        loss = ops.InBatchSoftmaxLoss.apply(Q, D, inv_tau, label_off, "bf16", None)
-        loss.backward(torch.tensor(0.75, device=DEV))
-        torch.cuda.synchronize()
-    finally:
-        ops.set_inbatch_fold(prev)
-    return loss.detach(), Q.grad, D.grad
-
-
-@pytest.mark.parametrize("B,M,H,label_off,case", [
-    (8192, 16384, 256, 0, "c3"), (8192, 8192, 256, 0, "square"), (300, 700, 256, 0, "ragged"),
-    (129, 129, 256, 0, "tiny"), (256, 1024, 256, 512, "label_off"), (96, 200, 256, 0, "exact_rows"),
-    (1000, 3000, 64, 0, "H64_unfolded")])
-def test_forward_combine_folded_into_engine_is_bit_identical(B, M, H, label_off, case):
-    """FwdFold (the split partials published sc1, the last split of each query block folds them
-    and runs the combine's row arithmetic lane-parallel, the last block forms the mean) against
-    fwd_combine_kernel + mean_kernel: the gradients (through lse2, dq_unscaled and the scaled query
-    copy) bit-identical; the loss within 1e-6 (the diagonal logit's dot product is summed in the
-    engine's lane layout, another fp32 order).  Three calls in a row each (counters reset between
-    launches); 'exact_rows' puts half the queries on the exact row path (tau 0.005, weakly aligned
-    rows); H 64 never folds (the switch must not change it)."""
-    rng = np.random.default_rng(B + M + label_off)
-    q = rng.standard_normal((B, H)).astype(np.float32)
-    d = rng.standard_normal((M, H)).astype(np.float32)
-    q /= np.linalg.norm(q, axis=1, keepdims=True)
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    inv_tau = 10.0
-    if case == "exact_rows":
-        d[: B // 2] = q[: B // 2]
-        inv_tau = 200.0
-    q, d = torch.as_tensor(q, device=DEV), torch.as_tensor(d, device=DEV)
-    prev = ops.set_inbatch_backward("stored")
-    try:
-        ref = _inbatch(q, d, inv_tau, label_off, False)
-        for _ in range(3):
-            got = _inbatch(q, d, inv_tau, label_off, True)
-            for a, b, name in zip(got, ref, ("loss", "dq", "dd")):
-                assert torch.isfinite(a).all(), name
-                if name == "loss":
-                    assert abs(a.item() - b.item()) <= 1e-6 * abs(b.item()), (a.item(), b.item())
-                else:
-                    assert torch.equal(a, b), (name, (a - b).abs().max().item())
-    finally:
-        ops.set_inbatch_backward(prev)

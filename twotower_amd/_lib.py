@@ -83,7 +83,6 @@ _SIGNATURES = {
     "tt_multi_neg_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp]),
     "tt_multi_neg_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
     "tt_inbatch_set_backward": (_c_int, [_c_int]),
-    "tt_inbatch_set_fold": (_c_int, [_c_int]),
     "tt_inbatch_ws_size": (_c_sz, [_c_i64, _c_i64, _c_int, _c_int]),
     "tt_inbatch_fwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp, _vp, _vp,
                                 _vp, _c_sz, _vp]),

@@ -584,11 +584,6 @@ __device__ long long g_tt_ktrace[2 * 1024 * 4];  // [bwd, fwd] per workgroup (wa
   do {                                                                                              \
     if (threadIdx.x == 0 && blockIdx.x < 1024) g_tt_ktrace[(k) * 4096 + blockIdx.x * 4 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-__device__ long long g_tt_ftrace[1024 * 8];  // folded forward combine: s_memrealtime per workgroup at its stages
-#define TT_FTRACE(slot)                                                                              \
-  do {                                                                                               \
-    if (threadIdx.x == 0 && blockIdx.x < 1024) g_tt_ftrace[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
 #define TT_TRACE_B(slot)                                                                             \
   do {                                                                                               \
     if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace_b[t * 8 + (slot)] = __builtin_amdgcn_s_memtime(); \
@@ -601,9 +596,6 @@ __device__ long long g_tt_ftrace[1024 * 8];  // folded forward combine: s_memrea
   do {                   \
   } while (0)
 #define TT_KTRACE(slot) \
-  do {                  \
-  } while (0)
-#define TT_FTRACE(slot) \
   do {                  \
   } while (0)
 #define TT_KTRACE_K(k, slot) \
@@ -757,223 +749,14 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
   return __builtin_fmaf(-dot, inv_tau, lse_i);
 }
 
-// Forward combine folded into the engine (score_bf16_kernel<..., FOLD = true>): what
-// fwd_combine_kernel and mean_kernel do after the engine, done by the workgroups themselves.
-// Every workgroup publishes its split partials (Acc^T, l) write-through (sc1 stores, drained by
-// every wave) and takes a ticket on its column block's counter; the last of the S splits to
-// arrive sums the partials in split order (the others' by sc1 loads), transposes the folded O^T
-// and l into LDS and runs fwd_combine_kernel's row body on them, one wave per query row (the same
-// arithmetic in the same order: bit-identical outputs).  The last column block to finish then
-// forms the mean loss from loss_rows in mean_kernel's order.  Hand-off form: MI355X_MICROARCH.md
-// § visibility, Valid forms, table row 1 (sc1 stores + agent atomic ticket + sc1 loads); no
-// workgroup waits on another, so nothing depends on residency or dispatch order.
-struct FwdFold {
-  int64_t label_off;
-  float inv_tau;
-  int n_pad;
-  float* lse;
-  float* lse2;
-  float* loss_rows;
-  float* loss;
-  float* dqu;
-  __bf16* qs;
-  int* xrows;
-  unsigned* tickets;  // [ncb] per column block, [ncb] the blocks' own counter; zeroed by the prep
-};
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kBufRsrcFlags = 0x00020000;  // raw buffer, dword data (cdna_hip_programming.md T8)
-constexpr int kSc1 = 16;                   // buffer aux: sc1 (write-through store / L2 load)
-
-// The folded forward combine (see FwdFold) at the end of score_bf16_kernel<FWD, ..., FOLD>, in
-// the engine's own register layout: lane (r32, hh) of wave w holds query r32 of the wave's 32
-// (my_col), O^T elements h = 32 ht + 8 g4 + 4 hh + 0..3 (acc) and its operand chunks h = 8 (2 kk +
-// hh) .. + 7 (cf); l_run its half-row sums, shift its row's shift bound.
-__device__ __forceinline__ void fwd_fold(f32x16 (&acc)[8], const bf16x8 (&cf)[16], float l_run, float shift,
-                                         int split, int S, int64_t cb, int64_t ncb, int64_t M,
-                                         const __bf16* __restrict__ Q, int64_t B, const __bf16* __restrict__ D,
-                                         float c2, float* __restrict__ acc_part, float* __restrict__ l_part,
-                                         const FwdFold& fa, char* smem) {
-  constexpr int H = 4 * kWave, NHT = H / 32, NK = H / 16;
-  const int lane = lane_id(), wid = threadIdx.x >> 6, r32 = lane & 31, hh = lane >> 5;
-  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
-  const bool col_ok = my_col < B;
-  const int64_t src_col = col_ok ? my_col : 0;
-  const float l_tot = l_run + __shfl_xor(l_run, 32);
-  int* flag = reinterpret_cast<int*>(smem);  // the engine's ring is free now
-  const auto ra = __builtin_amdgcn_make_buffer_rsrc(acc_part, 0, (int)((int64_t)S * B * H * 4), kBufRsrcFlags);
-  const auto rl = __builtin_amdgcn_make_buffer_rsrc(l_part, 0, (int)((int64_t)S * B * 4), kBufRsrcFlags);
-  const auto rr = __builtin_amdgcn_make_buffer_rsrc(fa.loss_rows, 0, (int)(B * 4), kBufRsrcFlags);
-  auto h_of = [&](int ht, int g4) { return ht * 32 + 8 * g4 + 4 * hh; };
-  TT_FTRACE(0);
-  // 1. publish this split's partial write-through; every wave drains its stores before the ticket
-  if (S > 1 && col_ok) {
-    const unsigned own = (unsigned)(((int64_t)split * B + my_col) * H * 4);
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-        __builtin_amdgcn_raw_buffer_store_b128(
-            __builtin_bit_cast(u32x4, f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2],
-                                            acc[ht][4 * g4 + 3]}),
-            ra, (int)(own + h_of(ht, g4) * 4), 0, kSc1);
-    if (hh == 0)
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, l_tot), rl,
-                                            (int)(((int64_t)split * B + my_col) * 4), 0, kSc1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  TT_FTRACE(1);
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(fa.tickets + cb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == (unsigned)(S - 1);
-    if (last) __hip_atomic_store(fa.tickets + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  const int is_last = *flag;
-  __syncthreads();  // the flag word is reused below
-  if (!is_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler fence: no load above the ticket
-  TT_FTRACE(2);
-  // 2. the last split folds O and l over the splits in fwd_combine's order (0 + s0 + s1 + ...), the
-  //    other splits' partials by sc1 loads (one split's 32 loads in flight at a time), in place
-  f32x4 o[NHT][4];
-#pragma unroll
-  for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) o[ht][g4] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float l = 0.f;
-  for (int s = 0; s < S; ++s) {
-    if (s == split) {
-#pragma unroll
-      for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-          o[ht][g4] += f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
-      l += l_tot;
-    } else {
-      const unsigned base = (unsigned)(((int64_t)s * B + src_col) * H * 4);
-      f32x4 v[NHT][4];
-#pragma unroll
-      for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-          v[ht][g4] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(base + h_of(ht, g4) * 4), 0, kSc1));
-      const float ls = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, (int)(((int64_t)s * B + src_col) * 4), 0, kSc1));
-#pragma unroll
-      for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) o[ht][g4] += v[ht][g4];
-      l += ls;
-    }
-  }
-  TT_FTRACE(3);
-  // 3. fwd_combine's row arithmetic (combine_row256), lane-parallel over the queries: the two lanes of
-  //    a query each hold half of its row (O elements as above, q~ chunks as in cf)
-  const float l_sum = l;
-  l = __builtin_fmaf(-(float)fa.n_pad, __builtin_amdgcn_exp2f(-shift), l);
-  const bool exact = !(l >= 7.888609052210118e-31f);  // l < 2^-100 (or NaN): the exact path below
-  const int64_t lab = src_col + fa.label_off;
-  const __bf16* dl = D + lab * H;
-  const float lse2_i = shift + log2f(l);
-  const float lse_i = lse2_i * kLn2;
-  float dot = 0.f;  // q~ . d~_label: this lane's 128 elements in chunk order, then the other half
-#pragma unroll
-  for (int kk = 0; kk < NK; ++kk) {
-    const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dl + (2 * kk + hh) * 8);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dot = __builtin_fmaf((float)cf[kk][e], (float)dv[e], dot);
-  }
-  dot += __shfl_xor(dot, 32);
-  const float loss_i = __builtin_fmaf(-dot, fa.inv_tau, lse_i);
-  if (col_ok && !exact) {
-    if (hh == 0) {
-      fa.lse[my_col] = lse_i;
-      fa.lse2[my_col] = lse2_i;
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, loss_i), rr, (int)(my_col * 4), 0, kSc1);
-    }
-    if (fa.qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
-      const float f = __builtin_amdgcn_exp2f(shift - lse2_i);
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        bf16x8 x;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = (__bf16)((float)cf[kk][e] * f);
-        *reinterpret_cast<bf16x8*>(fa.qs + my_col * H + (2 * kk + hh) * 8) = x;
-      }
-    }
-    const float inv_l = 1.f / l;
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int h0 = h_of(ht, g4);
-        const bf16x4 d4 = *reinterpret_cast<const bf16x4*>(dl + h0);
-        *reinterpret_cast<f32x4*>(fa.dqu + my_col * H + h0) =
-            f32x4{__builtin_fmaf(o[ht][g4][0], inv_l, -(float)d4[0]), __builtin_fmaf(o[ht][g4][1], inv_l, -(float)d4[1]),
-                  __builtin_fmaf(o[ht][g4][2], inv_l, -(float)d4[2]), __builtin_fmaf(o[ht][g4][3], inv_l, -(float)d4[3])};
-      }
-  }
-  // rows whose bound overshot: the whole wave redoes each one exactly (combine_row256's exact path)
-  unsigned long long xm = __ballot(col_ok && exact && hh == 0);
-  while (xm) {
-    const int j = __builtin_ctzll(xm);
-    xm &= xm - 1;
-    const int64_t i = cb * (32 * NW) + wid * 32 + j;
-    const float lx = __shfl(l_sum, j), shx = __shfl(shift, j);
-    const float loss_x = combine_row256<__bf16>(
-        i, lx, [&] { return f32x4{}; }, shx, fa.n_pad, M, c2,
-        fa.inv_tau, fa.label_off, Q, D, fa.lse, fa.lse2, fa.dqu, fa.qs, fa.xrows, lane);
-    if (lane == 0) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, loss_x), rr, (int)(i * 4), 0, kSc1);
-  }
-  // 4. the last column block to get here forms the mean loss in mean_kernel's order
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  TT_FTRACE(4);
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(fa.tickets + ncb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == (unsigned)(ncb - 1);
-    if (last) __hip_atomic_store(fa.tickets + ncb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  __syncthreads();  // every wave has read the flag before the LDS below is reused
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  TT_FTRACE(5);
-  // the zero tail of the scaled query copy (the stored-P backward streams BJ rows past B)
-  if (fa.qs)
-    for (int k = threadIdx.x; k < kTailRows * H / 8; k += NT)
-      reinterpret_cast<bf16x8*>(fa.qs + B * H)[k] = bf16x8{};
-  // mean_kernel: virtual thread t < 1024 sums x[t], x[t + 1024], ... from 0; then a fixed tree
-  float* part = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int k = 0; k < 1024 / NT; ++k) {
-    const int t = threadIdx.x + k * NT;
-    float sum = 0.f;
-    for (int64_t i = t; i < B; i += 1024)
-      sum += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, (int)(i * 4), 0, kSc1));
-    part[t] = sum;
-  }
-  __syncthreads();
-  for (int w = 512; w > 0; w >>= 1) {
-    for (int t = threadIdx.x; t < w; t += NT) part[t] += part[t + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) fa.loss[0] = part[0] / (float)B;
-  TT_FTRACE(6);
-}
-
-template <int MODE, bool PRECISE, int H, bool STOREP = false, bool FOLD = false>
+template <int MODE, bool PRECISE, int H, bool STOREP = false>
 __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
     const float* __restrict__ dmax_part, int n_dmax,
     const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part,
-    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0, FwdFold fa = FwdFold{}) {
+    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0) {
   static_assert(!STOREP || (MODE == FWD && !PRECISE), "stored probabilities: forward, single-rounded G");
-  static_assert(!FOLD || (MODE == FWD && !PRECISE && H == 4 * kWave), "folded combine: bf16 forward, H = 256");
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
   constexpr int NHT = H / 32;
@@ -1212,11 +995,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 #endif
   if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
-  if constexpr (FOLD) {
-    fwd_fold(acc, cf, l_run, shift, split, S, cb, (nC + 32 * NW - 1) / (32 * NW), nR, C, nC, R, c2, acc_part, l_part,
-             fa, smem);
-    return;
-  }
   write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 #ifdef TT_SCORER_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1615,11 +1393,10 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
                                                       __bf16* __restrict__ qb, __bf16* __restrict__ db,
                                                       float* __restrict__ qnorm, float* __restrict__ dmax_part,
                                                       char* __restrict__ pad, float* __restrict__ lse2,
-                                                      int* __restrict__ xrows, unsigned* __restrict__ tickets, int n_tickets) {
+                                                      int* __restrict__ xrows) {
   __shared__ float wmax[4];
   if (blockIdx.x == 0) {
     if (xrows && threadIdx.x == 0) xrows[0] = 0;
-    for (int t = threadIdx.x; t < n_tickets; t += blockDim.x) tickets[t] = 0u;  // the folded combine's counters
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
@@ -1705,12 +1482,11 @@ __global__ __launch_bounds__(256) void l2_prep_kernel(float* __restrict__ y, int
                                                       float* __restrict__ norms, __bf16* __restrict__ qb,
                                                       __bf16* __restrict__ db, float* __restrict__ qnorm,
                                                       float* __restrict__ dmax_part, char* __restrict__ pad,
-                                                      float* __restrict__ lse2, int* __restrict__ xrows, unsigned* __restrict__ tickets, int n_tickets) {
+                                                      float* __restrict__ lse2, int* __restrict__ xrows) {
   constexpr int H = 4 * kWave;
   __shared__ float wmax[4];
   if (blockIdx.x == 0) {  // prep_qd_kernel's block-0 set-up
     if (xrows && threadIdx.x == 0) xrows[0] = 0;
-    for (int t = threadIdx.x; t < n_tickets; t += blockDim.x) tickets[t] = 0u;  // the folded combine's counters
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
@@ -1962,8 +1738,6 @@ struct Ws {
   char* pad;
   float* l_part;
   float* acc_part;
-  unsigned* tickets;  // folded forward combine: one counter per query column block + one overall
-  int n_tickets;
   size_t total;
 };
 
@@ -1978,17 +1752,6 @@ std::atomic<int>& bwd_mode() {
   }()};
   return m;
 }
-// Forward combine folded into the bf16 stored-P engine (FwdFold): off by default (measured slower
-// than the separate combine and mean kernels so far); TT_SCORER_FOLD=1 (read at load) or
-// tt_inbatch_set_fold(1) turns it on.
-std::atomic<int>& fold_flag() {
-  static std::atomic<int> m{[] {
-    const char* e = std::getenv("TT_SCORER_FOLD");
-    return (e && std::strcmp(e, "1") == 0) ? 1 : 0;
-  }()};
-  return m;
-}
-bool fold_mode() { return fold_flag().load(std::memory_order_relaxed) != 0; }
 bool stored_p(int dtype, int64_t B, int64_t M) {
   return dtype == TT_BF16 && bwd_mode().load(std::memory_order_relaxed) == 1 && B * M <= (int64_t(1) << 31);
 }
@@ -2031,10 +1794,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   if (sp) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
   const size_t oa = take(parts);
-  const int nt = sp ? (int)((B + 32 * NW - 1) / (32 * NW)) + 1 : 0;
-  const size_t ot = take((size_t)nt * 4);
   Ws w{};
-  w.n_tickets = nt;
   char* b = static_cast<char*>(base);
   if (b) {
     w.Qb = reinterpret_cast<__bf16*>(b + oq);
@@ -2049,7 +1809,6 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.pad = b + opad;
     w.l_part = reinterpret_cast<float*>(b + ol);
     w.acc_part = reinterpret_cast<float*>(b + oa);
-    w.tickets = nt ? reinterpret_cast<unsigned*>(b + ot) : nullptr;
   }
   w.total = off;
   return w;
@@ -2057,7 +1816,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
 
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
-                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const FwdFold* fold = nullptr) {
+                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
   if (dtype == TT_F32) {
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -2066,11 +1825,6 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
-  } else if (MODE == FWD && w.P && fold) {
-    if constexpr (H == 4 * kWave)
-      score_bf16_kernel<FWD, false, H, true, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
-          static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-          w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, w.P, w.p_nqt, *fold);
   } else if (MODE == FWD && w.P) {
     score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -2086,13 +1840,12 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
 
 template <int MODE>
 int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
-                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s,
-                    const FwdFold* fold = nullptr) {
+                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
   switch (H) {
     case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
     case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
     case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
-    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s, fold);
+    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
 }
@@ -2121,11 +1874,6 @@ extern "C" int tt_inbatch_set_backward(int mode) {
   return bwd_mode().exchange(mode);
 }
 
-extern "C" int tt_inbatch_set_fold(int on) {
-  if (on != 0 && on != 1) return fold_flag().load();
-  return fold_flag().exchange(on);
-}
-
 extern "C" size_t tt_inbatch_ws_size(int64_t B, int64_t M, int H, int dtype) {
   return carve(nullptr, B, M, H, dtype).total + 256;
 }
@@ -2139,8 +1887,7 @@ namespace {
 int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, int H, const float* qnorm,
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
-             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr,
-             unsigned* tickets = nullptr) {
+             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr) {
   const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
@@ -2152,11 +1899,6 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   w.P = P;
   w.p_nqt = p_nqt;
   int rc;
-  if (tickets && P && dqu && dtype == TT_BF16 && H == 4 * kWave && fold_mode()) {
-    // the combine and the mean run inside the engine (FwdFold)
-    const FwdFold fold{label_off, inv_tau, p.n_pad, lse, lse2, loss_rows, loss, dqu, Qs, xrows, tickets};
-    return dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s, &fold);
-  }
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
   const dim3 grid((unsigned)((B + (Qs ? kTailRows : 0) + 3) / 4)), block(256);
   if (dtype == TT_F32)
@@ -2284,7 +2026,7 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
     const int gq = prep_blocks_q(B);
     prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
                                                                    bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad,
-                                                                   w.lse2, w.xrows, w.tickets, w.n_tickets);
+                                                                   w.lse2, w.xrows);
     TT_LAUNCH_CHECK("score_prep");
   }
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
@@ -2292,7 +2034,7 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
   const bool sp = want_grad && w.P;
   return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
                   want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s, sp ? w.P : nullptr, w.p_nqt,
-                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr, sp ? w.tickets : nullptr);
+                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr);
 }
 }  // namespace
 }  // namespace tt
@@ -2315,7 +2057,7 @@ extern "C" int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dty
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   const int gq = prep_blocks_q(B), gd = prep_blocks_d(M);
   l2_prep_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
-      y, B, M, gq, norms, w.Qb, w.Db, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows, w.tickets, w.n_tickets);
+      y, B, M, gq, norms, w.Qb, w.Db, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows);
   TT_LAUNCH_CHECK("score_l2_prep");
   return TT_OK;
 }
@@ -2404,9 +2146,6 @@ extern "C" int tt_debug_scorer_trace(long long* host_out) {
 }
 extern "C" int tt_debug_scorer_ktrace(long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_ktrace), sizeof(long long) * 2 * 1024 * 4);
-}
-extern "C" int tt_debug_scorer_ftrace(long long* host_out) {
-  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_ftrace), sizeof(long long) * 8 * 1024);
 }
 extern "C" int tt_debug_scorer_trace_bwd(long long* host_out) {
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(tt::g_tt_trace_b), sizeof(long long) * 8 * 64);

@@ -533,12 +533,6 @@ def set_inbatch_backward(form: str) -> str:
     return {v: k for k, v in _BWD_FORMS.items()}[prev]
 
 
-def set_inbatch_fold(on: bool) -> bool:
-    """Run the bf16 stored-P forward's combine and loss mean inside its engine (True) or as
-    separate kernels (False, the default; same gradient bits).  Returns the previous setting."""
-    return bool(_lib.lib().tt_inbatch_set_fold(1 if on else 0))
-
-
 def get_inbatch_backward() -> str:
     """The current single-process bf16 in-batch backward form ("stored" or "recompute")."""
     return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
