@@ -66,6 +66,121 @@ def pmc_traffic(abi: str, config: str) -> dict:
     return {"traffic": None}
 
 
+def normalise_ms(rows: int, d: int, dev, reps: int = 20) -> float:
+    """Device time of the head's plain L2-normalise pass on (rows, d): tt_head_gemm with the
+    normalise (epi 1) minus without it (epi 4), HIP events on the launch stream."""
+    if d != tt_ops.HEAD_WIDTH:
+        return 0.0
+    g = torch.Generator(device=dev).manual_seed(0)
+    h = torch.randn(rows, d, device=dev, generator=g)
+    W = torch.randn(d, d, device=dev, generator=g) * 0.05
+    b = torch.zeros(d, device=dev)
+    planes = tt_ops._planes(W, False)
+    norms = torch.empty(rows, device=dev)
+    t = {}
+    for epi in (1, 4, 1, 4):
+        tt_ops._head_gemm(h, planes, epi, bias=b, norms=norms)
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(reps):
+            tt_ops._head_gemm(h, planes, epi, bias=b, norms=norms)
+        en.record()
+        torch.cuda.synchronize()
+        t[epi] = st.elapsed_time(en) / reps
+    return max(0.0, t[1] - t[4])
+
+
+def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dtype: str, nnz: float,
+              tower_params: int, bwd_form: str, normalise=lambda: 0.0):
+    """Per-op rooflines from the per-op device times (HIP events on each C-ABI call's launch
+    stream, ops_t = _lib.TIMER.summary()) and the dominant main-stream op's roofline."""
+    cfg = CONFIGS[config]
+    V, d, L, B, K = cfg["V"], cfg["d"], cfg["L"], cfg["B"], cfg["negatives"]
+    nseq = (2 + K) * B
+    M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1
+    kernels = []
+
+    def add(name, key, algo, unit, peak, bound, per_launch_note, side_stream=False, executed=None):
+        if key not in ops_t:
+            return
+        ms = ops_t[key]["mean_ms"]
+        achieved = algo / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+        k = {"op": name, "abi": key, "bound": bound, "mean_ms": round(ms, 4),
+             "calls_per_step": ops_t[key]["calls"] / timing_steps, "achieved": round(achieved, 2),
+             "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "algorithmic": algo,
+             "per_launch": per_launch_note}
+        if executed is not None:  # work the kernels do beyond the algorithmic count (e.g. P.D in the forward)
+            k["executed"] = executed
+            k["executed_rate"] = round(executed / (ms * 1e-3) / 1e12, 2)
+        if side_stream:  # its event span covers the overlap with the forward, not its kernels alone
+            k["stream"] = "side (overlapped)"
+        kernels.append(k)
+
+    id_bytes = 4  # int32 ids on device
+    add("embedding bag forward (gather + masked mean)", "tt_bag_mean_fwd",
+        nseq * L * id_bytes + nnz * d * 4 + nseq * d * 4 + nseq * 4, "GB/s", HBM_PEAK_GBS, "hbm",
+        "ids N*L*4 + gathered rows nnz*E*4 + pooled N*E*4 + denom N*4 bytes")
+    add("embedding bag backward fused with table AdamW (apply half: scale rows + per-row reduce + AdamW)",
+        "tt_bag_mean_bwd_adamw_planned", nseq * d * 4 + nseq * 4 + 24 * V * d, "GB/s", HBM_PEAK_GBS, "hbm",
+        "d_pooled N*E*4 + denom N*4 + AdamW p,m,v read+write 24*V*E bytes")
+    add("embedding bag backward sort plan (ids -> sorted (row, seq) + segments; side stream, overlaps the towers)",
+        "tt_bag_plan", nseq * L * 4 + nnz * 8 + V * 8, "GB/s", HBM_PEAK_GBS, "hbm",
+        "ids N*L*4 + sorted (row, seq) pairs nnz*8 + segment bounds V*8 bytes (latency-bound radix sort)",
+        side_stream=True)
+    add("embedding bag backward (dense grad, apply half)", "tt_bag_mean_bwd_planned",
+        nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
+    pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
+    mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
+    # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
+    stored_p = scorer_dtype == "bf16" and world == 1 and bwd_form == "stored" and B * M <= 2 ** 31
+    fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
+    if fwd_key in ops_t and "tt_inbatch_bwd" in ops_t:
+        # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
+        # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
+        fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t["tt_inbatch_bwd"]["mean_ms"]
+        prep_ms = None
+        if fwd_key == "tt_inbatch_fwd_prepped" and "tt_inbatch_l2_prep" in ops_t:
+            # the operand prep runs inside the head's normalise pass (tt_inbatch_l2_prep): charge
+            # the scorer what that pass costs beyond the plain normalise, measured on the same rows
+            prep_ms = max(0.0, ops_t["tt_inbatch_l2_prep"]["mean_ms"] - normalise())
+        ms = fwd_ms + bwd_ms + (prep_ms or 0.0)
+        algo = 6.0 * B * M * d
+        executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
+        achieved = algo / (ms * 1e-3) / 1e12
+        form = ("bf16, backward from stored bf16 probabilities" if stored_p else
+                {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
+                 "fp32": "fp32 MFMA"}[scorer_dtype])
+        kernels.append({
+            "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
+            "abi": fwd_key + "+tt_inbatch_bwd", "bound": "mfma", "mean_ms": round(ms, 4),
+            "pass_ms": {"forward": round(fwd_ms, 4), "backward": round(bwd_ms, 4),
+                        **({"operand_prep_in_head_normalise": round(prep_ms, 4)} if prep_ms is not None else {})},
+            "calls_per_step": ops_t[fwd_key]["calls"] / timing_steps, "achieved": round(achieved, 2),
+            "peak": pk, "unit": "TFLOP/s", "frac": round(achieved / pk, 4), "algorithmic": algo,
+            "executed": executed, "executed_rate": round(executed / (ms * 1e-3) / 1e12, 2),
+            "per_launch": "6*B*M*H algorithmic flops (2BMH S + 4BMH dQ, dD) over both passes",
+            "form": form,
+            # measured max-abs-normalised gradient error at C3 (tools/scorer_error_table.py --big,
+            # profiles/r02_scorer_error_table.jsonl): against float64 on the same bf16-rounded
+            # operands, and against float64 on the fp32 operands (what the reference computes)
+            "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
+        })
+    add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
+        HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
+    add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
+        "q, p, negatives read + their gradients written 2*(2 + K)*B*H*4 bytes")
+    add("dense AdamW (tower FF, multi-tensor)", "tt_adamw_multi", 28 * tower_params, "GB/s", HBM_PEAK_GBS, "hbm",
+        "28 bytes per parameter")
+    main_stream = [k for k in kernels if "stream" not in k]
+    dominant = max(main_stream, key=lambda k: k["mean_ms"] * k["calls_per_step"]) if main_stream else None
+    roofline = None
+    if dominant:
+        roofline = {"bound": dominant["bound"], "achieved": dominant["achieved"], "peak": dominant["peak"],
+                    "unit": dominant["unit"], "frac": dominant["frac"], "traffic": None, "op": dominant["op"]}
+        roofline.update(pmc_traffic(dominant["abi"], config))
+    return kernels, roofline
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -178,84 +293,10 @@ def main():
         dist.destroy_process_group()
         return
 
-    # ---- per-op device times (HIP events on the launch stream) -> rooflines
-    nseq = (2 + K) * B
-    M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1
-    kernels = []
-
-    def add(name, key, algo, unit, peak, bound, per_launch_note, side_stream=False, executed=None):
-        if key not in ops_t:
-            return
-        ms = ops_t[key]["mean_ms"]
-        achieved = algo / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
-        k = {"op": name, "abi": key, "bound": bound, "mean_ms": round(ms, 4),
-             "calls_per_step": ops_t[key]["calls"] / timing_steps, "achieved": round(achieved, 2),
-             "peak": peak, "unit": unit, "frac": round(achieved / peak, 4), "algorithmic": algo,
-             "per_launch": per_launch_note}
-        if executed is not None:  # work the kernels do beyond the algorithmic count (e.g. P.D in the forward)
-            k["executed"] = executed
-            k["executed_rate"] = round(executed / (ms * 1e-3) / 1e12, 2)
-        if side_stream:  # its event span covers the overlap with the forward, not its kernels alone
-            k["stream"] = "side (overlapped)"
-        kernels.append(k)
-
-    id_bytes = 4  # int32 ids on device
-    add("embedding bag forward (gather + masked mean)", "tt_bag_mean_fwd",
-        nseq * L * id_bytes + nnz * d * 4 + nseq * d * 4 + nseq * 4, "GB/s", HBM_PEAK_GBS, "hbm",
-        "ids N*L*4 + gathered rows nnz*E*4 + pooled N*E*4 + denom N*4 bytes")
-    add("embedding bag backward fused with table AdamW (apply half: scale rows + per-row reduce + AdamW)",
-        "tt_bag_mean_bwd_adamw_planned", nseq * d * 4 + nseq * 4 + 24 * V * d, "GB/s", HBM_PEAK_GBS, "hbm",
-        "d_pooled N*E*4 + denom N*4 + AdamW p,m,v read+write 24*V*E bytes")
-    add("embedding bag backward sort plan (ids -> sorted (row, seq) + segments; side stream, overlaps the towers)",
-        "tt_bag_plan", nseq * L * 4 + nnz * 8 + V * 8, "GB/s", HBM_PEAK_GBS, "hbm",
-        "ids N*L*4 + sorted (row, seq) pairs nnz*8 + segment bounds V*8 bytes (latency-bound radix sort)",
-        side_stream=True)
-    add("embedding bag backward (dense grad, apply half)", "tt_bag_mean_bwd_planned",
-        nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
-    pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
-    mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
-    # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
-    stored_p = (scorer_dtype == "bf16" and world == 1 and tt_ops.get_inbatch_backward() == "stored"
-                and B * M <= 2 ** 31)
-    if "tt_inbatch_fwd" in ops_t and "tt_inbatch_bwd" in ops_t:
-        # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
-        # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
-        fwd_ms, bwd_ms = ops_t["tt_inbatch_fwd"]["mean_ms"], ops_t["tt_inbatch_bwd"]["mean_ms"]
-        ms = fwd_ms + bwd_ms
-        algo = 6.0 * B * M * d
-        executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
-        achieved = algo / (ms * 1e-3) / 1e12
-        form = ("bf16, backward from stored bf16 probabilities" if stored_p else
-                {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
-                 "fp32": "fp32 MFMA"}[scorer_dtype])
-        kernels.append({
-            "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
-            "abi": "tt_inbatch_fwd+tt_inbatch_bwd", "bound": "mfma", "mean_ms": round(ms, 4),
-            "pass_ms": {"forward": round(fwd_ms, 4), "backward": round(bwd_ms, 4)},
-            "calls_per_step": ops_t["tt_inbatch_fwd"]["calls"] / timing_steps, "achieved": round(achieved, 2),
-            "peak": pk, "unit": "TFLOP/s", "frac": round(achieved / pk, 4), "algorithmic": algo,
-            "executed": executed, "executed_rate": round(executed / (ms * 1e-3) / 1e12, 2),
-            "per_launch": "6*B*M*H algorithmic flops (2BMH S + 4BMH dQ, dD) over both passes",
-            "form": form,
-            # measured max-abs-normalised gradient error at C3 (tools/scorer_error_table.py --big,
-            # profiles/r02_scorer_error_table.jsonl): against float64 on the same bf16-rounded
-            # operands, and against float64 on the fp32 operands (what the reference computes)
-            "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
-        })
-    add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
-        HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
-    add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
-        "q, p, negatives read + their gradients written 2*(2 + K)*B*H*4 bytes")
-    add("dense AdamW (tower FF, multi-tensor)", "tt_adamw_multi", 28 * sum(p.numel() for n_, p in model.named_parameters()
-                                                      if "embedding" not in n_), "GB/s", HBM_PEAK_GBS, "hbm",
-        "28 bytes per parameter")
-    main_stream = [k for k in kernels if "stream" not in k]
-    dominant = max(main_stream, key=lambda k: k["mean_ms"] * k["calls_per_step"]) if main_stream else None
-    roofline = None
-    if dominant:
-        roofline = {"bound": dominant["bound"], "achieved": dominant["achieved"], "peak": dominant["peak"],
-                    "unit": dominant["unit"], "frac": dominant["frac"], "traffic": None, "op": dominant["op"]}
-        roofline.update(pmc_traffic(dominant["abi"], args.config))
+    M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1  # candidates per query
+    kernels, roofline = op_report(ops_t, timing_steps, args.config, world, scorer_dtype, nnz,
+                                  sum(p.numel() for n_, p in model.named_parameters() if "embedding" not in n_),
+                                  tt_ops.get_inbatch_backward(), lambda: normalise_ms((2 + K) * B, d, dev))
     gather = next((k for k in kernels if k["abi"] == "tt_bag_mean_fwd"), None)
 
     cpu = None

@@ -219,3 +219,28 @@ def test_checkpoint_round_trip_reference_format(tmp_path):
         assert torch.equal(a, b), n
     p0 = next(model2.parameters())
     assert torch.equal(opt2.state[p0]["exp_avg"], ref_opt.state[next(model.parameters())]["exp_avg"])
+
+
+def test_bench_op_report_shapes():
+    """bench.op_report on synthetic per-op times: the scorer entry with the operand prep in the
+    head's normalise pass (tt_inbatch_fwd_prepped + tt_inbatch_l2_prep) and without it, the
+    multiple-negatives workload, and the dominant-op roofline (no GPU: the report is pure host math)."""
+    import bench
+
+    def op(ms, calls=10):
+        return {"calls": calls, "mean_ms": ms, "total_ms": ms * calls}
+
+    base = {"tt_bag_mean_fwd": op(0.13), "tt_bag_mean_bwd_adamw_planned": op(0.27), "tt_bag_plan": op(0.15),
+            "tt_inbatch_bwd": op(0.097), "tt_adamw_multi": op(0.008)}
+    for extra, prep in (({"tt_inbatch_fwd": op(0.165)}, None),
+                        ({"tt_inbatch_fwd_prepped": op(0.155), "tt_inbatch_l2_prep": op(0.013)}, 0.003)):
+        kernels, roof = bench.op_report({**base, **extra}, 10, "c3", 1, "bf16", 848_000.0, 131_584, "stored",
+                                        normalise=lambda: 0.010)
+        sc = next(k for k in kernels if k["bound"] == "mfma")
+        want = 0.097 + extra.get("tt_inbatch_fwd", extra.get("tt_inbatch_fwd_prepped"))["mean_ms"] + (prep or 0.0)
+        assert abs(sc["mean_ms"] - want) < 1e-4 and 0 < sc["frac"] < 1
+        assert ("operand_prep_in_head_normalise" in sc["pass_ms"]) == (prep is not None)
+        assert roof["op"].startswith("embedding bag backward fused") and roof["unit"] == "GB/s"
+    kernels, roof = bench.op_report({"tt_bag_mean_fwd": op(0.34), "tt_multi_neg_fwd": op(0.026),
+                                     "tt_multi_neg_bwd": op(0.031)}, 10, "c5", 1, "fp32", 2.0e6, 131_584, "stored")
+    assert {k["abi"] for k in kernels} == {"tt_bag_mean_fwd", "tt_multi_neg_fwd", "tt_multi_neg_bwd"}

@@ -12,7 +12,8 @@ import threading
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwotower_amd.so")
+# TT_LIB: another build of the library (measurement variants, tools/build_variants.sh)
+LIB_PATH = os.environ.get("TT_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtwotower_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "twotower_amd.h")
 
 TT_IDS_I32, TT_IDS_I64 = 0, 1

@@ -154,8 +154,9 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_generic_kernel(
 template <typename IdT>
 __global__ __launch_bounds__(kBlock) void bag_plan_keys_kernel(
     const IdT* __restrict__ ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx,
-    uint32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    uint32_t* __restrict__ keys, int32_t* __restrict__ vals, int32_t* __restrict__ n_pieces) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i == 0) *n_pieces = 0;  // the piece counter bag_plan_bounds_kernel allocates from
   if (i >= nseq * L) return;
   const int64_t seq = i / L, t = i - seq * L;
   const int64_t id = (int64_t)ids[seq * ld + t];
@@ -181,19 +182,6 @@ __global__ __launch_bounds__(kBlock) void bag_scale_rows_kernel(const float* __r
   }
 }
 
-// Segment bounds of each row id in the sorted key array (rows absent stay [0,0)).
-__global__ __launch_bounds__(kBlock) void bag_bwd_mark_kernel(const uint32_t* __restrict__ keys,
-                                                              int64_t n, uint32_t V,
-                                                              int32_t* __restrict__ seg_start,
-                                                              int32_t* __restrict__ seg_end) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = keys[i];
-  if (k >= V) return;
-  if (i == 0 || keys[i - 1] != k) seg_start[k] = (int32_t)i;
-  if (i == n - 1 || keys[i + 1] != k) seg_end[k] = (int32_t)(i + 1);
-}
-
 // Long rows (Zipf-hot ids) are split so no wave walks tens of thousands of tokens: a row with
 // more than kPieceT tokens is cut into pieces of max(kPieceT, ceil(len / kMaxPieces)) tokens;
 // one wave per piece sums its gs rows (token order) into a partial, and the row's reduce wave
@@ -206,33 +194,49 @@ __device__ __forceinline__ int piece_len(int len) {
   return t > kPieceT ? t : kPieceT;
 }
 
-__global__ __launch_bounds__(kBlock) void bag_piece_count_kernel(const int32_t* __restrict__ seg_start,
-                                                                 const int32_t* __restrict__ seg_end, int64_t V,
-                                                                 int32_t* __restrict__ nch) {
+// Segment bounds and pieces of every row from the sorted keys, one thread per row r <= V:
+// seg_start[r] = the first sorted position with key >= r (lower bound), so row r's tokens are
+// [seg_start[r], seg_start[r + 1]) (seg_end aliases seg_start + 1; r = V: the masked tail).  A
+// long row takes its nch pieces' slots from one counter (n_pieces = piece_off[V], zeroed by the
+// keys kernel): the slot order across rows varies per run, a row's own pieces stay consecutive
+// and in token order, so every sum is deterministic.  One kernel instead of two memsets, a mark
+// pass, a piece count, a scan and a piece list.
+__global__ __launch_bounds__(kBlock) void bag_plan_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                                 int64_t V, int32_t* __restrict__ seg_start,
+                                                                 int32_t* __restrict__ nch,
+                                                                 int32_t* __restrict__ piece_off,
+                                                                 int32_t* __restrict__ piece_beg,
+                                                                 int32_t* __restrict__ piece_end) {
+  __shared__ int32_t lb[kBlock];
   const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  auto lower_bound = [&](int64_t key, int64_t lo) {
+    int64_t hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)keys[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo;
+  };
+  const int64_t st = r <= V ? lower_bound(r, 0) : n;
+  lb[threadIdx.x] = (int32_t)st;
+  __syncthreads();
   if (r > V) return;
+  seg_start[r] = (int32_t)st;
   if (r == V) {
     nch[V] = 0;
     return;
   }
-  const int len = seg_end[r] - seg_start[r];
-  nch[r] = len > kPieceT ? (len + piece_len(len) - 1) / piece_len(len) : 0;
-}
-
-__global__ __launch_bounds__(kBlock) void bag_piece_list_kernel(const int32_t* __restrict__ seg_start,
-                                                                const int32_t* __restrict__ seg_end,
-                                                                const int32_t* __restrict__ nch,
-                                                                const int32_t* __restrict__ piece_off, int64_t V,
-                                                                int32_t* __restrict__ piece_beg,
-                                                                int32_t* __restrict__ piece_end) {
-  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (r >= V) return;
-  const int np = nch[r];
+  const int64_t en = threadIdx.x + 1 < kBlock ? (int64_t)lb[threadIdx.x + 1] : lower_bound(r + 1, st);
+  const int len = (int)(en - st);
+  const int np = len > kPieceT ? (len + piece_len(len) - 1) / piece_len(len) : 0;
+  nch[r] = np;
   if (np == 0) return;
-  const int st = seg_start[r], en = seg_end[r], t = piece_len(en - st), k0 = piece_off[r];
+  const int k0 = atomicAdd(piece_off + V, np), t = piece_len(len);
+  piece_off[r] = k0;
   for (int k = 0; k < np; ++k) {
-    piece_beg[k0 + k] = st + k * t;
-    piece_end[k0 + k] = min(st + (k + 1) * t, en);
+    piece_beg[k0 + k] = (int32_t)st + k * t;
+    piece_end[k0 + k] = min((int32_t)st + (k + 1) * t, (int32_t)en);
   }
 }
 
@@ -560,17 +564,15 @@ struct BwdWs {
   int32_t* vals_in;
   int32_t* vals_out;
   float* gs;
-  int32_t* seg_start;
-  int32_t* seg_end;
+  int32_t* seg_start;  // V + 1 (bag_plan_bounds_kernel)
+  int32_t* seg_end;    // = seg_start + 1
   void* sort_tmp;
   size_t sort_bytes;
   int32_t* nch;        // V + 1 piece counts (0 = short row)
-  int32_t* piece_off;  // V + 1 exclusive scan of nch (piece_off[V] = number of pieces)
+  int32_t* piece_off;  // V + 1: a long row's first piece slot; piece_off[V] = number of pieces
   int32_t* piece_beg;  // max_pieces token ranges
   int32_t* piece_end;
   float* partial;      // max_pieces x E
-  void* scan_tmp;
-  size_t scan_bytes;
   int64_t max_pieces;
   size_t total;
 };
@@ -578,7 +580,7 @@ struct BwdWs {
 // sum over long rows of ceil(len / piece_len) <= sum (len / kPieceT + 1) < 2 n / kPieceT
 int64_t max_pieces_for(int64_t n) { return 2 * ((n + kPieceT - 1) / kPieceT) + 1; }
 
-BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes, size_t scan_bytes) {
+BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes) {
   BwdWs w{};
   const size_t n = (size_t)nseq * L;
   size_t off = 0;
@@ -590,28 +592,25 @@ BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes
   char* b = static_cast<char*>(base);
   const size_t o_ki = take(n * 4), o_ko = take(n * 4), o_vi = take(n * 4), o_vo = take(n * 4);
   const size_t o_gs = take((size_t)nseq * E * 4);
-  const size_t o_ss = take((size_t)V * 4), o_se = take((size_t)V * 4);
+  const size_t o_ss = take((size_t)(V + 1) * 4);
   const size_t o_tmp = take(sort_bytes);
   const int64_t mp = max_pieces_for((int64_t)n);
   const size_t o_nch = take((size_t)(V + 1) * 4), o_po = take((size_t)(V + 1) * 4);
   const size_t o_pb = take((size_t)mp * 4), o_pe = take((size_t)mp * 4), o_pp = take((size_t)mp * E * 4);
-  const size_t o_stmp = take(scan_bytes);
   w.max_pieces = mp;
-  w.scan_bytes = scan_bytes;
   if (b) {
     w.nch = reinterpret_cast<int32_t*>(b + o_nch);
     w.piece_off = reinterpret_cast<int32_t*>(b + o_po);
     w.piece_beg = reinterpret_cast<int32_t*>(b + o_pb);
     w.piece_end = reinterpret_cast<int32_t*>(b + o_pe);
     w.partial = reinterpret_cast<float*>(b + o_pp);
-    w.scan_tmp = b + o_stmp;
     w.keys_in = reinterpret_cast<uint32_t*>(b + o_ki);
     w.keys_out = reinterpret_cast<uint32_t*>(b + o_ko);
     w.vals_in = reinterpret_cast<int32_t*>(b + o_vi);
     w.vals_out = reinterpret_cast<int32_t*>(b + o_vo);
     w.gs = reinterpret_cast<float*>(b + o_gs);
     w.seg_start = reinterpret_cast<int32_t*>(b + o_ss);
-    w.seg_end = reinterpret_cast<int32_t*>(b + o_se);
+    w.seg_end = w.seg_start + 1;
     w.sort_tmp = b + o_tmp;
   }
   w.sort_bytes = sort_bytes;
@@ -619,16 +618,6 @@ BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes
   return w;
 }
 
-size_t scan_tmp_bytes(int64_t V) {
-  size_t bytes = 0;
-  hipError_t e = rocprim::exclusive_scan(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, 0,
-                                         (size_t)(V + 1), rocprim::plus<int32_t>(), (hipStream_t)0, false);
-  if (e != hipSuccess) {
-    set_error("rocprim::exclusive_scan size query: %s", hipGetErrorString(e));
-    return 0;
-  }
-  return bytes;
-}
 
 size_t sort_tmp_bytes(int64_t n, int64_t V) {
   size_t bytes = 0;
@@ -722,40 +711,29 @@ int launch_piece_sum(const BwdWs& w, int64_t V, int E, hipStream_t s) {
   return TT_OK;
 }
 
-// plan: keys/vals -> stable radix sort (key = row id, value = seq) -> segment bounds -> the
-// pieces of long rows.
+// plan: keys/vals -> stable radix sort (key = row id, value = seq) -> segment bounds and the
+// pieces of long rows (bag_plan_bounds_kernel).
 template <typename IdT>
 int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, const BwdWs& w,
                hipStream_t s) {
   const int64_t n = nseq * L;
   const dim3 block(kBlock);
-  TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)V * 4, s), "memset seg_start");
-  TT_HIP(hipMemsetAsync(w.seg_end, 0, (size_t)V * 4, s), "memset seg_end");
-  if (n == 0) {  // no pieces: nch = 0 and piece_off = 0 everywhere
+  if (n == 0) {  // no tokens: every segment empty, no pieces
+    TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)(V + 1) * 4, s), "memset seg_start");
     TT_HIP(hipMemsetAsync(w.nch, 0, (size_t)(V + 1) * 4, s), "memset nch");
     TT_HIP(hipMemsetAsync(w.piece_off, 0, (size_t)(V + 1) * 4, s), "memset piece_off");
     return TT_OK;
   }
   bag_plan_keys_kernel<IdT><<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
-      ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in);
+      ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in, w.piece_off + V);
   TT_LAUNCH_CHECK("bag_plan_keys");
   size_t tmp = w.sort_bytes;
   TT_HIP(rocprim::radix_sort_pairs<PlanSortConfig>(w.sort_tmp, tmp, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
                                    (size_t)n, 0, end_bit_for(V), s, false),
          "rocprim::radix_sort_pairs");
-  bag_bwd_mark_kernel<<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
-      w.keys_out, n, (uint32_t)V, w.seg_start, w.seg_end);
-  TT_LAUNCH_CHECK("bag_bwd_mark");
-  const dim3 rgrid((unsigned)((V + 1 + kBlock - 1) / kBlock));
-  bag_piece_count_kernel<<<rgrid, block, 0, s>>>(w.seg_start, w.seg_end, V, w.nch);
-  TT_LAUNCH_CHECK("bag_piece_count");
-  size_t stmp = w.scan_bytes;
-  TT_HIP(rocprim::exclusive_scan(w.scan_tmp, stmp, w.nch, w.piece_off, 0, (size_t)(V + 1), rocprim::plus<int32_t>(),
-                                 s, false),
-         "rocprim::exclusive_scan");
-  bag_piece_list_kernel<<<rgrid, block, 0, s>>>(w.seg_start, w.seg_end, w.nch, w.piece_off, V, w.piece_beg,
-                                                w.piece_end);
-  TT_LAUNCH_CHECK("bag_piece_list");
+  bag_plan_bounds_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
+      w.keys_out, n, V, w.seg_start, w.nch, w.piece_off, w.piece_beg, w.piece_end);
+  TT_LAUNCH_CHECK("bag_plan_bounds");
   return TT_OK;
 }
 
@@ -804,14 +782,14 @@ extern "C" int tt_bag_mean_fwd(const float* table, int64_t V, int E, const void*
 
 extern "C" size_t tt_bag_mean_bwd_ws_size(int64_t nseq, int L, int64_t V, int E) {
   const size_t sb = sort_tmp_bytes(nseq * (int64_t)L, V);
-  return carve(nullptr, nseq, L, V, E, sb, scan_tmp_bytes(V)).total + 256;
+  return carve(nullptr, nseq, L, V, E, sb).total + 256;
 }
 
 static BwdWs plan_layout(void* ws, int64_t nseq, int L, int64_t V, int E) {
   if (nseq == 0 || L == 0) nseq = 0, L = 0;
   const size_t sb = nseq > 0 ? sort_tmp_bytes(nseq * (int64_t)L, V) : 0;
   void* base = ws ? reinterpret_cast<void*>(align_up(reinterpret_cast<size_t>(ws), 256)) : nullptr;
-  return carve(base, nseq, L, V, E, sb, scan_tmp_bytes(V));
+  return carve(base, nseq, L, V, E, sb);
 }
 
 static int plan_impl(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld, int64_t V, int E,
