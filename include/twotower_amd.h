@@ -245,6 +245,22 @@ int tt_inbatch_fwd_ex(const void* Qb, const float* qnorm, int64_t B, const void*
                       const float* dmax_parts, int n_parts, int64_t M_all, int H, int dtype, float inv_tau,
                       int64_t label_off, int want_grad, float* lse, float* lse2, float* loss_rows,
                       float* loss, float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream);
+/* The same forward in two launches, so the caller's candidate all-gather overlaps the scoring of
+ * the rank's own candidates (bf16 / bf16_split; M and own_begin multiples of 64):
+ * tt_inbatch_fwd_ex_local: Db_loc = this rank's candidates (M rows + zero tail), dmax_loc its
+ *   n_loc max_parts; scores them with their own norm bound (no other rank's data needed).
+ * tt_inbatch_fwd_ex_remote: Db_all, dmax_parts as in tt_inbatch_fwd_ex (own block at rows
+ *   [own_begin, own_begin + M), labels i + own_begin); scores the other rows, then combines both
+ *   launches (the local partials rescaled to the global bound).  Same outputs as
+ *   tt_inbatch_fwd_ex within fp32 rounding; ws sized by tt_inbatch_ex_ws_size(B, M_all, nQ_all, M). */
+int tt_inbatch_fwd_ex_local(const void* Qb, const float* qnorm, int64_t B, const void* Db_loc,
+                            const float* dmax_loc, int n_loc, int64_t M, int64_t M_all, int64_t own_begin,
+                            int H, int dtype, float inv_tau, void* ws, size_t ws_bytes, tt_stream_t stream);
+int tt_inbatch_fwd_ex_remote(const void* Qb, const float* qnorm, int64_t B, const void* Db_all,
+                             const float* dmax_parts, int n_parts, const float* dmax_loc, int n_loc,
+                             int64_t M, int64_t M_all, int64_t own_begin, int H, int dtype, float inv_tau,
+                             int want_grad, float* lse, float* lse2, float* loss_rows, float* loss,
+                             float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream);
 int tt_inbatch_bwd_ex(const void* Qb_all, const float* lse2_all, int64_t nQ_all, int64_t q_row0,
                       const void* Db, int64_t M, int64_t B, int64_t label_off, int H, int dtype,
                       float inv_tau, const float* dq_unscaled, const float* grad_loss, float grad_scale,

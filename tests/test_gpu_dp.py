@@ -54,11 +54,11 @@ def _batch():
     return tt.data.synthetic_triplets(WORLD * B, L, V, seed=3, device="cuda:0")
 
 
-def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner"):
+def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1"):
     # every process recomputes G in the backward (the default; the candidate-owner passes always
     # do), so single process and ranks form the same bf16 products
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TT_INBATCH_DP=inbatch_dp,
-                      TT_INBATCH_BWD="recompute")
+                      TT_INBATCH_BWD="recompute", TT_INBATCH_OVERLAP=overlap)
     try:
         torch.cuda.set_device(0)
         if rank >= 0:
@@ -126,12 +126,13 @@ def test_dp_step_equals_global_batch(loss_name, table_sync):
             assert err < 1e-5, (name, k, float(err))
 
 
-@pytest.mark.parametrize("inbatch_dp", ["owner", "allgather"])
-def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp):
+@pytest.mark.parametrize("inbatch_dp,overlap", [("owner", "1"), ("owner", "0"), ("allgather", "1")])
+def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp, overlap):
     """bf16 scorer with cross-device negatives: candidate-owner gradients (bf16 copies gathered,
-    no gradient reduce-scatter) and the fp32-row all-gather + reduce-scatter form both give the
-    single process's bf16 gradients on the global batch (same bf16 products, other fp32 sum
-    orders), recovered from the parameter change as above."""
+    no gradient reduce-scatter; the forward in two launches, own candidates scored while the
+    others arrive, or in one launch after the gather) and the fp32-row all-gather + reduce-scatter
+    form all give the single process's bf16 gradients on the global batch (same bf16 products,
+    other fp32 sum orders), recovered from the parameter change as above."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ref = ctx.Process(target=_worker, args=(-1, 0, "in_batch_bf16", "gather", q))
@@ -140,7 +141,8 @@ def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp):
     ref.join(timeout=60)
     assert init is not None, r_loss
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, "in_batch_bf16", "gather", q, inbatch_dp)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, "in_batch_bf16", "gather", q, inbatch_dp, overlap))
+             for r in range(WORLD)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in procs]

@@ -96,6 +96,10 @@ _SIGNATURES = {
     "tt_inbatch_ex_ws_size": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_int, _c_int]),
     "tt_inbatch_fwd_ex": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_int, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+    "tt_inbatch_fwd_ex_local": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_int, _c_i64, _c_i64, _c_i64, _c_int, _c_int,
+                                         _c_f32, _vp, _c_sz, _vp]),
+    "tt_inbatch_fwd_ex_remote": (_c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_int, _vp, _c_int, _c_i64, _c_i64, _c_i64,
+                                          _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_bwd_ex": (_c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp,
                                    _vp, _c_f32, _vp, _vp, _vp, _c_sz, _vp]),
 }

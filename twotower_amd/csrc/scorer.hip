@@ -114,9 +114,14 @@ __device__ __forceinline__ float fold_dmax(const float* __restrict__ part, int n
 }
 
 // Column shift for the forward: an upper bound of row i's logits in log2 units,
-// |q~_i . d~_j| * c2 <= c2 * |q_i| * max_j |d_j| * (1 + 2^-6) (bf16 rounding slack included).
-// Computed where it is used (engine and combine) from the same floats, so both agree exactly.
-__device__ __forceinline__ float col_shift(float c2, float qn, float dmax) { return fabsf(c2) * qn * dmax * 1.015625f; }
+// |q~_i . d~_j| * c2 <= c2 * |q_i| * max_j |d_j| * (1 + 2^-6) (bf16 rounding slack included),
+// rounded up to an integer: two launches whose bounds differ (the data-parallel forward's local
+// and remote candidates) then form the same bf16 G up to an exact power of two, so rescaling the
+// local partials changes no product.  Computed where it is used (engine and combine) from the
+// same floats, so both agree exactly.
+__device__ __forceinline__ float col_shift(float c2, float qn, float dmax) {
+  return ceilf(fabsf(c2) * qn * dmax * 1.015625f);
+}
 
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const lds_char_t*)p;  // 32-bit LDS byte address
@@ -755,7 +760,11 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
     const float* __restrict__ dmax_part, int n_dmax,
     const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part,
-    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0) {
+    char* __restrict__ pstore = nullptr, int64_t p_nqt = 0, int64_t skip_begin = 0, int64_t skip_len = 0,
+    int split_base = 0) {
+  // skip_begin / skip_len: the streamed rows are R's rows with [skip_begin, skip_begin + skip_len)
+  // left out (a data-parallel rank's remote candidates around its own block; stages never straddle
+  // the gap: skip_begin % BJ == 0); split_base: the slot of split 0 in the partial buffers.
   static_assert(!STOREP || (MODE == FWD && !PRECISE), "stored probabilities: forward, single-rounded G");
   using T = Tile<__bf16, H>;
   constexpr int NK = H / 16;
@@ -811,7 +820,10 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
       glds_dword_s((unsigned)lane * 4, lse2_rows + r0, lds0 + T::LSE_OFF + b * 256);
     }
   };
-  auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
+  auto stage_row = [&](int64_t t) {
+    const int64_t r = t < ntiles ? row_begin + t * T::BJ : row_begin;
+    return r >= skip_begin ? r + skip_len : r;
+  };
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -995,7 +1007,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 #endif
   if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
-  write_partials<MODE, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+  write_partials<MODE, H>(acc, l_run, split + split_base, nC, my_col, hh, acc_part, l_part);
 #ifdef TT_SCORER_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -1546,7 +1558,10 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     const float* __restrict__ dmax_part, int n_dmax, const float* __restrict__ l_part,
     const float* __restrict__ acc_part, float inv_tau, int64_t label_off, const DT* __restrict__ Qmat,
     const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2, float* __restrict__ loss_rows,
-    float* __restrict__ dqu, __bf16* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr) {
+    float* __restrict__ dqu, __bf16* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr,
+    int S_loc = 0, const float* __restrict__ dmax_loc = nullptr, int n_dmax_loc = 0) {
+  // S_loc > 0 (data-parallel forward in two launches): slots [0, S_loc) hold the local launch's
+  // partials, formed with the local norm bound; they are rescaled to this launch's shift
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = lane_id();
   if (i >= B) {  // the zero tail of the scaled query copy (the stored-P backward's R rows)
@@ -1555,12 +1570,19 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     return;
   }
   const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
+  const float f_loc = S_loc > 0 ? __builtin_amdgcn_exp2f(col_shift(c2, qnorm[i], fold_dmax(dmax_loc, n_dmax_loc)) - sh)
+                                : 1.f;
   float l = 0.f;
-  for (int s = 0; s < S; ++s) l += l_part[(int64_t)s * B + i];
+  for (int s = 0; s < S; ++s) l += s < S_loc ? f_loc * l_part[(int64_t)s * B + i] : l_part[(int64_t)s * B + i];
   if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
     const float loss_i = combine_row256<DT>(
         i, l,
-        [&] { return sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane, B * (H / 4), S); },
+        [&] {
+          const f32x4* p = reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane;
+          if (S_loc == 0) return sum_parts4(p, B * (H / 4), S);
+          return sum_parts4(p + (int64_t)S_loc * B * (H / 4), B * (H / 4), S - S_loc) +
+                 f_loc * sum_parts4(p, B * (H / 4), S_loc);
+        },
         sh, n_pad, M, c2, inv_tau, label_off, Qmat, Dmat, lse, lse2, dqu, qs, xrows, lane);
     if (lane == 0) loss_rows[i] = loss_i;
     return;
@@ -1610,7 +1632,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     const float inv_l = 1.f / l;
     for (int h = lane; h < H; h += kWave) {
       float o = 0.f;
-      for (int s = 0; s < S; ++s) o += acc_part[((int64_t)s * B + i) * H + h];
+      for (int s = 0; s < S; ++s) o += (s < S_loc ? f_loc : 1.f) * acc_part[((int64_t)s * B + i) * H + h];
       dqu[i * H + h] = o * inv_l - (float)dl[h];
     }
   }
@@ -1704,10 +1726,10 @@ struct Plan {
 
 // Split the streamed rows so the grid is one round of resident workgroups (256 CUs x wg_per_cu):
 // a second round would only add prologues/epilogues and twice the split partials.
-Plan plan_for(int64_t nR, int64_t nC, int BJ, int wg_per_cu, int cols_per_block = 32 * NW) {
+Plan plan_for(int64_t nR, int64_t nC, int BJ, int wg_per_cu, int cols_per_block = 32 * NW, int cus = 256) {
   const int64_t ncb = (nC + cols_per_block - 1) / cols_per_block;
   const int64_t row_tiles = (nR + BJ - 1) / BJ;
-  const int64_t target = 256 * wg_per_cu;
+  const int64_t target = (int64_t)cus * wg_per_cu;
   int64_t S = (target + ncb - 1) / ncb;
   if (S > 8) S = 8;
   if (S > row_tiles) S = row_tiles;
@@ -1814,9 +1836,15 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   return w;
 }
 
+// Engine sub-range (data-parallel forward in two launches; see fwd_ex_local / fwd_ex_remote)
+struct Skip {
+  int64_t begin = 0, len = 0;  // streamed rows leave out R's rows [begin, begin + len)
+  int split_base = 0;          // partial slot of split 0
+};
+
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
-                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
+                  const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
   if (dtype == TT_F32) {
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -1824,7 +1852,7 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
   } else if (dtype == TT_BF16_SPLIT) {
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, nullptr, 0, sk.begin, sk.len, sk.split_base);
   } else if (MODE == FWD && w.P) {
     score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -1832,7 +1860,7 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
   } else {
     score_bf16_kernel<MODE, false, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, nullptr, 0, sk.begin, sk.len, sk.split_base);
   }
   TT_LAUNCH_CHECK(MODE == FWD ? "score_fwd" : "score_dd");
   return TT_OK;
@@ -1840,12 +1868,12 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
 
 template <int MODE>
 int dispatch_engine(int H, int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p,
-                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s) {
+                    float c2, const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
   switch (H) {
-    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
-    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
-    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
-    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s);
+    case 32: return launch_engine<MODE, 32>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s, sk);
+    case 64: return launch_engine<MODE, 64>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s, sk);
+    case 128: return launch_engine<MODE, 128>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s, sk);
+    case 256: return launch_engine<MODE, 256>(dtype, R, nR, C, nC, p, c2, lse2, w, n_dmax, s, sk);
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
 }
@@ -1985,12 +2013,26 @@ struct ExWs {
   float* acc_part;
   size_t total;
 };
+// The local launch of the two-launch data-parallel forward runs beside the candidate all-gather,
+// whose kernels hold CUs of their own: its one-round grid is sized for 3/4 of the chip, so no
+// workgroup waits for the collective to finish.
+constexpr int kLocalCus = 192;
+Plan plan_local(int64_t B, int64_t M, int H, int dtype) {
+  return plan_for(M, B, bj_for(dtype), wg_per_cu(H), 32 * NW, kLocalCus);
+}
+// split slots of the two-launch data-parallel forward (fwd_ex_local + fwd_ex_remote)
+int split_fwd_slots(int64_t B, int64_t M, int64_t M_all, int H, int dtype) {
+  if (M_all <= M || M % bj_for(dtype) != 0) return 0;  // no two-launch forward for this shape
+  return plan_local(B, M, H, dtype).S + plan_for(M_all - M, B, bj_for(dtype), wg_per_cu(H)).S;
+}
+
 ExWs carve_ex(void* base, int64_t B, int64_t M_all, int64_t nQ_all, int64_t M, int H, int dtype) {
   const int BJ = bj_for(dtype);
   const Plan pf = plan_for(M_all, B, BJ, wg_per_cu(H)), pd = plan_for(nQ_all, M, BJ, wg_per_cu(H));
+  const int64_t sf = std::max<int64_t>(pf.S, split_fwd_slots(B, M, M_all, H, dtype));
   const size_t ol = 0;
-  const size_t oa = align_up((size_t)pf.S * B * 4, 256);
-  const size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
+  const size_t oa = align_up((size_t)sf * B * 4, 256);
+  const size_t parts = std::max((size_t)sf * B, (size_t)pd.S * M) * H * 4;
   ExWs w{};
   if (base) {
     char* b = reinterpret_cast<char*>(align_up(reinterpret_cast<size_t>(base), 256));
@@ -2120,6 +2162,85 @@ extern "C" int tt_inbatch_fwd_ex(const void* Qb, const float* qnorm, int64_t B, 
   return fwd_core(dtype, Db_all, M_all, Qb, B, H, qnorm, dmax_parts, n_parts, inv_tau, label_off, lse, lse2,
                   loss_rows, loss, want_grad ? dq_unscaled : nullptr, nullptr, w.l_part, w.acc_part,
                   reinterpret_cast<hipStream_t>(stream));
+}
+
+// Data-parallel forward in two launches, so the candidate all-gather overlaps the scoring of the
+// rank's own candidates.  local: the engine over Db_loc (M rows + zero tail; this rank's own
+// candidates, global rows [own_begin, own_begin + M) of Db_all) with the local norm bound, into
+// partial slots [0, S_loc).  remote: the engine over Db_all's other M_all - M rows (the own block
+// skipped) with the global bound, into the next S_rem slots; then the combine over all slots, the
+// local ones rescaled by 2^(shift_loc - shift), and the mean.  Same result as tt_inbatch_fwd_ex on
+// Db_all within fp32 rounding.
+namespace tt {
+namespace {
+int check_split_fwd(int64_t B, int64_t M, int64_t M_all, int64_t own_begin, int H, int dtype) {
+  int rc = check_args(B, M_all, H, dtype, own_begin);
+  if (rc) return rc;
+  TT_REQUIRE(dtype != TT_F32, "explicit-operand passes take bf16 operand copies (dtype bf16 / bf16_split)");
+  const int BJ = bj_for(dtype);
+  TT_REQUIRE(M > 0 && M_all > M && M % BJ == 0 && own_begin % BJ == 0 && own_begin + M <= M_all,
+             "split forward: M=%lld own_begin=%lld must be multiples of %d inside M_all=%lld", (long long)M,
+             (long long)own_begin, BJ, (long long)M_all);
+  return TT_OK;
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" int tt_inbatch_fwd_ex_local(const void* Qb, const float* qnorm, int64_t B, const void* Db_loc,
+                                       const float* dmax_loc, int n_loc, int64_t M, int64_t M_all, int64_t own_begin,
+                                       int H, int dtype, float inv_tau, void* ws, size_t ws_bytes,
+                                       tt_stream_t stream) {
+  int rc = check_split_fwd(B, M, M_all, own_begin, H, dtype);
+  if (rc) return rc;
+  TT_REQUIRE(Qb && qnorm && Db_loc && dmax_loc && ws && n_loc > 0, "null pointer / n_loc");
+  const size_t need = tt_inbatch_ex_ws_size(B, M_all, B, M, H, dtype);
+  TT_REQUIRE(need <= ws_bytes, "workspace too small: need %zu have %zu", need, ws_bytes);
+  const ExWs w = carve_ex(ws, B, M_all, B, M, H, dtype);
+  Ws e{};
+  e.qnorm = const_cast<float*>(qnorm);
+  e.dmax_part = const_cast<float*>(dmax_loc);
+  e.l_part = w.l_part;
+  e.acc_part = w.acc_part;
+  const Plan p = plan_local(B, M, H, dtype);
+  return dispatch_engine<FWD>(H, dtype, Db_loc, M, Qb, B, p, inv_tau * kLog2e, nullptr, e, n_loc,
+                              reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_inbatch_fwd_ex_remote(const void* Qb, const float* qnorm, int64_t B, const void* Db_all,
+                                        const float* dmax_parts, int n_parts, const float* dmax_loc, int n_loc,
+                                        int64_t M, int64_t M_all, int64_t own_begin, int H, int dtype, float inv_tau,
+                                        int want_grad, float* lse, float* lse2, float* loss_rows, float* loss,
+                                        float* dq_unscaled, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  int rc = check_split_fwd(B, M, M_all, own_begin, H, dtype);
+  if (rc) return rc;
+  TT_REQUIRE(Qb && qnorm && Db_all && dmax_parts && dmax_loc && lse && lse2 && loss_rows && loss && ws, "null pointer");
+  TT_REQUIRE(n_parts > 0 && n_loc > 0, "n_parts=%d n_loc=%d", n_parts, n_loc);
+  TT_REQUIRE(!want_grad || dq_unscaled, "want_grad needs dq_unscaled");
+  const size_t need = tt_inbatch_ex_ws_size(B, M_all, B, M, H, dtype);
+  TT_REQUIRE(need <= ws_bytes, "workspace too small: need %zu have %zu", need, ws_bytes);
+  const ExWs w = carve_ex(ws, B, M_all, B, M, H, dtype);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int BJ = bj_for(dtype);
+  const Plan pl = plan_local(B, M, H, dtype), pr = plan_for(M_all - M, B, BJ, wg_per_cu(H));
+  const float c2 = inv_tau * kLog2e;
+  Ws e{};
+  e.qnorm = const_cast<float*>(qnorm);
+  e.dmax_part = const_cast<float*>(dmax_parts);
+  e.l_part = w.l_part;
+  e.acc_part = w.acc_part;
+  Skip sk;
+  sk.begin = own_begin;
+  sk.len = M;
+  sk.split_base = pl.S;
+  if ((rc = dispatch_engine<FWD>(H, dtype, Db_all, M_all - M, Qb, B, pr, c2, nullptr, e, n_parts, s, sk))) return rc;
+  const int S = pl.S + pr.S;
+  const dim3 grid((unsigned)((B + 3) / 4)), block(256);
+  fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(
+      B, M_all, H, S, pl.n_pad + pr.n_pad, c2, qnorm, dmax_parts, n_parts, w.l_part, w.acc_part, inv_tau, own_begin,
+      static_cast<const __bf16*>(Qb), static_cast<const __bf16*>(Db_all), lse, lse2, loss_rows,
+      want_grad ? dq_unscaled : nullptr, nullptr, nullptr, pl.S, dmax_loc, n_loc);
+  TT_LAUNCH_CHECK("score_fwd_combine (split)");
+  return launch_mean(loss_rows, B, loss, s);
 }
 
 extern "C" int tt_inbatch_bwd_ex(const void* Qb_all, const float* lse2_all, int64_t nQ_all, int64_t q_row0,

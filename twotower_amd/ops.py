@@ -683,12 +683,18 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
         db = torch.empty(M + T, H, dtype=bf, device=dev)
         parts = torch.empty(P, dtype=_FLOAT, device=dev)
         call("tt_inbatch_prep_rows", ptr(d), M, H, ptr(db), None, ptr(parts), st)
-        # bf16 rows travel as bytes (any backend), rank-major; the zero tail stays local
+        # bf16 rows travel as bytes (any backend), rank-major; the zero tail stays local.  From 4
+        # ranks on (M a multiple of 64) the forward runs in two launches: this rank's own
+        # candidates are scored while the other ranks' rows arrive.  Splitting costs 35-39 us on
+        # one GPU (tools/mb_split_fwd.py: the local launch leaves CUs to the collective); the
+        # gather it hides grows with N (~0.1 ms at 4 ranks).  TT_INBATCH_OVERLAP=1 / 0 forces it.
+        ov = os.environ.get("TT_INBATCH_OVERLAP", "auto")
+        split = M % 64 == 0 and (ov == "1" or (ov == "auto" and world >= 4))
         db_all = torch.empty(world * M + T, H, dtype=bf, device=dev)
         db_all[world * M:].zero_()
-        all_gather_rows(db_all[:world * M].view(torch.uint8), db[:M].view(torch.uint8), group)
         parts_all = torch.empty(world * P, dtype=_FLOAT, device=dev)
-        all_gather_rows(parts_all, parts, group)
+        w_p = all_gather_rows(parts_all, parts, group, async_op=split)
+        w_d = all_gather_rows(db_all[:world * M].view(torch.uint8), db[:M].view(torch.uint8), group, async_op=split)
         qb_all = torch.empty(world * B + T, H, dtype=bf, device=dev)
         qb_all[world * B:].zero_()
         w_q = all_gather_rows(qb_all[:world * B].view(torch.uint8), qb[:B].view(torch.uint8), group, async_op=True)
@@ -700,9 +706,18 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
         rows = torch.empty(B, dtype=_FLOAT, device=dev)
         loss = torch.empty((), dtype=_FLOAT, device=dev)
         dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
-        call("tt_inbatch_fwd_ex", ptr(qb), ptr(qnorm), B, ptr(db_all), ptr(parts_all), world * P, world * M, H, dt,
-             float(inv_tau), rank * M, int(want_grad), ptr(lse), ptr(lse2), ptr(rows), ptr(loss), ptr(dqu), ptr(ws),
-             ws.numel(), st)
+        if split:
+            call("tt_inbatch_fwd_ex_local", ptr(qb), ptr(qnorm), B, ptr(db), ptr(parts), P, M, world * M, rank * M,
+                 H, dt, float(inv_tau), ptr(ws), ws.numel(), st)
+            w_p.wait()
+            w_d.wait()
+            call("tt_inbatch_fwd_ex_remote", ptr(qb), ptr(qnorm), B, ptr(db_all), ptr(parts_all), world * P,
+                 ptr(parts), P, M, world * M, rank * M, H, dt, float(inv_tau), int(want_grad), ptr(lse), ptr(lse2),
+                 ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), st)
+        else:
+            call("tt_inbatch_fwd_ex", ptr(qb), ptr(qnorm), B, ptr(db_all), ptr(parts_all), world * P, world * M, H,
+                 dt, float(inv_tau), rank * M, int(want_grad), ptr(lse), ptr(lse2), ptr(rows), ptr(loss), ptr(dqu),
+                 ptr(ws), ws.numel(), st)
         lse2_all = torch.empty(world * B + T, dtype=_FLOAT, device=dev)
         lse2_all[world * B:].fill_(float("inf"))
         w_l = all_gather_rows(lse2_all[:world * B], lse2, group, async_op=True)
