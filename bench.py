@@ -90,8 +90,31 @@ def normalise_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     return max(0.0, t[1] - t[4])
 
 
+def l2_backward_ms(rows: int, d: int, dev, reps: int = 20) -> float:
+    """Device time of the head's plain F.normalize backward (tt_l2norm_bwd) on (rows, d), HIP
+    events on the launch stream."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    y = torch.nn.functional.normalize(torch.randn(rows, d, device=dev, generator=g), dim=1)
+    dout = torch.randn(rows, d, device=dev, generator=g)
+    norms = torch.ones(rows, device=dev)
+    dx = torch.empty_like(y)
+    args = lambda: (tt_ops.ptr(dout), tt_ops.ptr(y), tt_ops.ptr(norms), rows, d, tt_ops.ptr(dx),  # noqa: E731
+                    torch.cuda.current_stream(dev).cuda_stream)
+    t = 0.0
+    for _ in range(2):
+        tt_ops.call("tt_l2norm_bwd", *args())
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(reps):
+            tt_ops.call("tt_l2norm_bwd", *args())
+        en.record()
+        torch.cuda.synchronize()
+        t = st.elapsed_time(en) / reps
+    return t
+
+
 def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dtype: str, nnz: float,
-              tower_params: int, bwd_form: str, normalise=lambda: 0.0):
+              tower_params: int, bwd_form: str, normalise=lambda: 0.0, l2_backward=lambda: 0.0):
     """Per-op rooflines from the per-op device times (HIP events on each C-ABI call's launch
     stream, ops_t = _lib.TIMER.summary()) and the dominant main-stream op's roofline."""
     cfg = CONFIGS[config]
@@ -134,10 +157,17 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
     # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
     stored_p = scorer_dtype == "bf16" and world == 1 and bwd_form == "stored" and B * M <= 2 ** 31
     fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
-    if fwd_key in ops_t and "tt_inbatch_bwd" in ops_t:
+    bwd_key = "tt_inbatch_bwd_l2" if "tt_inbatch_bwd_l2" in ops_t else "tt_inbatch_bwd"
+    if fwd_key in ops_t and bwd_key in ops_t:
         # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
         # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
-        fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t["tt_inbatch_bwd"]["mean_ms"]
+        fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t[bwd_key]["mean_ms"]
+        l2_ms = None
+        if bwd_key == "tt_inbatch_bwd_l2":
+            # the backward combine also runs the tower head's F.normalize backward: the scorer is
+            # charged what that pass costs beyond a plain tt_l2norm_bwd over the same rows
+            l2_ms = l2_backward()
+            bwd_ms = max(0.0, bwd_ms - l2_ms)
         prep_ms = None
         if fwd_key == "tt_inbatch_fwd_prepped" and "tt_inbatch_l2_prep" in ops_t:
             # the operand prep runs inside the head's normalise pass (tt_inbatch_l2_prep): charge
@@ -152,9 +182,10 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
                  "fp32": "fp32 MFMA"}[scorer_dtype])
         kernels.append({
             "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
-            "abi": fwd_key + "+tt_inbatch_bwd", "bound": "mfma", "mean_ms": round(ms, 4),
+            "abi": fwd_key + "+" + bwd_key, "bound": "mfma", "mean_ms": round(ms, 4),
             "pass_ms": {"forward": round(fwd_ms, 4), "backward": round(bwd_ms, 4),
-                        **({"operand_prep_in_head_normalise": round(prep_ms, 4)} if prep_ms is not None else {})},
+                        **({"operand_prep_in_head_normalise": round(prep_ms, 4)} if prep_ms is not None else {}),
+                        **({"plain_l2_backward_subtracted": round(l2_ms, 4)} if l2_ms is not None else {})},
             "calls_per_step": ops_t[fwd_key]["calls"] / timing_steps, "achieved": round(achieved, 2),
             "peak": pk, "unit": "TFLOP/s", "frac": round(achieved / pk, 4), "algorithmic": algo,
             "executed": executed, "executed_rate": round(executed / (ms * 1e-3) / 1e12, 2),
@@ -296,7 +327,8 @@ def main():
     M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1  # candidates per query
     kernels, roofline = op_report(ops_t, timing_steps, args.config, world, scorer_dtype, nnz,
                                   sum(p.numel() for n_, p in model.named_parameters() if "embedding" not in n_),
-                                  tt_ops.get_inbatch_backward(), lambda: normalise_ms((2 + K) * B, d, dev))
+                                  tt_ops.get_inbatch_backward(), lambda: normalise_ms((2 + K) * B, d, dev),
+                                  lambda: l2_backward_ms((2 + K) * B, d, dev))
     gather = next((k for k in kernels if k["abi"] == "tt_bag_mean_fwd"), None)
 
     cpu = None

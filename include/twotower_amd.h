@@ -83,7 +83,9 @@ int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom,
  *   tt_bag_mean_bwd_planned        dense grad_table from d_pooled/denom and the plan;
  *   tt_bag_mean_bwd_adamw_planned  fused AdamW with the per-step scalars read from device
  *                       memory (`adam_args`, written by tt_adam_prepare).
- * Plan + apply compute exactly what tt_bag_mean_bwd / tt_bag_mean_bwd_adamw compute. */
+ * Plan + apply compute exactly what tt_bag_mean_bwd / tt_bag_mean_bwd_adamw compute.  In the two
+ * apply calls denom may be NULL: d_pooled then already holds gs = d_pooled / denom (formed by
+ * the tower head's dx epilogue, tt_head_gemm epi 5) and the scaling pass is skipped. */
 size_t tt_bag_plan_ws_size(int64_t nseq, int L, int64_t V, int E);
 int tt_bag_plan(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
                 int64_t V, int E, int64_t padding_idx, void* plan, size_t plan_bytes,
@@ -127,6 +129,11 @@ typedef struct {
 int tt_adam_prepare(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
                     double eps, double weight_decay, tt_stream_t stream);
 int tt_adamw_multi(const tt_adamw_tensor* tensors, int count, tt_stream_t stream);
+
+/* ---- mean of n floats (the loss reductions' F.cross_entropy / .mean(), losses.py:44,85,116):
+ * one workgroup, fixed-order sums (bitwise reproducible); the in-batch forward forms it itself
+ * unless its loss pointer is NULL. */
+int tt_mean(const float* x, int64_t n, float* out, tt_stream_t stream);
 
 /* ---- row L2 normalise (F.normalize(x, dim=-1), eps 1e-12; twotower/encoders.py:77) -- */
 int tt_l2norm_fwd(const float* x, int64_t rows, int H, float* out, float* norm, tt_stream_t stream);
@@ -236,6 +243,14 @@ int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B, int64_t M,
                            float inv_tau, int64_t label_off, int want_grad,
                            float* lse, float* loss_rows, float* loss, float* dq_unscaled,
                            void* ws, size_t ws_bytes, tt_stream_t stream);
+/* tt_inbatch_bwd fused with the tower head's F.normalize backward (encoders.py:77), for the fused
+ *   TwoTower output qd = [q; d] ((B + M) x 256 fp32, the rows tt_inbatch_l2_prep normalised,
+ *   norms[r] = their norms before it, bf16 / bf16_split operands in ws from the forward): dx
+ *   ((B + M) x 256) = the gradient w.r.t. the rows before F.normalize, i.e. tt_inbatch_bwd's dq, dd
+ *   followed by tt_l2norm_bwd, bit for bit, without writing dq and dd. */
+int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau, int64_t label_off,
+                      const float* lse, const float* dq_unscaled, const float* grad_loss, float grad_scale,
+                      const float* norms, float* dx, void* ws, size_t ws_bytes, tt_stream_t stream);
 #define TT_INBATCH_TAIL_ROWS 64
 #define TT_INBATCH_MAX_PARTS 512
 int tt_inbatch_prep_rows(const float* x, int64_t rows, int H, void* xb, float* norms, float* max_parts,
@@ -295,7 +310,10 @@ int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const 
  *                                     epi 0 for the same rows)
  *   epi 3: .                         (dx = dh W1)
  *   epi 4: . + bias                  (epi 1 before its normalise pass, which the caller runs:
- *                                     tt_inbatch_l2_prep). */
+ *                                     tt_inbatch_l2_prep)
+ *   epi 5: . / bias[r]               (dx = dh W1 divided by per-row divisors, IEEE division: the
+ *                                     bag backward's d_pooled / denom (encoders.py:72) formed in
+ *                                     the head's epilogue; bias = denom, length rows). */
 size_t tt_head_planes_bytes(int N, int K);
 int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream);
 /* the four plane sets of one Linear-ReLU-Linear head in one launch, each tt_head_planes_bytes(256,

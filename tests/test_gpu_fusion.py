@@ -88,3 +88,145 @@ def test_scorer_prep_set_by_trainstep_and_ignored_by_other_losses():
     b = trip(*model(*batch))
     assert torch.equal(a, b)
 
+
+
+def _train(model, opt, loss_fn, batches):
+    for b in batches:
+        opt.zero_grad(set_to_none=True)
+        loss_fn(*model(*b)).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    return {k: v.detach().clone() for k, v in model.named_parameters()}
+
+
+@pytest.mark.parametrize("fused_tables", [False, True])
+@pytest.mark.parametrize("tied", [True, False])
+def test_bag_scaling_in_head_dx_epilogue_is_bit_identical(fused_tables, tied, monkeypatch):
+    """The tower head's dx GEMM divides each row by its bag denominator (tt_head_gemm epi 5) and
+    the bag backward skips its scaling pass: table and head parameters after three AdamW steps
+    equal the unfused launches (TT_BAG_PRESCALE=0), for the fused scatter + AdamW and for the
+    dense table gradient, for the one-head TwoTower path and towers called one by one."""
+    V, B, L = 3000, 200, 24
+    rng = np.random.default_rng(5)
+    batches = [[_ids(B, L, V, rng) for _ in range(3)] for _ in range(3)]
+    loss_fn = tt.losses.build("in_batch", temperature=0.1)
+
+    class PerTower(torch.nn.Module):  # each tower called on its own (BaseTower.forward, three bag calls)
+        def __init__(self, tower):
+            super().__init__()
+            self.tower = tower
+
+        def forward(self, q, p, n):
+            return self.tower(q), self.tower(p), self.tower(n)
+
+    def run():
+        torch.manual_seed(3)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
+        model = tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
+        if not tied:
+            model = PerTower(model.query_tower)
+        kw = dict(fused_tables=True, tables=[emb]) if fused_tables else {}
+        return _train(model, tt.optim.AdamW(model.parameters(), lr=1e-3, **kw), loss_fn, batches)
+
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append((name, args[6] if name == "tt_head_gemm" else None))
+        return real_call(name, *args)
+
+    monkeypatch.setattr(ops, "call", spy)
+    monkeypatch.setenv("TT_BAG_PRESCALE", "1")
+    got = run()
+    assert ("tt_head_gemm", 5) in seen
+    monkeypatch.setenv("TT_BAG_PRESCALE", "0")
+    seen.clear()
+    want = run()
+    assert ("tt_head_gemm", 5) not in seen
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("dtype,bwd", [("bf16", "stored"), ("bf16", "recompute"), ("bf16_split", "stored")])
+def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dtype, bwd, monkeypatch):
+    """TrainStep runs the bf16 in-batch loss's backward combine fused with the tower head's
+    F.normalize backward (tt_inbatch_bwd_l2: dq, dd never written); parameters and losses after
+    four steps equal the unfused combine + tt_l2norm_bwd (TT_FUSED_L2_BWD=0) bit for bit."""
+    V, B, L = 4000, 320, 20
+    rng = np.random.default_rng(9)
+    batches = [[_ids(B, L, V, rng) for _ in range(3)] for _ in range(4)]
+
+    def run():
+        torch.manual_seed(4)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
+        model = tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.05, compute_dtype=dtype), opt,
+                            graph=graph, eager_steps=1)
+        losses = [step(*b).clone() for b in batches]
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().clone() for k, v in model.named_parameters()}
+
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
+    prev = ops.set_inbatch_backward(bwd)
+    try:
+        monkeypatch.setattr(ops, "call", spy)
+        got_l, got = run()
+        assert "tt_inbatch_bwd_l2" in seen and "tt_l2norm_bwd" not in seen
+        monkeypatch.setenv("TT_FUSED_L2_BWD", "0")
+        seen.clear()
+        want_l, want = run()
+        assert "tt_inbatch_bwd_l2" not in seen and "tt_l2norm_bwd" in seen
+    finally:
+        ops.set_inbatch_backward(prev)
+    for a, b in zip(got_l, want_l):
+        assert torch.equal(a, b)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainstep_deferred_loss_mean_equals_inline(graph, monkeypatch):
+    """TrainStep leaves the in-batch loss mean to a side-stream tt_mean after the optimizer is
+    queued: the returned losses and the parameters equal the inline mean (TT_DEFER_MEAN=0)."""
+    V, B, L = 3000, 256, 16
+    rng = np.random.default_rng(13)
+    batches = [[_ids(B, L, V, rng) for _ in range(3)] for _ in range(4)]
+
+    def run():
+        torch.manual_seed(6)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
+        model = tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16"), opt,
+                            graph=graph, eager_steps=1)
+        losses = [step(*b).clone() for b in batches]
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().clone() for k, v in model.named_parameters()}
+
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
+    monkeypatch.setattr(ops, "call", spy)
+    monkeypatch.setenv("TT_DEFER_MEAN", "1")
+    got_l, got = run()
+    assert "tt_mean" in seen
+    monkeypatch.setenv("TT_DEFER_MEAN", "0")
+    seen.clear()
+    want_l, want = run()
+    assert "tt_mean" not in seen
+    for a, b in zip(got_l, want_l):
+        assert torch.equal(a, b) and torch.isfinite(a)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k

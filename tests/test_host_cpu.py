@@ -241,6 +241,14 @@ def test_bench_op_report_shapes():
         assert abs(sc["mean_ms"] - want) < 1e-4 and 0 < sc["frac"] < 1
         assert ("operand_prep_in_head_normalise" in sc["pass_ms"]) == (prep is not None)
         assert roof["op"].startswith("embedding bag backward fused") and roof["unit"] == "GB/s"
+    # the backward combine fused with the head's F.normalize backward: charged beyond a plain one
+    fused = {k: v for k, v in base.items() if k != "tt_inbatch_bwd"}
+    fused.update({"tt_inbatch_bwd_l2": op(0.100), "tt_inbatch_fwd_prepped": op(0.155)})
+    kernels, _ = bench.op_report(fused, 10, "c3", 1, "bf16", 848_000.0, 131_584, "stored",
+                                 l2_backward=lambda: 0.012)
+    sc = next(k for k in kernels if k["bound"] == "mfma")
+    assert sc["abi"] == "tt_inbatch_fwd_prepped+tt_inbatch_bwd_l2" and abs(sc["mean_ms"] - (0.155 + 0.088)) < 1e-4
+    assert sc["pass_ms"]["plain_l2_backward_subtracted"] == 0.012
     kernels, roof = bench.op_report({"tt_bag_mean_fwd": op(0.34), "tt_multi_neg_fwd": op(0.026),
                                      "tt_multi_neg_bwd": op(0.031)}, 10, "c5", 1, "fp32", 2.0e6, 131_584, "stored")
     assert {k["abi"] for k in kernels} == {"tt_bag_mean_fwd", "tt_multi_neg_fwd", "tt_multi_neg_bwd"}

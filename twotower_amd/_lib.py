@@ -76,6 +76,7 @@ _SIGNATURES = {
     "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
     "tt_l2norm_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _vp]),
     "tt_l2norm_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _vp, _vp]),
+    "tt_mean": (_c_int, [_vp, _c_i64, _vp, _vp]),
     "tt_colsum_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_colsum": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_sz, _vp]),
     "tt_relu_bwd": (_c_int, [_vp, _vp, _c_i64, _vp]),
@@ -89,6 +90,8 @@ _SIGNATURES = {
                                 _vp, _c_sz, _vp]),
     "tt_inbatch_bwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
                                 _vp, _vp, _c_sz, _vp]),
+    "tt_inbatch_bwd_l2": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
+                                   _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_l2_prep": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_fwd_prepped": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp,
                                         _vp, _vp, _vp, _c_sz, _vp]),
@@ -122,7 +125,9 @@ def side_stream(device: torch.device, role: str = "plan") -> torch.cuda.Stream:
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), role)
     st = _SIDE.get(key)
     if st is None:
-        st = _SIDE[key] = torch.cuda.Stream(device=key[0])
+        # TT_SIDE_PRIO=role[,role]: those side streams at high priority (measurement switch)
+        hi = role in os.environ.get("TT_SIDE_PRIO", "").split(",")
+        st = _SIDE[key] = torch.cuda.Stream(device=key[0], priority=-1 if hi else 0)
     return st
 
 

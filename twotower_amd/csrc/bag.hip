@@ -742,14 +742,19 @@ template <bool FUSED>
 int apply_plan(const float* dpooled, const float* denom, int64_t nseq, int64_t V, int E, const BwdWs& w,
                float* grad, float* param, float* m, float* v, const AdamArgs& aa, const AdamArgs* aa_dev,
                hipStream_t s) {
+  BwdWs wa = w;
   if (nseq > 0) {
-    bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
-        dpooled, denom, nseq, E, w.gs);
-    TT_LAUNCH_CHECK("bag_scale_rows");
-    int rc = launch_piece_sum(w, V, E, s);
+    if (denom) {
+      bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
+          dpooled, denom, nseq, E, w.gs);
+      TT_LAUNCH_CHECK("bag_scale_rows");
+    } else {
+      wa.gs = const_cast<float*>(dpooled);  // the caller passed gs = d_pooled / denom itself
+    }
+    int rc = launch_piece_sum(wa, V, E, s);
     if (rc) return rc;
   }
-  return launch_reduce<FUSED>(w, V, E, grad, param, m, v, aa, aa_dev, s);
+  return launch_reduce<FUSED>(wa, V, E, grad, param, m, v, aa, aa_dev, s);
 }
 
 int check_common(int64_t V, int E, const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld) {
@@ -830,7 +835,7 @@ extern "C" int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom
                                        int E, const void* plan, size_t plan_bytes, float* grad_table,
                                        tt_stream_t stream) {
   TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
-  TT_REQUIRE(grad_table && (nseq == 0 || (d_pooled && denom)), "null pointer");
+  TT_REQUIRE(grad_table && (nseq == 0 || d_pooled), "null pointer");  // denom NULL: d_pooled is gs
   AdamArgs aa{};
   return apply_impl<false>(d_pooled, denom, nseq, L, V, E, const_cast<void*>(plan), plan_bytes, grad_table, nullptr,
                            nullptr, nullptr, aa, nullptr, reinterpret_cast<hipStream_t>(stream));
@@ -842,7 +847,7 @@ extern "C" int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float*
                                              tt_stream_t stream) {
   TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
   TT_REQUIRE(table && exp_avg && exp_avg_sq && adam_args, "null pointer");
-  TT_REQUIRE(nseq == 0 || (d_pooled && denom), "null pointer");
+  TT_REQUIRE(nseq == 0 || d_pooled, "null pointer");  // denom NULL: d_pooled is gs already
   AdamArgs aa{};
   return apply_impl<true>(d_pooled, denom, nseq, L, V, E, const_cast<void*>(plan), plan_bytes, nullptr, table,
                           exp_avg, exp_avg_sq, aa, static_cast<const AdamArgs*>(adam_args),

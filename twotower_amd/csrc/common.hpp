@@ -33,6 +33,21 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// F.normalize backward (encoders.py:77, autograd of x / max(|x|, 1e-12)) of one H = 256 row held
+// as one float4 per lane: g = d(out), o = out, nrm = |x|.  Every fma spelled out, so the tower
+// head's own backward (l2norm_bwd_kernel) and the in-batch combine that fuses it
+// (bwd_combine_l2_kernel) produce the same bits.
+__device__ __forceinline__ f32x4 l2_bwd_row4(const f32x4& g, const f32x4& o, float nrm) {
+  const float den = fmaxf(nrm, 1e-12f);
+  const float dot = __builtin_fmaf(g[3], o[3], __builtin_fmaf(g[2], o[2], __builtin_fmaf(g[1], o[1], g[0] * o[0])));
+  const float sx4 = wave_sum(dot) * den;
+  const float coef4 = (nrm >= 1e-12f && nrm > 0.f) ? sx4 / ((den * den) * nrm) : 0.f;
+  f32x4 y;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) y[k] = __builtin_fmaf(-coef4, o[k] * den, g[k] / den);
+  return y;
+}
+
 template <typename IdT>
 __device__ __forceinline__ int64_t load_id(const IdT* p) { return (int64_t)(*p); }
 

@@ -34,7 +34,7 @@ constexpr int kSteps = kK / kKS;                    // 16
 constexpr int kWaves = 4;
 constexpr int kTileRows = 32;
 
-enum Epi { EPI_BIAS_RELU = 0, EPI_BIAS_L2 = 1, EPI_RELU_MASK = 2, EPI_PLAIN = 3 };
+enum Epi { EPI_BIAS_RELU = 0, EPI_BIAS_L2 = 1, EPI_RELU_MASK = 2, EPI_PLAIN = 3, EPI_ROWDIV = 5 };
 
 __device__ __forceinline__ void split3(float x, __bf16& a0, __bf16& a1, __bf16& a2) {
   a0 = (__bf16)x;
@@ -216,6 +216,14 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     unsigned mword = 0;
     if constexpr (EPI == EPI_RELU_MASK)  // issued before the tile's A refills: no flush to wait on it
       mword = relu_mask[mask_idx];
+    float rdiv[16];  // EPI_ROWDIV: the divisor of each of this lane's 16 rows (bias = per-row divisors)
+    if constexpr (EPI == EPI_ROWDIV) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t r = trow0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+        rdiv[v] = bias[r < rows ? r : rows - 1];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kSteps; ++j) {
       const int jn = (j + 1) % kSteps;
@@ -283,6 +291,7 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         }
         if constexpr (EPI == EPI_BIAS_L2) y += bv[ct];
         if constexpr (EPI == EPI_RELU_MASK) y = (mword >> (16 * ct + v)) & 1u ? y : 0.f;
+        if constexpr (EPI == EPI_ROWDIV) y = y / rdiv[v];  // IEEE division, as bag_scale_rows_kernel
         acc[ct][v] = y;
       }
     }
@@ -602,7 +611,8 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
   // epi 4: the Linear of epi 1 without its normalise pass (tt_inbatch_l2_prep normalises)
   const bool defer_l2 = epi == 4;
   if (defer_l2) epi = EPI_BIAS_L2;
-  TT_REQUIRE(epi >= EPI_BIAS_RELU && epi <= EPI_PLAIN, "epi=%d", epi);
+  TT_REQUIRE((epi >= EPI_BIAS_RELU && epi <= EPI_PLAIN) || epi == EPI_ROWDIV, "epi=%d", epi);
+  TT_REQUIRE(epi != EPI_ROWDIV || bias, "epilogue 5 needs the row divisors (bias)");
   TT_REQUIRE((epi != EPI_BIAS_RELU && epi != EPI_BIAS_L2) || bias, "epilogue needs bias");
   TT_REQUIRE(epi != EPI_RELU_MASK || relu_mask, "epilogue needs the ReLU mask of the forward");
   TT_REQUIRE(epi != EPI_BIAS_L2 || norms || defer_l2, "epilogue needs norms");
@@ -627,6 +637,9 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
       break;
     case EPI_RELU_MASK:
       head_gemm_kernel<EPI_RELU_MASK><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
+      break;
+    case EPI_ROWDIV:
+      head_gemm_kernel<EPI_ROWDIV><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
       break;
     default:
       head_gemm_kernel<EPI_PLAIN><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);

@@ -42,12 +42,7 @@ __global__ __launch_bounds__(kBlock) void l2norm_bwd_kernel(const float* __restr
   if (H == 4 * kWave) {  // one float4 per lane, both rows kept in registers
     const f32x4 g = reinterpret_cast<const f32x4*>(dout + r * H)[lane];
     const f32x4 o = reinterpret_cast<const f32x4*>(out + r * H)[lane];
-    const float sx4 = wave_sum(g[0] * o[0] + g[1] * o[1] + g[2] * o[2] + g[3] * o[3]) * den;
-    const float coef4 = (nrm >= 1e-12f && nrm > 0.f) ? sx4 / (den * den * nrm) : 0.f;
-    f32x4 y;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) y[k] = g[k] / den - coef4 * (o[k] * den);
-    reinterpret_cast<f32x4*>(dx + r * H)[lane] = y;
+    reinterpret_cast<f32x4*>(dx + r * H)[lane] = l2_bwd_row4(g, o, nrm);
     return;
   }
   // x = out * den; s_x = sum(dout * x)
@@ -428,6 +423,11 @@ int launch_mean(const float* x, int64_t n, float* out, hipStream_t s) {
   mean_kernel<<<dim3(1), dim3(1024), 0, s>>>(x, n, out);
   TT_LAUNCH_CHECK("mean");
   return TT_OK;
+}
+
+extern "C" int tt_mean(const float* x, int64_t n, float* out, tt_stream_t stream) {
+  TT_REQUIRE(out && (x || n == 0) && n >= 0, "bad mean arguments");
+  return launch_mean(x, n, out, reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // namespace tt

@@ -1715,6 +1715,66 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
   }
 }
 
+// bwd_combine_kernel fused with the tower head's F.normalize backward, for the fused TwoTower
+// output y = [q; d] (H = 256): row r < B takes dq_r, row B + j takes dd_j, each formed exactly as
+// bwd_combine_kernel forms it, and the row goes straight into l2_bwd_row4 (the arithmetic of
+// l2norm_bwd_kernel) with y_r and norms[r]: dx = d loss / d(pre-normalise row).  dq and dd are
+// never written; the result equals bwd_combine_kernel + l2norm_bwd_kernel bit for bit.
+template <typename DT>
+__global__ __launch_bounds__(256) void bwd_combine_l2_kernel(int64_t B, int64_t M, int S, int64_t label_off,
+                                                             const float* __restrict__ acc_part,
+                                                             const DT* __restrict__ Qmat, const float* __restrict__ dqu,
+                                                             const float* __restrict__ grad_loss, float grad_scale,
+                                                             float inv_tau, const float* __restrict__ y,
+                                                             const float* __restrict__ norms, float* __restrict__ dx,
+                                                             const int* __restrict__ xrows, const DT* __restrict__ Dmat,
+                                                             const float* __restrict__ lse2, float c2) {
+  constexpr int H = 4 * kWave;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B + M) return;
+  const int lane = lane_id();
+  const float scale = grad_loss[0] * grad_scale * inv_tau;
+  const f32x4 o = reinterpret_cast<const f32x4*>(y + r * H)[lane];  // issued first: independent of g
+  const float nrm = norms[r];
+  f32x4 g;
+  if (r < B) {
+    g = reinterpret_cast<const f32x4*>(dqu + r * H)[lane] * scale;
+  } else {
+    const int64_t j = r - B, qi = j - label_off;
+    f32x4 a = sum_parts4(reinterpret_cast<const f32x4*>(acc_part) + j * (H / 4) + lane, M * (H / 4), S);
+    if (xrows) add_exact_rows(a, xrows, B, Qmat, Dmat + j * H, lse2, c2, H, lane);
+    if (qi >= 0 && qi < B) a -= load4(Qmat + qi * H, lane);
+    g = a * scale;
+  }
+  reinterpret_cast<f32x4*>(dx + r * H)[lane] = l2_bwd_row4(g, o, nrm);
+}
+
+// Where the backward's combine goes: dq / dd (the loss gradients), or, with `dx` set, the fused
+// F.normalize backward above (y = [q; d] rows, norms of the tower head; H = 256, bf16 operands).
+struct BwdOut {
+  float* dq;
+  float* dd;
+  const float* y = nullptr;
+  const float* norms = nullptr;
+  float* dx = nullptr;
+};
+
+template <typename DT>
+void launch_bwd_combine(int64_t B, int64_t M, int H, int S, int64_t label_off, const float* acc_part, const DT* Qlab,
+                        const float* dqu, const float* grad_loss, float grad_scale, float inv_tau, const BwdOut& out,
+                        const int* xrows, const DT* Db, const float* lse2, hipStream_t s) {
+  const float c2 = inv_tau * kLog2e;
+  if (out.dx) {
+    bwd_combine_l2_kernel<DT><<<dim3((unsigned)((B + M + 3) / 4)), dim3(256), 0, s>>>(
+        B, M, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.y, out.norms, out.dx, xrows, Db,
+        lse2, c2);
+    return;
+  }
+  const int64_t rows = std::max(B, M);
+  bwd_combine_kernel<DT><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(
+      B, M, H, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.dq, out.dd, xrows, Db, lse2, c2);
+}
+
 // ------------------------------------------------------------------------------------------
 // Host side.
 struct Plan {
@@ -1939,7 +1999,7 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
                                                      static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu, Qs,
                                                      xrows);
   TT_LAUNCH_CHECK("score_fwd_combine");
-  return launch_mean(loss_rows, B, loss, s);
+  return loss ? launch_mean(loss_rows, B, loss, s) : TT_OK;
 }
 
 // Backward from prepared operands: Rm = queries (nQ rows + zero tail for bf16), lse2_R (nQ rows
@@ -1947,7 +2007,7 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
 // Qlab (j - label_off in [0, B)); dq = scale * dq_unscaled (B rows).
 int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const void* Cm, int64_t M, const void* Qlab,
              int64_t B, int64_t label_off, int H, float inv_tau, const float* dqu, const float* grad_loss,
-             float grad_scale, float* dq, float* dd, const char* pad, float* acc_part, hipStream_t s) {
+             float grad_scale, const BwdOut& out, const char* pad, float* acc_part, hipStream_t s) {
   const Plan p = plan_for(nQ, M, bj_for(dtype), wg_per_cu(H));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
@@ -1955,16 +2015,12 @@ int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const v
   w.acc_part = acc_part;
   int rc;
   if ((rc = dispatch_engine<DD>(H, dtype, Rm, nQ, Cm, M, p, c2, lse2_R, w, 0, s))) return rc;
-  const int64_t rows = std::max(B, M);
-  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   if (dtype == TT_F32)
-    bwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, acc_part,
-                                                    static_cast<const float*>(Qlab), dqu, grad_loss, grad_scale,
-                                                    inv_tau, dq, dd);
+    launch_bwd_combine<float>(B, M, H, p.S, label_off, acc_part, static_cast<const float*>(Qlab), dqu, grad_loss,
+                              grad_scale, inv_tau, out, nullptr, nullptr, nullptr, s);
   else
-    bwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, label_off, acc_part,
-                                                     static_cast<const __bf16*>(Qlab), dqu, grad_loss, grad_scale,
-                                                     inv_tau, dq, dd);
+    launch_bwd_combine<__bf16>(B, M, H, p.S, label_off, acc_part, static_cast<const __bf16*>(Qlab), dqu, grad_loss,
+                               grad_scale, inv_tau, out, nullptr, nullptr, nullptr, s);
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
@@ -1973,7 +2029,7 @@ int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const v
 // zero tail) and P, then the same combine (label terms from the unscaled q~).
 int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, const __bf16* Qs, const char* P,
                int64_t p_nqt, const __bf16* Qlab, const float* dqu, const float* grad_loss, float grad_scale,
-               float* dq, float* dd, float* acc_part, const int* xrows, const __bf16* Db, const float* lse2,
+               const BwdOut& out, float* acc_part, const int* xrows, const __bf16* Db, const float* lse2,
                hipStream_t s) {
   const Plan p = ddp_plan(B, M, H);
   switch (H) {
@@ -1990,10 +2046,8 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
   TT_LAUNCH_CHECK("score_ddp");
-  const int64_t rows = std::max(B, M);
-  bwd_combine_kernel<__bf16><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(
-      B, M, H, p.S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, dq, dd, xrows, Db, lse2,
-      inv_tau * kLog2e);
+  launch_bwd_combine<__bf16>(B, M, H, p.S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out, xrows,
+                             Db, lse2, s);
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
@@ -2056,7 +2110,7 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
                 void* ws, size_t ws_bytes, hipStream_t s, bool prepped) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
-  TT_REQUIRE(q && d && lse && loss_rows && loss && ws, "null pointer");
+  TT_REQUIRE(q && d && lse && loss_rows && ws, "null pointer");  // loss NULL: the caller forms the mean (tt_mean)
   TT_REQUIRE(!want_grad || dq_unscaled, "want_grad needs dq_unscaled");
   TT_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(d)) & 15) == 0, "q/d must be 16-byte aligned");
   TT_REQUIRE(!prepped || dtype != TT_F32, "prepared operands are bf16 copies (dtype bf16 / bf16_split)");
@@ -2112,23 +2166,47 @@ extern "C" int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B,
                      ws_bytes, reinterpret_cast<hipStream_t>(stream), true);
 }
 
+namespace tt {
+namespace {
+int inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                int64_t label_off, const float* dq_unscaled, const float* grad_loss, float grad_scale,
+                const BwdOut& out, void* ws, size_t ws_bytes, hipStream_t s) {
+  const Ws w = carve_user(ws, B, M, H, dtype);
+  TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
+  const bool bf = dtype != TT_F32;
+  // lse in log2 units (ws.lse2) and the pad rows were left in the workspace by the forward
+  const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
+  const void* Cm = bf ? (const void*)w.Db : (const void*)d;
+  if (w.P) return bwd_core_p(B, M, H, label_off, inv_tau, w.Qs, w.P, w.p_nqt, w.Qb, dq_unscaled, grad_loss, grad_scale,
+                             out, w.acc_part, w.xrows, w.Db, w.lse2, s);
+  return bwd_core(dtype, Rm, B, w.lse2, Cm, M, Rm, B, label_off, H, inv_tau, dq_unscaled, grad_loss, grad_scale, out,
+                  w.pad, w.acc_part, s);
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                                 int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
+                                 float grad_scale, const float* norms, float* dx, void* ws, size_t ws_bytes,
+                                 tt_stream_t stream) {
+  int rc = check_args(B, M, H, dtype, label_off);
+  if (rc) return rc;
+  TT_REQUIRE(H == 4 * kWave && dtype != TT_F32, "tt_inbatch_bwd_l2: H = 256 with bf16 operands only (H=%d dtype=%d)",
+             H, dtype);
+  TT_REQUIRE(qd && lse && dq_unscaled && grad_loss && norms && dx && ws, "null pointer");
+  BwdOut out{nullptr, nullptr, qd, norms, dx};
+  return inbatch_bwd(qd, qd + B * H, B, M, H, dtype, inv_tau, label_off, dq_unscaled, grad_loss, grad_scale, out, ws,
+                     ws_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
 extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
                               int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
                               float grad_scale, float* dq, float* dd, void* ws, size_t ws_bytes, tt_stream_t stream) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
   TT_REQUIRE(q && d && lse && dq_unscaled && grad_loss && dq && dd && ws, "null pointer");
-  const Ws w = carve_user(ws, B, M, H, dtype);
-  TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool bf = dtype != TT_F32;
-  // lse in log2 units (ws.lse2) and the pad rows were left in the workspace by the forward
-  const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
-  const void* Cm = bf ? (const void*)w.Db : (const void*)d;
-  if (w.P) return bwd_core_p(B, M, H, label_off, inv_tau, w.Qs, w.P, w.p_nqt, w.Qb, dq_unscaled, grad_loss, grad_scale,
-                             dq, dd, w.acc_part, w.xrows, w.Db, w.lse2, s);
-  return bwd_core(dtype, Rm, B, w.lse2, Cm, M, Rm, B, label_off, H, inv_tau, dq_unscaled, grad_loss, grad_scale, dq,
-                  dd, w.pad, w.acc_part, s);
+  return inbatch_bwd(q, d, B, M, H, dtype, inv_tau, label_off, dq_unscaled, grad_loss, grad_scale, BwdOut{dq, dd}, ws,
+                     ws_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
 // ---- explicit operands (data parallel with candidate-owner gradients; see twotower_amd.h)
@@ -2258,7 +2336,7 @@ extern "C" int tt_inbatch_bwd_ex(const void* Qb_all, const float* lse2_all, int6
   const ExWs w = carve_ex(ws, 1, 1, nQ_all, M, H, dtype);
   const void* Qlab = static_cast<const __bf16*>(Qb_all) + q_row0 * H;
   return bwd_core(dtype, Qb_all, nQ_all, lse2_all, Db, M, Qlab, B, label_off, H, inv_tau, dq_unscaled, grad_loss,
-                  grad_scale, dq, dd, nullptr, w.acc_part, reinterpret_cast<hipStream_t>(stream));
+                  grad_scale, BwdOut{dq, dd}, nullptr, w.acc_part, reinterpret_cast<hipStream_t>(stream));
 }
 
 #ifdef TT_SCORER_TRACE

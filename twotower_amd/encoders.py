@@ -38,6 +38,15 @@ def _table_of(embedding: nn.Module) -> torch.Tensor | None:
     return inner.weight if isinstance(inner, nn.Embedding) else None
 
 
+def _sole_head(tower: nn.Module, pooled: torch.Tensor):
+    """The pooled rows go to this tower's own fused head and nowhere else (MeanPoolingTower's
+    encode_pooled, not overridden): its backward may then hand the bag backward d_pooled / denom
+    (ops.bag_head_prescale)."""
+    if type(tower).encode_pooled is MeanPoolingTower.encode_pooled:
+        return ops.bag_head_prescale(pooled)
+    return contextlib.nullcontext()
+
+
 class BaseTower(nn.Module):
     """Base class for tower/encoder architectures (encoders.py:12-22)."""
 
@@ -54,7 +63,9 @@ class BaseTower(nn.Module):
         raise NotImplementedError
 
     def forward(self, input_ids: torch.Tensor) -> torch.Tensor:
-        return self.encode_pooled(pool_mean(self.embedding, input_ids))
+        pooled = pool_mean(self.embedding, input_ids)
+        with _sole_head(self, pooled):
+            return self.encode_pooled(pooled)
 
 
 class MeanPoolingTower(BaseTower):
@@ -169,7 +180,8 @@ class TwoTower(nn.Module):
         nq = sizes[0]
         if self.query_tower is self.document_tower:
             prep = ops.scorer_prep(nq, self.scorer_prep) if self.scorer_prep else contextlib.nullcontext()
-            with prep:  # one head over all rows: its normalise pass may also prep the in-batch scorer
+            with prep, _sole_head(self.query_tower, pooled):
+                # one head over all rows: its normalise pass may also prep the in-batch scorer
                 return list(torch.split(self.query_tower.encode_pooled(pooled), sizes, dim=0))
         q = self.query_tower.encode_pooled(pooled[:nq])
         docs = self.document_tower.encode_pooled(pooled[nq:])

@@ -121,6 +121,34 @@ class BagPlan:
         self.buf.record_stream(cur)  # allocated on the side stream, read here
 
 
+class _BagGradToken:
+    """Shared by a BagMeanPool node and the TowerHead that is the sole consumer of its output:
+    the head's dx GEMM divides each row by its bag denominator in its epilogue (tt_head_gemm epi
+    5) and leaves the result here, so the bag backward skips its scaling pass."""
+
+    __slots__ = ("denom", "grad")
+
+    def __init__(self, denom: torch.Tensor):
+        self.denom, self.grad = denom, None
+
+
+_SOLE_HEAD: list = []  # pooled tensors whose only consumer is the TowerHead about to run
+
+
+@contextlib.contextmanager
+def bag_head_prescale(pooled: torch.Tensor):
+    """While open, a TowerHead applied to ``pooled`` (the output of bag_mean_pool, consumed by
+    nothing else: the encoders' own forward paths open it) forms the bag backward's
+    d_pooled / denom in its dx epilogue.  TT_BAG_PRESCALE=0 turns it off."""
+    tok = getattr(pooled, "_tt_bag_token", None)
+    on = tok is not None and os.environ.get("TT_BAG_PRESCALE", "0") != "0"
+    _SOLE_HEAD.append(pooled if on else None)
+    try:
+        yield
+    finally:
+        _SOLE_HEAD.pop()
+
+
 def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan: BagPlan,
                               out: torch.Tensor | None = None) -> torch.Tensor:
     """Dense (V, E) table gradient from a BagPlan (every row written), into `out` if given."""
@@ -165,6 +193,9 @@ class BagMeanPool(torch.autograd.Function):
             group = deferred.gather_group if deferred is not None else None
             ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
         ctx.save_for_backward(ids, denom)
+        ctx.token = None
+        if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
+            ctx.token = pooled._tt_bag_token = _BagGradToken(denom)
         ctx.V = weight.shape[0]
         ctx.padding_idx = padding_idx
         ctx.scatter_mode = scatter_mode
@@ -176,6 +207,13 @@ class BagMeanPool(torch.autograd.Function):
         ids, denom = ctx.saved_tensors
         weight = ctx.weight_ref
         plan, ctx.plan = ctx.plan, None
+        tok, ctx.token = ctx.token, None
+        if tok is not None and tok.grad is not None:
+            # the sole consuming head already divided each row by its denominator
+            if tok.grad.data_ptr() != d_pooled.data_ptr() or tok.grad.shape != d_pooled.shape:
+                raise RuntimeError("bag output pre-scaled by its head was combined with another gradient")
+            tok.grad = None
+            denom = None
         if not ctx.needs_input_grad[0]:
             return None, None, None, None, None
         deferred = getattr(weight, "_tt_deferred", None)
@@ -185,6 +223,8 @@ class BagMeanPool(torch.autograd.Function):
             return None, None, None, None, None
         if plan is not None:
             return bag_mean_backward_planned(d_pooled, denom, plan), None, None, None, None
+        if denom is None:  # (no plan: an unplanned backward divides again; never taken by the head path)
+            raise RuntimeError("pre-scaled bag gradient without a plan")
         grad = bag_mean_backward(d_pooled, denom, ids, ctx.V, ctx.padding_idx, ctx.scatter_mode)
         return grad, None, None, None, None
 
@@ -346,6 +386,33 @@ def scorer_prep(nq: int, compute_dtype: str):
         _SCORER_PREP.pop()
 
 
+class _L2Token:
+    """Shared by a TowerHead whose output went to an in-batch loss under scorer_prep and that
+    loss: under ``fused_head_backward`` the loss's backward applies the head's F.normalize
+    backward in its combine (tt_inbatch_bwd_l2) and leaves dy here for the head."""
+
+    __slots__ = ("norms", "dy")
+
+    def __init__(self, norms: torch.Tensor):
+        self.norms, self.dy = norms, None
+
+
+_FUSED_HEAD_BWD = [0]  # > 0 while the caller runs a backward in which the head output feeds only the loss
+
+
+@contextlib.contextmanager
+def fused_head_backward():
+    """Opened by train_step.TrainStep around its loss.backward(): the tower head's outputs reach
+    the in-batch loss and nothing else, so the loss may hand the head the gradient after
+    F.normalize (TT_FUSED_L2_BWD=0 turns it off)."""
+    on = os.environ.get("TT_FUSED_L2_BWD", "1") != "0"
+    _FUSED_HEAD_BWD[0] += on
+    try:
+        yield
+    finally:
+        _FUSED_HEAD_BWD[0] -= on
+
+
 class TowerHead(torch.autograd.Function):
     """F.normalize(Linear-ReLU-Linear(x)) for E = H = 256 (encoders.py:38-42,77) on the split-bf16
     MFMA GEMMs with fused epilogues: bias + ReLU (+ the ReLU bitmask), bias + row L2 normalise
@@ -355,6 +422,7 @@ class TowerHead(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2):
         require_gpu(x, W1, W2)
+        ctx.bag_token = x._tt_bag_token if _SOLE_HEAD and _SOLE_HEAD[-1] is x else None
         x = _contig_f32(x, "x")
         rows = x.shape[0]
         nb = _lib.lib().tt_head_planes_bytes(HEAD_WIDTH, HEAD_WIDTH)
@@ -371,9 +439,12 @@ class TowerHead(torch.autograd.Function):
                              device=x.device)
             call("tt_inbatch_l2_prep", ptr(out), nq, rows - nq, HEAD_WIDTH, dt, ptr(norm), ptr(ws), ws.numel(),
                  stream_of(x))
-            out._tt_inbatch_prep = (nq, rows - nq, dt, ws)
+            ctx.l2_token = _L2Token(norm)
+            out._tt_inbatch_prep = (nq, rows - nq, dt, ws, ctx.l2_token)
         else:
             out = _head_gemm(h, planes[nb:2 * nb], 1, bias=b2, norms=norm)
+        if req is None or not 0 < req[0] < rows:
+            ctx.l2_token = None
         ctx.save_for_backward(x, h, mask, out, norm, planes)
         sides = {id(getattr(w, "_tt_side_grads", None)) for w in (W1, b1, W2, b2)}
         ctx.side_grads = W1._tt_side_grads if len(sides) == 1 and hasattr(W1, "_tt_side_grads") else None
@@ -387,11 +458,24 @@ class TowerHead(torch.autograd.Function):
     def backward(ctx, dout):
         x, h, mask, out, norm, planes = ctx.saved_tensors
         nb = planes.numel() // 4
-        dout = _contig_f32(dout, "dout")
-        dy = torch.empty_like(out)
-        call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy), stream_of(out))
+        tok, ctx.l2_token = ctx.l2_token, None
+        if tok is not None and tok.dy is not None:  # the loss applied F.normalize's backward (tt_inbatch_bwd_l2)
+            if tok.dy.data_ptr() != dout.data_ptr() or tok.dy.shape != dout.shape:
+                raise RuntimeError("tower head output fed the fused in-batch loss and another consumer")
+            dy, tok.dy = tok.dy, None
+        else:
+            dout = _contig_f32(dout, "dout")
+            dy = torch.empty_like(out)
+            call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy),
+                 stream_of(out))
         dh = _head_gemm(dy, planes[3 * nb:], 2, mask=mask)
-        dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3) if ctx.needs_input_grad[0] else None
+        tok, ctx.bag_token = ctx.bag_token, None
+        dx = None
+        if ctx.needs_input_grad[0] and tok is not None:  # dx / denom for the bag backward (epi 5)
+            dx = _head_gemm(dh, planes[2 * nb:3 * nb], 5, bias=tok.denom)
+            tok.grad = dx
+        elif ctx.needs_input_grad[0]:
+            dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3)
         side = ctx.side_grads
         N = out.shape[1]
         dW1, dW2 = (torch.empty(N, N, dtype=_FLOAT, device=dy.device) for _ in range(2))
@@ -538,6 +622,40 @@ def get_inbatch_backward() -> str:
     return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
 
 
+_DEFER_MEAN: list = []  # open defer_loss_mean() scopes: lists of (loss_rows, loss, event) to reduce later
+
+
+@contextlib.contextmanager
+def defer_loss_mean():
+    """Opened by train_step.TrainStep around its forward: the in-batch loss leaves its mean (a
+    one-workgroup kernel no later kernel reads) for ``flush_loss_means``, which the step calls
+    after queueing the optimizer, so the forward combine hands straight to the backward.
+    TT_DEFER_MEAN=0 turns it off."""
+    pend: list = []
+    _DEFER_MEAN.append(pend if os.environ.get("TT_DEFER_MEAN", "0") != "0" else None)
+    try:
+        yield pend
+    finally:
+        _DEFER_MEAN.pop()
+        flush_loss_means(pend)
+
+
+def flush_loss_means(pend: list) -> None:
+    """Form the deferred loss means on a side stream (each after its forward's rows are written)
+    and make the current stream wait for them."""
+    if not pend:
+        return
+    cur = torch.cuda.current_stream(pend[0][0].device)
+    side = _lib.side_stream(pend[0][0].device, "loss")
+    for rows, loss, ev in pend:
+        side.wait_event(ev)
+        rows.record_stream(side)
+        loss.record_stream(side)
+        call("tt_mean", ptr(rows), rows.numel(), ptr(loss), side.cuda_stream)
+    pend.clear()
+    cur.wait_stream(side)
+
+
 def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad, prep=None):
     B, H = q.shape
     M = d.shape[0]
@@ -555,8 +673,13 @@ def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_
     rows = torch.empty(B, dtype=_FLOAT, device=dev)
     loss = torch.empty((), dtype=_FLOAT, device=dev)
     dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
+    pend = _DEFER_MEAN[-1] if _DEFER_MEAN else None
     call(entry, ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
-         ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
+         ptr(lse), ptr(rows), ptr(loss) if pend is None else None, ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
+    if pend is not None:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(q.device))
+        pend.append((rows, loss, ev))
     ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off), float(1.0 / B) if grad_scale is None else float(grad_scale))
     return loss, lse, dqu, ws
 
@@ -598,7 +721,9 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         qd = _contig_f32(qd, "qd")
         q, d = qd[:nq], qd[nq:]
         want_grad = bool(ctx.needs_input_grad[0])
-        loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad, prep)
+        ctx.l2_token = prep[4] if prep is not None else None
+        loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad,
+                                          prep[:4] if prep is not None else None)
         if want_grad:
             ctx.save_for_backward(qd, lse, dqu, ws)
         ctx.nq = nq
@@ -609,6 +734,15 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         qd, lse, dqu, ws = ctx.saved_tensors
         grad = torch.empty_like(qd)
         nq = ctx.nq
+        tok, ctx.l2_token = ctx.l2_token, None
+        B, M, H, dt, inv_tau, label_off, grad_scale = ctx.meta
+        if tok is not None and _FUSED_HEAD_BWD[0] > 0 and H == HEAD_WIDTH and dt != _lib.TT_F32:
+            # the head's F.normalize backward in the combine: grad is the head's dy (see _L2Token)
+            gs = g.to(_FLOAT).contiguous().reshape(1)
+            call("tt_inbatch_bwd_l2", ptr(qd), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(gs),
+                 grad_scale, ptr(tok.norms), ptr(grad), ptr(ws), ws.numel(), stream_of(qd))
+            tok.dy = grad
+            return grad, None, None, None, None
         _inbatch_bwd(ctx.meta, qd[:nq], qd[nq:], lse, dqu, ws, g, grad[:nq], grad[nq:])
         return grad, None, None, None, None
 

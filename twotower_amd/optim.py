@@ -236,9 +236,11 @@ def _gather_parts(parts, group):
     ids, dp, den, plan = parts
     world = torch.distributed.get_world_size(group)
     dp_all = dp.new_empty((world * dp.shape[0],) + tuple(dp.shape[1:]))
-    den_all = den.new_empty((world * den.shape[0],))
     distributed.all_gather_rows(dp_all, dp.contiguous(), group)
-    distributed.all_gather_rows(den_all, den.contiguous(), group)
+    den_all = None  # None: d_pooled arrived divided by its denominators (ops.bag_head_prescale)
+    if den is not None:
+        den_all = den.new_empty((world * den.shape[0],))
+        distributed.all_gather_rows(den_all, den.contiguous(), group)
     if plan is None or plan.nseq != dp_all.shape[0]:
         raise RuntimeError("replicated table sync needs the all-ranks plan built in the forward")
     return plan.ids, dp_all, den_all, plan
@@ -262,6 +264,10 @@ def _merge_parts(parts, table: torch.Tensor, padding_idx):
         return ids, dp, den, plan
     L = max(p[0].shape[1] for p in parts)
     ids = torch.cat([F.pad(p[0].to(torch.int64), (0, L - p[0].shape[1])) for p in parts], 0)
-    dp = torch.cat([p[1] for p in parts], 0)
-    den = torch.cat([p[2] for p in parts], 0)
+    if any(p[2] is None for p in parts):  # some parts arrived pre-divided: divide the others here
+        dp = torch.cat([p[1] if p[2] is None else p[1] / p[2].unsqueeze(1) for p in parts], 0)
+        den = None
+    else:
+        dp = torch.cat([p[1] for p in parts], 0)
+        den = torch.cat([p[2] for p in parts], 0)
     return ids, dp, den, ops.BagPlan(ids, table.shape[0], table.shape[1], padding_idx, gather_group=group)

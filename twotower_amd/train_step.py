@@ -54,6 +54,8 @@ class TrainStep:
         if side is not None:
             side.join()
             side.active = True
+        means = ops.defer_loss_mean()  # the loss mean leaves the forward -> backward hand-off
+        pend = means.__enter__()
         try:
             q, p, n = self.model(queries, positive_docs, negative_docs)
             loss = self.loss_fn(q, p, n)
@@ -64,12 +66,15 @@ class TrainStep:
             if seed is None:
                 scale = self.sync.loss_scale() if self.sync is not None else 1.0
                 seed = self._seed[loss.device] = torch.full((), scale, dtype=loss.dtype, device=loss.device)
-            with ops.uniform_loss_seed():  # every rank seeds its loss alike (1/world)
+            # every rank seeds its loss alike (1/world); the heads' outputs reach only the loss
+            with ops.uniform_loss_seed(), ops.fused_head_backward():
                 loss.backward(seed)
             if self.sync is not None and not self._sync_in_step:
                 self.sync.sync()
             self.optimizer.step()
+            ops.flush_loss_means(pend)  # on a side stream beside the table update; joined here
         finally:
+            means.__exit__(None, None, None)
             if side is not None:
                 side.active = False
                 side.join()  # no-op after the optimizer's own join
