@@ -190,43 +190,3 @@ def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dty
         assert torch.equal(a, b)
     for k in want:
         assert torch.equal(got[k], want[k]), k
-
-
-@pytest.mark.parametrize("graph", [False, True])
-def test_trainstep_deferred_loss_mean_equals_inline(graph, monkeypatch):
-    """TrainStep leaves the in-batch loss mean to a side-stream tt_mean after the optimizer is
-    queued: the returned losses and the parameters equal the inline mean (TT_DEFER_MEAN=0)."""
-    V, B, L = 3000, 256, 16
-    rng = np.random.default_rng(13)
-    batches = [[_ids(B, L, V, rng) for _ in range(3)] for _ in range(4)]
-
-    def run():
-        torch.manual_seed(6)
-        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
-        model = tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
-        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
-        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16"), opt,
-                            graph=graph, eager_steps=1)
-        losses = [step(*b).clone() for b in batches]
-        torch.cuda.synchronize()
-        return losses, {k: v.detach().clone() for k, v in model.named_parameters()}
-
-    seen = []
-    real_call = ops.call
-
-    def spy(name, *args):
-        seen.append(name)
-        return real_call(name, *args)
-
-    monkeypatch.setattr(ops, "call", spy)
-    monkeypatch.setenv("TT_DEFER_MEAN", "1")
-    got_l, got = run()
-    assert "tt_mean" in seen
-    monkeypatch.setenv("TT_DEFER_MEAN", "0")
-    seen.clear()
-    want_l, want = run()
-    assert "tt_mean" not in seen
-    for a, b in zip(got_l, want_l):
-        assert torch.equal(a, b) and torch.isfinite(a)
-    for k in want:
-        assert torch.equal(got[k], want[k]), k

@@ -125,9 +125,7 @@ def side_stream(device: torch.device, role: str = "plan") -> torch.cuda.Stream:
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), role)
     st = _SIDE.get(key)
     if st is None:
-        # TT_SIDE_PRIO=role[,role]: those side streams at high priority (measurement switch)
-        hi = role in os.environ.get("TT_SIDE_PRIO", "").split(",")
-        st = _SIDE[key] = torch.cuda.Stream(device=key[0], priority=-1 if hi else 0)
+        st = _SIDE[key] = torch.cuda.Stream(device=key[0])
     return st
 
 

@@ -468,6 +468,29 @@ class TowerHead(torch.autograd.Function):
             dy = torch.empty_like(out)
             call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy),
                  stream_of(out))
+        side = ctx.side_grads
+        N = out.shape[1]
+        dW1, dW2 = (torch.empty(N, N, dtype=_FLOAT, device=dy.device) for _ in range(2))
+        db1, db2 = (torch.empty(N, dtype=_FLOAT, device=dy.device) for _ in range(2))
+        # The optimizer joins these (optim.AdamW), so the weight gradients may run on a side stream
+        # beside what follows on this one: dx feeds the fused table scatter + AdamW, an
+        # HBM-bound pass the MFMA-bound weight-gradient kernels overlap.  Autograd must hand the
+        # returned buffers to .grad as they are (checked at the join): no extra references.
+        on_side = not (side is None or not side.active or not all(ctx.needs_input_grad[1:5])
+                       or not side.single_use(ctx.params)
+                       or any(p.grad is not None for p in ctx.params))  # (an existing .grad accumulates now)
+        main = torch.cuda.current_stream(dy.device)
+        aux = _lib.side_stream(dy.device, "wgrad") if on_side else None
+
+        def wgrad_aside(G, X, dW, db):
+            aux.wait_stream(main)
+            # cross-stream lifetimes (also during capture, where the allocator then defers the
+            # blocks' reuse to the end of the capture instead of handing them to a later node)
+            for t in (G, X, dW, db):
+                t.record_stream(aux)
+            with torch.cuda.stream(aux):
+                head_wgrad(G, X, dW, db)
+
         dh = _head_gemm(dy, planes[3 * nb:], 2, mask=mask)
         tok, ctx.bag_token = ctx.bag_token, None
         dx = None
@@ -476,29 +499,14 @@ class TowerHead(torch.autograd.Function):
             tok.grad = dx
         elif ctx.needs_input_grad[0]:
             dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3)
-        side = ctx.side_grads
-        N = out.shape[1]
-        dW1, dW2 = (torch.empty(N, N, dtype=_FLOAT, device=dy.device) for _ in range(2))
-        db1, db2 = (torch.empty(N, dtype=_FLOAT, device=dy.device) for _ in range(2))
-        if (side is None or not side.active or not all(ctx.needs_input_grad[1:5]) or not side.single_use(ctx.params)
-                or any(p.grad is not None for p in ctx.params)):  # (an existing .grad accumulates now)
+        if not on_side:
             head_wgrad(dh, x, dW1, db1)
             head_wgrad(dy, h, dW2, db2)
             return dx, dW1, db1, dW2, db2
-        # The optimizer joins these (optim.AdamW), so the weight gradients run on a side stream
-        # beside what follows on this one: dx feeds the fused table scatter + AdamW, an
-        # HBM-bound pass the MFMA-bound weight-gradient kernels overlap.  Autograd must hand the
-        # returned buffers to .grad as they are (checked at the join): no extra references.
-        main = torch.cuda.current_stream(dy.device)
-        aux = _lib.side_stream(dy.device, "wgrad")
-        aux.wait_stream(main)
-        # cross-stream lifetimes (also during capture, where the allocator then defers the
-        # blocks' reuse to the end of the capture instead of handing them to a later node)
-        for t in (dh, dy, x, h, dW1, db1, dW2, db2):
-            t.record_stream(aux)
-        with torch.cuda.stream(aux):
-            head_wgrad(dh, x, dW1, db1)
-            head_wgrad(dy, h, dW2, db2)
+        # both forked after the dx GEMM: forked earlier (dW2 beside the dh GEMM, dW1 beside the dx
+        # GEMM) they time-share the CUs with those GEMMs and the step took 20 us longer
+        wgrad_aside(dh, x, dW1, db1)
+        wgrad_aside(dy, h, dW2, db2)
         done = torch.cuda.Event()
         done.record(aux)
         side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)))
@@ -622,40 +630,6 @@ def get_inbatch_backward() -> str:
     return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
 
 
-_DEFER_MEAN: list = []  # open defer_loss_mean() scopes: lists of (loss_rows, loss, event) to reduce later
-
-
-@contextlib.contextmanager
-def defer_loss_mean():
-    """Opened by train_step.TrainStep around its forward: the in-batch loss leaves its mean (a
-    one-workgroup kernel no later kernel reads) for ``flush_loss_means``, which the step calls
-    after queueing the optimizer, so the forward combine hands straight to the backward.
-    TT_DEFER_MEAN=0 turns it off."""
-    pend: list = []
-    _DEFER_MEAN.append(pend if os.environ.get("TT_DEFER_MEAN", "0") != "0" else None)
-    try:
-        yield pend
-    finally:
-        _DEFER_MEAN.pop()
-        flush_loss_means(pend)
-
-
-def flush_loss_means(pend: list) -> None:
-    """Form the deferred loss means on a side stream (each after its forward's rows are written)
-    and make the current stream wait for them."""
-    if not pend:
-        return
-    cur = torch.cuda.current_stream(pend[0][0].device)
-    side = _lib.side_stream(pend[0][0].device, "loss")
-    for rows, loss, ev in pend:
-        side.wait_event(ev)
-        rows.record_stream(side)
-        loss.record_stream(side)
-        call("tt_mean", ptr(rows), rows.numel(), ptr(loss), side.cuda_stream)
-    pend.clear()
-    cur.wait_stream(side)
-
-
 def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad, prep=None):
     B, H = q.shape
     M = d.shape[0]
@@ -673,13 +647,8 @@ def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_
     rows = torch.empty(B, dtype=_FLOAT, device=dev)
     loss = torch.empty((), dtype=_FLOAT, device=dev)
     dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
-    pend = _DEFER_MEAN[-1] if _DEFER_MEAN else None
     call(entry, ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
-         ptr(lse), ptr(rows), ptr(loss) if pend is None else None, ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
-    if pend is not None:
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(q.device))
-        pend.append((rows, loss, ev))
+         ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
     ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off), float(1.0 / B) if grad_scale is None else float(grad_scale))
     return loss, lse, dqu, ws
 

@@ -54,8 +54,6 @@ class TrainStep:
         if side is not None:
             side.join()
             side.active = True
-        means = ops.defer_loss_mean()  # the loss mean leaves the forward -> backward hand-off
-        pend = means.__enter__()
         try:
             q, p, n = self.model(queries, positive_docs, negative_docs)
             loss = self.loss_fn(q, p, n)
@@ -72,9 +70,7 @@ class TrainStep:
             if self.sync is not None and not self._sync_in_step:
                 self.sync.sync()
             self.optimizer.step()
-            ops.flush_loss_means(pend)  # on a side stream beside the table update; joined here
         finally:
-            means.__exit__(None, None, None)
             if side is not None:
                 side.active = False
                 side.join()  # no-op after the optimizer's own join
