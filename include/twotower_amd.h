@@ -128,6 +128,12 @@ typedef struct {
 } tt_adamw_tensor;
 int tt_adam_prepare(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
                     double eps, double weight_decay, tt_stream_t stream);
+/* tt_adam_prepare_ex: step += increment (0 or 1), then the scalars of step + ahead (0 or 1).
+ * tt_adam_prepare is (1, 0).  (1, 1) after a step's updates forms the NEXT step's scalars while
+ * advancing the counter, so that step's updates need no prepare launch in front of them;
+ * (0, 1) forms them for counters nobody prepared ahead (first step, new hyper-parameters). */
+int tt_adam_prepare_ex(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
+                       double eps, double weight_decay, int increment, int ahead, tt_stream_t stream);
 int tt_adamw_multi(const tt_adamw_tensor* tensors, int count, tt_stream_t stream);
 
 /* ---- mean of n floats (the loss reductions' F.cross_entropy / .mean(), losses.py:44,85,116):

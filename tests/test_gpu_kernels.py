@@ -646,6 +646,65 @@ def test_adamw_multi_matches_host_adamw():
     assert ob.state[b[0]]["step"].device.type == "cuda" and ob.state[b[0]]["step"].item() == 4.0
 
 
+def test_adamw_scalars_ahead_follow_lr_changes_and_state_loads():
+    """Capturable AdamW forms each step's scalars at the previous step's tail (tt_adam_prepare_ex
+    increment 1, ahead 1): an lr changed between steps, a parameter skipped for a step and a
+    state_dict loaded mid-run still give torch's AdamW trajectory and step counters."""
+    rng = np.random.default_rng(23)
+    shapes = [(64, 32), (32,), (5, 7)]
+    params = [cuda(rng.standard_normal(s).astype(np.float32)) for s in shapes]
+    grads = [[cuda(rng.standard_normal(s).astype(np.float32)) for s in shapes] for _ in range(7)]
+    ours = [torch.nn.Parameter(p.clone()) for p in params]
+    ref = [torch.nn.Parameter(p.clone()) for p in params]
+    oo = tt.optim.AdamW(ours, lr=2e-3, weight_decay=0.05, capturable=True)
+    orf = torch.optim.AdamW(ref, lr=2e-3, weight_decay=0.05)
+    for k in range(7):
+        if k == 3:  # lr schedule step
+            for o in (oo, orf):
+                o.param_groups[0]["lr"] = 5e-4
+        if k == 5:  # round trip through a state_dict (fresh optimizer, loaded state)
+            sd = oo.state_dict()
+            oo = tt.optim.AdamW(ours, lr=5e-4, weight_decay=0.05, capturable=True)
+            oo.load_state_dict(sd)
+        for i, (a, b) in enumerate(zip(ours, ref)):
+            skip = k == 4 and i == 1  # no gradient for this parameter this step
+            a.grad = None if skip else grads[k][i].clone()
+            b.grad = None if skip else grads[k][i].clone()
+        oo.step()
+        orf.step()
+    for a, b in zip(ours, ref):
+        assert rel(a, b) < 1e-6
+        assert oo.state[a]["step"].item() == float(orf.state[b]["step"])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainstep_adam_scalars_ahead_equal_in_front(graph, monkeypatch):
+    """TrainStep with the scalars formed a step ahead (default) equals the prepare-in-front order
+    (TT_ADAM_AHEAD=0) bit for bit, eager and graph-replayed."""
+    V, E, B, L = 4000, 256, 128, 16
+
+    def run():
+        torch.manual_seed(12)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16"), opt,
+                            graph=graph, eager_steps=2)
+        losses = [step(*tt.data.synthetic_triplets(B, L, V, seed=90 + k, device=DEV)).clone() for k in range(5)]
+        torch.cuda.synchronize()
+        return losses, [p.detach().clone() for p in model.parameters()], [opt.state[p]["step"].item()
+                                                                          for p in model.parameters()]
+
+    got = run()
+    monkeypatch.setenv("TT_ADAM_AHEAD", "0")
+    want = run()
+    for a, b in zip(got[0], want[0]):
+        assert torch.equal(a, b)
+    for a, b in zip(got[1], want[1]):
+        assert torch.equal(a, b)
+    assert got[2] == want[2] == [5.0] * len(got[2])
+
+
 @pytest.mark.parametrize("loss_name", ["in_batch", "triplet"])
 def test_graph_step_equals_eager(loss_name):
     """The graph-replayed step computes exactly what the eager step computes."""

@@ -58,6 +58,8 @@ _SIGNATURES = {
     "tt_bag_mean_bwd_adamw_planned": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _vp, _vp, _vp,
                                                _vp, _vp]),
     "tt_adam_prepare": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _vp]),
+    "tt_adam_prepare_ex": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64,
+                                    _c_int, _c_int, _vp]),
     "tt_adamw_multi": (_c_int, [ctypes.POINTER(AdamwTensor), _c_int, _vp]),
     "tt_cosine_scores": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),

@@ -84,13 +84,14 @@ struct PrepArgs {
 };
 
 __global__ void adam_prepare_kernel(PrepArgs pa, int count, double lr, double beta1, double beta2, double eps,
-                                    double wd) {
+                                    double wd, float inc, float ahead) {
   const int i = threadIdx.x;
   if (i >= count) return;
-  const float step = *pa.s[i].step + 1.0f;
-  *pa.s[i].step = step;
-  const double bc1 = 1.0 - pow(beta1, (double)step);
-  const double bc2 = 1.0 - pow(beta2, (double)step);
+  const float step = *pa.s[i].step + inc;
+  if (inc != 0.f) *pa.s[i].step = step;
+  const float at = step + ahead;  // the step whose scalars are formed
+  const double bc1 = 1.0 - pow(beta1, (double)at);
+  const double bc2 = 1.0 - pow(beta2, (double)at);
   AdamArgs a;
   a.wd_factor = (float)(1.0 - lr * wd);
   a.one_m_b1 = (float)(1.0 - beta1);
@@ -111,6 +112,13 @@ using namespace tt;
 
 extern "C" int tt_adam_prepare(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
                                double eps, double weight_decay, tt_stream_t stream) {
+  return tt_adam_prepare_ex(slots, count, lr, beta1, beta2, eps, weight_decay, 1, 0, stream);
+}
+
+extern "C" int tt_adam_prepare_ex(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
+                                  double eps, double weight_decay, int increment, int ahead, tt_stream_t stream) {
+  TT_REQUIRE(increment == 0 || increment == 1, "increment=%d", increment);
+  TT_REQUIRE(ahead == 0 || ahead == 1, "ahead=%d", ahead);
   TT_REQUIRE(count >= 0 && count <= TT_ADAM_MAX_TENSORS, "count=%d (max %d)", count, TT_ADAM_MAX_TENSORS);
   if (count == 0) return TT_OK;
   TT_REQUIRE(slots != nullptr, "null slots");
@@ -120,8 +128,8 @@ extern "C" int tt_adam_prepare(const tt_adam_slot* slots, int count, double lr, 
     TT_REQUIRE((reinterpret_cast<uintptr_t>(slots[i].args) & 3) == 0, "args of slot %d misaligned", i);
     pa.s[i] = slots[i];
   }
-  adam_prepare_kernel<<<dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream)>>>(pa, count, lr, beta1, beta2,
-                                                                                      eps, weight_decay);
+  adam_prepare_kernel<<<dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      pa, count, lr, beta1, beta2, eps, weight_decay, (float)increment, (float)ahead);
   TT_LAUNCH_CHECK("tt_adam_prepare");
   return TT_OK;
 }

@@ -874,15 +874,17 @@ def adamw_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, e
 
 
 def adam_prepare(slots: list[tuple[torch.Tensor, torch.Tensor]], *, lr: float, beta1: float, beta2: float, eps: float,
-                 weight_decay: float) -> None:
-    """Device step += 1 and per-step scalars for each (step, args) pair (tt_adam_prepare)."""
+                 weight_decay: float, increment: int = 1, ahead: int = 0) -> None:
+    """Device step += increment and the scalars of step + ahead for each (step, args) pair
+    (tt_adam_prepare_ex; the defaults are tt_adam_prepare)."""
     if not slots:
         return
     stream = stream_of(slots[0][0])
     for i in range(0, len(slots), _lib.TT_ADAM_MAX_TENSORS):
         chunk = slots[i:i + _lib.TT_ADAM_MAX_TENSORS]
         arr = (_lib.AdamSlot * len(chunk))(*[_lib.AdamSlot(ptr(st), ptr(a)) for st, a in chunk])
-        call("tt_adam_prepare", arr, len(chunk), lr, beta1, beta2, eps, weight_decay, stream)
+        call("tt_adam_prepare_ex", arr, len(chunk), lr, beta1, beta2, eps, weight_decay, int(increment), int(ahead),
+             stream)
 
 
 def adamw_multi(items: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]]) -> None:

@@ -17,6 +17,7 @@ training step can be captured in a HIP graph and replayed (train_step.TrainStep(
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -37,6 +38,9 @@ class AdamW(torch.optim.Optimizer):
         self._grad_sync = None  # distributed.GradSync set by train_step.TrainStep: launched inside step()
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
+        # capturable: id(step tensor) -> (hyper-parameters, that tensor) of the args formed one step
+        # ahead by the previous step's tail launch; see _step_device
+        self._ahead: dict[int, tuple] = {}
         if fused_tables:
             ids = {id(p) for g in self.param_groups for p in g["params"]}
             for t in tables:
@@ -115,6 +119,7 @@ class AdamW(torch.optim.Optimizer):
         """torch semantics, except that `capturable` stays what this optimizer was built with (it
         selects the execution path, not the math); step counters move on first use."""
         modes = [g["capturable"] for g in self.param_groups]
+        self._ahead.clear()  # scalars formed ahead belong to the replaced counters
         super().load_state_dict(state_dict)
         for g, c in zip(self.param_groups, modes):
             g["capturable"] = c
@@ -206,7 +211,24 @@ class AdamW(torch.optim.Optimizer):
             slots.append((st["step"], a))
             dense.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], a))
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
-        ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd)
+        hyper = (lr, b1, b2, eps, wd)
+        # Scalars one step ahead (TT_ADAM_AHEAD=0: torch's order, a prepare in front of the
+        # updates): the previous step's tail formed this step's scalars while advancing its counters
+        # (tt_adam_prepare_ex increment 1, ahead 1), so the fused table update follows the
+        # backward directly instead of waiting on a prepare launched after it.  Counters nobody
+        # prepared, or prepared with other hyper-parameters, get theirs here (increment 0, ahead 1).
+        ahead = os.environ.get("TT_ADAM_AHEAD", "1") != "0"
+        if ahead:
+            def warm(st):
+                h, t = self._ahead.get(id(st), (None, None))
+                return t is st and h == hyper
+
+            cold = [sl for sl in slots if not warm(sl[0])]
+            ops.adam_prepare(cold, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=0, ahead=1)
+        else:
+            for st, _ in slots:
+                self._ahead.pop(id(st), None)
+            ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd)
         # the fused table updates first: they read no dense gradient, so side-stream gradients
         # (ops.TowerHead's weight gradients) are still being computed beside them
         for p, st, (ids, dp, den, plan) in fused:
@@ -218,6 +240,10 @@ class AdamW(torch.optim.Optimizer):
             self._grad_sync.launch(self._side_grads)
         self._side_grads.join()
         ops.adamw_multi(dense)
+        if ahead:  # counters advanced, next step's scalars formed, behind every update that read them
+            ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
+            for st, _ in slots:
+                self._ahead[id(st)] = (hyper, st)  # the tensor itself: an id alone could be reused
         for sh in gathers:
             sh.all_gather_params()
 
