@@ -646,10 +646,11 @@ def test_adamw_multi_matches_host_adamw():
     assert ob.state[b[0]]["step"].device.type == "cuda" and ob.state[b[0]]["step"].item() == 4.0
 
 
-def test_adamw_scalars_ahead_follow_lr_changes_and_state_loads():
+def test_adamw_scalars_ahead_follow_lr_changes_and_state_loads(monkeypatch):
     """Capturable AdamW forms each step's scalars at the previous step's tail (tt_adam_prepare_ex
     increment 1, ahead 1): an lr changed between steps, a parameter skipped for a step and a
     state_dict loaded mid-run still give torch's AdamW trajectory and step counters."""
+    monkeypatch.setenv("TT_ADAM_AHEAD", "1")
     rng = np.random.default_rng(23)
     shapes = [(64, 32), (32,), (5, 7)]
     params = [cuda(rng.standard_normal(s).astype(np.float32)) for s in shapes]
@@ -695,6 +696,7 @@ def test_trainstep_adam_scalars_ahead_equal_in_front(graph, monkeypatch):
         return losses, [p.detach().clone() for p in model.parameters()], [opt.state[p]["step"].item()
                                                                           for p in model.parameters()]
 
+    monkeypatch.setenv("TT_ADAM_AHEAD", "1")
     got = run()
     monkeypatch.setenv("TT_ADAM_AHEAD", "0")
     want = run()
