@@ -331,6 +331,17 @@ int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t
 size_t tt_head_wgrad_ws_size(int64_t rows, int N);
 int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
                   size_t ws_bytes, tt_stream_t stream);
+/* tt_head_wgrad2: both weight gradients of a Linear-ReLU-Linear head in one launch, as slab
+ * partials in ws (tt_head_wgrad2_ws_size bytes): problem 1 (G1, X1), problem 2 (G2, X2), each
+ * rows x 256 fp32; tt_head_wgrad2_reduce then writes dW1 = G1^T X1, db1 = colsum G1, dW2, db2
+ * (fixed-order slab sums, deterministic).  The reduce may be queued later on another stream (the
+ * partials stay in ws): train_step runs the partials on a side stream beside the table update and
+ * the reduce where the optimizer joins it. */
+size_t tt_head_wgrad2_ws_size(int64_t rows, int N);
+int tt_head_wgrad2(const float* G1, const float* X1, const float* G2, const float* X2, int64_t rows, int N,
+                   void* ws, size_t ws_bytes, tt_stream_t stream);
+int tt_head_wgrad2_reduce(const void* ws, int N, float* dW1, float* db1, float* dW2, float* db2,
+                          tt_stream_t stream);
 size_t tt_head_relu_mask_bytes(int64_t rows);
 size_t tt_head_gemm_ws_size(int64_t rows, int epi); /* epi 1: per-slice row sums of squares */
 int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,

@@ -983,6 +983,30 @@ def test_head_wgrad_vs_fp64(rows):
     assert torch.equal(dW, dW2) and torch.equal(db, db2)  # deterministic
 
 
+@pytest.mark.parametrize("rows", [0, 1, 200, 24576])
+def test_head_wgrad2_vs_fp64(rows):
+    """Both head weight gradients in one launch (tt_head_wgrad2, slab partials) and their
+    fixed-order sums (tt_head_wgrad2_reduce, queued later, here on another stream) vs float64."""
+    rng = np.random.default_rng(31 + rows)
+    mats = [rng.standard_normal((rows, 256)).astype(np.float32) for _ in range(4)]
+    g1, x1, g2, x2 = (cuda(m) for m in mats)
+    ws = ops.head_wgrad2(g1, x1, g2, x2)
+    out = [torch.empty(256, 256, device=DEV), torch.empty(256, device=DEV), torch.empty(256, 256, device=DEV),
+           torch.empty(256, device=DEV)]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.head_wgrad2_reduce(ws, *out)
+    torch.cuda.synchronize()
+    dW1, db1, dW2, db2 = out
+    if rows == 0:
+        assert all(float(t.abs().max()) == 0.0 for t in out)
+        return
+    m = [a.astype(np.float64) for a in mats]
+    assert rel(dW1, m[0].T @ m[1]) < 1e-5 and rel(db1, m[0].sum(0)) < 1e-5
+    assert rel(dW2, m[2].T @ m[3]) < 1e-5 and rel(db2, m[2].sum(0)) < 1e-5
+
+
 def test_c5_shaped_step_matches_cpu_oracle():
     """The bench's C5 step shape (1 positive + 4 negatives per query, multiple_negatives loss,
     E = H = 256 TowerHead, fused table AdamW, graph replay) against the CPU restatement of the

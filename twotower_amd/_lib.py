@@ -5,6 +5,7 @@ GPU, the call raises.  Torch only supplies device memory and the current HIP str
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import re
@@ -73,6 +74,9 @@ _SIGNATURES = {
     "tt_head_relu_mask_bytes": (_c_sz, [_c_i64]),
     "tt_head_wgrad_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _c_sz, _vp]),
+    "tt_head_wgrad2_ws_size": (_c_sz, [_c_i64, _c_int]),
+    "tt_head_wgrad2": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_int, _vp, _c_sz, _vp]),
+    "tt_head_wgrad2_reduce": (_c_int, [_vp, _c_int, _vp, _vp, _vp, _vp, _vp]),
     "tt_head_gemm": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_sz,
                               _vp]),
     "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
@@ -150,6 +154,7 @@ class SideGrads:
         self.events: list[torch.cuda.Event] = []
         self.grads: list[tuple] = []  # (param, gradient storage) pairs produced on the side
         self.uses: dict[int, int] = {}  # forward uses per parameter since the last join
+        self.finals: list = []  # callables the join queues after its wait
         self.active = False
 
     def use(self, param: torch.Tensor) -> None:
@@ -160,20 +165,36 @@ class SideGrads:
         autograd as they arrive, before any join)."""
         return all(self.uses.get(id(p), 0) == 1 for p in params)
 
-    def add(self, event: torch.cuda.Event, grads=()) -> None:
+    def add(self, event: torch.cuda.Event, grads=(), finalize=None) -> None:
+        """finalize: queued on the joining stream after the wait (e.g. the fixed-order slab sums
+        of gradients whose partials the side stream computed)."""
         self.events.append(event)
         self.grads.extend((p, g.data_ptr()) for p, g in grads)
+        if finalize is not None:
+            self.finals.append(finalize)
+
+    def run_finals(self) -> None:
+        """Queue the pending finalize callables on the current stream (after its waits)."""
+        finals, self.finals = self.finals, []
+        for f in finals:
+            f()
 
     def join(self, stream: torch.cuda.Stream | None = None) -> None:
         for ev in self.events:
             (stream or torch.cuda.current_stream()).wait_event(ev)
         self.events.clear()
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            self.run_finals()
         self.uses.clear()
         grads, self.grads = self.grads, []
         for p, at in grads:  # autograd must have handed the side-stream buffer to .grad as is
             if p.grad is None or p.grad.data_ptr() != at:
                 raise RuntimeError("twotower_amd: a side-stream gradient was copied or accumulated before "
                                    "its kernel ran (SideGrads needs .grad set to None before backward)")
+
+
+def _nullctx():
+    return contextlib.nullcontext()
 
 
 def join_side_grads(params) -> None:

@@ -359,17 +359,36 @@ __device__ __forceinline__ int wg_off(int row, int col) {  // byte offset in a p
   return row * (kWgBlk * 2) + ((col * 2) ^ ((row & 3) << 6));
 }
 
+// Two problems in one launch (tt_head_wgrad2): blocks [0, 4 slabs) take (G, X), the rest (G2, X2)
+// with partials at part_w2 / part_b2; each problem keeps the one-problem block mapping.
+struct WgradProblem2 {
+  const float* G;
+  const float* X;
+  float* part_w;
+  float* part_b;
+  int nblk;  // blocks of the first problem (4 * slabs); 0: one problem
+};
+
 __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ X,
                                                             int64_t rows, int64_t slab_rows,
-                                                            float* __restrict__ part_w, float* __restrict__ part_b) {
+                                                            float* __restrict__ part_w, float* __restrict__ part_b,
+                                                            WgradProblem2 second = WgradProblem2{}) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
   typedef __attribute__((address_space(3))) char lds_char_t;
   typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
   lds_char_t* lds = (lds_char_t*)smem;
+  unsigned bid = blockIdx.x;
+  if (second.nblk && bid >= (unsigned)second.nblk) {  // block-uniform: the second problem
+    bid -= second.nblk;
+    G = second.G;
+    X = second.X;
+    part_w = second.part_w;
+    part_b = second.part_b;
+  }
   // blocks b, b+8, b+16, b+24 share an XCD (round-robin dispatch): they take the four output
   // blocks of one slab, so its G / X rows come from HBM once and from that XCD's L2 after
-  const int blk = (blockIdx.x >> 3) & 3, slab = (blockIdx.x >> 5) * 8 + (blockIdx.x & 7);
+  const int blk = (bid >> 3) & 3, slab = (bid >> 5) * 8 + (bid & 7);
   const int bi = blk & 1, bj = blk >> 1;  // output block rows i in [128 bi, +128), cols j in [128 bj, +128)
   const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
   const int64_t r_begin = (int64_t)slab * slab_rows;
@@ -536,15 +555,35 @@ __device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t s
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
+struct WgradReduce2 {
+  const float* part_w;
+  const float* part_b;
+  float* dW;
+  float* db;
+  int nblk;  // blocks of the first problem; 0: one problem
+};
+
 __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part_w,
                                                                 const float* __restrict__ part_b, int slabs,
-                                                                float* __restrict__ dW, float* __restrict__ db) {
+                                                                float* __restrict__ dW, float* __restrict__ db,
+                                                                WgradReduce2 second = WgradReduce2{}) {
   __shared__ f32x4 red[kRedQ][64];
+  unsigned bid = blockIdx.x, nb = gridDim.x;
+  if (second.nblk) {  // block-uniform: the first or the second problem
+    nb = second.nblk;
+    if (bid >= nb) {
+      bid -= nb;
+      part_w = second.part_w;
+      part_b = second.part_b;
+      dW = second.dW;
+      db = second.db;
+    }
+  }
   const int o = threadIdx.x & 63, qq = threadIdx.x >> 6;  // output float4 of the block, slab quarter
-  const int i = blockIdx.x * 64 + o;
+  const int i = bid * 64 + o;
   const int per = (slabs + kRedQ - 1) / kRedQ;
   const int s0 = qq * per, s1 = min(slabs, s0 + per);
-  const bool is_b = blockIdx.x == gridDim.x - 1;  // the last block folds db (64 float4 = 256 columns)
+  const bool is_b = bid == nb - 1;  // the last block folds db (64 float4 = 256 columns)
   const f32x4 t = is_b ? (db ? sum_slabs(reinterpret_cast<const f32x4*>(part_b) + o, kN / 4, s0, s1)
                              : f32x4{0.f, 0.f, 0.f, 0.f})
                        : sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, kN * kN / 4, s0, s1);
@@ -650,6 +689,62 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
     head_normalize_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
     TT_LAUNCH_CHECK("tt_head_gemm normalize");
   }
+  return TT_OK;
+}
+
+// Both weight gradients of a head in one launch, 32 slabs each (one workgroup per CU over the two
+// problems): (dW1, db1) from (G1, X1) and (dW2, db2) from (G2, X2), slab partials into ws; the
+// fixed-order slab sums in a second call (tt_head_wgrad2_reduce), which a caller may queue later
+// on another stream.  Deterministic.
+constexpr int kWgSlabs2 = 32;
+
+extern "C" size_t tt_head_wgrad2_ws_size(int64_t rows, int N) {
+  (void)rows;
+  return (size_t)2 * kWgSlabs2 * N * (N + 1) * sizeof(float);
+}
+
+extern "C" int tt_head_wgrad2(const float* G1, const float* X1, const float* G2, const float* X2, int64_t rows, int N,
+                              void* ws, size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(N == kN, "tt_head_wgrad2: only N = %d (got %d)", kN, N);
+  TT_REQUIRE(rows >= 0, "bad rows %lld", (long long)rows);
+  TT_REQUIRE(rows == 0 || (G1 && X1 && G2 && X2), "null pointer");
+  TT_REQUIRE(ws && ws_bytes >= tt_head_wgrad2_ws_size(rows, N), "workspace too small (%zu < %zu)", ws_bytes,
+             tt_head_wgrad2_ws_size(rows, N));
+  TT_REQUIRE(((reinterpret_cast<uintptr_t>(G1) | reinterpret_cast<uintptr_t>(X1) | reinterpret_cast<uintptr_t>(G2) |
+               reinterpret_cast<uintptr_t>(X2) | reinterpret_cast<uintptr_t>(ws)) & 15) == 0,
+             "buffers must be 16-byte aligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {  // zero partials: the reduce then writes zero gradients
+    TT_HIP(hipMemsetAsync(ws, 0, tt_head_wgrad2_ws_size(rows, N), s), "memset wgrad2 partials");
+    return TT_OK;
+  }
+  float* pw1 = static_cast<float*>(ws);
+  float* pb1 = pw1 + (size_t)kWgSlabs2 * kN * kN;
+  float* pw2 = pb1 + (size_t)kWgSlabs2 * kN;
+  float* pb2 = pw2 + (size_t)kWgSlabs2 * kN * kN;
+  constexpr int64_t kQuant = 3 * kWgChunk;
+  const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + kWgSlabs2 * kQuant - 1) / (kWgSlabs2 * kQuant) * kQuant);
+  head_wgrad_kernel<<<dim3(2 * 4 * kWgSlabs2), dim3(256), 2 * kWgBuf, s>>>(
+      G1, X1, rows, slab_rows, pw1, pb1, WgradProblem2{G2, X2, pw2, pb2, 4 * kWgSlabs2});
+  TT_LAUNCH_CHECK("tt_head_wgrad2");
+  return TT_OK;
+}
+
+extern "C" int tt_head_wgrad2_reduce(const void* ws, int N, float* dW1, float* db1, float* dW2, float* db2,
+                                     tt_stream_t stream) {
+  TT_REQUIRE(N == kN, "tt_head_wgrad2_reduce: only N = %d (got %d)", kN, N);
+  TT_REQUIRE(ws && dW1 && db1 && dW2 && db2, "null pointer");
+  TT_REQUIRE(((reinterpret_cast<uintptr_t>(ws) | reinterpret_cast<uintptr_t>(dW1) | reinterpret_cast<uintptr_t>(db1) |
+               reinterpret_cast<uintptr_t>(dW2) | reinterpret_cast<uintptr_t>(db2)) & 15) == 0,
+             "buffers must be 16-byte aligned");
+  const float* pw1 = static_cast<const float*>(ws);
+  const float* pb1 = pw1 + (size_t)kWgSlabs2 * kN * kN;
+  const float* pw2 = pb1 + (size_t)kWgSlabs2 * kN;
+  const float* pb2 = pw2 + (size_t)kWgSlabs2 * kN * kN;
+  const int nb = kN * kN / 4 / 64 + 1;
+  head_wgrad_reduce_kernel<<<dim3(2 * nb), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      pw1, pb1, kWgSlabs2, dW1, db1, WgradReduce2{pw2, pb2, dW2, db2, nb});
+  TT_LAUNCH_CHECK("tt_head_wgrad2_reduce");
   return TT_OK;
 }
 

@@ -217,6 +217,7 @@ class GradSync:
         for ev in side.events:  # ... and by the wgrad side stream
             comm.wait_event(ev)
         with torch.cuda.stream(comm):
+            side.run_finals()  # e.g. the weight gradients' slab sums, before they are reduced
             self._reduce(small, large)
             done = torch.cuda.Event()
             done.record(comm)

@@ -141,7 +141,7 @@ def bag_head_prescale(pooled: torch.Tensor):
     nothing else: the encoders' own forward paths open it) forms the bag backward's
     d_pooled / denom in its dx epilogue.  TT_BAG_PRESCALE=0 turns it off."""
     tok = getattr(pooled, "_tt_bag_token", None)
-    on = tok is not None and os.environ.get("TT_BAG_PRESCALE", "0") != "0"
+    on = tok is not None and os.environ.get("TT_BAG_PRESCALE", "1") != "0"
     _SOLE_HEAD.append(pooled if on else None)
     try:
         yield
@@ -499,12 +499,40 @@ class TowerHead(torch.autograd.Function):
             tok.grad = dx
         elif ctx.needs_input_grad[0]:
             dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3)
+        two = os.environ.get("TT_WGRAD2", "1") != "0"
         if not on_side:
-            head_wgrad(dh, x, dW1, db1)
-            head_wgrad(dy, h, dW2, db2)
+            if two:
+                head_wgrad2_reduce(head_wgrad2(dh, x, dy, h), dW1, db1, dW2, db2)
+            else:
+                head_wgrad(dh, x, dW1, db1)
+                head_wgrad(dy, h, dW2, db2)
             return dx, dW1, db1, dW2, db2
-        # both forked after the dx GEMM: forked earlier (dW2 beside the dh GEMM, dW1 beside the dx
-        # GEMM) they time-share the CUs with those GEMMs and the step took 20 us longer
+        # forked after the dx GEMM: forked earlier (dW2 beside the dh GEMM, dW1 beside the dx GEMM)
+        # they time-share the CUs with those GEMMs and the step took 20 us longer.  Both weight
+        # gradients are ONE launch (tt_head_wgrad2), whose slab partials the optimizer's join sums
+        # on its own stream: a chain of four side-stream kernels starved behind the table reduce,
+        # which holds every CU once it runs (its last kernels ran 10-30x their own time).
+        if two:
+            ws = torch.empty(_lib.lib().tt_head_wgrad2_ws_size(dy.shape[0], N), dtype=torch.uint8, device=dy.device)
+            aux.wait_stream(main)  # dh, dy written on this stream
+            ws.record_stream(aux)
+            for t in (dh, dy, x, h):
+                t.record_stream(aux)
+            with torch.cuda.stream(aux):
+                head_wgrad2(dh, x, dy, h, ws)
+            done = torch.cuda.Event()
+            done.record(aux)
+            params = ctx.params
+
+            def finalize():  # on the joining stream (the optimizer's, or the DP all-reduce's)
+                # the sums go into the .grad tensors autograd stole from this backward: no
+                # reference to them is kept here (an extra one would make autograd copy instead)
+                cur = torch.cuda.current_stream(ws.device)
+                ws.record_stream(cur)
+                head_wgrad2_reduce(ws, *(p.grad for p in params))
+
+            side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)), finalize=finalize)
+            return dx, dW1, db1, dW2, db2
         wgrad_aside(dh, x, dW1, db1)
         wgrad_aside(dy, h, dW2, db2)
         done = torch.cuda.Event()
@@ -523,6 +551,23 @@ def head_wgrad(G: torch.Tensor, X: torch.Tensor, dW: torch.Tensor | None = None,
     ws = torch.empty(nws, dtype=torch.uint8, device=G.device)
     call("tt_head_wgrad", ptr(G), ptr(X), rows, N, ptr(dW), ptr(db), ptr(ws), nws, stream_of(G))
     return dW, db
+
+
+def head_wgrad2(G1: torch.Tensor, X1: torch.Tensor, G2: torch.Tensor, X2: torch.Tensor,
+                ws: torch.Tensor | None = None) -> torch.Tensor:
+    """Slab partials of both head weight gradients in one launch (tt_head_wgrad2); returns ws."""
+    rows, N = G1.shape
+    nbytes = _lib.lib().tt_head_wgrad2_ws_size(rows, N)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=G1.device) if ws is None else ws
+    call("tt_head_wgrad2", ptr(G1), ptr(X1), ptr(G2), ptr(X2), rows, N, ptr(ws), ws.numel(),
+         torch.cuda.current_stream(G1.device).cuda_stream)
+    return ws
+
+
+def head_wgrad2_reduce(ws: torch.Tensor, dW1, db1, dW2, db2) -> None:
+    """(G1^T X1, colsum G1, G2^T X2, colsum G2) from tt_head_wgrad2's partials, on the current stream."""
+    call("tt_head_wgrad2_reduce", ptr(ws), dW1.shape[0], ptr(dW1), ptr(db1), ptr(dW2), ptr(db2),
+         torch.cuda.current_stream(ws.device).cuda_stream)
 
 
 def tower_head(x, W1, b1, W2, b2):

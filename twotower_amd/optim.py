@@ -217,7 +217,7 @@ class AdamW(torch.optim.Optimizer):
         # (tt_adam_prepare_ex increment 1, ahead 1), so the fused table update follows the
         # backward directly instead of waiting on a prepare launched after it.  Counters nobody
         # prepared, or prepared with other hyper-parameters, get theirs here (increment 0, ahead 1).
-        ahead = os.environ.get("TT_ADAM_AHEAD", "0") != "0"
+        ahead = os.environ.get("TT_ADAM_AHEAD", "1") != "0"
         if ahead:
             def warm(st):
                 h, t = self._ahead.get(id(st), (None, None))
