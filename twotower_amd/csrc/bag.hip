@@ -673,13 +673,7 @@ int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, f
     const int LPR = E / (4 * NS);
     const int64_t rpb = kWavesPerBlock * (kWave / LPR), rbs = (V + rpb - 1) / rpb, gps = 8 / NS;
     const dim3 grid((unsigned)(((rbs + gps - 1) / gps) * 8));
-    // TT_REDUCE_LDS (measurement): LDS bytes reserved per workgroup, to cap the workgroups a CU
-    // holds (160 KiB / bytes) and leave room for other streams' kernels beside the reduce
-    static const unsigned lds_reserve = [] {
-      const char* e = std::getenv("TT_REDUCE_LDS");
-      return e ? (unsigned)std::strtoul(e, nullptr, 10) : 0u;
-    }();
-#define TT_SL(L) bag_bwd_reduce_sliced_kernel<L, 4, FUSED, true><<<grid, block, lds_reserve, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, NS, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial)
+#define TT_SL(L) bag_bwd_reduce_sliced_kernel<L, 4, FUSED, true><<<grid, block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, NS, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial)
     if (LPR == 16) TT_SL(16);
     else if (LPR == 32) TT_SL(32);
     else TT_SL(64);
