@@ -184,23 +184,16 @@ class BagMeanPool(torch.autograd.Function):
         if ids.dim() != 2:
             raise ValueError(f"ids must be (batch, seq_len), got shape {tuple(ids.shape)}")
         ids = ids.contiguous()
+        pooled, denom = bag_mean_forward(weight, ids)
         ctx.plan = None
-        plan_now = want_plan and scatter_mode == _lib.TT_SCATTER_SORTED
-        # TT_PLAN_EARLY=1 (measurement): the sort forked before the gather, beside it
-        early = plan_now and os.environ.get("TT_PLAN_EARLY", "0") != "0"
-
-        def fork_plan():
+        if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
+            # forked after the gather: the sort runs beside the towers and the scorer (forked
+            # before it, beside the gather, the step took 22 us longer: 0.887 vs 0.864 ms; again
+            # after the weight-gradient fix, 0.8825 vs 0.8785: the gather holds the CUs and the
+            # sort still ends beside the scorer)
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
             ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
-
-        if early:
-            fork_plan()
-        pooled, denom = bag_mean_forward(weight, ids)
-        if plan_now and not early:
-            # forked after the gather: the sort runs beside the towers and the scorer (forked
-            # before it, beside the gather, the step took 22 us longer: 0.887 vs 0.864 ms)
-            fork_plan()
         ctx.save_for_backward(ids, denom)
         ctx.token = None
         if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
