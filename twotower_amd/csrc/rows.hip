@@ -353,7 +353,15 @@ __global__ __launch_bounds__(kBlock) void multi_neg_bwd_h256_kernel(const float*
 __global__ __launch_bounds__(1024) void mean_kernel(const float* __restrict__ x, int64_t n, float* __restrict__ out) {
   __shared__ float part[1024];
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < n; i += 1024) s += x[i];
+  int64_t i = threadIdx.x;
+  for (; i + 7 * 1024 < n; i += 8 * 1024) {  // eight loads in flight, then the same sequential adds
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = x[i + u * 1024];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; i < n; i += 1024) s += x[i];
   part[threadIdx.x] = s;
   __syncthreads();
   for (int w = 512; w > 0; w >>= 1) {
