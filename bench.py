@@ -51,6 +51,27 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md chip table (spec)
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 
 
+def scorer_pmc(config: str) -> dict | None:
+    """MFMA busy of the two scorer engines (SQ_VALU_MFMA_BUSY_CYCLES per SIMD-cycle) from the newest
+    committed scorer PMC profile (profiles/<tag>_scorer_pmc.json, tools/pmc_scorer.sh +
+    tools/pmc_report.py at the C3 scorer shape): the counter view of "MFMA utilisation", beside
+    the algorithmic rate over every scorer kernel that `frac` reports."""
+    import glob
+
+    if config != "c3":
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_scorer_pmc.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    out = {k: v.get("mfma_busy") for k, v in d.get("passes", {}).items()}
+    out = {f"mfma_busy_{k}": v for k, v in out.items() if v is not None}
+    if "engines_mfma_busy" in d:
+        out["mfma_busy_engines"] = d["engines_mfma_busy"]
+    out["source"] = os.path.relpath(files[-1], ROOT)
+    return out
+
+
 def pmc_traffic(abi: str, config: str) -> dict:
     """roofline.traffic: HBM bytes per launch of the dominant op from the newest committed PMC
     profile of this workload (profiles/<tag>_pmc_traffic.json, written by tools/profile_round.sh:
@@ -196,6 +217,10 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
             # operands, and against float64 on the fp32 operands (what the reference computes)
             "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
         })
+        if scorer_dtype == "bf16" and world == 1:
+            pmc = scorer_pmc(config)
+            if pmc:
+                kernels[-1]["pmc"] = pmc
     add("multiple-negatives loss forward (cosines + CE)", "tt_multi_neg_fwd", (2 + K) * B * d * 4 + B * 4, "GB/s",
         HBM_PEAK_GBS, "hbm", "q, p, negatives read (2 + K)*B*H*4 + loss rows B*4 bytes")
     add("multiple-negatives loss backward", "tt_multi_neg_bwd", 2 * (2 + K) * B * d * 4, "GB/s", HBM_PEAK_GBS, "hbm",
