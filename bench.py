@@ -227,6 +227,11 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
         "q, p, negatives read + their gradients written 2*(2 + K)*B*H*4 bytes")
     add("dense AdamW (tower FF, multi-tensor)", "tt_adamw_multi", 28 * tower_params, "GB/s", HBM_PEAK_GBS, "hbm",
         "28 bytes per parameter")
+    # the step's fused tail: the head weight gradients' slab sums (2 x 32 slabs of 256 x 257
+    # partials read, the gradients written) + the dense AdamW + the next step's scalars
+    add("step tail: head weight-gradient slab sums + dense AdamW + next scalars", "tt_adamw_multi_ex",
+        28 * tower_params + 2 * 32 * 256 * 257 * 4 + 2 * 256 * 257 * 4, "GB/s", HBM_PEAK_GBS, "hbm",
+        "28 bytes per parameter + 2*32*256*257*4 partial bytes read + 2*256*257*4 gradient bytes written")
     main_stream = [k for k in kernels if "stream" not in k]
     dominant = max(main_stream, key=lambda k: k["mean_ms"] * k["calls_per_step"]) if main_stream else None
     roofline = None

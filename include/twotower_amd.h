@@ -135,6 +135,22 @@ int tt_adam_prepare(const tt_adam_slot* slots, int count, double lr, double beta
 int tt_adam_prepare_ex(const tt_adam_slot* slots, int count, double lr, double beta1, double beta2,
                        double eps, double weight_decay, int increment, int ahead, tt_stream_t stream);
 int tt_adamw_multi(const tt_adamw_tensor* tensors, int count, tt_stream_t stream);
+/* tt_adamw_multi_ex: tt_adamw_multi that can also (1) form a tensor's gradient from slab
+ * partials first -- parts[i].part != NULL: grad[k] = the fixed-order slab sum of
+ * part[s * stride + k], s < slabs, the same sum tt_head_wgrad2_reduce forms, written to
+ * tensors[i].grad (which must then be writable, 16-byte aligned, n % 4 == 0) and used -- and
+ * (2) run tt_adam_prepare_ex(next, nnext, ..., increment 1, ahead 1) in the same launch, after
+ * every update has read its scalars (the last workgroup to finish, by a ticket: `ticket` is one
+ * zeroed device unsigned the kernel leaves zeroed).  parts may be NULL; nnext 0 skips (2).
+ * The tail of a step as one launch instead of slab sums + updates + prepare. */
+typedef struct {
+  const float* part;
+  int64_t stride;  /* floats between slabs */
+  int slabs;
+} tt_adamw_grad_parts;
+int tt_adamw_multi_ex(const tt_adamw_tensor* tensors, const tt_adamw_grad_parts* parts, int count,
+                      const tt_adam_slot* next, int nnext, double lr, double beta1, double beta2, double eps,
+                      double weight_decay, unsigned* ticket, tt_stream_t stream);
 
 /* ---- mean of n floats (the loss reductions' F.cross_entropy / .mean(), losses.py:44,85,116):
  * one workgroup, fixed-order sums (bitwise reproducible); the in-batch forward forms it itself
@@ -302,6 +318,10 @@ int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float
  * id rows; an index outside [0, n_src) yields an all-padding row and sets *bad to 1 (caller zeroes). */
 int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n, int L,
                        int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream);
+/* tt_pack_blocks: `count` (<= 8) contiguous byte blocks copied into consecutive ranges of dst
+ * in one launch (TrainStep's copy of a batch into the replayed graph's packed [q; p; n] input,
+ * instead of torch.cat). */
+int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int count, void* dst, tt_stream_t stream);
 
 /* ---- tower head GEMMs, E = H = 256 (MeanPoolingTower feed_forward + F.normalize,
  * twotower/encoders.py:38-42,77): fp32 GEMMs run on the bf16 MFMA with each operand split
@@ -342,6 +362,10 @@ int tt_head_wgrad2(const float* G1, const float* X1, const float* G2, const floa
                    void* ws, size_t ws_bytes, tt_stream_t stream);
 int tt_head_wgrad2_reduce(const void* ws, int N, float* dW1, float* db1, float* dW2, float* db2,
                           tt_stream_t stream);
+/* Where gradient k (0 dW1, 1 db1, 2 dW2, 3 db2) has its slab partials in tt_head_wgrad2's ws:
+ * float offset and stride between slabs; returns the slab count (< 0 on bad arguments).  With
+ * these a tt_adamw_multi_ex launch forms the same sums as tt_head_wgrad2_reduce. */
+int tt_head_wgrad2_parts(int N, int k, int64_t* offset, int64_t* stride);
 size_t tt_head_relu_mask_bytes(int64_t rows);
 size_t tt_head_gemm_ws_size(int64_t rows, int epi); /* epi 1: per-slice row sums of squares */
 int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,

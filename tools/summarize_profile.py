@@ -26,6 +26,7 @@ OPS = [
     (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|prep_qd|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
     (r"score_bf16_kernel<1|score_f32_kernel<1|score_ddp_kernel|to_log2|bwd_combine", "tt_inbatch_bwd"),
     (r"adamw_(vec4|scalar)", "tt_adamw"),
+    (r"adamw_multi_ex", "tt_adamw_multi_ex"),
     (r"adamw_multi|adam_prepare", "tt_adamw_multi"),
     (r"multi_neg_fwd", "tt_multi_neg_fwd"),
     (r"multi_neg_bwd", "tt_multi_neg_bwd"),

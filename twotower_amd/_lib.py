@@ -43,6 +43,11 @@ class AdamwTensor(ctypes.Structure):
     _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("n", _c_i64), ("args", _vp)]
 
 
+class AdamwGradParts(ctypes.Structure):
+    """tt_adamw_grad_parts"""
+    _fields_ = [("part", _vp), ("stride", _c_i64), ("slabs", _c_int)]
+
+
 # name -> (restype, argtypes); must mirror include/twotower_amd.h
 _SIGNATURES = {
     "tt_version": (_c_int, []),
@@ -62,8 +67,12 @@ _SIGNATURES = {
     "tt_adam_prepare_ex": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64,
                                     _c_int, _c_int, _vp]),
     "tt_adamw_multi": (_c_int, [ctypes.POINTER(AdamwTensor), _c_int, _vp]),
+    "tt_adamw_multi_ex": (_c_int, [ctypes.POINTER(AdamwTensor), ctypes.POINTER(AdamwGradParts), _c_int,
+                                   ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _vp,
+                                   _vp]),
     "tt_cosine_scores": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
+    "tt_pack_blocks": (_c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_c_i64), _c_int, _vp, _vp]),
     "tt_gather_rows_i32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
     "tt_ln_l2_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_f32, _vp, _vp, _vp]),
     "tt_ln_l2_bwd": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -77,6 +86,7 @@ _SIGNATURES = {
     "tt_head_wgrad2_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad2": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_int, _vp, _c_sz, _vp]),
     "tt_head_wgrad2_reduce": (_c_int, [_vp, _c_int, _vp, _vp, _vp, _vp, _vp]),
+    "tt_head_wgrad2_parts": (_c_int, [_c_int, _c_int, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "tt_head_gemm": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _c_sz,
                               _vp]),
     "tt_adamw": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp]),
@@ -179,10 +189,23 @@ class SideGrads:
         for f in finals:
             f()
 
-    def join(self, stream: torch.cuda.Stream | None = None) -> None:
+    def join(self, stream: torch.cuda.Stream | None = None, claim=None) -> dict:
+        """Wait for the side stream and queue the finalize callables.  claim: ids of parameters
+        whose gradient sums the caller forms itself (optim.AdamW: tt_adamw_multi_ex); a finalize
+        that exposes ``grad_parts()`` (slab partials) for parameters all in claim is not run, and
+        its {id(param): (part pointer, stride, slabs, owner)} are returned instead."""
         for ev in self.events:
             (stream or torch.cuda.current_stream()).wait_event(ev)
         self.events.clear()
+        deferred = {}
+        if claim:
+            keep = []
+            for f in self.finals:
+                if hasattr(f, "grad_parts") and all(id(p) in claim for p in f.params):
+                    deferred.update(f.grad_parts())
+                else:
+                    keep.append(f)
+            self.finals = keep
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             self.run_finals()
         self.uses.clear()
@@ -191,6 +214,7 @@ class SideGrads:
             if p.grad is None or p.grad.data_ptr() != at:
                 raise RuntimeError("twotower_amd: a side-stream gradient was copied or accumulated before "
                                    "its kernel ran (SideGrads needs .grad set to None before backward)")
+        return deferred
 
 
 def _nullctx():

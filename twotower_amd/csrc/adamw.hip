@@ -83,12 +83,10 @@ struct PrepArgs {
   tt_adam_slot s[TT_ADAM_MAX_TENSORS];
 };
 
-__global__ void adam_prepare_kernel(PrepArgs pa, int count, double lr, double beta1, double beta2, double eps,
-                                    double wd, float inc, float ahead) {
-  const int i = threadIdx.x;
-  if (i >= count) return;
-  const float step = *pa.s[i].step + inc;
-  if (inc != 0.f) *pa.s[i].step = step;
+__device__ void prepare_slot(const tt_adam_slot& sl, double lr, double beta1, double beta2, double eps, double wd,
+                             float inc, float ahead) {
+  const float step = *sl.step + inc;
+  if (inc != 0.f) *sl.step = step;
   const float at = step + ahead;  // the step whose scalars are formed
   const double bc1 = 1.0 - pow(beta1, (double)at);
   const double bc2 = 1.0 - pow(beta2, (double)at);
@@ -100,7 +98,107 @@ __global__ void adam_prepare_kernel(PrepArgs pa, int count, double lr, double be
   a.step_size = (float)(lr / bc1);
   a.bc2_sqrt = (float)sqrt(bc2);
   a.eps = (float)eps;
-  *static_cast<AdamArgs*>(pa.s[i].args) = a;
+  *static_cast<AdamArgs*>(sl.args) = a;
+}
+
+__global__ void adam_prepare_kernel(PrepArgs pa, int count, double lr, double beta1, double beta2, double eps,
+                                    double wd, float inc, float ahead) {
+  const int i = threadIdx.x;
+  if (i >= count) return;
+  prepare_slot(pa.s[i], lr, beta1, beta2, eps, wd, inc, ahead);
+}
+
+// tt_adamw_multi_ex: tensors with slab partials form their gradient first (the sums of
+// tt_head_wgrad2_reduce, bit for bit), write it to .grad and update; the last workgroup to
+// finish (ticket) advances the counters and forms the next step's scalars (prepare_slot with
+// increment 1, ahead 1), after every workgroup has read this step's.
+struct MultiExArgs {
+  tt_adamw_tensor t[TT_ADAM_MAX_TENSORS];
+  tt_adamw_grad_parts g[TT_ADAM_MAX_TENSORS];
+  tt_adam_slot next[TT_ADAM_MAX_TENSORS];
+  int nnext;
+  double lr, beta1, beta2, eps, wd;
+  unsigned* ticket;
+};
+
+__device__ __forceinline__ void adam_update4(f32x4* p, f32x4* m, f32x4* v, int64_t i, f32x4 gg, const AdamArgs& a) {
+  f32x4 pp = p[i], mm = m[i], vv = v[i];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float pj = pp[j], mj = mm[j], vj = vv[j];
+    adam_update(pj, gg[j], mj, vj, a);
+    pp[j] = pj;
+    mm[j] = mj;
+    vv[j] = vj;
+  }
+  p[i] = pp;
+  m[i] = mm;
+  v[i] = vv;
+}
+
+__global__ __launch_bounds__(kBlock) void adamw_multi_ex_kernel(MultiExArgs ma) {
+  __shared__ f32x4 red[kRedQ][64];
+  const tt_adamw_tensor& t = ma.t[blockIdx.y];
+  const tt_adamw_grad_parts& gp = ma.g[blockIdx.y];
+  if (t.n > 0) {
+    const AdamArgs a = *static_cast<const AdamArgs*>(t.args);
+    f32x4* p4 = reinterpret_cast<f32x4*>(t.param);
+    f32x4* m4 = reinterpret_cast<f32x4*>(t.exp_avg);
+    f32x4* v4 = reinterpret_cast<f32x4*>(t.exp_avg_sq);
+    if (gp.part) {
+      // host-checked: 16-byte aligned, n % 4 == 0, stride % 4 == 0.  64 outputs per block pass,
+      // four threads per output each summing a quarter of the slabs (sum_slabs), folded through
+      // LDS as (q0 + q1) + (q2 + q3): tt_head_wgrad2_reduce's sums, bit for bit
+      const int o = threadIdx.x & 63, qq = threadIdx.x >> 6;
+      const int per = (gp.slabs + kRedQ - 1) / kRedQ;
+      const int s0 = qq * per, s1 = min(gp.slabs, s0 + per);
+      const int64_t n4 = t.n / 4;
+      const f32x4* part4 = reinterpret_cast<const f32x4*>(gp.part);
+      for (int64_t base = (int64_t)blockIdx.x * 64; base < n4; base += (int64_t)gridDim.x * 64) {
+        const int64_t i = base + o;
+        red[qq][o] = i < n4 ? sum_slabs(part4 + i, (size_t)gp.stride / 4, s0, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
+        __syncthreads();
+        if (qq == 0 && i < n4) {
+          const f32x4 gg = (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
+          reinterpret_cast<f32x4*>(const_cast<float*>(t.grad))[i] = gg;
+          adam_update4(p4, m4, v4, i, gg, a);
+        }
+        __syncthreads();
+      }
+    } else {
+      const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
+                         reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
+      const int64_t n4 = vec ? t.n / 4 : 0;
+      const int64_t stride = (int64_t)gridDim.x * kBlock;
+      for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride)
+        adam_update4(p4, m4, v4, i, reinterpret_cast<const f32x4*>(t.grad)[i], a);
+      for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < t.n; i += stride) {
+        float pp = t.param[i], mm = t.exp_avg[i], vv = t.exp_avg_sq[i];
+        adam_update(pp, t.grad[i], mm, vv, a);
+        t.param[i] = pp;
+        t.exp_avg[i] = mm;
+        t.exp_avg_sq[i] = vv;
+      }
+    }
+  }
+  if (ma.nnext == 0) return;
+  __shared__ unsigned last;
+  // The ticket orders only this launch's reads of the scalars before the last workgroup's
+  // writes of the next ones (the counters it reads were written by earlier launches): every
+  // wave waits for its own loads, then one relaxed device-scope increment per workgroup.  (A
+  // device-scope fence per workgroup, i.e. an L2 write-back on each of 1,000 workgroups right
+  // after the table update, made the launch 68 us instead of a few.)
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned total = gridDim.x * gridDim.y;
+    last = __hip_atomic_fetch_add(ma.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if ((int)threadIdx.x < ma.nnext)
+    prepare_slot(ma.next[threadIdx.x], ma.lr, ma.beta1, ma.beta2, ma.eps, ma.wd, 1.f, 1.f);
+  if (threadIdx.x == 0) __hip_atomic_store(ma.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 static_assert(sizeof(AdamArgs) <= TT_ADAM_ARGS_BYTES, "AdamArgs does not fit TT_ADAM_ARGS_BYTES");
@@ -179,5 +277,54 @@ extern "C" int tt_adamw(float* param, const float* grad, float* exp_avg, float* 
                                                                      exp_avg_sq + done, rest, a);
     TT_LAUNCH_CHECK("tt_adamw(scalar)");
   }
+  return TT_OK;
+}
+
+extern "C" int tt_adamw_multi_ex(const tt_adamw_tensor* tensors, const tt_adamw_grad_parts* parts, int count,
+                                 const tt_adam_slot* next, int nnext, double lr, double beta1, double beta2,
+                                 double eps, double weight_decay, unsigned* ticket, tt_stream_t stream) {
+  TT_REQUIRE(count >= 0 && count <= TT_ADAM_MAX_TENSORS, "count=%d (max %d)", count, TT_ADAM_MAX_TENSORS);
+  TT_REQUIRE(nnext >= 0 && nnext <= TT_ADAM_MAX_TENSORS, "nnext=%d (max %d)", nnext, TT_ADAM_MAX_TENSORS);
+  TT_REQUIRE(count == 0 || tensors != nullptr, "null tensors");
+  TT_REQUIRE(nnext == 0 || (next != nullptr && ticket != nullptr), "nnext=%d needs slots and a ticket", nnext);
+  MultiExArgs ma{};
+  int64_t nmax = 0;
+  for (int i = 0; i < count; ++i) {
+    const tt_adamw_tensor& t = tensors[i];
+    TT_REQUIRE(t.n >= 0, "tensor %d: n=%lld", i, (long long)t.n);
+    TT_REQUIRE(t.n == 0 || (t.param && t.grad && t.exp_avg && t.exp_avg_sq && t.args), "tensor %d: null pointer", i);
+    ma.t[i] = t;
+    if (parts && parts[i].part && t.n > 0) {
+      const tt_adamw_grad_parts& g = parts[i];
+      TT_REQUIRE(g.slabs >= 1 && g.stride >= t.n && g.stride % 4 == 0 && t.n % 4 == 0,
+                 "tensor %d: slab partials need slabs >= 1, stride >= n, stride and n multiples of 4", i);
+      TT_REQUIRE(((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
+                   reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq) |
+                   reinterpret_cast<uintptr_t>(g.part)) & 15) == 0,
+                 "tensor %d: slab partials need 16-byte aligned buffers", i);
+      ma.g[i] = g;
+    }
+    nmax = std::max(nmax, t.n);
+  }
+  for (int i = 0; i < nnext; ++i) {
+    TT_REQUIRE(next[i].step && next[i].args, "null step/args in slot %d", i);
+    TT_REQUIRE((reinterpret_cast<uintptr_t>(next[i].args) & 3) == 0, "args of slot %d misaligned", i);
+    ma.next[i] = next[i];
+  }
+  ma.nnext = nnext;
+  ma.lr = lr;
+  ma.beta1 = beta1;
+  ma.beta2 = beta2;
+  ma.eps = eps;
+  ma.wd = weight_decay;
+  ma.ticket = ticket;
+  if (count == 0 && nnext == 0) return TT_OK;
+  int64_t bx = (nmax / 4 + kBlock - 1) / kBlock + 1;
+  for (int i = 0; i < count; ++i)
+    if (ma.g[i].part) bx = std::max<int64_t>(bx, (tensors[i].n / 4 + 63) / 64);
+  bx = std::min<int64_t>(bx, 512);
+  adamw_multi_ex_kernel<<<dim3((unsigned)bx, (unsigned)std::max(count, 1)), dim3(kBlock), 0,
+                          reinterpret_cast<hipStream_t>(stream)>>>(ma);
+  TT_LAUNCH_CHECK("tt_adamw_multi_ex");
   return TT_OK;
 }

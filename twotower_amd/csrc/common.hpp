@@ -79,12 +79,34 @@ inline AdamArgs make_adam(double lr, double beta1, double beta2, double eps, dou
   return a;
 }
 
+// Every fused multiply-add is spelled out, so the rounding does not depend on how the
+// compiler contracts the expression in each kernel that inlines it (it had picked different
+// contractions of v's update in two kernels: 1-ulp differences).
 __device__ __forceinline__ void adam_update(float& p, float g, float& m, float& v, const AdamArgs& a) {
-  p = p * a.wd_factor;                   // param.mul_(1 - lr * wd)
-  m = m + a.one_m_b1 * (g - m);          // exp_avg.lerp_(grad, 1 - beta1)
-  v = v * a.beta2 + a.one_m_b2 * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+  m = __builtin_fmaf(a.one_m_b1, g - m, m);               // exp_avg.lerp_(grad, 1 - beta1)
+  v = __builtin_fmaf(v, a.beta2, (a.one_m_b2 * g) * g);   // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
   const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
-  p = p - a.step_size * (m / den);       // param.addcdiv_(exp_avg, denom, -step_size)
+  // param.mul_(1 - lr * wd), then param.addcdiv_(exp_avg, denom, -step_size)
+  p = __builtin_fmaf(p, a.wd_factor, -(a.step_size * (m / den)));
+}
+
+
+// Fixed-order sum of slab partials (tt_head_wgrad2_reduce, tt_adamw_multi_ex): slabs are cut
+// into kRedQ quarters; a quarter's slab s goes to partial s % 8 (8 loads in flight), the eight
+// partials fold in a fixed tree, and the callers add the quarters as (q0 + q1) + (q2 + q3).
+constexpr int kRedQ = 4;
+__device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t stride4, int s_begin, int s_end) {
+  f32x4 a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = s_begin; s0 < s_end; s0 += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = s0 + u < s_end ? p[(size_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += v[u];
+  }
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 }  // namespace tt

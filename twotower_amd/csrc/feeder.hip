@@ -36,10 +36,64 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(const int32_t* __re
   }
 }
 
+// tt_pack_blocks: up to kPackMax contiguous byte blocks copied into consecutive ranges of one
+// buffer (the graph-replayed step's packed [q; p; n] input) in one launch, 16 bytes per lane
+// when every block is 16-byte sized and aligned, bytes otherwise.
+constexpr int kPackMax = 8;
+struct PackArgs {
+  const char* src[kPackMax];
+  int64_t start[kPackMax + 1];  // units (16 B or 1 B) before each block; start[count] = total
+  int count;
+};
+
+template <typename U>
+__global__ __launch_bounds__(kBlock) void pack_blocks_kernel(PackArgs pa, char* __restrict__ dst) {
+  const int64_t total = pa.start[pa.count];
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBlock) {
+    int k = 0;
+    while (k + 1 < pa.count && i >= pa.start[k + 1]) ++k;
+    reinterpret_cast<U*>(dst)[i] = reinterpret_cast<const U*>(pa.src[k])[i - pa.start[k]];
+  }
+}
+
 }  // namespace
 }  // namespace tt
 
 using namespace tt;
+
+extern "C" int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int count, void* dst,
+                              tt_stream_t stream) {
+  TT_REQUIRE(count >= 0 && count <= kPackMax, "count=%d (max %d)", count, kPackMax);
+  TT_REQUIRE(count == 0 || (srcs && bytes), "null srcs/bytes");
+  PackArgs pa{};
+  pa.count = count;
+  int64_t total = 0;
+  bool vec = (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+  for (int k = 0; k < count; ++k) {
+    TT_REQUIRE(bytes[k] >= 0, "block %d: bytes=%lld", k, (long long)bytes[k]);
+    TT_REQUIRE(bytes[k] == 0 || srcs[k], "block %d: null source", k);
+    pa.src[k] = static_cast<const char*>(srcs[k]);
+    vec = vec && bytes[k] % 16 == 0 && (reinterpret_cast<uintptr_t>(srcs[k]) & 15) == 0;
+    total += bytes[k];
+  }
+  if (total == 0) return TT_OK;
+  TT_REQUIRE(dst, "null dst");
+  const int64_t unit = vec ? 16 : 1;
+  int64_t acc = 0;
+  for (int k = 0; k < count; ++k) {
+    pa.start[k] = acc;
+    acc += bytes[k] / unit;
+  }
+  pa.start[count] = acc;
+  const int64_t blocks = std::min<int64_t>((acc + kBlock - 1) / kBlock, 256 * 16);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (vec)
+    pack_blocks_kernel<int4><<<dim3((unsigned)blocks), dim3(kBlock), 0, s>>>(pa, static_cast<char*>(dst));
+  else
+    pack_blocks_kernel<char><<<dim3((unsigned)blocks), dim3(kBlock), 0, s>>>(pa, static_cast<char*>(dst));
+  TT_LAUNCH_CHECK("tt_pack_blocks");
+  return TT_OK;
+}
 
 extern "C" int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n,
                                   int L, int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream) {

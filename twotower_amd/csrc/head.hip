@@ -540,21 +540,6 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
 // dW[i, j] = sum over slabs of the partials, db likewise.  Four threads per output float4 take
 // a quarter of the slabs each (8 loads in flight, slab s to partial s % 8, folded in a fixed
 // tree); the quarters are added in a fixed order through LDS -- deterministic.
-constexpr int kRedQ = 4;
-__device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t stride4, int s_begin, int s_end) {
-  f32x4 a[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s0 = s_begin; s0 < s_end; s0 += 8) {
-    f32x4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = s0 + u < s_end ? p[(size_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] += v[u];
-  }
-  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-}
-
 struct WgradReduce2 {
   const float* part_w;
   const float* part_b;
@@ -746,6 +731,19 @@ extern "C" int tt_head_wgrad2_reduce(const void* ws, int N, float* dW1, float* d
       pw1, pb1, kWgSlabs2, dW1, db1, WgradReduce2{pw2, pb2, dW2, db2, nb});
   TT_LAUNCH_CHECK("tt_head_wgrad2_reduce");
   return TT_OK;
+}
+
+extern "C" int tt_head_wgrad2_parts(int N, int k, int64_t* offset, int64_t* stride) {
+  if (N != kN || k < 0 || k > 3 || !offset || !stride) {
+    set_error("tt_head_wgrad2_parts: N=%d k=%d", N, k);
+    return -1;
+  }
+  // ws layout (tt_head_wgrad2): dW1 slabs, db1 slabs, dW2 slabs, db2 slabs
+  const int64_t w = (int64_t)kWgSlabs2 * kN * kN, b = (int64_t)kWgSlabs2 * kN;
+  const int64_t off[4] = {0, w, w + b, 2 * w + b};
+  *offset = off[k];
+  *stride = (k & 1) ? kN : (int64_t)kN * kN;
+  return kWgSlabs2;
 }
 
 extern "C" size_t tt_head_wgrad_ws_size(int64_t rows, int N) {

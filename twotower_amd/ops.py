@@ -6,7 +6,7 @@ Reference call sites each op replaces are cited per function (paths inside k0r1g
 from __future__ import annotations
 
 import contextlib
-
+import ctypes
 import os
 
 import torch
@@ -524,16 +524,7 @@ class TowerHead(torch.autograd.Function):
                 head_wgrad2(dh, x, dy, h, ws)
             done = torch.cuda.Event()
             done.record(aux)
-            params = ctx.params
-
-            def finalize():  # on the joining stream (the optimizer's, or the DP all-reduce's)
-                # the sums go into the .grad tensors autograd stole from this backward: no
-                # reference to them is kept here (an extra one would make autograd copy instead)
-                cur = torch.cuda.current_stream(ws.device)
-                ws.record_stream(cur)
-                head_wgrad2_reduce(ws, *(p.grad for p in params))
-
-            side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)), finalize=finalize)
+            side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)), finalize=_Wgrad2Sums(ws, ctx.params))
             return dx, dW1, db1, dW2, db2
         wgrad_aside(dh, x, dW1, db1)
         wgrad_aside(dy, h, dW2, db2)
@@ -564,6 +555,33 @@ def head_wgrad2(G1: torch.Tensor, X1: torch.Tensor, G2: torch.Tensor, X2: torch.
     call("tt_head_wgrad2", ptr(G1), ptr(X1), ptr(G2), ptr(X2), rows, N, ptr(ws), ws.numel(),
          torch.cuda.current_stream(G1.device).cuda_stream)
     return ws
+
+
+class _Wgrad2Sums:
+    """The join's finalize for tt_head_wgrad2's partials: called, it queues the fixed-order slab
+    sums (tt_head_wgrad2_reduce) on the joining stream (the optimizer's, or the DP all-reduce's)
+    into the .grad tensors autograd stole from the backward (no reference to them is kept here:
+    an extra one would make autograd copy instead).  An optimizer that forms the sums inside its
+    own update launch (optim.AdamW, tt_adamw_multi_ex) takes ``grad_parts()`` instead."""
+
+    def __init__(self, ws: torch.Tensor, params):
+        self.ws, self.params = ws, tuple(params)
+
+    def __call__(self) -> None:
+        self.ws.record_stream(torch.cuda.current_stream(self.ws.device))
+        head_wgrad2_reduce(self.ws, *(p.grad for p in self.params))
+
+    def grad_parts(self) -> dict:
+        self.ws.record_stream(torch.cuda.current_stream(self.ws.device))
+        N = self.params[0].shape[0]
+        out = {}
+        for k, p in enumerate(self.params):
+            off, stride = ctypes.c_int64(), ctypes.c_int64()
+            slabs = _lib.lib().tt_head_wgrad2_parts(N, k, ctypes.byref(off), ctypes.byref(stride))
+            if slabs < 0:
+                raise RuntimeError(_lib.lib().tt_last_error().decode())
+            out[id(p)] = (ptr(self.ws) + 4 * off.value, stride.value, slabs, self.ws)
+        return out
 
 
 def head_wgrad2_reduce(ws: torch.Tensor, dW1, db1, dW2, db2) -> None:
@@ -944,6 +962,40 @@ def adamw_multi(items: list[tuple[torch.Tensor, torch.Tensor, torch.Tensor, torc
         arr = (_lib.AdamwTensor * len(chunk))(
             *[_lib.AdamwTensor(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(a)) for p, g, m, v, a in chunk])
         call("tt_adamw_multi", arr, len(chunk), stream)
+
+
+def pack_blocks(srcs, dst: torch.Tensor) -> None:
+    """Contiguous device tensors copied into consecutive ranges of dst in one launch
+    (tt_pack_blocks), on the current stream."""
+    require_gpu(dst, *srcs)
+    n = len(srcs)
+    arr = (ctypes.c_void_p * max(n, 1))(*[ptr(t) for t in srcs])
+    nb = (ctypes.c_int64 * max(n, 1))(*[t.numel() * t.element_size() for t in srcs])
+    if sum(nb[:n]) > dst.numel() * dst.element_size():
+        raise ValueError("pack_blocks: sources larger than the destination")
+    call("tt_pack_blocks", arr, nb, n, ptr(dst), stream_of(dst))
+
+
+def adamw_multi_ex(items, parts: list | None, next_slots: list, *, lr: float, beta1: float, beta2: float, eps: float,
+                   weight_decay: float, ticket: torch.Tensor) -> None:
+    """One tt_adamw_multi_ex launch (at most 16 tensors, 16 next slots): items as adamw_multi;
+    parts[i] None or (part pointer, stride, slabs, owner) whose fixed-order sum becomes items[i]'s
+    gradient; then the next step's scalars of next_slots (increment 1, ahead 1)."""
+    if len(items) > _lib.TT_ADAM_MAX_TENSORS or len(next_slots) > _lib.TT_ADAM_MAX_TENSORS:
+        raise ValueError("adamw_multi_ex: at most 16 tensors and 16 slots per launch")
+    if not items and not next_slots:
+        return
+    stream = stream_of(items[0][0] if items else next_slots[0][0])
+    n = max(len(items), 1)
+    arr = (_lib.AdamwTensor * n)(
+        *[_lib.AdamwTensor(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(a)) for p, g, m, v, a in items])
+    gp = (_lib.AdamwGradParts * n)()
+    for i, pt in enumerate(parts or []):
+        if pt is not None:
+            gp[i] = _lib.AdamwGradParts(pt[0], pt[1], pt[2])
+    sl = (_lib.AdamSlot * max(len(next_slots), 1))(*[_lib.AdamSlot(ptr(st), ptr(a)) for st, a in next_slots])
+    call("tt_adamw_multi_ex", arr, gp, len(items), sl, len(next_slots), lr, beta1, beta2, eps, weight_decay,
+         ptr(ticket), stream)
 
 
 def bag_mean_backward_adamw_planned(d_pooled, denom, plan: BagPlan, table, exp_avg, exp_avg_sq,

@@ -41,6 +41,7 @@ class AdamW(torch.optim.Optimizer):
         # capturable: id(step tensor) -> (hyper-parameters, that tensor) of the args formed one step
         # ahead by the previous step's tail launch; see _step_device
         self._ahead: dict[int, tuple] = {}
+        self._tickets: dict[torch.device, torch.Tensor] = {}  # tt_adamw_multi_ex's last-workgroup ticket
         if fused_tables:
             ids = {id(p) for g in self.param_groups for p in g["params"]}
             for t in tables:
@@ -180,7 +181,7 @@ class AdamW(torch.optim.Optimizer):
     def _step_device(self, group: dict) -> None:
         """Capturable form: one tt_adam_prepare launch, one multi-tensor launch per 16 dense
         parameters, one fused scatter + AdamW launch per table."""
-        slots, dense, fused, gathers = [], [], [], []
+        slots, dense, fused, gathers, dense_ids = [], [], [], [], []
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
             if deferred is not None and deferred.parts:
@@ -193,6 +194,7 @@ class AdamW(torch.optim.Optimizer):
                 if sh is not None:  # data parallel: reduce-scatter, AdamW on own rows, all-gather
                     g_shard = self._table_grad_shard(sh, parts[1], parts[2], parts[3])
                     dense.append((sh.rows(sh.storage()), g_shard, st["exp_avg"], st["exp_avg_sq"], a))
+                    dense_ids.append(None)
                     gathers.append(sh)
                 else:
                     if deferred.gather_group is not None:  # data parallel: every rank's factored grad
@@ -210,6 +212,7 @@ class AdamW(torch.optim.Optimizer):
             a = self._adam_args(p)
             slots.append((st["step"], a))
             dense.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], a))
+            dense_ids.append(id(p))
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
         hyper = (lr, b1, b2, eps, wd)
         # Scalars one step ahead (TT_ADAM_AHEAD=0: torch's order, a prepare in front of the
@@ -238,10 +241,31 @@ class AdamW(torch.optim.Optimizer):
         # the table update, overlaps that update on a communication stream; the join waits for it
         if self._grad_sync is not None:
             self._grad_sync.launch(self._side_grads)
-        self._side_grads.join()
-        ops.adamw_multi(dense)
-        if ahead:  # counters advanced, next step's scalars formed, behind every update that read them
-            ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
+        # The step's tail (TT_FUSED_TAIL=0: the slab sums as their own launch): the dense updates
+        # form the head weight gradients from their side-stream slab partials themselves (the sums
+        # of tt_head_wgrad2_reduce, bit for bit, also written to .grad; tt_adamw_multi_ex).  The
+        # next step's scalars stay a launch of their own: formed by the same launch's last
+        # workgroup (TT_FUSED_PREPARE=1) they cost more than that launch, one same-address
+        # device-scope increment per workgroup (1,000 of them) serialising at the memory side.
+        fuse = (os.environ.get("TT_FUSED_TAIL", "1") != "0" and len(dense) <= _lib.TT_ADAM_MAX_TENSORS
+                and len(slots) <= _lib.TT_ADAM_MAX_TENSORS and (dense or ahead))
+        parts = self._side_grads.join(claim={i for i in dense_ids if i is not None} if fuse else None)
+        if fuse:
+            dev = (dense[0][0] if dense else slots[0][0]).device
+            ticket = self._tickets.get(dev)
+            if ticket is None:
+                ticket = self._tickets[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+            in_launch = ahead and os.environ.get("TT_FUSED_PREPARE", "0") == "1"
+            ops.adamw_multi_ex(dense, [parts.get(i) if i is not None else None for i in dense_ids],
+                               slots if in_launch else [], lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
+                               ticket=ticket)
+            if ahead and not in_launch:
+                ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
+        else:
+            ops.adamw_multi(dense)
+            if ahead:  # counters advanced, next step's scalars formed, behind every update that read them
+                ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
+        if ahead:
             for st, _ in slots:
                 self._ahead[id(st)] = (hyper, st)  # the tensor itself: an id alone could be reused
         for sh in gathers:

@@ -89,7 +89,11 @@ class TrainStep:
             hit = self._graphs[key] = self._capture(inputs)
         graph, static_all, static_loss = hit
         if all(t.shape[1:] == inputs[0].shape[1:] and t.dtype == inputs[0].dtype for t in inputs):
-            torch.cat(inputs, 0, out=static_all)  # one copy into the packed static buffer
+            if (all(t.device == static_all.device and t.is_contiguous() for t in inputs) and len(inputs) <= 8
+                    and os.environ.get("TT_PACK_INPUT", "1") != "0"):  # TT_PACK_INPUT=0: torch.cat
+                ops.pack_blocks(inputs, static_all)  # one launch into the packed static buffer
+            else:
+                torch.cat(inputs, 0, out=static_all)
         else:
             for dst, src in zip(_views(static_all, inputs), inputs):
                 dst.copy_(src)
