@@ -178,13 +178,14 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
     # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
     stored_p = scorer_dtype == "bf16" and world == 1 and bwd_form == "stored" and B * M <= 2 ** 31
     fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
-    bwd_key = "tt_inbatch_bwd_l2" if "tt_inbatch_bwd_l2" in ops_t else "tt_inbatch_bwd"
+    bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd") if k in ops_t or
+                   k == "tt_inbatch_bwd")
     if fwd_key in ops_t and bwd_key in ops_t:
         # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
         # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
         fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t[bwd_key]["mean_ms"]
         l2_ms = None
-        if bwd_key == "tt_inbatch_bwd_l2":
+        if bwd_key in ("tt_inbatch_bwd_l2", "tt_inbatch_bwd_l2_mean"):
             # the backward combine also runs the tower head's F.normalize backward: the scorer is
             # charged what that pass costs beyond a plain tt_l2norm_bwd over the same rows
             l2_ms = l2_backward()

@@ -273,6 +273,14 @@ int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B, int64_t M,
 int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau, int64_t label_off,
                       const float* lse, const float* dq_unscaled, const float* grad_loss, float grad_scale,
                       const float* norms, float* dx, void* ws, size_t ws_bytes, tt_stream_t stream);
+/* tt_inbatch_bwd_l2_mean: the same, and *loss = the mean of loss_rows (B floats, the forward's
+ *   per-row losses) formed in one extra workgroup of the same launch, bit for bit tt_mean's
+ *   result: for a step whose forward passed loss = NULL (TrainStep: the loss is read only after
+ *   the step), so the mean's own launch leaves the forward-to-backward critical path. */
+int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                           int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
+                           float grad_scale, const float* norms, float* dx, const float* loss_rows, float* loss,
+                           void* ws, size_t ws_bytes, tt_stream_t stream);
 #define TT_INBATCH_TAIL_ROWS 64
 #define TT_INBATCH_MAX_PARTS 512
 int tt_inbatch_prep_rows(const float* x, int64_t rows, int H, void* xb, float* norms, float* max_parts,

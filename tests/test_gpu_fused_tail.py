@@ -118,3 +118,33 @@ def test_pack_blocks_equals_cat(dtype, rows):
     ops.pack_blocks(srcs, dst)
     torch.cuda.synchronize()
     assert torch.equal(dst, torch.cat(srcs, 0))
+
+
+@pytest.mark.parametrize("graph,B", [(False, 300), (True, 300), (True, 9000)])
+def test_trainstep_deferred_loss_mean_equals_own_launch(graph, B, monkeypatch):
+    """The loss mean formed by the backward combine's extra workgroup (tt_inbatch_bwd_l2_mean)
+    equals tt_mean's launch bit for bit, and so does everything after it.  B 300: short strided
+    tails; B 9000: past 8 x 1024 rows, the eight-load loop."""
+    V, E, L = 3000, 256, 12
+
+    def run():
+        torch.manual_seed(17)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.05, compute_dtype="bf16"), opt,
+                            graph=graph, eager_steps=2)
+        losses = [step(*tt.data.synthetic_triplets(B, L, V, seed=40 + k, device=DEV)).clone() for k in range(4)]
+        torch.cuda.synchronize()
+        return losses, [p.detach().clone() for p in model.parameters()]
+
+    monkeypatch.setenv("TT_DEFER_MEAN", "1")
+    got = run()
+    monkeypatch.setenv("TT_DEFER_MEAN", "0")
+    want = run()
+    assert all(bool(torch.isfinite(x)) for x in got[0])
+    for a, b in zip(got[0], want[0]):
+        assert torch.equal(a, b)
+    for a, b in zip(got[1], want[1]):
+        assert torch.equal(a, b)
+

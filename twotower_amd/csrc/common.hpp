@@ -109,6 +109,37 @@ __device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t s
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
+// mean_kernel's arithmetic (rows.hip: 1024 threads, thread t adds x[t + 1024 k] in order with
+// eight loads in flight, then a halving tree over the 1024 partials) run by one 256-thread
+// block, each thread standing in for threads t, t + 256, t + 512, t + 768: the same adds in the
+// same order, so the same bits.  `part` is 1024 floats of LDS.  Every thread returns the mean.
+__device__ inline float block256_mean_as_1024(const float* __restrict__ x, int64_t n, float* part) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float s = 0.f;
+    int64_t i = t + 256 * k;
+    for (; i + 7 * 1024 < n; i += 8 * 1024) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = x[i + u * 1024];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; i < n; i += 1024) s += x[i];
+    part[t + 256 * k] = s;
+  }
+  __syncthreads();
+  part[t] += part[t + 512];  // w = 512: threads t and t + 256 of the 1024
+  part[t + 256] += part[t + 768];
+  __syncthreads();
+  for (int w = 256; w > 0; w >>= 1) {
+    if (t < w) part[t] += part[t + w];
+    __syncthreads();
+  }
+  return n > 0 ? part[0] / (float)n : __builtin_nanf("");
+}
+
 }  // namespace tt
 
 #define TT_REQUIRE(cond, ...)                 \

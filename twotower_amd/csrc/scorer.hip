@@ -1728,9 +1728,19 @@ __global__ __launch_bounds__(256) void bwd_combine_l2_kernel(int64_t B, int64_t 
                                                              float inv_tau, const float* __restrict__ y,
                                                              const float* __restrict__ norms, float* __restrict__ dx,
                                                              const int* __restrict__ xrows, const DT* __restrict__ Dmat,
-                                                             const float* __restrict__ lse2, float c2) {
+                                                             const float* __restrict__ lse2, float c2,
+                                                             const float* __restrict__ mean_x = nullptr,
+                                                             float* __restrict__ mean_out = nullptr) {
   constexpr int H = 4 * kWave;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // one extra block, dispatched first so its serial ~7 us hide under the other blocks (placed
+  // last it ran after them and lengthened the launch by as much): the forward's deferred loss mean
+  if (mean_out && blockIdx.x == 0) {
+    __shared__ float part[1024];
+    const float m = block256_mean_as_1024(mean_x, B, part);
+    if (threadIdx.x == 0) mean_out[0] = m;
+    return;
+  }
+  const int64_t r = (int64_t)(blockIdx.x - (mean_out ? 1 : 0)) * 4 + (threadIdx.x >> 6);
   if (r >= B + M) return;
   const int lane = lane_id();
   const float scale = grad_loss[0] * grad_scale * inv_tau;
@@ -1757,6 +1767,8 @@ struct BwdOut {
   const float* y = nullptr;
   const float* norms = nullptr;
   float* dx = nullptr;
+  const float* loss_rows = nullptr;  // with dx: the forward's per-row losses, whose mean this launch
+  float* loss = nullptr;             // forms in one extra block (the forward deferred it)
 };
 
 template <typename DT>
@@ -1765,9 +1777,9 @@ void launch_bwd_combine(int64_t B, int64_t M, int H, int S, int64_t label_off, c
                         const int* xrows, const DT* Db, const float* lse2, hipStream_t s) {
   const float c2 = inv_tau * kLog2e;
   if (out.dx) {
-    bwd_combine_l2_kernel<DT><<<dim3((unsigned)((B + M + 3) / 4)), dim3(256), 0, s>>>(
+    bwd_combine_l2_kernel<DT><<<dim3((unsigned)((B + M + 3) / 4 + (out.loss ? 1 : 0))), dim3(256), 0, s>>>(
         B, M, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.y, out.norms, out.dx, xrows, Db,
-        lse2, c2);
+        lse2, c2, out.loss_rows, out.loss);
     return;
   }
   const int64_t rows = std::max(B, M);
@@ -2189,12 +2201,22 @@ extern "C" int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, i
                                  int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
                                  float grad_scale, const float* norms, float* dx, void* ws, size_t ws_bytes,
                                  tt_stream_t stream) {
+  return tt_inbatch_bwd_l2_mean(qd, B, M, H, dtype, inv_tau, label_off, lse, dq_unscaled, grad_loss, grad_scale, norms,
+                                dx, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau,
+                                      int64_t label_off, const float* lse, const float* dq_unscaled,
+                                      const float* grad_loss, float grad_scale, const float* norms, float* dx,
+                                      const float* loss_rows, float* loss, void* ws, size_t ws_bytes,
+                                      tt_stream_t stream) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
   TT_REQUIRE(H == 4 * kWave && dtype != TT_F32, "tt_inbatch_bwd_l2: H = 256 with bf16 operands only (H=%d dtype=%d)",
              H, dtype);
   TT_REQUIRE(qd && lse && dq_unscaled && grad_loss && norms && dx && ws, "null pointer");
-  BwdOut out{nullptr, nullptr, qd, norms, dx};
+  TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd_l2_mean: loss and loss_rows together");
+  BwdOut out{nullptr, nullptr, qd, norms, dx, loss_rows, loss};
   return inbatch_bwd(qd, qd + B * H, B, M, H, dtype, inv_tau, label_off, dq_unscaled, grad_loss, grad_scale, out, ws,
                      ws_bytes, reinterpret_cast<hipStream_t>(stream));
 }

@@ -695,7 +695,7 @@ def get_inbatch_backward() -> str:
     return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
 
 
-def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad, prep=None):
+def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_grad, prep=None, defer_mean=False):
     B, H = q.shape
     M = d.shape[0]
     if d.shape[1] != H:
@@ -713,8 +713,9 @@ def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_
     loss = torch.empty((), dtype=_FLOAT, device=dev)
     dqu = torch.empty(B, H, dtype=_FLOAT, device=dev) if want_grad else None
     call(entry, ptr(q), ptr(d), B, M, H, dt, float(inv_tau), int(label_off), int(want_grad),
-         ptr(lse), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
+         ptr(lse), ptr(rows), None if defer_mean else ptr(loss), ptr(dqu), ptr(ws), ws.numel(), stream_of(q))
     ctx.meta = (B, M, H, dt, float(inv_tau), int(label_off), float(1.0 / B) if grad_scale is None else float(grad_scale))
+    ctx.deferred_mean = (rows, loss) if defer_mean else None
     return loss, lse, dqu, ws
 
 
@@ -756,8 +757,12 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         q, d = qd[:nq], qd[nq:]
         want_grad = bool(ctx.needs_input_grad[0])
         ctx.l2_token = prep[4] if prep is not None else None
+        # inside TrainStep (deferred_loss_mean) the loss is read only after the step: its mean is
+        # formed by the backward's combine launch (tt_inbatch_bwd_l2_mean) instead of a launch of
+        # its own between the forward combine and the backward engine
+        defer = want_grad and prep is not None and _DEFER_MEAN[0] > 0 and os.environ.get("TT_DEFER_MEAN", "1") != "0"
         loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad,
-                                          prep[:4] if prep is not None else None)
+                                          prep[:4] if prep is not None else None, defer_mean=defer)
         if want_grad:
             ctx.save_for_backward(qd, lse, dqu, ws)
         ctx.nq = nq
@@ -770,15 +775,33 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         nq = ctx.nq
         tok, ctx.l2_token = ctx.l2_token, None
         B, M, H, dt, inv_tau, label_off, grad_scale = ctx.meta
+        dm, ctx.deferred_mean = ctx.deferred_mean, None
         if tok is not None and _FUSED_HEAD_BWD[0] > 0 and H == HEAD_WIDTH and dt != _lib.TT_F32:
             # the head's F.normalize backward in the combine: grad is the head's dy (see _L2Token)
             gs = g.to(_FLOAT).contiguous().reshape(1)
-            call("tt_inbatch_bwd_l2", ptr(qd), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(gs),
-                 grad_scale, ptr(tok.norms), ptr(grad), ptr(ws), ws.numel(), stream_of(qd))
+            call("tt_inbatch_bwd_l2_mean", ptr(qd), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(gs),
+                 grad_scale, ptr(tok.norms), ptr(grad), ptr(dm[0]) if dm else None, ptr(dm[1]) if dm else None,
+                 ptr(ws), ws.numel(), stream_of(qd))
             tok.dy = grad
             return grad, None, None, None, None
+        if dm is not None:
+            call("tt_mean", ptr(dm[0]), dm[0].numel(), ptr(dm[1]), stream_of(qd))
         _inbatch_bwd(ctx.meta, qd[:nq], qd[nq:], lse, dqu, ws, g, grad[:nq], grad[nq:])
         return grad, None, None, None, None
+
+
+_DEFER_MEAN = [0]  # > 0 while a caller (TrainStep) runs the backward before anyone reads the loss
+
+
+@contextlib.contextmanager
+def deferred_loss_mean():
+    """Declare that the loss of the forward run inside is read only after its backward has run
+    (TrainStep): the in-batch loss may then leave its mean to the backward's combine launch."""
+    _DEFER_MEAN[0] += 1
+    try:
+        yield
+    finally:
+        _DEFER_MEAN[0] -= 1
 
 
 _UNIFORM_SEED = [0]  # > 0 while a caller guarantees every rank seeds its loss backward alike

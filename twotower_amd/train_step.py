@@ -55,8 +55,9 @@ class TrainStep:
             side.join()
             side.active = True
         try:
-            q, p, n = self.model(queries, positive_docs, negative_docs)
-            loss = self.loss_fn(q, p, n)
+            with ops.deferred_loss_mean():  # the loss is read after the backward below
+                q, p, n = self.model(queries, positive_docs, negative_docs)
+                loss = self.loss_fn(q, p, n)
             self.optimizer.zero_grad(set_to_none=True)
             # backward seeded with the (1/world pre-scaled) unit gradient from a resident tensor:
             # no fill / scale kernels per step
