@@ -46,14 +46,15 @@ struct PackArgs {
   int count;
 };
 
+// blockIdx.y = the block of the source (a uniform index into the kernel arguments), one unit
+// per lane over a grid that covers the largest source.  (Four units per lane over a quarter of
+// the grid measured 20-24 us for the C3 batch instead of 6-7.)
 template <typename U>
 __global__ __launch_bounds__(kBlock) void pack_blocks_kernel(PackArgs pa, char* __restrict__ dst) {
-  const int64_t total = pa.start[pa.count];
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBlock) {
-    int k = 0;
-    while (k + 1 < pa.count && i >= pa.start[k + 1]) ++k;
-    reinterpret_cast<U*>(dst)[i] = reinterpret_cast<const U*>(pa.src[k])[i - pa.start[k]];
-  }
+  const int k = blockIdx.y;
+  const int64_t n = pa.start[k + 1] - pa.start[k];
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) (reinterpret_cast<U*>(dst) + pa.start[k])[i] = reinterpret_cast<const U*>(pa.src[k])[i];
 }
 
 }  // namespace
@@ -85,12 +86,17 @@ extern "C" int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int
     acc += bytes[k] / unit;
   }
   pa.start[count] = acc;
-  const int64_t blocks = std::min<int64_t>((acc + kBlock - 1) / kBlock, 256 * 16);
+  int64_t most = 0;
+  for (int k = 0; k < count; ++k) most = std::max(most, pa.start[k + 1] - pa.start[k]);
+  TT_REQUIRE((most + kBlock - 1) / kBlock < (int64_t(1) << 31), "pack_blocks: a block of %lld units is too large",
+             (long long)most);
+  const int64_t blocks = std::max<int64_t>(1, (most + kBlock - 1) / kBlock);
+  const dim3 grid((unsigned)blocks, (unsigned)count);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (vec)
-    pack_blocks_kernel<int4><<<dim3((unsigned)blocks), dim3(kBlock), 0, s>>>(pa, static_cast<char*>(dst));
+    pack_blocks_kernel<int4><<<grid, dim3(kBlock), 0, s>>>(pa, static_cast<char*>(dst));
   else
-    pack_blocks_kernel<char><<<dim3((unsigned)blocks), dim3(kBlock), 0, s>>>(pa, static_cast<char*>(dst));
+    pack_blocks_kernel<char><<<grid, dim3(kBlock), 0, s>>>(pa, static_cast<char*>(dst));
   TT_LAUNCH_CHECK("tt_pack_blocks");
   return TT_OK;
 }
