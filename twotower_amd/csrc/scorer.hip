@@ -1267,8 +1267,19 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 // fp32 engine (exact f32 MFMA, 32x32x2).  The k order inside the X product is permuted
 // (k = 8*blk + 4*hh + u) so each lane reads one 16-byte chunk per four MFMAs; the Acc product
 // consumes X register t directly as its B operand (k = row of X held by register t).
+// Waves per SIMD the H = 128 fp32 engine is compiled for.  Two waves spill 80 B/lane of scratch
+// in the forward (256 VGPRs, no AGPRs); one wave keeps the whole forward in registers (217 VGPRs
+// + 64 AGPRs): C2 forward 222 -> 195 us, while the backward is faster at two waves (174 vs 182 us;
+// profiles/r02zl_f32_occupancy_ab.txt).
+#ifndef TT_F32_MINW128_FWD
+#define TT_F32_MINW128_FWD 1
+#endif
+#ifndef TT_F32_MINW128_DD
+#define TT_F32_MINW128_DD 2
+#endif
 template <int MODE, int H>
-__global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_f32_kernel(
+__global__ __launch_bounds__(NT, (H < 128 ? 2 : H > 128 ? 1 : MODE == FWD ? TT_F32_MINW128_FWD : TT_F32_MINW128_DD))
+void score_f32_kernel(
     const float* __restrict__ R, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
     const float* __restrict__ dmax_part, int n_dmax,
@@ -1817,7 +1828,10 @@ Plan plan_for(int64_t nR, int64_t nC, int BJ, int wg_per_cu, int cols_per_block 
 int bj_for(int dtype) { return dtype == TT_F32 ? Tile<float, 64>::BJ : Tile<__bf16, 64>::BJ; }
 
 // resident workgroups per CU (register-limited: launch_bounds min-blocks of the engines)
-int wg_per_cu(int H) { return H <= 128 ? 2 : 1; }
+int wg_per_cu(int H, int dtype, int mode) {
+  if (H == 128 && dtype == TT_F32) return mode == FWD ? TT_F32_MINW128_FWD : TT_F32_MINW128_DD;
+  return H <= 128 ? 2 : 1;
+}
 
 struct Ws {
   __bf16* Qb;
@@ -1861,14 +1875,14 @@ int64_t p_nct_for(int64_t M) { return (M + 255) / 256 * 8; }  // also the 256-ca
 #endif
 int ddp_cw(int H) { return H == 256 ? TT_DDP_CW256 : 1; }
 Plan ddp_plan(int64_t B, int64_t M, int H) {
-  return plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H), 32 * NW * ddp_cw(H));
+  return plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H, TT_BF16, DD), 32 * NW * ddp_cw(H));
 }
 
 // Layout: [Qb | Db | Qs | P] persist from forward to backward (the backward's MFMA operands);
 // everything else is scratch reused by both passes.
 Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const int BJ = bj_for(dtype);
-  const Plan pf = plan_for(M, B, BJ, wg_per_cu(H)), pd = plan_for(B, M, BJ, wg_per_cu(H));
+  const Plan pf = plan_for(M, B, BJ, wg_per_cu(H, dtype, FWD)), pd = plan_for(B, M, BJ, wg_per_cu(H, dtype, DD));
   const bool bf = dtype != TT_F32;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -1988,7 +2002,7 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
              hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr) {
-  const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H));
+  const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H, dtype, FWD));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
   w.qnorm = const_cast<float*>(qnorm);
@@ -2020,7 +2034,7 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
 int bwd_core(int dtype, const void* Rm, int64_t nQ, const float* lse2_R, const void* Cm, int64_t M, const void* Qlab,
              int64_t B, int64_t label_off, int H, float inv_tau, const float* dqu, const float* grad_loss,
              float grad_scale, const BwdOut& out, const char* pad, float* acc_part, hipStream_t s) {
-  const Plan p = plan_for(nQ, M, bj_for(dtype), wg_per_cu(H));
+  const Plan p = plan_for(nQ, M, bj_for(dtype), wg_per_cu(H, dtype, DD));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
   w.pad = const_cast<char*>(pad);
@@ -2084,17 +2098,17 @@ struct ExWs {
 // workgroup waits for the collective to finish.
 constexpr int kLocalCus = 192;
 Plan plan_local(int64_t B, int64_t M, int H, int dtype) {
-  return plan_for(M, B, bj_for(dtype), wg_per_cu(H), 32 * NW, kLocalCus);
+  return plan_for(M, B, bj_for(dtype), wg_per_cu(H, dtype, FWD), 32 * NW, kLocalCus);
 }
 // split slots of the two-launch data-parallel forward (fwd_ex_local + fwd_ex_remote)
 int split_fwd_slots(int64_t B, int64_t M, int64_t M_all, int H, int dtype) {
   if (M_all <= M || M % bj_for(dtype) != 0) return 0;  // no two-launch forward for this shape
-  return plan_local(B, M, H, dtype).S + plan_for(M_all - M, B, bj_for(dtype), wg_per_cu(H)).S;
+  return plan_local(B, M, H, dtype).S + plan_for(M_all - M, B, bj_for(dtype), wg_per_cu(H, dtype, FWD)).S;
 }
 
 ExWs carve_ex(void* base, int64_t B, int64_t M_all, int64_t nQ_all, int64_t M, int H, int dtype) {
   const int BJ = bj_for(dtype);
-  const Plan pf = plan_for(M_all, B, BJ, wg_per_cu(H)), pd = plan_for(nQ_all, M, BJ, wg_per_cu(H));
+  const Plan pf = plan_for(M_all, B, BJ, wg_per_cu(H, dtype, FWD)), pd = plan_for(nQ_all, M, BJ, wg_per_cu(H, dtype, DD));
   const int64_t sf = std::max<int64_t>(pf.S, split_fwd_slots(B, M, M_all, H, dtype));
   const size_t ol = 0;
   const size_t oa = align_up((size_t)sf * B * 4, 256);
@@ -2321,7 +2335,7 @@ extern "C" int tt_inbatch_fwd_ex_remote(const void* Qb, const float* qnorm, int6
   const ExWs w = carve_ex(ws, B, M_all, B, M, H, dtype);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int BJ = bj_for(dtype);
-  const Plan pl = plan_local(B, M, H, dtype), pr = plan_for(M_all - M, B, BJ, wg_per_cu(H));
+  const Plan pl = plan_local(B, M, H, dtype), pr = plan_for(M_all - M, B, BJ, wg_per_cu(H, dtype, FWD));
   const float c2 = inv_tau * kLog2e;
   Ws e{};
   e.qnorm = const_cast<float*>(qnorm);
