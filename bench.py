@@ -263,6 +263,9 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=8192,
                     help="queries per CPU step (the full per-GPU batch: the dense AdamW over the table is a "
                          "fixed per-step cost, so a smaller batch would understate the CPU rate)")
+    ap.add_argument("--no-helpers", action="store_true",
+                    help="skip the scorer-attribution helper timings (normalise / plain L2 backward on the same rows): "
+                         "tools/profile_round.sh sets it so every kernel in the trace belongs to a step")
     ap.add_argument("--zipf", type=float, default=None,
                     help="token ids ~ Zipf(s) over the vocabulary (text-like hot rows); default uniform")
     return ap.parse_args()
@@ -358,8 +361,9 @@ def main():
     M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1  # candidates per query
     kernels, roofline = op_report(ops_t, timing_steps, args.config, world, scorer_dtype, nnz,
                                   sum(p.numel() for n_, p in model.named_parameters() if "embedding" not in n_),
-                                  tt_ops.get_inbatch_backward(), lambda: normalise_ms((2 + K) * B, d, dev),
-                                  lambda: l2_backward_ms((2 + K) * B, d, dev))
+                                  tt_ops.get_inbatch_backward(),
+                                  *(() if args.no_helpers else (lambda: normalise_ms((2 + K) * B, d, dev),
+                                                                lambda: l2_backward_ms((2 + K) * B, d, dev))))
     gather = next((k for k in kernels if k["abi"] == "tt_bag_mean_fwd"), None)
 
     cpu = None
@@ -371,23 +375,39 @@ def main():
         if K > 1:
             cpu_batches = [tuple(t.to("cpu", torch.int64) for t in (b[0][:cb], b[1][:cb], b[2][:cb * K]))
                            for b in batches[:2]]
-        r = time_cpu_step(V, d, d, cpu_batches, loss=cfg["loss"], min_seconds=args.cpu_seconds)
         hc = host_cores()
+        # all physical host cores.  The box's CPU share may be smaller than the cores
+        # it shows, so a short sweep over thread counts up to every physical core picks the count
+        # the full-length measurement then runs at (the sweep is reported beside it).
+        counts = sorted({c for c in (16, 32, 64, 128, hc["physical_cores"]) if c <= hc["physical_cores"]}
+                        or {hc["physical_cores"]})
+        sweep = {n: time_cpu_step(V, d, d, cpu_batches, loss=cfg["loss"], threads=n, min_seconds=1.0,
+                                  max_steps=2)["pairs_per_s"] for n in counts}
+        best = max(sweep, key=sweep.get)
+        r = time_cpu_step(V, d, d, cpu_batches, loss=cfg["loss"], threads=best, min_seconds=args.cpu_seconds)
         # C1 (BASELINE.json configs[0]: configs/char_tower.yml, char vocab 34, E 64, H 128, triplet,
-        # batch 64, L 64): the reference's own CPU configuration, a few seconds
+        # batch 64, L 64): the reference's own CPU configuration, a few seconds; a batch of 64 is
+        # too small for many threads, so it gets its own short sweep
         c1_batches = [tuple(t.long() for t in tt.data.synthetic_triplets(64, 64, 34, seed=k, device="cpu"))
                       for k in range(2)]
-        r1 = time_cpu_step(34, 64, 128, c1_batches, loss="triplet", min_seconds=3.0, max_steps=5000)
+        c1_counts = sorted({c for c in (1, 4, 16, best) if c <= hc["physical_cores"]})
+        c1_sweep = {n: time_cpu_step(34, 64, 128, c1_batches, loss="triplet", threads=n, min_seconds=0.5,
+                                     max_steps=500)["pairs_per_s"] for n in c1_counts}
+        c1_best = max(c1_sweep, key=c1_sweep.get)
+        r1 = time_cpu_step(34, 64, 128, c1_batches, loss="triplet", threads=c1_best, min_seconds=3.0, max_steps=5000)
         cpu = {"value": round(r["pairs_per_s"], 1), "unit": "pairs/s", "cores": r["threads"], "kind": "port",
                "physical_cores": hc["physical_cores"], "logical_cpus": hc["logical_cpus"],
+               "threads_sweep": {str(n): round(v, 1) for n, v in sweep.items()},
                "sample": f"torch-CPU restatement of the reference step (oracle/cpu_step.py: train.py's step "
                          f"body incl. its per-batch monitors, within 1-8 % of the reference's own train_epoch "
                          f"on the same cores, profiles/r02_cpu_baseline_validation.json), same V/d/L, batch "
                          f"{min(cb, B)}" + (f" instead of {B}" if cb < B else "") + f", {cfg['loss']} loss fp32, "
-                         f"{r['steps']} steps in {r['seconds']:.1f}s on {r['threads']} threads",
-               "c1": {"value": round(r1["pairs_per_s"], 1), "unit": "pairs/s",
+                         f"{r['steps']} steps in {r['seconds']:.1f}s on {r['threads']} threads (the fastest of a "
+                         f"{'/'.join(map(str, counts))}-thread sweep over the {hc['physical_cores']} physical cores)",
+               "c1": {"value": round(r1["pairs_per_s"], 1), "unit": "pairs/s", "cores": r1["threads"],
+                      "threads_sweep": {str(n): round(v, 1) for n, v in c1_sweep.items()},
                       "sample": f"C1 (configs/char_tower.yml shape, batch 64): {r1['steps']} steps in "
-                                f"{r1['seconds']:.1f}s"}}
+                                f"{r1['seconds']:.1f}s on {r1['threads']} threads"}}
 
     line = {
         "metric": "(query,doc) pairs/sec whole node at B=8192 d=256; HBM GB/s on embed gather",

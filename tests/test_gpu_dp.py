@@ -31,7 +31,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _build(loss_name, world, table_sync="auto"):
+def _build(loss_name, world, table_sync="auto", groups=False):
     import twotower_amd as tt
 
     torch.manual_seed(7)
@@ -42,7 +42,12 @@ def _build(loss_name, world, table_sync="auto"):
               "compute_dtype": "bf16" if loss_name.endswith("bf16") else "fp32"}
     else:
         kw = {"margin": 0.2}
-    opt = tt.optim.AdamW(model.parameters(), lr=LR, eps=1.0, weight_decay=0.0, fused_tables=True, tables=[emb],
+    params = model.parameters()
+    if groups:  # e.g. no weight decay on biases: the gradient all-reduce must still run once per step
+        named = dict(model.named_parameters())
+        params = [{"params": [p for n, p in named.items() if not n.endswith("bias")]},
+                  {"params": [p for n, p in named.items() if n.endswith("bias")], "weight_decay": 0.0}]
+    opt = tt.optim.AdamW(params, lr=LR, eps=1.0, weight_decay=0.0, fused_tables=True, tables=[emb],
                          capturable=True, table_sync=table_sync)
     name = "in_batch" if loss_name.startswith("in_batch") else loss_name
     return model, tt.TrainStep(model, tt.losses.build(name, **kw), opt)
@@ -54,7 +59,7 @@ def _batch():
     return tt.data.synthetic_triplets(WORLD * B, L, V, seed=3, device="cuda:0")
 
 
-def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1"):
+def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1", groups=False):
     # every process recomputes G in the backward (the default; the candidate-owner passes always
     # do), so single process and ranks form the same bf16 products
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TT_INBATCH_DP=inbatch_dp,
@@ -63,7 +68,7 @@ def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1
         torch.cuda.set_device(0)
         if rank >= 0:
             dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-        model, step = _build(loss_name, WORLD if rank >= 0 else 1, table_sync)
+        model, step = _build(loss_name, WORLD if rank >= 0 else 1, table_sync, groups)
         init = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
         full = _batch()
         b = full if rank < 0 else tuple(t[rank * B:(rank + 1) * B] for t in full)
@@ -89,22 +94,26 @@ KEYS = {"table": "query_tower.embedding.embedding.weight", "W1": "query_tower.fe
         "b2": "query_tower.feed_forward.2.bias"}
 
 
-@pytest.mark.parametrize("loss_name,table_sync", [("in_batch", "gather"), ("in_batch", "shard"),
-                                                  ("triplet", "gather"), ("triplet", "shard")])
-def test_dp_step_equals_global_batch(loss_name, table_sync):
+@pytest.mark.parametrize("loss_name,table_sync,groups", [("in_batch", "gather", False), ("in_batch", "shard", False),
+                                                         ("triplet", "gather", False), ("triplet", "shard", False),
+                                                         ("triplet", "gather", True), ("in_batch", "shard", True)])
+def test_dp_step_equals_global_batch(loss_name, table_sync, groups):
     """One step, eps 1, no decay: delta = -lr g / (|g| + 1), so g is recovered from the parameter
-    change and compared with the float64 oracle on the global batch."""
+    change and compared with the float64 oracle on the global batch.  groups: the parameters in
+    two param groups (weights with the table, biases apart), where a per-group all-reduce would
+    sum the gradients twice."""
     from oracle import reference_math as O
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, table_sync, q))
+    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, table_sync, q, "owner", "1", groups))
     ref.start()
     _, r_loss, init, r_delta, ids = q.get(timeout=300)
     ref.join(timeout=60)
     assert init is not None, r_loss
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, table_sync, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, table_sync, q, "owner", "1", groups))
+             for r in range(WORLD)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in procs]

@@ -73,14 +73,33 @@ def test_head_normalise_fused_with_scorer_prep_is_bit_identical(B, L, dtype, bwd
 def test_scorer_prep_set_by_trainstep_and_ignored_by_other_losses():
     model = _model(100, 0)
     opt = tt.optim.AdamW(model.parameters(), lr=1e-3)
-    tt.TrainStep(model, tt.losses.build("in_batch", compute_dtype="bf16"), opt)
-    assert model.scorer_prep == "bf16"
-    model2 = _model(100, 0)
-    tt.TrainStep(model2, tt.losses.build("in_batch", compute_dtype="fp32"), tt.optim.AdamW(model2.parameters()))
-    assert model2.scorer_prep is None
-    # a head output carrying prepared operands into a triplet loss: ignored, same loss
+    st = tt.TrainStep(model, tt.losses.build("in_batch", compute_dtype="bf16"), opt)
+    assert st._scorer_prep == "bf16" and model.scorer_prep is None
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
     rng = np.random.default_rng(3)
     batch = [_ids(64, 8, 100, rng) for _ in range(3)]
+    ops.call = spy
+    try:
+        st(*batch)  # the prep is open for the step's own forward only
+        assert "tt_inbatch_l2_prep" in seen
+        assert model.scorer_prep is None
+        seen.clear()
+        with torch.no_grad():
+            model(*batch)  # a later forward outside the step: no operand prep
+        assert "tt_inbatch_l2_prep" not in seen
+    finally:
+        ops.call = real_call
+    model2 = _model(100, 0)
+    st2 = tt.TrainStep(model2, tt.losses.build("in_batch", compute_dtype="fp32"), tt.optim.AdamW(model2.parameters()))
+    assert st2._scorer_prep is None and model2.scorer_prep is None
+    # a head output carrying prepared operands into a triplet loss: ignored, same loss
+    model.scorer_prep = "bf16"
     trip = tt.losses.build("triplet")
     model.zero_grad(set_to_none=True)
     a = trip(*model(*batch))

@@ -657,15 +657,19 @@ def test_adamw_scalars_ahead_follow_lr_changes_and_state_loads(monkeypatch):
     grads = [[cuda(rng.standard_normal(s).astype(np.float32)) for s in shapes] for _ in range(7)]
     ours = [torch.nn.Parameter(p.clone()) for p in params]
     ref = [torch.nn.Parameter(p.clone()) for p in params]
-    oo = tt.optim.AdamW(ours, lr=2e-3, weight_decay=0.05, capturable=True)
-    orf = torch.optim.AdamW(ref, lr=2e-3, weight_decay=0.05)
+    # a second param group that never has a gradient (frozen): torch does nothing for it, and
+    # the capturable step must not fail on it
+    frozen_o, frozen_r = (torch.nn.Parameter(cuda(np.ones(6, np.float32))) for _ in range(2))
+    oo = tt.optim.AdamW([{"params": ours}, {"params": [frozen_o]}], lr=2e-3, weight_decay=0.05, capturable=True)
+    orf = torch.optim.AdamW([{"params": ref}, {"params": [frozen_r]}], lr=2e-3, weight_decay=0.05)
     for k in range(7):
         if k == 3:  # lr schedule step
             for o in (oo, orf):
                 o.param_groups[0]["lr"] = 5e-4
         if k == 5:  # round trip through a state_dict (fresh optimizer, loaded state)
             sd = oo.state_dict()
-            oo = tt.optim.AdamW(ours, lr=5e-4, weight_decay=0.05, capturable=True)
+            oo = tt.optim.AdamW([{"params": ours}, {"params": [frozen_o]}], lr=5e-4, weight_decay=0.05,
+                                capturable=True)
             oo.load_state_dict(sd)
         for i, (a, b) in enumerate(zip(ours, ref)):
             skip = k == 4 and i == 1  # no gradient for this parameter this step
@@ -676,6 +680,7 @@ def test_adamw_scalars_ahead_follow_lr_changes_and_state_loads(monkeypatch):
     for a, b in zip(ours, ref):
         assert rel(a, b) < 1e-6
         assert oo.state[a]["step"].item() == float(orf.state[b]["step"])
+    assert torch.equal(frozen_o.detach(), frozen_r.detach()) and frozen_o not in oo.state
 
 
 @pytest.mark.parametrize("graph", [False, True])

@@ -7,7 +7,9 @@ TAG=${1:?tag}; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-ARGS=${*:---steps 10 --warmup 3 --no-cpu-baseline}
+# --no-helpers: bench.py's scorer-attribution helpers (bench.py normalise_ms / l2_backward_ms) would
+# otherwise land in the trace and be charged to the step
+ARGS="${*:---steps 10 --warmup 3 --no-cpu-baseline} --no-helpers"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace" -o run -- \
   python3 bench.py $ARGS > "$OUT/ktrace.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \

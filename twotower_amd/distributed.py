@@ -198,10 +198,13 @@ class GradSync:
         join_side_grads(self.params)  # gradients computed on a side stream (ops.TowerHead)
         self._reduce(*self._split())
 
-    def launch(self, side) -> None:
+    def launch(self, side, after=None) -> None:
         """The all-reduce on a communication stream; its completion joins ``side`` (a
-        _lib.SideGrads the caller joins before reading the gradients).  CPU tensors (gloo tests)
-        or no side object: the plain synchronous ``sync()``."""
+        _lib.SideGrads the caller joins before reading the gradients).  ``after``: an event the
+        caller recorded on the current stream where the gradients are complete (optim.AdamW: the
+        end of backward, before it queues the table update); without it the communication stream
+        waits for everything queued so far.  CPU tensors (gloo tests) or no side object: the plain
+        synchronous ``sync()``."""
         if not is_active(self.group):
             return
         small, large = self._split()
@@ -213,7 +216,10 @@ class GradSync:
         comm = self._streams.get(dev)
         if comm is None:
             comm = self._streams[dev] = torch.cuda.Stream(device=dev)
-        comm.wait_stream(torch.cuda.current_stream(dev))  # gradients written by the main-stream backward
+        if after is not None:  # gradients written by the main-stream backward
+            comm.wait_event(after)
+        else:
+            comm.wait_stream(torch.cuda.current_stream(dev))
         for ev in side.events:  # ... and by the wgrad side stream
             comm.wait_event(ev)
         with torch.cuda.stream(comm):

@@ -35,7 +35,9 @@ class AdamW(torch.optim.Optimizer):
                                       capturable=bool(capturable)))
         self._tables: list[torch.Tensor] = []
         self._side_grads = _lib.SideGrads()
-        self._grad_sync = None  # distributed.GradSync set by train_step.TrainStep: launched inside step()
+        self._grad_sync = None  # distributed.GradSync set by train_step.TrainStep around its step(): launched inside
+        self._sync_todo = False
+        self._backward_done = None
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
         # capturable: id(step tensor) -> (hyper-parameters, that tensor) of the args formed one step
@@ -137,18 +139,36 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
-            if group["capturable"]:
-                self._step_device(group)
-            else:
-                self._step_host(group)
+        # The tower-gradient all-reduce (data parallel, set by TrainStep for its step) runs once
+        # per step whatever the number of param groups; the communication stream waits for this
+        # point of the current stream (the end of backward), not for the table update queued next.
+        self._sync_todo = self._grad_sync is not None
+        self._backward_done = None
+        if self._sync_todo and torch.cuda.is_available() and any(
+                p.is_cuda for g in self.param_groups for p in g["params"]):
+            self._backward_done = torch.cuda.Event()
+            self._backward_done.record()
+        try:
+            for group in self.param_groups:
+                if group["capturable"]:
+                    self._step_device(group)
+                else:
+                    self._step_host(group)
+        finally:
+            self._sync_todo = False
+            self._backward_done = None
         return loss
+
+    def _launch_grad_sync(self) -> None:
+        """Launch the all-reduce of the dense gradients, once per step (see step)."""
+        if getattr(self, "_sync_todo", False):
+            self._sync_todo = False
+            self._grad_sync.launch(self._side_grads, after=self._backward_done)
 
     def _step_host(self, group: dict) -> None:
         """torch's default (non-capturable) form: step counters on the host."""
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
-        if self._grad_sync is not None:
-            self._grad_sync.launch(self._side_grads)
+        self._launch_grad_sync()
         self._side_grads.join()
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
@@ -213,6 +233,9 @@ class AdamW(torch.optim.Optimizer):
             slots.append((st["step"], a))
             dense.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], a))
             dense_ids.append(id(p))
+        if not slots:  # nothing to update in this group (frozen, unused, or no backward): torch does nothing
+            self._launch_grad_sync()
+            return
         lr, (b1, b2), eps, wd = group["lr"], group["betas"], group["eps"], group["weight_decay"]
         hyper = (lr, b1, b2, eps, wd)
         # Scalars one step ahead (TT_ADAM_AHEAD=0: torch's order, a prepare in front of the
@@ -239,8 +262,7 @@ class AdamW(torch.optim.Optimizer):
                                                 self._adam_args(p))
         # data parallel: the tower-gradient all-reduce, issued after the table's collectives and
         # the table update, overlaps that update on a communication stream; the join waits for it
-        if self._grad_sync is not None:
-            self._grad_sync.launch(self._side_grads)
+        self._launch_grad_sync()
         # The step's tail (TT_FUSED_TAIL=0: the slab sums as their own launch): the dense updates
         # form the head weight gradients from their side-stream slab partials themselves (the sums
         # of tt_head_wgrad2_reduce, bit for bit, also written to .grad; tt_adamw_multi_ex).  The

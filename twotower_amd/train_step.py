@@ -12,6 +12,7 @@ optimizer (optim.AdamW(capturable=True)); a new input shape is captured anew.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -31,15 +32,16 @@ class TrainStep:
         self.sync = GradSync(model.parameters(), group=group) if is_active(group) else None
         # an optimizer that launches the gradient all-reduce itself, after its own table exchange
         # (optim.AdamW): the all-reduce then overlaps the table update
+        # (set on the optimizer only for the duration of this step's optimizer.step(): a plain loop
+        # that calls GradSync.sync() itself must not see a second all-reduce)
         self._sync_in_step = self.sync is not None and hasattr(optimizer, "_grad_sync")
-        if self._sync_in_step:
-            optimizer._grad_sync = self.sync
         # a single-device bf16 in-batch loss: the tied towers' head prepares its operands
         # (TT_SCORER_PREP=0: the loss's own prep pass, for comparison)
+        # Opened only around this step's own forward (_scorer_prep_open): set on the model for
+        # good, every later forward (eval, export, another loss) would prep operands no one reads.
         dt = scorer_prep_dtype(loss_fn)
-        if (dt is not None and hasattr(model, "scorer_prep") and not is_active(group)
-                and os.environ.get("TT_SCORER_PREP", "1") != "0"):
-            model.scorer_prep = dt
+        self._scorer_prep = (dt if dt is not None and hasattr(model, "scorer_prep") and not is_active(group)
+                             and os.environ.get("TT_SCORER_PREP", "1") != "0" else None)
         self.graph = graph
         if graph and not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("TrainStep(graph=True) needs an optimizer built with capturable=True")
@@ -55,7 +57,7 @@ class TrainStep:
             side.join()
             side.active = True
         try:
-            with ops.deferred_loss_mean():  # the loss is read after the backward below
+            with ops.deferred_loss_mean(), self._scorer_prep_open():  # the loss is read after the backward below
                 q, p, n = self.model(queries, positive_docs, negative_docs)
                 loss = self.loss_fn(q, p, n)
             self.optimizer.zero_grad(set_to_none=True)
@@ -70,12 +72,28 @@ class TrainStep:
                 loss.backward(seed)
             if self.sync is not None and not self._sync_in_step:
                 self.sync.sync()
+            if self._sync_in_step:  # the optimizer launches the all-reduce inside this step only
+                self.optimizer._grad_sync = self.sync
             self.optimizer.step()
         finally:
+            if self._sync_in_step:
+                self.optimizer._grad_sync = None
             if side is not None:
                 side.active = False
                 side.join()  # no-op after the optimizer's own join
         return loss.detach()
+
+    @contextlib.contextmanager
+    def _scorer_prep_open(self):
+        if self._scorer_prep is None:
+            yield
+            return
+        prev = self.model.scorer_prep
+        self.model.scorer_prep = self._scorer_prep
+        try:
+            yield
+        finally:
+            self.model.scorer_prep = prev
 
     def __call__(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
         if not self.graph:
