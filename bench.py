@@ -8,7 +8,7 @@ in HBM), tied mean-pool towers, in-batch sampled softmax over all 2B documents o
 fp32 embedding gradient, AdamW over every parameter.  A step = forward (3 towers) + loss +
 backward + gradient sync + optimizer step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c2|c5] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -32,6 +32,11 @@ CONFIGS = {
     "c3": dict(V=200_000, d=256, L=64, B=8192, dtype="bf16", loss="in_batch", negatives=1,
                workload="C3: vocab 200k, d 256, seq 64, batch 8192, in-batch negatives (M = 2B), bf16 MFMA scorer, "
                "fp32 embedding grad"),
+    # BASELINE.json configs[3] as SURVEY §8(a) a5 / §8(d) size it: (query, positive) pairs, every rank's
+    # positives all-gathered as the candidates, M = N * B (65,536 at N = 8; 825 GFLOP per GPU)
+    "c4": dict(V=200_000, d=256, L=64, B=8192, dtype="bf16", loss="in_batch", negatives=0,
+               workload="C4 (pairs form): vocab 200k, d 256, seq 64, batch 8192 (query, positive) pairs per GPU, "
+               "in-batch negatives over every rank's positives (M = N * B), bf16 MFMA scorer, fp32 embedding grad"),
     "c2": dict(V=50_000, d=128, L=32, B=4096, dtype="fp32", loss="in_batch", negatives=1,
                workload="C2: vocab 50k, d 128, seq 32, batch 4096, in-batch negatives (M = 2B), fp32"),
     # BASELINE.json configs[4] per GPU: presets/multi_pos_multi_neg.yml shape (1 positive + 4 negatives
@@ -141,7 +146,7 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
     cfg = CONFIGS[config]
     V, d, L, B, K = cfg["V"], cfg["d"], cfg["L"], cfg["B"], cfg["negatives"]
     nseq = (2 + K) * B
-    M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1
+    M = (1 + K) * B * world if cfg["loss"] == "in_batch" else K + 1
     kernels = []
 
     def add(name, key, algo, unit, peak, bound, per_launch_note, side_stream=False, executed=None):
@@ -253,6 +258,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the step as one HIP graph (auto: on for a single GPU)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="rehearsal: one rank runs every data-parallel exchange of the N-rank step (RCCL at world "
+                         "size 1, TT_DIST_FORCE=1), e.g. to check the N-rank step under HIP-graph capture on one GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard"],
@@ -271,13 +279,20 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist(backend: str):
+def setup_dist(backend: str, force: bool = False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend == "gloo":  # rehearsal of the DP path on one GPU (ranks share it); RCCL is the real path
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    if force and world == 1:  # one-rank rehearsal of every collective (distributed.is_active)
+        os.environ["TT_DIST_FORCE"] = "1"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=0, world_size=1, **kw)
+        return world, rank
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -288,7 +303,8 @@ def setup_dist(backend: str):
 
 def main():
     args = parse()
-    world, rank = setup_dist(args.dist_backend)
+    world, rank = setup_dist(args.dist_backend, args.force_dist)
+    dp = world > 1 or args.force_dist
     cfg = CONFIGS[args.config]
     V, d, L, B = cfg["V"], cfg["d"], cfg["L"], cfg["B"]
     scorer_dtype = args.scorer_dtype or cfg["dtype"]
@@ -300,13 +316,14 @@ def main():
     K = cfg["negatives"]
     if cfg["loss"] == "in_batch":
         loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
-                                  cross_device_negatives=world > 1)
+                                  cross_device_negatives=dp)
     else:  # multiple_negatives over (q, p, n viewed as (B, K, H)); per-sample, no cross-rank exchange
         mn = tt.losses.build("multiple_negatives", temperature=0.1)
 
         def loss_fn(q, p, n):
             return mn(q, p, n.view(q.shape[0], K, q.shape[1]))
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    # N ranks: the step is captured with its RCCL collectives (gloo cannot be captured)
+    use_graph = args.graph == "on" or (args.graph == "auto" and (not dp or args.dist_backend == "nccl"))
     # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
     # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
     opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
@@ -314,7 +331,7 @@ def main():
     step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
     batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev, zipf_s=args.zipf,
-                                          negatives=K)
+                                          negatives=max(K, 1))[:(2 if K == 0 else 3)]
                for k in range(4)]
     nnz = sum(int((t > 0).sum()) for b in batches for t in b) / len(batches)  # tokens per step
 
@@ -355,10 +372,11 @@ def main():
     value = B * world * args.steps / elapsed
 
     if rank != 0:
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
         return
 
-    M = 2 * B * world if cfg["loss"] == "in_batch" else K + 1  # candidates per query
+    M = (1 + K) * B * world if cfg["loss"] == "in_batch" else K + 1  # candidates per query
     kernels, roofline = op_report(ops_t, timing_steps, args.config, world, scorer_dtype, nnz,
                                   sum(p.numel() for n_, p in model.named_parameters() if "embedding" not in n_),
                                   tt_ops.get_inbatch_backward(),
@@ -371,7 +389,7 @@ def main():
         from oracle.cpu_step import host_cores, time_cpu_step  # CPU baseline only: the GPU path never uses it
 
         cb = args.cpu_batch
-        cpu_batches = [tuple(t[:cb].to("cpu", torch.int64) for t in b) for b in batches[:2]]
+        cpu_batches = [tuple(t[:cb].to("cpu", torch.int64) for t in b) for b in batches[:2]]  # (q, p[, n])
         if K > 1:
             cpu_batches = [tuple(t.to("cpu", torch.int64) for t in (b[0][:cb], b[1][:cb], b[2][:cb * K]))
                            for b in batches[:2]]
@@ -422,10 +440,12 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16" if scorer_dtype != "fp32" else "fp32",
         "data": "synthetic MS-MARCO-shaped id triplets (q 3-12 tokens, docs L/2-L), random-init weights",
-        "config": {"workload": cfg["workload"] + ("; candidates all-gathered over ranks" if world > 1 else ""),
+        "config": {"workload": cfg["workload"] + (
+                       f"; candidates all-gathered over ranks (C4, {'triplet form: M = N * 2B' if K == 1 else 'M = N * B'}"
+                       f" = {M})" if world > 1 and cfg["loss"] == "in_batch" else ""),
                    "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
                    "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
-                   "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if world > 1 else "local"),
+                   "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if dp else "local"),
                    "hip_graph": use_graph},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "roofline": roofline,
@@ -434,7 +454,7 @@ def main():
         "final_loss": float(loss.item()) if loss is not None else None,
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -98,6 +98,23 @@ int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float* denom, int
                                   float* table, float* exp_avg, float* exp_avg_sq,
                                   const void* adam_args, tt_stream_t stream);
 
+/* Row-range form of tt_bag_mean_bwd_planned, for a data-parallel table gradient exchanged in
+ * row chunks (the row-sharded optimizer pipelines each chunk's reduce-scatter / AdamW /
+ * all-gather behind the next chunk's gradient; the exchange sits where the reference runs
+ * loss.backward(); optimizer.step(), twotower/train.py:138-139):
+ *   tt_bag_mean_bwd_planned_prepare  once per step: gs = d_pooled / denom (skipped when denom is
+ *                       NULL) and the long rows' piece sums, into the plan workspace;
+ *   tt_bag_mean_bwd_planned_rows     rows [row_begin, row_end) of the dense gradient into
+ *                       grad_rows ((row_end - row_begin) x E), the same sums in the same order as
+ *                       tt_bag_mean_bwd_planned writes for those rows. */
+int tt_bag_mean_bwd_planned_prepare(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                    int64_t V, int E, void* plan, size_t plan_bytes,
+                                    tt_stream_t stream);
+int tt_bag_mean_bwd_planned_rows(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                 int64_t V, int E, const void* plan, size_t plan_bytes,
+                                 int64_t row_begin, int64_t row_end, float* grad_rows,
+                                 tt_stream_t stream);
+
 /* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
  * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
  * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps).   step is 1-based.

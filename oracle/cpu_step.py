@@ -31,10 +31,10 @@ class RefTower(nn.Module):
 def ref_loss(name: str, q, p, n, temperature=0.1, margin=0.2):
     if name == "triplet":                                                # losses.py:9-44
         return F.relu(margin - F.cosine_similarity(q, p, dim=1) + F.cosine_similarity(q, n, dim=1)).mean()
-    if name == "in_batch":                                               # losses.py:88-118 on cat[p, n]
-        d = torch.cat([p, n])
+    if name == "in_batch":                                               # losses.py:88-118 on cat[p, n] (or p)
+        d = p if n is None else torch.cat([p, n])
         logits = (q @ d.T) / temperature
-        return F.cross_entropy(logits, torch.arange(q.shape[0]))
+        return F.cross_entropy(logits, torch.arange(q.shape[0], device=q.device))
     if name == "multiple_negatives":                                     # losses.py:47-85, n (B*K, H)
         d = torch.cat([p.unsqueeze(1), n.view(q.shape[0], -1, q.shape[1])], dim=1)
         logits = F.cosine_similarity(q.unsqueeze(1).expand_as(d), d, dim=2) / temperature
@@ -78,15 +78,18 @@ def time_cpu_step(V: int, E: int, H: int, batches, loss: str = "in_batch", threa
     opt = torch.optim.AdamW(tower.parameters(), lr=1e-3)
 
     def step(b):
-        q, p, n = b
-        qv, pv, nv = tower(q), tower(p), tower(n)                        # tied towers (char_tower.yml)
+        q, p = b[0], b[1]
+        n = b[2] if len(b) > 2 else None                                 # (q, p) pairs: no negatives
+        qv, pv = tower(q), tower(p)                                      # tied towers (char_tower.yml)
+        nv = tower(n) if n is not None else None
         loss_v = ref_loss(loss, qv, pv, nv)
         opt.zero_grad()
         loss_v.backward()
         opt.step()
         with torch.no_grad():  # the loop's per-batch monitors (train.py:143-156)
             F.cosine_similarity(qv, pv).mean().item()
-            F.cosine_similarity(qv, nv[:qv.shape[0]]).mean().item()
+            if nv is not None:
+                F.cosine_similarity(qv, nv[:qv.shape[0]]).mean().item()
         loss_v.item()
         return loss_v
 

@@ -83,15 +83,18 @@ def _ref_adamw(p, g, m, v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, wd=0.01):
     p.addcdiv_(m, denom, value=-lr / (1 - b1 ** step))
 
 
-def _sharded_table(rank, V):
-    """Row-sharded AdamW on the reduce-scattered gradient == full AdamW on the global gradient."""
+def _sharded_table(rank, V, chunks):
+    """Row-sharded AdamW on the reduce-scattered gradient == full AdamW on the global gradient,
+    with the rows in `chunks` chunks of interleaved ownership (each chunk's slabs updated on
+    their own, as optim.AdamW's pipelined exchange does); the sharded moments gather back into
+    the full layout (state_dict) and split again (load)."""
     E = 4
     torch.manual_seed(1)
     table0 = torch.randn(V, E)
     grads = [torch.randn(V, E) for _ in range(WORLD)]  # each rank's local (pre-scaled) gradient
     w = torch.nn.Parameter(table0.clone())
-    sh = D.ShardedRows(w, None)
-    assert sh.Vp % WORLD == 0 and sh.Vp >= V and w.shape == (V, E)
+    sh = D.ShardedRows(w, None, chunks=chunks)
+    assert sh.NC == chunks and sh.Vp == chunks * WORLD * sh.R and sh.Vp >= V and w.shape == (V, E)
     m = torch.zeros(sh.Vs, E)
     v = torch.zeros(sh.Vs, E)
     ref_p, ref_m, ref_v = table0.clone(), torch.zeros(V, E), torch.zeros(V, E)
@@ -99,17 +102,22 @@ def _sharded_table(rank, V):
         gbuf = sh.new_grad_buffer()
         gbuf[:V] = grads[rank] * step
         g_shard = sh.reduce_scatter(gbuf)
-        _ref_adamw(sh.rows(sh.storage()), g_shard, m, v, step)
+        st = sh.storage()
+        for c in range(sh.NC):
+            _ref_adamw(sh.own(st, c), sh.shard_chunk(g_shard, c), sh.shard_chunk(m, c), sh.shard_chunk(v, c), step)
         sh.all_gather_params()
         _ref_adamw(ref_p, sum(g * step for g in grads), ref_m, ref_v, step)
         assert torch.allclose(w.data, ref_p, rtol=0, atol=1e-6), step
     if sh.Vp > V:
         assert torch.equal(sh.storage()[V:], torch.zeros(sh.Vp - V, E))  # padding rows stay zero
+    full = sh.gather_full(m)
+    assert torch.allclose(full[:V], ref_m, rtol=0, atol=1e-6)  # the full-layout moments (state_dict)
+    assert torch.equal(sh.rows(full), m)                       # ... and back to this rank's rows (load)
 
 
-@pytest.mark.parametrize("V", [10, 11])
-def test_sharded_table_adamw_equals_global(V):
-    _run(_sharded_table, V)
+@pytest.mark.parametrize("V,chunks", [(10, 1), (11, 1), (11, 3), (40, 4)])
+def test_sharded_table_adamw_equals_global(V, chunks):
+    _run(_sharded_table, V, chunks)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -313,11 +313,12 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_kernel(
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
     float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev,
-    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial) {
+    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial,
+    int64_t row_lo) {
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
-  const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  const int64_t row = row_lo + ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   if (row >= V) return;
   // a long row sums its piece partials (in piece order) instead of its tokens
   const int np = nch[row];
@@ -416,14 +417,15 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_sliced_kernel(
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E, int NS,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
     float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev,
-    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial) {
+    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial,
+    int64_t row_lo) {
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
   const int xg = blockIdx.x & 7, gps = 8 / NS;
   const int slice = xg % NS;
   const int64_t rb = (int64_t)(blockIdx.x >> 3) * gps + xg / NS;
-  const int64_t row = (rb * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  const int64_t row = row_lo + (rb * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   if (row >= V) return;
   const int col = slice * LPR + c;  // float4 index inside the row
   const int np = nch[row];
@@ -478,9 +480,10 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_generic_kernel(
     const int32_t* __restrict__ vals, const float* __restrict__ gs, int64_t V, int E,
     float* __restrict__ grad, float* __restrict__ param, float* __restrict__ exp_avg,
     float* __restrict__ exp_avg_sq, AdamArgs aa, const AdamArgs* __restrict__ aa_dev,
-    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial) {
+    const int32_t* __restrict__ nch, const int32_t* __restrict__ piece_off, const float* __restrict__ partial,
+    int64_t row_lo) {
   const int lane = lane_id();
-  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t row = row_lo + (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (row >= V) return;
   if (FUSED && aa_dev) aa = *aa_dev;
   const int np = nch[row];
@@ -658,11 +661,15 @@ bool use_sliced_reduce(int E) {
   return !rows && (E == 256 || E == 512 || E == 1024);
 }
 
+// Rows [row_lo, V) of the table (row_lo > 0: a row range of the dense gradient; `grad` then
+// points at row 0's position, so row r lands at grad + r * E).
 template <bool FUSED>
 int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, float* m, float* v,
-                  const AdamArgs& aa, const AdamArgs* aa_dev, hipStream_t s) {
+                  const AdamArgs& aa, const AdamArgs* aa_dev, hipStream_t s, int64_t row_lo = 0) {
+  const int64_t nrows = V - row_lo;
+  if (nrows <= 0) return TT_OK;
   auto grid_for = [&](int rpi) {
-    const int64_t waves = (V + rpi - 1) / rpi;
+    const int64_t waves = (nrows + rpi - 1) / rpi;
     return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
   };
   const dim3 block(kBlock);
@@ -671,9 +678,9 @@ int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, f
     // are dealt to 8 / NS = 2 block groups, the grid padded to whole groups of 8 blocks
     constexpr int NS = 4;
     const int LPR = E / (4 * NS);
-    const int64_t rpb = kWavesPerBlock * (kWave / LPR), rbs = (V + rpb - 1) / rpb, gps = 8 / NS;
+    const int64_t rpb = kWavesPerBlock * (kWave / LPR), rbs = (nrows + rpb - 1) / rpb, gps = 8 / NS;
     const dim3 grid((unsigned)(((rbs + gps - 1) / gps) * 8));
-#define TT_SL(L) bag_bwd_reduce_sliced_kernel<L, 4, FUSED, true><<<grid, block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, NS, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial)
+#define TT_SL(L) bag_bwd_reduce_sliced_kernel<L, 4, FUSED, true><<<grid, block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, NS, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo)
     if (LPR == 16) TT_SL(16);
     else if (LPR == 32) TT_SL(32);
     else TT_SL(64);
@@ -682,12 +689,12 @@ int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, f
     return TT_OK;
   }
   switch (E) {
-    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
-    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
-    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
-    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
-    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
-    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial); break;
+    case 64: bag_bwd_reduce_kernel<16, 1, 4, FUSED><<<grid_for(4), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo); break;
+    case 128: bag_bwd_reduce_kernel<32, 1, 4, FUSED><<<grid_for(2), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo); break;
+    case 256: bag_bwd_reduce_kernel<64, 1, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo); break;
+    case 512: bag_bwd_reduce_kernel<64, 2, 4, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo); break;
+    case 1024: bag_bwd_reduce_kernel<64, 4, 2, FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo); break;
+    default: bag_bwd_reduce_generic_kernel<FUSED><<<grid_for(1), block, 0, s>>>(w.seg_start, w.seg_end, w.vals_out, w.gs, V, E, grad, param, m, v, aa, aa_dev, w.nch, w.piece_off, w.partial, row_lo); break;
   }
   TT_LAUNCH_CHECK("bag_bwd_reduce");
   return TT_OK;
@@ -737,23 +744,34 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   return TT_OK;
 }
 
+// apply, first half: gs = dpooled / denom (denom NULL: the caller passed gs itself) and the long
+// rows' piece sums.  Returns the workspace view whose gs the reduce reads.
+int apply_prepare(const float* dpooled, const float* denom, int64_t nseq, int64_t V, int E, const BwdWs& w,
+                  BwdWs& wa, hipStream_t s, bool launch = true) {
+  wa = w;
+  if (nseq > 0) {
+    if (denom) {
+      if (launch) {
+        bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
+            dpooled, denom, nseq, E, w.gs);
+        TT_LAUNCH_CHECK("bag_scale_rows");
+      }
+    } else {
+      wa.gs = const_cast<float*>(dpooled);
+    }
+    if (launch) return launch_piece_sum(wa, V, E, s);
+  }
+  return TT_OK;
+}
+
 // apply: gs = dpooled / denom, then the row reduce (dense gradient or fused AdamW).
 template <bool FUSED>
 int apply_plan(const float* dpooled, const float* denom, int64_t nseq, int64_t V, int E, const BwdWs& w,
                float* grad, float* param, float* m, float* v, const AdamArgs& aa, const AdamArgs* aa_dev,
                hipStream_t s) {
-  BwdWs wa = w;
-  if (nseq > 0) {
-    if (denom) {
-      bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
-          dpooled, denom, nseq, E, w.gs);
-      TT_LAUNCH_CHECK("bag_scale_rows");
-    } else {
-      wa.gs = const_cast<float*>(dpooled);  // the caller passed gs = d_pooled / denom itself
-    }
-    int rc = launch_piece_sum(wa, V, E, s);
-    if (rc) return rc;
-  }
+  BwdWs wa;
+  int rc = apply_prepare(dpooled, denom, nseq, V, E, w, wa, s);
+  if (rc) return rc;
   return launch_reduce<FUSED>(wa, V, E, grad, param, m, v, aa, aa_dev, s);
 }
 
@@ -839,6 +857,38 @@ extern "C" int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom
   AdamArgs aa{};
   return apply_impl<false>(d_pooled, denom, nseq, L, V, E, const_cast<void*>(plan), plan_bytes, grad_table, nullptr,
                            nullptr, nullptr, aa, nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_bag_mean_bwd_planned_prepare(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                               int64_t V, int E, void* plan, size_t plan_bytes, tt_stream_t stream) {
+  TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
+  TT_REQUIRE(nseq == 0 || d_pooled, "null pointer");
+  const BwdWs w = plan_layout(plan, nseq, L, V, E);
+  TT_REQUIRE(plan != nullptr && w.total + 256 <= plan_bytes, "plan workspace too small: need %zu have %zu",
+             w.total + 256, plan_bytes);
+  BwdWs wa;
+  return apply_prepare(d_pooled, denom, (nseq == 0 || L == 0) ? 0 : nseq, V, E, w, wa,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_bag_mean_bwd_planned_rows(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                            int64_t V, int E, const void* plan, size_t plan_bytes, int64_t row_begin,
+                                            int64_t row_end, float* grad_rows, tt_stream_t stream) {
+  TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
+  TT_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= V, "rows [%lld, %lld) outside [0, %lld)",
+             (long long)row_begin, (long long)row_end, (long long)V);
+  TT_REQUIRE(grad_rows && (nseq == 0 || d_pooled), "null pointer");
+  const BwdWs w = plan_layout(const_cast<void*>(plan), nseq, L, V, E);
+  TT_REQUIRE(plan != nullptr && w.total + 256 <= plan_bytes, "plan workspace too small: need %zu have %zu",
+             w.total + 256, plan_bytes);
+  BwdWs wa;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc = apply_prepare(d_pooled, denom, (nseq == 0 || L == 0) ? 0 : nseq, V, E, w, wa, s, false);
+  if (rc) return rc;
+  AdamArgs aa{};
+  // row r of the range lands at grad_rows + (r - row_begin) * E
+  return launch_reduce<false>(wa, row_end, E, grad_rows - row_begin * (int64_t)E, nullptr, nullptr, nullptr, aa,
+                              nullptr, s, row_begin);
 }
 
 extern "C" int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,

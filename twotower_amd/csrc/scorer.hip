@@ -489,6 +489,14 @@ __device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int 
 #endif
 template <int H>
 constexpr int kSdFor = TT_SD < H / 8 ? TT_SD : H / 8;  // <= NSTEP: never past the next unit
+// Where the softmax map of X tile j runs: TT_FWD_MAP_S=1 puts all 16 slots beside the S chain of
+// tile j+1 (the Acc chain then carries only its operand reads, the P stores and the fills);
+// 0 splits them 8 + 8 between the S chain and the first half of the Acc chain.  Same arithmetic
+// in the same order either way.
+#ifndef TT_FWD_MAP_S
+#define TT_FWD_MAP_S 0
+#endif
+constexpr bool kMapInS = TT_FWD_MAP_S != 0;
 
 #ifdef TT_S_BUILTIN  // diagnostic: the S chain through the builtin (compiler-placed accumulators)
 __device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
@@ -562,10 +570,13 @@ __device__ __forceinline__ void fwd_unit(const UnitSrc<H>& u, const LdsOffs<H>& 
       if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op, bl[s2], acc[ht], 0, 0, 0);
     }
     ring[i % kSd] = unit_operand<H>(i + kSd, u, lo);
-    if (i < NK) {
+    if (kMapInS && i < NK) {  // all 16 map slots beside the S chain (one exp per MFMA gap at H = 256)
+#pragma unroll
+      for (int v = 16 * i / NK; v < 16 * (i + 1) / NK; ++v) ms.slot(v, xa, bh, bl);
+    } else if (i < NK) {
 #pragma unroll
       for (int v = 8 * i / NK; v < 8 * (i + 1) / NK; ++v) ms.slot(v, xa, bh, bl);
-    } else if (i - NK < NHT) {  // map slots 8-15 (G rows 16-31, first used at Acc step NHT)
+    } else if (!kMapInS && i - NK < NHT) {  // map slots 8-15 (G rows 16-31, first used at Acc step NHT)
       const int st = i - NK;
 #pragma unroll
       for (int v = 8 + 8 * st / NHT; v < 8 + 8 * (st + 1) / NHT; ++v) ms.slot(v, xa, bh, bl);
@@ -1264,6 +1275,176 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Stored-P backward with two waves per SIMD (8-wave workgroups, 128 candidates).  Waves w and
+// w + 4 (one SIMD) own the same 32 candidates and split every 64-row query stage: wave w takes
+// its first 32-row tile, wave w + 4 the second, so each wave issues 16 MFMAs, 2 P loads and 4
+// fill pieces per stage.  In the one-wave engine every vector-memory instruction stalls the
+// only wave of its SIMD (40-75 cycles each while all waves issue them); here the
+// partner's MFMAs run through those stalls.  The pair's dD^T accumulators (the same 32
+// candidates over disjoint queries) are added through LDS at the end: acc(w) + acc(w + 4).
+// Per stage t (steps 0..NS-1 of this wave's tile): P(t+3) and fills(t+2) are issued before the
+// stage barrier at step NS - kDd, which waits for fills(t+1) (vmcnt: this stage's 2 + NPC ops may
+// stay in flight) in every wave; after it the operand reads run ahead into stage t+1.  fills(t+2)
+// go into buffer (t+2) & 3, last read in stage t-2, which every wave left behind at the barrier
+// of stage t-1.
+template <int H>
+__global__ __launch_bounds__(2 * NT, 2) void score_ddp2_kernel(const __bf16* __restrict__ R, int64_t nR, int64_t nC,
+                                                              int S, int64_t rows_per_split, const char* __restrict__ P,
+                                                              int64_t p_nqt, float* __restrict__ acc_part) {
+  using T = Tile<__bf16, H>;
+  constexpr int NHT = H / 32;
+  constexpr int NS = 2 * NHT;                   // MFMA steps per 32-row tile (and per stage)
+  constexpr int NW2 = 2 * NW;                   // waves per workgroup
+  constexpr int NPC = T::STAGE_B / 1024 / NW2;  // fill pieces per stage per wave
+  static_assert(NPC * 1024 * NW2 == T::STAGE_B && T::BJ == 64 && T::NSTAGE == 4, "8 waves over 64-row stages");
+  constexpr int kDd = kSdFor<H> < NS ? kSdFor<H> : NS;
+  constexpr int BAR = NS - kDd;  // the stage barrier: before the first read of stage t+1
+  static_assert(BAR >= 4, "the stage's VMEM issue slots sit before the barrier");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;
+
+  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wc = wid & (NW - 1), jt = wid / NW;  // candidate tile of the pair, query tile of the stage
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t ct = cb * NW + wc;
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
+
+  unsigned fo[NPC];
+#pragma unroll
+  for (int c = 0; c < NPC; ++c) {
+    const int p = (c * NW2 + wid) * 1024 + lane * 16;
+    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
+    fo[c] = (unsigned)(row * T::ROWB + ((slot ^ T::swz(row)) << 4));
+  }
+  LdsOffs<H> lo;
+  lo.init(lane);
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
+  auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
+  auto fill = [&](int c, int b, int64_t r0) {
+    glds_dwordx4_s(fo[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW2 * 1024);
+  };
+  const char* pcol = P + ct * p_nqt * 2048;
+  const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
+  struct PSet {
+    bf16x8 v[2];
+  };
+  PSet pf[5];
+  auto pload = [&](PSet& dst, int64_t t, int k) {
+    const char* b = pcol + (stage_row(t) / 32 + jt) * 2048;
+    if (k == 0) dst.v[0] = p_load<0>(b, pvo);
+    else dst.v[1] = p_load<1>(b, pvo);
+  };
+  auto tie = [&](PSet& x) {
+    asm volatile("" : "+v"(x.v[0]));
+    asm volatile("" : "+v"(x.v[1]));
+  };
+  // prologue in steady-state issue order: P(0); [P(1), fills(0)]; [P(2), fills(1)]
+  pload(pf[0], 0, 0);
+  pload(pf[0], 0, 1);
+#pragma unroll
+  for (int k = 1; k < 3; ++k) {
+    pload(pf[k], k, 0);
+    pload(pf[k], k, 1);
+#pragma unroll
+    for (int c = 0; c < NPC; ++c) fill(c, k - 1, stage_row(k - 1));
+  }
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  // fills(0) and P(0), P(1) landed: P(2) and fills(1) may be in flight
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + NPC) : "memory");
+  __syncthreads();
+  tie(pf[0]);
+
+  auto opnd = [&](const lds_char_t* stile, int i) {  // A operand of step i of this wave's tile of a stage
+    const int s2 = i / NHT, ht = i % NHT;
+    const lds_char_t* tb = stile + jt * 32 * T::ROWB;
+    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
+    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
+    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+  };
+  bf16x8 ring[kDd];
+#pragma unroll
+  for (int k = 0; k < kDd; ++k) ring[k] = opnd(lds, k);
+  auto stage = [&](int64_t t, PSet& cur, PSet& ahead, PSet& next) {
+    const int buf = (int)(t & 3), fbuf = (buf + 2) & 3;
+    const int64_t frow = stage_row(t + 2);
+    const lds_char_t* tile = lds + buf * T::STAGE_B;
+    const lds_char_t* ntile = lds + ((buf + 1) & 3) * T::STAGE_B;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      if (i == BAR) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + NPC) : "memory");
+        asm volatile("s_barrier" ::: "memory");
+        tie(next);
+      }
+      const int s2 = i / NHT, ht = i % NHT;
+      acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[i % kDd], cur.v[s2], acc[ht], 0, 0, 0);
+      const int j = i + kDd;
+      ring[i % kDd] = j < NS ? opnd(tile, j) : opnd(ntile, j - NS);
+      // this stage's VMEM, all before the barrier: P(t+3) at steps 0 and BAR / 2, fills(t+2) between
+      if (i == 0) pload(ahead, t + 3, 0);
+      if (i == BAR / 2) pload(ahead, t + 3, 1);
+#pragma unroll
+      for (int c = 0; c < NPC; ++c)
+        if (i == 1 + c * (BAR - 1) / NPC + (1 + c * (BAR - 1) / NPC == BAR / 2 ? 1 : 0)) fill(c, fbuf, frow);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // full rounds of five stages, then the rest as nested conditionals (score_ddp_kernel: no register
+  // set is dead on any path while its load is in flight)
+  int64_t t = 0;
+  for (; t + 5 <= ntiles; t += 5) {
+    stage(t, pf[0], pf[3], pf[1]);
+    stage(t + 1, pf[1], pf[4], pf[2]);
+    stage(t + 2, pf[2], pf[0], pf[3]);
+    stage(t + 3, pf[3], pf[1], pf[4]);
+    stage(t + 4, pf[4], pf[2], pf[0]);
+  }
+  if (t < ntiles) {
+    stage(t, pf[0], pf[3], pf[1]);
+    if (t + 1 < ntiles) {
+      stage(t + 1, pf[1], pf[4], pf[2]);
+      if (t + 2 < ntiles) {
+        stage(t + 2, pf[2], pf[0], pf[3]);
+        if (t + 3 < ntiles) stage(t + 3, pf[3], pf[1], pf[4]);
+      }
+    }
+  }
+  drain_dma();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 5; ++k) tie(pf[k]);
+  __syncthreads();  // every wave's LDS-DMA landed and its reads of the ring done: the ring is free
+  // pair sum through LDS (the ring's first 4 x 32 KB): acc(w) + acc(w + 4), in that order
+  lds_f32x4_t* xch = (lds_f32x4_t*)((lds_char_t*)smem) + wc * (NHT * 4 * kWave);
+  if (jt == 1) {
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        xch[(ht * 4 + g) * kWave + lane] = f32x4{acc[ht][4 * g], acc[ht][4 * g + 1], acc[ht][4 * g + 2], acc[ht][4 * g + 3]};
+  }
+  __syncthreads();
+  if (jt == 0) {
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 o = xch[(ht * 4 + g) * kWave + lane];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[ht][4 * g + u] += o[u];
+      }
+    write_partials<DD, H>(acc, 0.f, split, nC, ct * 32 + r32, hh, acc_part, nullptr);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // fp32 engine (exact f32 MFMA, 32x32x2).  The k order inside the X product is permuted
 // (k = 8*blk + 4*hh + u) so each lane reads one 16-byte chunk per four MFMAs; the Acc product
 // consumes X register t directly as its B operand (k = row of X held by register t).
@@ -1453,13 +1634,17 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
 // the normalised row then takes prep_rows' path (bf16 copy, its norm, the per-block max) from the
 // registers, so the scorer's prep pass and its 25 MB re-read disappear.  Same block partition
 // and arithmetic as prep_qd_kernel + head_normalize_kernel: the workspace is bit-identical.
+// One block of kL2PrepWaves waves: the grid keeps prep_qd_kernel's block counts (the candidate
+// blocks' maxima are what the engines fold), but 16-wave blocks put 4x the rows in flight: with
+// 4-wave blocks the pass ran 20 us for 63 MB (each wave walked 4-8 rows in dependent rounds).
+constexpr int kL2PrepWaves = 16;
 __device__ __forceinline__ void l2_prep_rows(float* __restrict__ x, int64_t rows, __bf16* __restrict__ xb,
                                              float* __restrict__ norms, float* __restrict__ pnorms, int64_t b0,
                                              int64_t nb, float& mx) {
-  constexpr int H = 4 * kWave, U = 4;
+  constexpr int H = 4 * kWave, U = 2;
   const int lane = lane_id(), wid = threadIdx.x >> 6;
-  const int64_t step = nb * 4;
-  for (int64_t r0 = b0 * 4 + wid; r0 < rows; r0 += U * step) {
+  const int64_t step = nb * kL2PrepWaves;
+  for (int64_t r0 = b0 * kL2PrepWaves + wid; r0 < rows; r0 += U * step) {
     f32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1501,13 +1686,13 @@ __device__ __forceinline__ void l2_prep_rows(float* __restrict__ x, int64_t rows
   }
 }
 
-__global__ __launch_bounds__(256) void l2_prep_kernel(float* __restrict__ y, int64_t B, int64_t M, int gq,
+__global__ __launch_bounds__(64 * kL2PrepWaves) void l2_prep_kernel(float* __restrict__ y, int64_t B, int64_t M, int gq,
                                                       float* __restrict__ norms, __bf16* __restrict__ qb,
                                                       __bf16* __restrict__ db, float* __restrict__ qnorm,
                                                       float* __restrict__ dmax_part, char* __restrict__ pad,
                                                       float* __restrict__ lse2, int* __restrict__ xrows) {
   constexpr int H = 4 * kWave;
-  __shared__ float wmax[4];
+  __shared__ float wmax[kL2PrepWaves];
   if (blockIdx.x == 0) {  // prep_qd_kernel's block-0 set-up
     if (xrows && threadIdx.x == 0) xrows[0] = 0;
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
@@ -1531,7 +1716,12 @@ __global__ __launch_bounds__(256) void l2_prep_kernel(float* __restrict__ y, int
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   if (lane == 0) wmax[wid] = mx;
   __syncthreads();
-  if (threadIdx.x == 0) dmax_part[b] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  if (threadIdx.x == 0) {
+    float m = wmax[0];
+#pragma unroll
+    for (int k = 1; k < kL2PrepWaves; ++k) m = fmaxf(m, wmax[k]);
+    dmax_part[b] = m;
+  }
 }
 
 // One matrix: optional bf16 copy (with a kTailRows zero tail written by block 0), optional row
@@ -1874,6 +2064,18 @@ int64_t p_nct_for(int64_t M) { return (M + 255) / 256 * 8; }  // also the 256-ca
 #define TT_DDP_CW256 1  // CW = 2 runs the loop ~15 % faster but doubles the split partials (S = 4): net slower (round 2)
 #endif
 int ddp_cw(int H) { return H == 256 ? TT_DDP_CW256 : 1; }
+// H = 256 stored-P backward at two waves per SIMD (score_ddp2_kernel); TT_DDP_W2=0 (read at load)
+// selects the one-wave engine
+#ifndef TT_DDP_W2_DEFAULT
+#define TT_DDP_W2_DEFAULT 1
+#endif
+bool ddp_w2() {
+  static const bool on = [] {
+    const char* e = std::getenv("TT_DDP_W2");
+    return (e ? std::strcmp(e, "0") != 0 : TT_DDP_W2_DEFAULT != 0) && TT_DDP_CW256 == 1;
+  }();
+  return on;
+}
 Plan ddp_plan(int64_t B, int64_t M, int H) {
   return plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H, TT_BF16, DD), 32 * NW * ddp_cw(H));
 }
@@ -2067,7 +2269,15 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
     TT_DDP(32, 1)
     TT_DDP(64, 1)
     TT_DDP(128, 1)
-    TT_DDP(256, TT_DDP_CW256)
+    case 256:
+      if (ddp_w2()) {
+        score_ddp2_kernel<256><<<dim3(p.grid), dim3(2 * NT), Tile<__bf16, 256>::LDS_BYTES, s>>>(
+            Qs, B, M, p.S, p.rows_per_split, P, p_nqt, acc_part);
+        break;
+      }
+      score_ddp_kernel<256, TT_DDP_CW256><<<dim3(p.grid), dim3(NT), Tile<__bf16, 256>::LDS_BYTES, s>>>(
+          Qs, B, M, p.S, p.rows_per_split, P, p_nqt, acc_part);
+      break;
 #undef TT_DDP
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }
@@ -2178,7 +2388,7 @@ extern "C" int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dty
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   const int gq = prep_blocks_q(B), gd = prep_blocks_d(M);
-  l2_prep_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+  l2_prep_kernel<<<dim3((unsigned)(gq + gd)), dim3(64 * kL2PrepWaves), 0, reinterpret_cast<hipStream_t>(stream)>>>(
       y, B, M, gq, norms, w.Qb, w.Db, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows);
   TT_LAUNCH_CHECK("score_l2_prep");
   return TT_OK;

@@ -12,15 +12,24 @@ the step needs:
     reduce-scattered by row range, each rank runs AdamW on its own 1/world of the rows (and keeps
     only that shard's moments), and the updated rows are all-gathered in place -- the same bytes
     on the links as an all-reduce, 1/world of the optimizer's 24 B/param HBM traffic per rank.
+    The rows go in chunks with interleaved ownership, so chunk c's exchange runs on a
+    communication stream while the gradient of chunk c + 1 is formed.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
 
 
 def is_active(group=None) -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    """Data-parallel exchanges on: more than one rank, or TT_DIST_FORCE=1 with any initialised
+    group (a one-rank rehearsal of every collective of the N-rank step, e.g. RCCL under HIP-graph
+    capture on a one-GPU box: bench.py --force-dist)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or os.environ.get("TT_DIST_FORCE") == "1"
 
 
 def table_sync_mode(requested: str, group=None) -> str:
@@ -66,20 +75,34 @@ def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: 
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
+def shard_chunks(V: int, world: int) -> int:
+    """Row chunks of the pipelined sharded-table exchange (TT_SHARD_CHUNKS, default 8): chunk c's
+    reduce-scatter, AdamW and all-gather run on a communication stream while the gradient rows of
+    chunk c + 1 are formed.  1 = one exchange after the whole gradient."""
+    n = int(os.environ.get("TT_SHARD_CHUNKS", "8"))
+    return max(1, min(n, V // max(1, world)))
+
+
 class ShardedRows:
     """Row partition of a (V, E) table over the ranks of `group` for the sharded table optimizer.
 
-    The parameter's storage is padded to Vp = world * ceil(V / world) rows (the padding rows stay
-    zero and are never read by a lookup), so rank r owns rows [r*Vs, (r+1)*Vs) and both
-    collectives move equal, contiguous slabs."""
+    The rows are cut into NC chunks of world * R rows, and rank r owns rows
+    [c*Cr + r*R, c*Cr + (r+1)*R) of every chunk c (Cr = world * R): interleaved ownership, so each
+    chunk's reduce-scatter and all-gather move one contiguous slab per rank and can start as
+    soon as that chunk's gradient rows exist (optim.AdamW pipelines them).  The parameter's
+    storage is padded to Vp = NC * Cr rows (the padding rows stay zero and are never read by a
+    lookup); this rank's moments are its Vs = NC * R own rows, chunk-major."""
 
-    def __init__(self, weight: torch.Tensor, group=None):
+    def __init__(self, weight: torch.Tensor, group=None, chunks: int | None = None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.V, self.E = weight.shape
-        self.Vs = -(-self.V // self.world)
-        self.Vp = self.Vs * self.world
+        self.NC = chunks or shard_chunks(self.V, self.world)
+        self.R = -(-self.V // (self.NC * self.world))
+        self.Cr = self.R * self.world
+        self.Vp = self.NC * self.Cr
+        self.Vs = self.NC * self.R
         base = weight.data
         room = base.untyped_storage().nbytes() // base.element_size() - base.storage_offset()
         if not base.is_contiguous() or room < self.Vp * self.E:
@@ -87,15 +110,39 @@ class ShardedRows:
             padded[:self.V].copy_(base)
             weight.data = padded[:self.V]
         self.weight = weight
+        self._bufs = None
+        self._comm = None
 
     def storage(self) -> torch.Tensor:
         """The (Vp, E) tensor the parameter is a view of."""
         w = self.weight.data
         return w if self.Vp == self.V else torch.as_strided(w, (self.Vp, self.E), (self.E, 1))
 
+    def chunk(self, c: int) -> tuple[int, int]:
+        """Rows [lo, hi) of chunk c in the (Vp, E) layout."""
+        return c * self.Cr, (c + 1) * self.Cr
+
+    def own(self, t: torch.Tensor, c: int) -> torch.Tensor:
+        """This rank's slab of chunk c of a (Vp, E) tensor (a view)."""
+        lo = c * self.Cr + self.rank * self.R
+        return t[lo:lo + self.R]
+
+    def shard_chunk(self, t: torch.Tensor, c: int) -> torch.Tensor:
+        """Chunk c of a (Vs, E) per-rank tensor (a view)."""
+        return t[c * self.R:(c + 1) * self.R]
+
     def rows(self, t: torch.Tensor) -> torch.Tensor:
-        """This rank's slab of a (Vp, E) tensor."""
-        return t[self.rank * self.Vs:(self.rank + 1) * self.Vs]
+        """This rank's rows of a (Vp, E) tensor as a (Vs, E) tensor, chunk-major (a view for one
+        chunk, a copy otherwise)."""
+        if self.NC == 1:
+            return self.own(t, 0)
+        return t.view(self.NC, self.world, self.R, -1)[:, self.rank].reshape(self.Vs, -1)
+
+    def gather_full(self, shard: torch.Tensor) -> torch.Tensor:
+        """The (Vp, E) tensor whose own rows on every rank are that rank's (Vs, E) shard."""
+        buf = shard.new_empty(self.world * self.Vs, shard.shape[1])
+        all_gather_rows(buf, shard.contiguous(), self.group)
+        return buf.view(self.world, self.NC, self.R, -1).transpose(0, 1).reshape(self.Vp, -1)
 
     def new_grad_buffer(self) -> torch.Tensor:
         g = torch.empty(self.Vp, self.E, dtype=torch.float32, device=self.weight.device)
@@ -103,14 +150,31 @@ class ShardedRows:
             g[self.V:].zero_()
         return g
 
-    def reduce_scatter(self, gbuf: torch.Tensor) -> torch.Tensor:
-        shard = torch.empty(self.Vs, self.E, dtype=gbuf.dtype, device=gbuf.device)
-        reduce_scatter_rows(shard, gbuf, self.group)
+    def step_buffers(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """Persistent (gradient (Vp, E), reduced shard (Vs, E)) buffers of the pipelined update
+        (fixed addresses, so the step can be captured in a HIP graph)."""
+        if self._bufs is None:
+            self._bufs = (self.new_grad_buffer(),
+                          torch.empty(self.Vs, self.E, dtype=torch.float32, device=self.weight.device))
+        return self._bufs
+
+    def comm_stream(self) -> torch.cuda.Stream:
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=self.weight.device)
+        return self._comm
+
+    def reduce_scatter(self, gbuf: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        shard = torch.empty(self.Vs, self.E, dtype=gbuf.dtype, device=gbuf.device) if out is None else out
+        for c in range(self.NC):
+            lo, hi = self.chunk(c)
+            reduce_scatter_rows(self.shard_chunk(shard, c), gbuf[lo:hi], self.group)
         return shard
 
     def all_gather_params(self) -> None:
         st = self.storage()
-        all_gather_rows(st, self.rows(st), self.group)
+        for c in range(self.NC):
+            lo, hi = self.chunk(c)
+            all_gather_rows(st[lo:hi], self.own(st, c), self.group)
 
 
 class AllGatherRows(torch.autograd.Function):

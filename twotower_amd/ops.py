@@ -162,6 +162,27 @@ def bag_mean_backward_planned(d_pooled: torch.Tensor, denom: torch.Tensor, plan:
     return grad
 
 
+def bag_mean_backward_planned_prepare(d_pooled: torch.Tensor, denom: torch.Tensor | None, plan: BagPlan) -> None:
+    """First half of a row-range table gradient (tt_bag_mean_bwd_planned_prepare): the scaled rows
+    and the long rows' piece sums, into the plan workspace; then bag_mean_backward_planned_rows."""
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    plan.wait()
+    call("tt_bag_mean_bwd_planned_prepare", ptr(d_pooled), ptr(denom), plan.nseq, plan.L, plan.V, plan.E,
+         ptr(plan.buf), plan.buf.numel(), stream_of(d_pooled))
+
+
+def bag_mean_backward_planned_rows(d_pooled: torch.Tensor, denom: torch.Tensor | None, plan: BagPlan, row_begin: int,
+                                   row_end: int, out: torch.Tensor) -> torch.Tensor:
+    """Rows [row_begin, row_end) of the dense table gradient into `out` ((row_end - row_begin, E)
+    contiguous float32), after bag_mean_backward_planned_prepare on the same stream."""
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    if tuple(out.shape) != (row_end - row_begin, plan.E) or not out.is_contiguous() or out.dtype != _FLOAT:
+        raise ValueError("out must be a contiguous float32 (row_end - row_begin, E) tensor")
+    call("tt_bag_mean_bwd_planned_rows", ptr(d_pooled), ptr(denom), plan.nseq, plan.L, plan.V, plan.E, ptr(plan.buf),
+         plan.buf.numel(), int(row_begin), int(row_end), ptr(out), stream_of(d_pooled))
+    return out
+
+
 class DeferredTableGrad:
     """Table gradient kept in its factored form (ids, d_pooled, denom, plan) so a fused optimizer
     can apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer.

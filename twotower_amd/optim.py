@@ -113,9 +113,7 @@ class AdamW(torch.optim.Optimizer):
                 continue
             st = sd["state"][index[id(p)]] = dict(st)  # the packed dict aliases the live state
             for k in ("exp_avg", "exp_avg_sq"):
-                full = st[k].new_empty(sh.Vp, sh.E)
-                distributed.all_gather_rows(full, st[k].contiguous(), sh.group)
-                st[k] = full[:sh.V].clone()
+                st[k] = sh.gather_full(st[k])[:sh.V].clone()
         return sd
 
     def load_state_dict(self, state_dict) -> None:
@@ -181,10 +179,9 @@ class AdamW(torch.optim.Optimizer):
                     ids, dp, den, plan = _gather_parts((ids, dp, den, plan), deferred.gather_group)
                 sh = self._shards.get(id(p))
                 if sh is not None:
-                    g_shard = self._table_grad_shard(sh, dp, den, plan)
-                    ops.adamw_step(sh.rows(sh.storage()), g_shard, st["exp_avg"], st["exp_avg_sq"], lr=lr,
-                                   beta1=b1, beta2=b2, eps=eps, weight_decay=wd, step=int(st["step"]))
-                    sh.all_gather_params()
+                    args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
+                    self._shard_update(sh, (ids, dp, den, plan), st, args)
+                    torch.cuda.current_stream(p.device).wait_stream(sh.comm_stream())
                     continue
                 args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
                 ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"], args)
@@ -201,7 +198,7 @@ class AdamW(torch.optim.Optimizer):
     def _step_device(self, group: dict) -> None:
         """Capturable form: one tt_adam_prepare launch, one multi-tensor launch per 16 dense
         parameters, one fused scatter + AdamW launch per table."""
-        slots, dense, fused, gathers, dense_ids = [], [], [], [], []
+        slots, dense, fused, shards, dense_ids = [], [], [], [], []
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
             if deferred is not None and deferred.parts:
@@ -211,11 +208,8 @@ class AdamW(torch.optim.Optimizer):
                 parts = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
                 sh = self._shards.get(id(p))
-                if sh is not None:  # data parallel: reduce-scatter, AdamW on own rows, all-gather
-                    g_shard = self._table_grad_shard(sh, parts[1], parts[2], parts[3])
-                    dense.append((sh.rows(sh.storage()), g_shard, st["exp_avg"], st["exp_avg_sq"], a))
-                    dense_ids.append(None)
-                    gathers.append(sh)
+                if sh is not None:  # data parallel: chunked reduce-scatter, AdamW on own rows, all-gather
+                    shards.append((sh, parts, st, a))
                 else:
                     if deferred.gather_group is not None:  # data parallel: every rank's factored grad
                         parts = _gather_parts(parts, deferred.gather_group)
@@ -260,6 +254,14 @@ class AdamW(torch.optim.Optimizer):
         for p, st, (ids, dp, den, plan) in fused:
             ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
                                                 self._adam_args(p))
+        # data parallel, row-sharded tables: the chunk-pipelined exchange (its collectives are
+        # issued before the tower all-reduce, so they lead on the communicator)
+        for sh, parts, st, a in shards:
+            self._shard_update(sh, parts, st, a)
+
+        def join_shards():  # the chunk updates read this step's scalars on their own stream: the
+            for sh, _, _, _ in shards:  # next step's scalars (and the next forward) wait for them
+                torch.cuda.current_stream(sh.weight.device).wait_stream(sh.comm_stream())
         # data parallel: the tower-gradient all-reduce, issued after the table's collectives and
         # the table update, overlaps that update on a communication stream; the join waits for it
         self._launch_grad_sync()
@@ -278,27 +280,54 @@ class AdamW(torch.optim.Optimizer):
             if ticket is None:
                 ticket = self._tickets[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
             in_launch = ahead and os.environ.get("TT_FUSED_PREPARE", "0") == "1"
+            if in_launch:
+                join_shards()
             ops.adamw_multi_ex(dense, [parts.get(i) if i is not None else None for i in dense_ids],
                                slots if in_launch else [], lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
                                ticket=ticket)
+            join_shards()
             if ahead and not in_launch:
                 ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
         else:
             ops.adamw_multi(dense)
+            join_shards()
             if ahead:  # counters advanced, next step's scalars formed, behind every update that read them
                 ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
         if ahead:
             for st, _ in slots:
                 self._ahead[id(st)] = (hyper, st)  # the tensor itself: an id alone could be reused
-        for sh in gathers:
-            sh.all_gather_params()
 
     @staticmethod
-    def _table_grad_shard(sh, d_pooled, denom, plan) -> torch.Tensor:
-        """This rank's rows of the summed table gradient (the loss is pre-scaled by 1/world)."""
-        gbuf = sh.new_grad_buffer()
-        ops.bag_mean_backward_planned(d_pooled, denom, plan, out=gbuf[:sh.V])
-        return sh.reduce_scatter(gbuf)
+    def _shard_update(sh, parts, st, args) -> None:
+        """Row-sharded table update under data parallelism (the loss is pre-scaled by 1/world, so
+        the reduce-scattered sums are global-batch mean gradients), pipelined over the row chunks
+        of ShardedRows: the current stream forms chunk c's dense gradient rows
+        (tt_bag_mean_bwd_planned_rows) and hands them to the communication stream, which
+        reduce-scatters them, runs AdamW on this rank's slab (moments: its chunk of the sharded
+        state) and all-gathers the updated slab into every rank's table, while the current stream
+        goes on with chunk c + 1.  The caller joins sh.comm_stream() before anything reads the
+        table or the step scalars `args` again."""
+        _, dp, den, plan = parts
+        dev = dp.device
+        main = torch.cuda.current_stream(dev)
+        comm = sh.comm_stream()
+        gbuf, gsh = sh.step_buffers()
+        stor = sh.storage()
+        ops.bag_mean_backward_planned_prepare(dp, den, plan)
+        for c in range(sh.NC):
+            lo, hi = sh.chunk(c)
+            top = min(hi, sh.V)
+            if lo < top:
+                ops.bag_mean_backward_planned_rows(dp, den, plan, lo, top, gbuf[lo:top])
+            ready = torch.cuda.Event()
+            ready.record(main)
+            comm.wait_event(ready)
+            with torch.cuda.stream(comm):
+                g = sh.shard_chunk(gsh, c)
+                distributed.reduce_scatter_rows(g, gbuf[lo:hi], sh.group)
+                ops.adamw_multi([(sh.own(stor, c), g, sh.shard_chunk(st["exp_avg"], c),
+                                  sh.shard_chunk(st["exp_avg_sq"], c), args)])
+                distributed.all_gather_rows(stor[lo:hi], sh.own(stor, c), sh.group)
 
 
 def _gather_parts(parts, group):

@@ -49,7 +49,10 @@ class TrainStep:
         self._graphs: dict[tuple, tuple] = {}
         self._seed: dict[torch.device, torch.Tensor] = {}  # d(loss) seed of backward, kept on device
 
-    def eager(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
+    def eager(self, queries: torch.Tensor, positive_docs: torch.Tensor,
+              negative_docs: torch.Tensor | None = None) -> torch.Tensor:
+        """One step.  negative_docs None: a (query, positive) pair step -- model(q, p), loss_fn(q, p)
+        (e.g. the in-batch loss over the positives alone)."""
         # forward, backward and step back to back: the optimizer may take gradients computed on
         # a side stream and join them itself (_lib.SideGrads)
         side = getattr(self.optimizer, "_side_grads", None)
@@ -58,8 +61,8 @@ class TrainStep:
             side.active = True
         try:
             with ops.deferred_loss_mean(), self._scorer_prep_open():  # the loss is read after the backward below
-                q, p, n = self.model(queries, positive_docs, negative_docs)
-                loss = self.loss_fn(q, p, n)
+                ins = (queries, positive_docs) if negative_docs is None else (queries, positive_docs, negative_docs)
+                loss = self.loss_fn(*self.model(*ins))
             self.optimizer.zero_grad(set_to_none=True)
             # backward seeded with the (1/world pre-scaled) unit gradient from a resident tensor:
             # no fill / scale kernels per step
@@ -95,17 +98,25 @@ class TrainStep:
         finally:
             self.model.scorer_prep = prev
 
-    def __call__(self, queries: torch.Tensor, positive_docs: torch.Tensor, negative_docs: torch.Tensor) -> torch.Tensor:
+    def __call__(self, queries: torch.Tensor, positive_docs: torch.Tensor,
+                 negative_docs: torch.Tensor | None = None) -> torch.Tensor:
         if not self.graph:
             return self.eager(queries, positive_docs, negative_docs)
-        inputs = (queries, positive_docs, negative_docs)
+        inputs = (queries, positive_docs) if negative_docs is None else (queries, positive_docs, negative_docs)
         key = tuple((tuple(t.shape), t.dtype, t.device) for t in inputs)
         hit = self._graphs.get(key)
         if hit is None:
             if self._eager_left > 0:
                 self._eager_left -= 1
                 return self.eager(*inputs)
-            hit = self._graphs[key] = self._capture(inputs)
+            try:
+                hit = self._graphs[key] = self._capture(inputs)
+            except RuntimeError as e:  # e.g. a collective this backend cannot capture: stay eager
+                import warnings
+
+                warnings.warn(f"TrainStep: HIP graph capture failed ({e}); running the step eagerly")
+                self.graph = False
+                return self.eager(*inputs)
         graph, static_all, static_loss = hit
         if all(t.shape[1:] == inputs[0].shape[1:] and t.dtype == inputs[0].dtype for t in inputs):
             if (all(t.device == static_all.device and t.is_contiguous() for t in inputs) and len(inputs) <= 8
