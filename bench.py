@@ -92,6 +92,34 @@ def pmc_traffic(abi: str, config: str) -> dict:
     return {"traffic": None}
 
 
+def gather_hbm_evidence(config: str, gather: dict | None, V: int, d: int) -> dict | None:
+    """The gather's GB/s with what backs it: the C3 table (205 MB) fits the 256 MiB Infinity
+    Cache, so its algorithmic rate is not an HBM figure; the C5 table (1.02 GB) does not, and the
+    newest committed C5 profile (profiles/<tag>_c5_pmc_traffic.json: FETCH_SIZE x2 + WRITE_SIZE per
+    launch, tools/profile_round.sh --config c5) gives counter-measured bytes over the kernel's
+    time there, plus the C5 table update's counter-to-algorithmic traffic ratio."""
+    import glob
+
+    if gather is None:
+        return None
+    out = {"gbs": gather["achieved"], "table_bytes": V * d * 4, "mall_resident": V * d * 4 <= 256 * 2 ** 20,
+           "basis": "algorithmic bytes / kernel time (HIP events), this run"}
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_c5_pmc_traffic.json")))
+    if files:
+        ops = json.load(open(files[-1])).get("ops", {})
+        g, u = ops.get("tt_bag_mean_fwd"), ops.get("tt_bag_mean_bwd_adamw_planned")
+        if g and g.get("device_us_per_step"):
+            out["c5_counter_gbs"] = round(g["hbm_bytes_per_call"] / (g["device_us_per_step"] * 1e-6) / 1e9, 1)
+            out["c5_counter_frac"] = round(out["c5_counter_gbs"] / HBM_PEAK_GBS, 4)
+        if u and u.get("hbm_bytes_per_call"):
+            c5 = CONFIGS["c5"]
+            nseq = (2 + c5["negatives"]) * c5["B"]
+            algo = nseq * c5["d"] * 4 + nseq * 4 + 24 * c5["V"] * c5["d"]
+            out["c5_table_update_traffic_ratio"] = round(u["hbm_bytes_per_call"] / algo, 3)
+        out["c5_source"] = os.path.relpath(files[-1], ROOT)
+    return out
+
+
 def normalise_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     """Device time of the head's plain L2-normalise pass on (rows, d): tt_head_gemm with the
     normalise (epi 1) minus without it (epi 4), HIP events on the launch stream."""
@@ -322,8 +350,10 @@ def main():
 
         def loss_fn(q, p, n):
             return mn(q, p, n.view(q.shape[0], K, q.shape[1]))
-    # N ranks: the step is captured with its RCCL collectives (gloo cannot be captured)
-    use_graph = args.graph == "on" or (args.graph == "auto" and (not dp or args.dist_backend == "nccl"))
+    # one rank: the step is one HIP graph.  N ranks: eager by default -- capturing the step with
+    # its RCCL collectives segfaulted in hipStreamEndCapture on this image ("graph
+    # capture with RCCL"); --graph on still asks for it
+    use_graph = args.graph == "on" or (args.graph == "auto" and not dp)
     # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
     # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
     opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
@@ -448,6 +478,7 @@ def main():
                    "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if dp else "local"),
                    "hip_graph": use_graph},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
+        "gather_hbm": gather_hbm_evidence(args.config, gather, V, d),
         "roofline": roofline,
         "kernels": kernels,
         "cpu_baseline": cpu,

@@ -348,7 +348,7 @@ int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const 
  * instead of torch.cat). */
 int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int count, void* dst, tt_stream_t stream);
 
-/* ---- tower head GEMMs, E = H = 256 (MeanPoolingTower feed_forward + F.normalize,
+/* ---- tower head GEMMs, E = H in {128, 256} (MeanPoolingTower feed_forward + F.normalize,
  * twotower/encoders.py:38-42,77): fp32 GEMMs run on the bf16 MFMA with each operand split
  * into three bf16 terms (six cross products, fp32-equivalent).
  * tt_head_split: W (N x K fp32, or its transpose) -> three bf16 planes [3][N][K]
@@ -370,15 +370,19 @@ int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_
 /* the four plane sets of one Linear-ReLU-Linear head in one launch, each tt_head_planes_bytes(256,
  * 256) long, in the order W1, W2, W1^T, W2^T (forward operands, then backward operands) */
 int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t stream);
-/* tt_head_wgrad: dW = G^T X (N x N) and, if db is not null, db = column sums of G, for G, X
- * (rows x N fp32): the weight and bias gradients of a head Linear (encoders.py:38-42; autograd's
+/* the same for an E -> H head (W1 H x E, W2 H x H; E, H in {128, 256}): W1 (3 H E bf16), W2
+ * (3 H H), W1^T (3 E H), W2^T (3 H H), consecutive.  tt_head_split_ff = tt_head_split_ff2(.., 256,
+ * 256, ..). */
+int tt_head_split_ff2(const float* W1, const float* W2, int E, int H, void* planes, tt_stream_t stream);
+/* tt_head_wgrad: dW = G^T X (N x N, N in {128, 256}) and, if db is not null, db = column sums of
+ * G, for G, X (rows x N fp32): the weight and bias gradients of a head Linear (encoders.py:38-42; autograd's
  * grad_W = grad_out^T input, grad_b = grad_out.sum(0)).  Deterministic (fixed-order slab sums). */
 size_t tt_head_wgrad_ws_size(int64_t rows, int N);
 int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
                   size_t ws_bytes, tt_stream_t stream);
 /* tt_head_wgrad2: both weight gradients of a Linear-ReLU-Linear head in one launch, as slab
  * partials in ws (tt_head_wgrad2_ws_size bytes): problem 1 (G1, X1), problem 2 (G2, X2), each
- * rows x 256 fp32; tt_head_wgrad2_reduce then writes dW1 = G1^T X1, db1 = colsum G1, dW2, db2
+ * rows x N fp32 (N in {128, 256}); tt_head_wgrad2_reduce then writes dW1 = G1^T X1, db1 = colsum G1, dW2, db2
  * (fixed-order slab sums, deterministic).  The reduce may be queued later on another stream (the
  * partials stay in ws): train_step runs the partials on a side stream beside the table update and
  * the reduce where the optimizer joins it. */

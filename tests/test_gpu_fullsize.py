@@ -240,10 +240,11 @@ def test_c2_step_full_size_at_reference_settings():
 
 def test_c3_step_full_size_at_reference_settings():
     """The C3 training step (V 200k, d 256, L 64, B 8192, bf16 in-batch scorer over 2B
-    candidates) at the reference's AdamW settings: the loss within 1e-5 and the gradients of every
-    parameter against float64 on the same bf16-rounded scorer operands at 5e-5 (about 3x the
-    scorer's measured 1.6e-5, profiles/r02_scorer_error_table.jsonl), then the fused update of
-    a graph-replayed TrainStep against torch.optim.AdamW on the HIP gradients, elementwise."""
+    candidates) at the reference's AdamW settings: the loss within 1e-5; the scorer's operand
+    gradients against float64 on the same bf16-rounded operands at 5e-5 (about 3x its measured
+    1.6e-5, profiles/r02_scorer_error_table.jsonl); every parameter gradient against the float64
+    towers driven by those HIP operand gradients at 1e-5; then the fused update of a
+    graph-replayed TrainStep against torch.optim.AdamW on the HIP gradients, elementwise."""
     import _step_parity
 
     r = _step_parity.run(V, E, L, B, "in_batch", "bf16", grad_tol=5e-5, seed=23, graph=True)

@@ -617,6 +617,26 @@ def test_planned_backward_equals_one_shot(E):
     assert torch.equal(t1, t2) and torch.equal(m1, m2) and torch.equal(v1, v2)
 
 
+@pytest.mark.parametrize("E,denom", [(256, True), (64, True), (48, False), (256, False)])
+def test_planned_backward_row_ranges_equal_whole(E, denom):
+    """The row-range form the sharded exchange uses (tt_bag_mean_bwd_planned_prepare once, then
+    tt_bag_mean_bwd_planned_rows per chunk, in any order and size, hot rows with pieces included)
+    writes exactly the rows of the whole planned gradient, bit for bit; denom None: pre-divided."""
+    rng = np.random.default_rng(24)
+    V, N, L = 3001, 500, 300  # L 300: rows with > 128 tokens take the piece path
+    ids = edge_ids(N, L, V, rng, torch.int32)
+    ids[:40, :200] = 17  # a hot row
+    dp = cuda(rng.standard_normal((N, E)).astype(np.float32))
+    den = cuda((rng.integers(1, L, N) + 1e-9).astype(np.float32)) if denom else None
+    plan = ops.BagPlan(ids, V, E, 0)
+    want = ops.bag_mean_backward_planned(dp, den, plan)
+    ops.bag_mean_backward_planned_prepare(dp, den, plan)
+    got = torch.full((V, E), float("nan"), device=DEV)
+    for lo, hi in ((2000, 3001), (0, 17), (17, 18), (18, 1000), (1000, 2000)):
+        ops.bag_mean_backward_planned_rows(dp, den, plan, lo, hi, got[lo:hi])
+    assert torch.equal(got, want)
+
+
 def test_planned_backward_empty_batch():
     V, E = 50, 64
     ids = torch.zeros(0, 8, dtype=torch.int32, device=DEV)
@@ -923,10 +943,12 @@ def test_layernorm_l2_normalize_vs_torch_fp64(rows, H):
 
 # ---------------------------------------------------------------------------------------------
 # tower head on split-bf16 MFMA GEMMs (E = H = 256)
-@pytest.mark.parametrize("rows", [1, 130, 24576])
-def test_tower_head_vs_oracle(rows):
+@pytest.mark.parametrize("rows,width", [(1, 256), (130, 256), (24576, 256), (288, 256), (1, 128), (130, 128),
+                                        (12288, 128), (300, 128)])
+def test_tower_head_vs_oracle(rows, width):
+    """The hand-written head at both widths (C3 / C5 d = 256, C2 d = 128) against float64."""
     rng = np.random.default_rng(rows)
-    E = H = 256
+    E = H = width
     x = rng.standard_normal((rows, E)).astype(np.float32)
     W1 = (rng.standard_normal((H, E)) / 16).astype(np.float32)
     b1 = (rng.standard_normal(H) / 16).astype(np.float32)
@@ -972,12 +994,13 @@ def test_head_relu_mask_bits(rows):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N", [256, 128])
 @pytest.mark.parametrize("rows", [0, 1, 17, 1000, 24576 + 5])
-def test_head_wgrad_vs_fp64(rows):
+def test_head_wgrad_vs_fp64(rows, N):
     """dW = G^T X and db = colsum(G) (autograd's Linear weight / bias gradients) vs float64."""
     rng = np.random.default_rng(11 + rows)
-    g = rng.standard_normal((rows, 256)).astype(np.float32)
-    x = rng.standard_normal((rows, 256)).astype(np.float32)
+    g = rng.standard_normal((rows, N)).astype(np.float32)
+    x = rng.standard_normal((rows, N)).astype(np.float32)
     dW, db = ops.head_wgrad(cuda(g), cuda(x))
     if rows == 0:
         assert float(dW.abs().max()) == 0.0 and float(db.abs().max()) == 0.0
@@ -988,16 +1011,17 @@ def test_head_wgrad_vs_fp64(rows):
     assert torch.equal(dW, dW2) and torch.equal(db, db2)  # deterministic
 
 
+@pytest.mark.parametrize("N", [256, 128])
 @pytest.mark.parametrize("rows", [0, 1, 200, 24576])
-def test_head_wgrad2_vs_fp64(rows):
+def test_head_wgrad2_vs_fp64(rows, N):
     """Both head weight gradients in one launch (tt_head_wgrad2, slab partials) and their
     fixed-order sums (tt_head_wgrad2_reduce, queued later, here on another stream) vs float64."""
     rng = np.random.default_rng(31 + rows)
-    mats = [rng.standard_normal((rows, 256)).astype(np.float32) for _ in range(4)]
+    mats = [rng.standard_normal((rows, N)).astype(np.float32) for _ in range(4)]
     g1, x1, g2, x2 = (cuda(m) for m in mats)
     ws = ops.head_wgrad2(g1, x1, g2, x2)
-    out = [torch.empty(256, 256, device=DEV), torch.empty(256, device=DEV), torch.empty(256, 256, device=DEV),
-           torch.empty(256, device=DEV)]
+    out = [torch.empty(N, N, device=DEV), torch.empty(N, device=DEV), torch.empty(N, N, device=DEV),
+           torch.empty(N, device=DEV)]
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):

@@ -50,8 +50,8 @@ def test_library_is_gfx950_only():
     (lambda L: L.tt_adamw_multi_ex(None, None, 0, None, 2, 1e-3, 0.9, 0.999, 1e-8, 0.01, None, None),
      "needs slots and a ticket"),
     (lambda L: L.tt_pack_blocks(None, None, 9, None, None), "count=9"),
-    (lambda L: L.tt_head_wgrad2_parts(128, 0, ctypes.byref(ctypes.c_int64()), ctypes.byref(ctypes.c_int64())),
-     "tt_head_wgrad2_parts: N=128"),
+    (lambda L: L.tt_head_wgrad2_parts(64, 0, ctypes.byref(ctypes.c_int64()), ctypes.byref(ctypes.c_int64())),
+     "tt_head_wgrad2_parts: N=64"),
     (lambda L: L.tt_colsum(ctypes.c_void_p(16), 8, 6, ctypes.c_void_p(16), ctypes.c_void_p(16), 1 << 20, None), "cols % 4"),
     (lambda L: L.tt_inbatch_fwd(None, None, 8, 4, 64, 0, 10.0, 0, 1, None, None, None, None, None, 0, None),
      "label"),

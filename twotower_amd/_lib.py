@@ -82,6 +82,7 @@ _SIGNATURES = {
     "tt_head_planes_bytes": (_c_sz, [_c_int, _c_int]),
     "tt_head_split": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "tt_head_split_ff": (_c_int, [_vp, _vp, _vp, _vp]),
+    "tt_head_split_ff2": (_c_int, [_vp, _vp, _c_int, _c_int, _vp, _vp]),
     "tt_head_gemm_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_relu_mask_bytes": (_c_sz, [_c_i64]),
     "tt_head_wgrad_ws_size": (_c_sz, [_c_i64, _c_int]),

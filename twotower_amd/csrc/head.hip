@@ -24,15 +24,24 @@
 namespace tt {
 namespace {
 
-constexpr int kN = 256, kK = 256;  // the specialised head width
 constexpr int kColsWG = 64;                         // output column slice per workgroup
-constexpr int kSlices = kN / kColsWG;               // 4
-constexpr int kPlaneB = kColsWG * kK * 2;           // 32 KiB: one bf16 plane of the slice
-constexpr int kSliceB = 3 * kPlaneB;                // 96 KiB resident in LDS
 constexpr int kKS = 16;                             // k per MFMA step
-constexpr int kSteps = kK / kKS;                    // 16
 constexpr int kWaves = 4;
 constexpr int kTileRows = 32;
+constexpr int kMaxSlices = 4;                       // N <= 256: the ReLU mask is sized for 4 slices
+
+// A head GEMM shape: out (rows x N) = A (rows x K) W^T, K, N in {128, 256} (MeanPoolingTower with
+// E = H = d: C2's d = 128, C3 / C5's d = 256).
+template <int K, int N>
+struct HeadShape {
+  static_assert((K == 128 || K == 256) && (N == 128 || N == 256), "head GEMM shapes: K, N in {128, 256}");
+  static constexpr int kSlices = N / kColsWG;       // column slices (workgroups per row group)
+  static constexpr int kRowB = K * 2;               // one bf16 row of W (bytes)
+  static constexpr int kCH = K / 8;                 // 16-B chunks per row
+  static constexpr int kPlaneB = kColsWG * kRowB;   // one bf16 plane of the slice
+  static constexpr int kSliceB = 3 * kPlaneB;       // resident in LDS (96 KiB at K = 256)
+  static constexpr int kSteps = K / kKS;
+};
 
 enum Epi { EPI_BIAS_RELU = 0, EPI_BIAS_L2 = 1, EPI_RELU_MASK = 2, EPI_PLAIN = 3, EPI_ROWDIV = 5 };
 
@@ -43,35 +52,40 @@ __device__ __forceinline__ void split3(float x, __bf16& a0, __bf16& a1, __bf16& 
   a2 = (__bf16)(r1 - (float)a1);
 }
 
-// blockIdx.y selects one of up to 4 (weight, transpose) jobs; job j writes planes + j * 3 N K.
+// blockIdx.y selects one of up to 4 (weight, transpose) jobs; job j writes its three planes of
+// an n x k matrix (W is n x k, or k x n when transposed) at planes_base + off[j].
 struct SplitJobs {
   const float* W[4];
   int transpose[4];
+  int n[4], k[4];
+  int64_t off[4];
 };
 
 __global__ __launch_bounds__(256) void split_planes_kernel(SplitJobs jobs, __bf16* __restrict__ planes_base) {
-  const int i = blockIdx.x * 256 + threadIdx.x;  // output index n * kK + k
-  if (i >= kN * kK) return;
   const int job = blockIdx.y;
+  const int nn = jobs.n[job], kk = jobs.k[job];
+  const int i = blockIdx.x * 256 + threadIdx.x;  // output index n * kk + k
+  if (i >= nn * kk) return;
   const float* W = jobs.W[job];
-  __bf16* planes = planes_base + (size_t)job * 3 * kN * kK;
-  const int n = i / kK, k = i % kK;
-  const float x = jobs.transpose[job] ? W[k * kN + n] : W[n * kK + k];
+  __bf16* planes = planes_base + jobs.off[job];
+  const int n = i / kk, k = i % kk;
+  const float x = jobs.transpose[job] ? W[k * nn + n] : W[n * kk + k];
   __bf16 a0, a1, a2;
   split3(x, a0, a1, a2);
   planes[i] = a0;
-  planes[kN * kK + i] = a1;
-  planes[2 * kN * kK + i] = a2;
+  planes[nn * kk + i] = a1;
+  planes[2 * nn * kk + i] = a2;
 }
 
-// Workgroup b -> (row group g, column slice c).  Blocks b, b+8, b+16, b+24 share an XCD
-// (round-robin dispatch over the 8 XCDs) and take the four slices of one row group.
+// Workgroup b -> (row group g, column slice c).  Blocks b, b+8, ... share an XCD (round-robin
+// dispatch over the 8 XCDs) and take the S slices of one row group.
+template <int S>
 __device__ __forceinline__ void head_block(int b, int& g, int& c) {
-  c = (b >> 3) & 3;
-  g = (b >> 5) * 8 + (b & 7);
+  c = (b >> 3) % S;
+  g = (b >> 3) / S * 8 + (b & 7);
 }
 
-template <int EPI>
+template <int EPI, int K, int N>
 __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restrict__ A, int64_t rows, int64_t lda,
                                                            const __bf16* __restrict__ planes,
                                                            const float* __restrict__ bias,
@@ -81,27 +95,31 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
   typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8_t;
   typedef __attribute__((address_space(3))) char lds_char_t;
   lds_char_t* lds = (lds_char_t*)smem;
+  using HS = HeadShape<K, N>;
+  constexpr int kSlices = HS::kSlices, kPlaneB = HS::kPlaneB, kSliceB = HS::kSliceB, kSteps = HS::kSteps;
+  constexpr int kCH = HS::kCH, kRowB = HS::kRowB;
   int g, c;
-  head_block(blockIdx.x, g, c);
+  head_block<kSlices>(blockIdx.x, g, c);
   if (g >= groups) return;
   const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5;
 
-  // resident B slice: lds[p][n][chunk ^ (n & 31)], chunk = 8 k (16 B), n = local column.
-  // LDS-DMA writes each 1 KiB piece linearly (lane l -> byte 16 l = row n0 + l/32, slot l%32),
-  // so the swizzle goes on the source: slot s of row n holds chunk s ^ (n & 31).  24 pieces per
-  // wave, all in flight together, no staging registers.
+  // resident B slice: lds[p][n][chunk ^ (n % kCH)], chunk = 8 k (16 B), n = local column.
+  // LDS-DMA writes each 1 KiB piece linearly (lane l -> byte 16 l = row n0 + l / kCH, slot
+  // l % kCH), so the swizzle goes on the source: slot s of row n holds chunk s ^ (n % kCH).
+  // kSliceB / 4 KiB pieces per wave (24 at K = 256), all in flight together, no staging registers.
 #ifndef TT_HABL_NOFILL
   {
-    constexpr int kPiecesW = kSliceB / 1024 / kWaves;  // 24
+    constexpr int kPiecesW = kSliceB / 1024 / kWaves;
+    constexpr int kRowsPiece = 1024 / kRowB;
     const unsigned wl = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
     const char* src = reinterpret_cast<const char*>(planes);
 #pragma unroll
     for (int u = 0; u < kPiecesW; ++u) {
-      const int piece = u * kWaves + wid;  // 1 KiB = rows 2 piece, 2 piece + 1 of the slice image
-      const int row = 2 * piece + (lane >> 5), p = row / kColsWG, n = row % kColsWG;
-      const int q = (lane & 31) ^ (n & 31);
-      const unsigned off = (unsigned)(((size_t)p * kN * kK + (size_t)(c * kColsWG + n) * kK + q * 8) * 2);
+      const int piece = u * kWaves + wid;  // 1 KiB = kRowsPiece rows of the slice image
+      const int row = kRowsPiece * piece + lane / kCH, p = row / kColsWG, n = row % kColsWG;
+      const int q = (lane % kCH) ^ (n % kCH);
+      const unsigned off = (unsigned)(((size_t)p * N * K + (size_t)(c * kColsWG + n) * K + q * 8) * 2);
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(src),
                    "s"(__builtin_amdgcn_readfirstlane(wl + piece * 1024))
                    : "memory");
@@ -137,14 +155,15 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
   __syncthreads();                                   // B slice resident
 
   // B operand of column tile ct, plane p, step j: local column n = 32 ct + r32, chunk 2 j + hh
-  const lds_char_t* bbase = lds + r32 * 512;
-  auto rdb = [&](int ct, int p, int j) {  // (32 ct + r32) & 31 == r32 picks the swizzle
+  const lds_char_t* bbase = lds + r32 * kRowB;
+  auto rdb = [&](int ct, int p, int j) {  // (32 ct + r32) % kCH == r32 % kCH picks the swizzle
 #ifdef TT_HABL_NOLDS
     bf16x8 z;
     asm volatile("" : "=v"(z));
     return z;
 #endif
-    return *reinterpret_cast<const lds_bf16x8_t*>(bbase + ct * 32 * 512 + p * kPlaneB + (((2 * j + hh) ^ r32) << 4));
+    return *reinterpret_cast<const lds_bf16x8_t*>(bbase + ct * 32 * kRowB + p * kPlaneB +
+                                                  (((2 * j + hh) ^ (r32 % kCH)) << 4));
   };
 
   // Software pipeline: while step j's twelve MFMAs run, the wave reads step j+1's B operands from
@@ -295,13 +314,13 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         acc[ct][v] = y;
       }
     }
-    float* orow = out + trow0 * kN + c * kColsWG + r32;
+    float* orow = out + trow0 * N + c * kColsWG + r32;
     if (__builtin_amdgcn_readfirstlane((int)(trow0 + kTileRows <= rows))) {
 #ifndef TT_HABL_NOSTORE
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) orow[((v & 3) + 8 * (v >> 2) + 4 * hh) * kN + ct * 32] = acc[ct][v];
+        for (int v = 0; v < 16; ++v) orow[((v & 3) + 8 * (v >> 2) + 4 * hh) * N + ct * 32] = acc[ct][v];
 #endif
     } else {
 #pragma unroll
@@ -309,7 +328,7 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
           const int rl = (v & 3) + 8 * (v >> 2) + 4 * hh;
-          if (trow0 + rl < rows) orow[rl * kN + ct * 32] = acc[ct][v];
+          if (trow0 + rl < rows) orow[rl * N + ct * 32] = acc[ct][v];
         }
     }
     if constexpr (EPI == EPI_BIAS_RELU) {
@@ -318,15 +337,28 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
   }
 }
 
-// Finishes F.normalize (ATen: x / max(|x|, 1e-12)) from the slices' partial sums of squares:
-// one 64-lane wave per row, 4 floats per lane.
+// Finishes F.normalize (ATen: x / max(|x|, 1e-12)): one 64-lane wave per row, N / 64 floats per
+// lane (N = 256: one float4, the arithmetic tt_inbatch_l2_prep repeats bit for bit).
+template <int N>
 __global__ __launch_bounds__(256) void head_normalize_kernel(float* __restrict__ y, int64_t rows,
                                                              const float* __restrict__ part,
                                                              float* __restrict__ norms) {
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = lane_id();
-  f32x4* p = reinterpret_cast<f32x4*>(y + row * kN) + lane;
+  if constexpr (N == 128) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x2* p = reinterpret_cast<f32x2*>(y + row * N) + lane;
+    f32x2 v = *p;
+    const float ss = wave_sum(__builtin_fmaf(v[1], v[1], v[0] * v[0]));
+    const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
+    v[0] *= inv;
+    v[1] *= inv;
+    *p = v;
+    if (lane == 0) norms[row] = nrm;
+    return;
+  }
+  f32x4* p = reinterpret_cast<f32x4*>(y + row * N) + lane;
   f32x4 v = *p;
   const float ss = wave_sum(sumsq4(v));
   const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
@@ -353,7 +385,6 @@ constexpr int kWgChunk = 16;                              // rows per chunk
 constexpr int kWgBlk = 128;                               // output block edge
 constexpr int kWgPlane = kWgChunk * kWgBlk * 2;           // 4 KiB: one bf16 plane of a chunk
 constexpr int kWgBuf = 2 * 3 * kWgPlane;                  // G and X planes: 24 KiB
-constexpr int kWgSlabs = 64;  // a multiple of 8 (XCD-aware block mapping)
 
 __device__ __forceinline__ int wg_off(int row, int col) {  // byte offset in a plane
   return row * (kWgBlk * 2) + ((col * 2) ^ ((row & 3) << 6));
@@ -369,6 +400,7 @@ struct WgradProblem2 {
   int nblk;  // blocks of the first problem (4 * slabs); 0: one problem
 };
 
+template <int N>
 __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ X,
                                                             int64_t rows, int64_t slab_rows,
                                                             float* __restrict__ part_w, float* __restrict__ part_b,
@@ -386,10 +418,11 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
     part_w = second.part_w;
     part_b = second.part_b;
   }
-  // blocks b, b+8, b+16, b+24 share an XCD (round-robin dispatch): they take the four output
-  // blocks of one slab, so its G / X rows come from HBM once and from that XCD's L2 after
-  const int blk = (bid >> 3) & 3, slab = (bid >> 5) * 8 + (bid & 7);
-  const int bi = blk & 1, bj = blk >> 1;  // output block rows i in [128 bi, +128), cols j in [128 bj, +128)
+  // blocks b, b+8, ... share an XCD (round-robin dispatch): they take the NB output blocks of
+  // one slab, so its G / X rows come from HBM once and from that XCD's L2 after
+  constexpr int NB1 = N / kWgBlk, NB = NB1 * NB1;  // output blocks per slab (4 at N = 256, 1 at 128)
+  const int blk = (bid >> 3) % NB, slab = (bid >> 3) / NB * 8 + (bid & 7);
+  const int bi = blk % NB1, bj = blk / NB1;  // output block rows i in [128 bi, +128), cols j in [128 bj, +128)
   const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
   const int64_t r_begin = (int64_t)slab * slab_rows;
   const int64_t r_end = r_begin + slab_rows < rows ? r_begin + slab_rows : rows;
@@ -408,8 +441,8 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
     for (int h = 0; h < 2; ++h) {
       int64_t row = r_begin + (int64_t)ch * kWgChunk + lr + 8 * h;
       row = row < rows ? row : 0;
-      r[h] = *reinterpret_cast<const f32x4*>(gsrc + row * kN);  // rows past the end: zeroed when staged
-      r[2 + h] = *reinterpret_cast<const f32x4*>(xsrc + row * kN);
+      r[h] = *reinterpret_cast<const f32x4*>(gsrc + row * N);  // rows past the end: zeroed when staged
+      r[2 + h] = *reinterpret_cast<const f32x4*>(xsrc + row * N);
     }
   };
   f32x4 colsum = {0.f, 0.f, 0.f, 0.f};
@@ -509,7 +542,7 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
 
   // partial dW of this slab: acc[ti][tj][v] = (i, j) with i = 128 bi + 32 (2 wi + ti) + (v & 3) +
   // 8 (v >> 2) + 4 kh, j = 128 bj + 32 (2 wj + tj) + (lane & 31)
-  float* pw = part_w + (size_t)slab * kN * kN;
+  float* pw = part_w + (size_t)slab * N * N;
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -521,7 +554,7 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
 #ifdef TT_WABL_NOSTORE
         if (acc[ti][tj][v] == 12345.678f)
 #endif
-        pw[i * kN + j] = acc[ti][tj][v];
+        pw[i * N + j] = acc[ti][tj][v];
       }
   if (bj == 0 && part_b) {  // fold the 8 row groups (lr) of each column group in LDS, fixed order
     __syncthreads();
@@ -532,7 +565,7 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
       f32x4 t = red[tid];
 #pragma unroll
       for (int g = 1; g < 8; ++g) t += red[g * 32 + tid];
-      *reinterpret_cast<f32x4*>(part_b + (size_t)slab * kN + 128 * bi + 4 * tid) = t;
+      *reinterpret_cast<f32x4*>(part_b + (size_t)slab * N + 128 * bi + 4 * tid) = t;
     }
   }
 }
@@ -548,6 +581,7 @@ struct WgradReduce2 {
   int nblk;  // blocks of the first problem; 0: one problem
 };
 
+template <int N>
 __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part_w,
                                                                 const float* __restrict__ part_b, int slabs,
                                                                 float* __restrict__ dW, float* __restrict__ db,
@@ -568,17 +602,18 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __r
   const int i = bid * 64 + o;
   const int per = (slabs + kRedQ - 1) / kRedQ;
   const int s0 = qq * per, s1 = min(slabs, s0 + per);
-  const bool is_b = bid == nb - 1;  // the last block folds db (64 float4 = 256 columns)
-  const f32x4 t = is_b ? (db ? sum_slabs(reinterpret_cast<const f32x4*>(part_b) + o, kN / 4, s0, s1)
-                             : f32x4{0.f, 0.f, 0.f, 0.f})
-                       : sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, kN * kN / 4, s0, s1);
+  const bool is_b = bid == nb - 1;  // the last block folds db (N / 4 float4 columns)
+  const bool ob = is_b && o < N / 4;
+  const f32x4 t = is_b ? (db && ob ? sum_slabs(reinterpret_cast<const f32x4*>(part_b) + o, N / 4, s0, s1)
+                                   : f32x4{0.f, 0.f, 0.f, 0.f})
+                       : sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, N * N / 4, s0, s1);
   red[qq][o] = t;
   __syncthreads();
   if (qq == 0) {
     const f32x4 r = (red[0][o] + red[1][o]) + (red[2][o] + red[3][o]);
     if (!is_b)
       reinterpret_cast<f32x4*>(dW)[i] = r;
-    else if (db)
+    else if (db && ob)
       reinterpret_cast<f32x4*>(db)[o] = r;
   }
 }
@@ -588,31 +623,52 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __r
 
 using namespace tt;
 
+namespace tt {
+namespace {
+bool head_width_ok(int n) { return n == 128 || n == 256; }
+// weight-gradient slabs: one round of 256 workgroups over the two problems of tt_head_wgrad2
+// (4 output blocks per slab at N = 256, 1 at N = 128); 64 / 256 for the one-problem form
+int wg_slabs2(int N) { return N == 256 ? 32 : 128; }
+int wg_slabs1(int N) { return N == 256 ? 64 : 256; }
+int wg_blocks(int N) { return (N / kWgBlk) * (N / kWgBlk); }
+}  // namespace
+}  // namespace tt
+
 extern "C" size_t tt_head_planes_bytes(int N, int K) { return (size_t)3 * N * K * 2; }
 
 extern "C" int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream) {
-  TT_REQUIRE(N == kN && K == kK, "tt_head_split: only %dx%d weights (got %dx%d)", kN, kK, N, K);
+  TT_REQUIRE(head_width_ok(N) && head_width_ok(K), "tt_head_split: N, K in {128, 256} (got %dx%d)", N, K);
   TT_REQUIRE(W && planes, "null pointer");
   SplitJobs jobs{};
   jobs.W[0] = W;
   jobs.transpose[0] = transpose;
-  split_planes_kernel<<<dim3(kN * kK / 256, 1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+  jobs.n[0] = N;
+  jobs.k[0] = K;
+  split_planes_kernel<<<dim3(N * K / 256, 1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
       jobs, static_cast<__bf16*>(planes));
   TT_LAUNCH_CHECK("tt_head_split");
   return TT_OK;
 }
 
-extern "C" int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t stream) {
+extern "C" int tt_head_split_ff2(const float* W1, const float* W2, int E, int H, void* planes, tt_stream_t stream) {
+  TT_REQUIRE(head_width_ok(E) && head_width_ok(H), "tt_head_split_ff2: E, H in {128, 256} (got E=%d H=%d)", E, H);
   TT_REQUIRE(W1 && W2 && planes, "null pointer");
-  const SplitJobs jobs{{W1, W2, W1, W2}, {0, 0, 1, 1}};
-  split_planes_kernel<<<dim3(kN * kK / 256, 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+  // W1 (H x E), W2 (H x H), W1^T (E x H), W2^T (H x H), each as three bf16 planes, in that order
+  const int64_t a = 3LL * H * E, b = 3LL * H * H;
+  const SplitJobs jobs{{W1, W2, W1, W2}, {0, 0, 1, 1}, {H, H, E, H}, {E, H, H, H}, {0, a, a + b, 2 * a + b}};
+  const int big = std::max(H * E, H * H);
+  split_planes_kernel<<<dim3(big / 256, 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
       jobs, static_cast<__bf16*>(planes));
-  TT_LAUNCH_CHECK("tt_head_split_ff");
+  TT_LAUNCH_CHECK("tt_head_split_ff2");
   return TT_OK;
 }
 
+extern "C" int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t stream) {
+  return tt_head_split_ff2(W1, W2, 256, 256, planes, stream);
+}
+
 extern "C" size_t tt_head_relu_mask_bytes(int64_t rows) {
-  return (size_t)((rows + kTileRows - 1) / kTileRows) * kSlices * 64 * sizeof(uint32_t);
+  return (size_t)((rows + kTileRows - 1) / kTileRows) * kMaxSlices * 64 * sizeof(uint32_t);
 }
 
 extern "C" size_t tt_head_gemm_ws_size(int64_t rows, int epi) {
@@ -621,10 +677,39 @@ extern "C" size_t tt_head_gemm_ws_size(int64_t rows, int epi) {
   return 0;  // the L2 epilogue's row norms are formed by head_normalize_kernel from the rows
 }
 
+namespace tt {
+namespace {
+template <int K, int N>
+int launch_head_gemm(const float* A, int64_t rows, int64_t lda, const __bf16* P, int epi, const float* bias,
+                     uint32_t* relu_mask, float* out, float* part, hipStream_t s) {
+  using HS = HeadShape<K, N>;
+  // tiles per wave: enough row groups to give every CU one workgroup of the column slices
+  const int64_t tile_rows = kWaves * kTileRows;
+  const int64_t wgs_per_group = HS::kSlices;
+  const int64_t target_groups = 256 / wgs_per_group;
+  const int64_t tiles = std::max<int64_t>(1, (rows + tile_rows * target_groups - 1) / (tile_rows * target_groups));
+  const int64_t groups = (rows + tiles * tile_rows - 1) / (tiles * tile_rows);
+  const int64_t padded = (groups + 7) / 8 * 8;  // head_block: 8 groups per 8 * kSlices blocks
+  const dim3 grid((unsigned)(padded * HS::kSlices)), block(256);
+  const int G = (int)groups, T = (int)tiles;
+  constexpr int L = HS::kSliceB;
+  switch (epi) {
+    case EPI_BIAS_RELU: head_gemm_kernel<EPI_BIAS_RELU, K, N><<<grid, block, L, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T); break;
+    case EPI_BIAS_L2: head_gemm_kernel<EPI_BIAS_L2, K, N><<<grid, block, L, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T); break;
+    case EPI_RELU_MASK: head_gemm_kernel<EPI_RELU_MASK, K, N><<<grid, block, L, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T); break;
+    case EPI_ROWDIV: head_gemm_kernel<EPI_ROWDIV, K, N><<<grid, block, L, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T); break;
+    default: head_gemm_kernel<EPI_PLAIN, K, N><<<grid, block, L, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T); break;
+  }
+  TT_LAUNCH_CHECK("tt_head_gemm");
+  return TT_OK;
+}
+}  // namespace
+}  // namespace tt
+
 extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,
                             const float* bias, uint32_t* relu_mask, float* out, float* norms, void* ws,
                             size_t ws_bytes, tt_stream_t stream) {
-  TT_REQUIRE(N == kN && K == kK, "tt_head_gemm: only K = N = 256 (got K=%d N=%d)", K, N);
+  TT_REQUIRE(head_width_ok(K) && head_width_ok(N), "tt_head_gemm: K, N in {128, 256} (got K=%d N=%d)", K, N);
   TT_REQUIRE(rows >= 0 && lda >= K, "bad shape rows=%lld lda=%lld", (long long)rows, (long long)lda);
   if (rows == 0) return TT_OK;
   TT_REQUIRE(rows < (int64_t(1) << 31), "rows=%lld too large", (long long)rows);
@@ -643,54 +728,35 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
   TT_REQUIRE(ws_bytes >= tt_head_gemm_ws_size(rows, epi) && (ws || !tt_head_gemm_ws_size(rows, epi)),
              "workspace too small (%zu < %zu)", ws_bytes, tt_head_gemm_ws_size(rows, epi));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  // tiles per wave: enough row groups to give every CU one workgroup of the four slices
-  const int64_t tile_rows = kWaves * kTileRows;
-  const int64_t tiles = std::max<int64_t>(1, (rows + tile_rows * 64 - 1) / (tile_rows * 64));
-  const int64_t groups = (rows + tiles * tile_rows - 1) / (tiles * tile_rows);
-  const int64_t padded = (groups + 7) / 8 * 8;  // head_block: 8 groups per 32 blocks
-  const dim3 grid((unsigned)(padded * kSlices)), block(256);
   const __bf16* P = static_cast<const __bf16*>(planes);
   float* part = static_cast<float*>(ws);
-  const int G = (int)groups, T = (int)tiles;
-  switch (epi) {
-    case EPI_BIAS_RELU:
-      head_gemm_kernel<EPI_BIAS_RELU><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
-      break;
-    case EPI_BIAS_L2:
-      head_gemm_kernel<EPI_BIAS_L2><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
-      break;
-    case EPI_RELU_MASK:
-      head_gemm_kernel<EPI_RELU_MASK><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
-      break;
-    case EPI_ROWDIV:
-      head_gemm_kernel<EPI_ROWDIV><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
-      break;
-    default:
-      head_gemm_kernel<EPI_PLAIN><<<grid, block, kSliceB, s>>>(A, rows, lda, P, bias, relu_mask, out, part, G, T);
-      break;
-  }
-  TT_LAUNCH_CHECK("tt_head_gemm");
+  int rc;
+  if (K == 256 && N == 256) rc = launch_head_gemm<256, 256>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
+  else if (K == 128 && N == 128) rc = launch_head_gemm<128, 128>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
+  else if (K == 256) rc = launch_head_gemm<256, 128>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
+  else rc = launch_head_gemm<128, 256>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
+  if (rc) return rc;
   if (epi == EPI_BIAS_L2 && !defer_l2) {
-    head_normalize_kernel<<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
+    if (N == 256) head_normalize_kernel<256><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
+    else head_normalize_kernel<128><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
     TT_LAUNCH_CHECK("tt_head_gemm normalize");
   }
   return TT_OK;
 }
 
-// Both weight gradients of a head in one launch, 32 slabs each (one workgroup per CU over the two
+// Both weight gradients of a head in one launch (one round of 256 workgroups over the two
 // problems): (dW1, db1) from (G1, X1) and (dW2, db2) from (G2, X2), slab partials into ws; the
 // fixed-order slab sums in a second call (tt_head_wgrad2_reduce), which a caller may queue later
-// on another stream.  Deterministic.
-constexpr int kWgSlabs2 = 32;
-
+// on another stream.  Deterministic.  N = K (the head width, 128 or 256).
 extern "C" size_t tt_head_wgrad2_ws_size(int64_t rows, int N) {
   (void)rows;
-  return (size_t)2 * kWgSlabs2 * N * (N + 1) * sizeof(float);
+  if (!head_width_ok(N)) return 0;
+  return (size_t)2 * wg_slabs2(N) * N * (N + 1) * sizeof(float);
 }
 
 extern "C" int tt_head_wgrad2(const float* G1, const float* X1, const float* G2, const float* X2, int64_t rows, int N,
                               void* ws, size_t ws_bytes, tt_stream_t stream) {
-  TT_REQUIRE(N == kN, "tt_head_wgrad2: only N = %d (got %d)", kN, N);
+  TT_REQUIRE(head_width_ok(N), "tt_head_wgrad2: N in {128, 256} (got %d)", N);
   TT_REQUIRE(rows >= 0, "bad rows %lld", (long long)rows);
   TT_REQUIRE(rows == 0 || (G1 && X1 && G2 && X2), "null pointer");
   TT_REQUIRE(ws && ws_bytes >= tt_head_wgrad2_ws_size(rows, N), "workspace too small (%zu < %zu)", ws_bytes,
@@ -703,57 +769,70 @@ extern "C" int tt_head_wgrad2(const float* G1, const float* X1, const float* G2,
     TT_HIP(hipMemsetAsync(ws, 0, tt_head_wgrad2_ws_size(rows, N), s), "memset wgrad2 partials");
     return TT_OK;
   }
+  const int slabs = wg_slabs2(N), nb = wg_blocks(N) * slabs;
   float* pw1 = static_cast<float*>(ws);
-  float* pb1 = pw1 + (size_t)kWgSlabs2 * kN * kN;
-  float* pw2 = pb1 + (size_t)kWgSlabs2 * kN;
-  float* pb2 = pw2 + (size_t)kWgSlabs2 * kN * kN;
+  float* pb1 = pw1 + (size_t)slabs * N * N;
+  float* pw2 = pb1 + (size_t)slabs * N;
+  float* pb2 = pw2 + (size_t)slabs * N * N;
   constexpr int64_t kQuant = 3 * kWgChunk;
-  const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + kWgSlabs2 * kQuant - 1) / (kWgSlabs2 * kQuant) * kQuant);
-  head_wgrad_kernel<<<dim3(2 * 4 * kWgSlabs2), dim3(256), 2 * kWgBuf, s>>>(
-      G1, X1, rows, slab_rows, pw1, pb1, WgradProblem2{G2, X2, pw2, pb2, 4 * kWgSlabs2});
+  const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + slabs * kQuant - 1) / (slabs * kQuant) * kQuant);
+  if (N == 256)
+    head_wgrad_kernel<256><<<dim3(2 * nb), dim3(256), 2 * kWgBuf, s>>>(G1, X1, rows, slab_rows, pw1, pb1,
+                                                                      WgradProblem2{G2, X2, pw2, pb2, nb});
+  else
+    head_wgrad_kernel<128><<<dim3(2 * nb), dim3(256), 2 * kWgBuf, s>>>(G1, X1, rows, slab_rows, pw1, pb1,
+                                                                      WgradProblem2{G2, X2, pw2, pb2, nb});
   TT_LAUNCH_CHECK("tt_head_wgrad2");
   return TT_OK;
 }
 
 extern "C" int tt_head_wgrad2_reduce(const void* ws, int N, float* dW1, float* db1, float* dW2, float* db2,
                                      tt_stream_t stream) {
-  TT_REQUIRE(N == kN, "tt_head_wgrad2_reduce: only N = %d (got %d)", kN, N);
+  TT_REQUIRE(head_width_ok(N), "tt_head_wgrad2_reduce: N in {128, 256} (got %d)", N);
   TT_REQUIRE(ws && dW1 && db1 && dW2 && db2, "null pointer");
   TT_REQUIRE(((reinterpret_cast<uintptr_t>(ws) | reinterpret_cast<uintptr_t>(dW1) | reinterpret_cast<uintptr_t>(db1) |
                reinterpret_cast<uintptr_t>(dW2) | reinterpret_cast<uintptr_t>(db2)) & 15) == 0,
              "buffers must be 16-byte aligned");
+  const int slabs = wg_slabs2(N);
   const float* pw1 = static_cast<const float*>(ws);
-  const float* pb1 = pw1 + (size_t)kWgSlabs2 * kN * kN;
-  const float* pw2 = pb1 + (size_t)kWgSlabs2 * kN;
-  const float* pb2 = pw2 + (size_t)kWgSlabs2 * kN * kN;
-  const int nb = kN * kN / 4 / 64 + 1;
-  head_wgrad_reduce_kernel<<<dim3(2 * nb), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
-      pw1, pb1, kWgSlabs2, dW1, db1, WgradReduce2{pw2, pb2, dW2, db2, nb});
+  const float* pb1 = pw1 + (size_t)slabs * N * N;
+  const float* pw2 = pb1 + (size_t)slabs * N;
+  const float* pb2 = pw2 + (size_t)slabs * N * N;
+  const int nb = N * N / 4 / 64 + 1;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (N == 256)
+    head_wgrad_reduce_kernel<256><<<dim3(2 * nb), dim3(256), 0, s>>>(pw1, pb1, slabs, dW1, db1,
+                                                                    WgradReduce2{pw2, pb2, dW2, db2, nb});
+  else
+    head_wgrad_reduce_kernel<128><<<dim3(2 * nb), dim3(256), 0, s>>>(pw1, pb1, slabs, dW1, db1,
+                                                                    WgradReduce2{pw2, pb2, dW2, db2, nb});
   TT_LAUNCH_CHECK("tt_head_wgrad2_reduce");
   return TT_OK;
 }
 
 extern "C" int tt_head_wgrad2_parts(int N, int k, int64_t* offset, int64_t* stride) {
-  if (N != kN || k < 0 || k > 3 || !offset || !stride) {
+  if (!head_width_ok(N) || k < 0 || k > 3 || !offset || !stride) {
     set_error("tt_head_wgrad2_parts: N=%d k=%d", N, k);
     return -1;
   }
   // ws layout (tt_head_wgrad2): dW1 slabs, db1 slabs, dW2 slabs, db2 slabs
-  const int64_t w = (int64_t)kWgSlabs2 * kN * kN, b = (int64_t)kWgSlabs2 * kN;
+  const int slabs = wg_slabs2(N);
+  const int64_t w = (int64_t)slabs * N * N, b = (int64_t)slabs * N;
   const int64_t off[4] = {0, w, w + b, 2 * w + b};
   *offset = off[k];
-  *stride = (k & 1) ? kN : (int64_t)kN * kN;
-  return kWgSlabs2;
+  *stride = (k & 1) ? N : (int64_t)N * N;
+  return slabs;
 }
 
 extern "C" size_t tt_head_wgrad_ws_size(int64_t rows, int N) {
   (void)rows;
-  return (size_t)kWgSlabs * N * (N + 1) * sizeof(float);
+  if (!head_width_ok(N)) return 0;
+  return (size_t)wg_slabs1(N) * N * (N + 1) * sizeof(float);
 }
 
 extern "C" int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
                              size_t ws_bytes, tt_stream_t stream) {
-  TT_REQUIRE(N == kN, "tt_head_wgrad: only N = %d (got %d)", kN, N);
+  TT_REQUIRE(head_width_ok(N), "tt_head_wgrad: N in {128, 256} (got %d)", N);
   TT_REQUIRE(rows >= 0, "bad rows %lld", (long long)rows);
   TT_REQUIRE(dW && (rows == 0 || (G && X)), "null pointer");
   TT_REQUIRE(ws && ws_bytes >= tt_head_wgrad_ws_size(rows, N), "workspace too small (%zu < %zu)", ws_bytes,
@@ -767,15 +846,24 @@ extern "C" int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N
     if (db) TT_HIP(hipMemsetAsync(db, 0, (size_t)N * sizeof(float), s), "memset db");
     return TT_OK;
   }
+  const int slabs = wg_slabs1(N);
   float* part_w = static_cast<float*>(ws);
-  float* part_b = part_w + (size_t)kWgSlabs * kN * kN;
+  float* part_b = part_w + (size_t)slabs * N * N;
   // slab rows: a multiple of the chunk, every slab launched (empty slabs write zero partials)
   constexpr int64_t kQuant = 3 * kWgChunk;  // whole ring turns (kRing chunks) per slab
-  const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + kWgSlabs * kQuant - 1) / (kWgSlabs * kQuant) * kQuant);
-  head_wgrad_kernel<<<dim3(4 * kWgSlabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
-                                                                      db ? part_b : nullptr);
-  TT_LAUNCH_CHECK("tt_head_wgrad");
-  head_wgrad_reduce_kernel<<<dim3(kN * kN / 4 / 64 + 1), dim3(256), 0, s>>>(part_w, part_b, kWgSlabs, dW, db);
+  const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + slabs * kQuant - 1) / (slabs * kQuant) * kQuant);
+  const int nred = N * N / 4 / 64 + 1;
+  if (N == 256) {
+    head_wgrad_kernel<256><<<dim3(wg_blocks(N) * slabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
+                                                                                    db ? part_b : nullptr);
+    TT_LAUNCH_CHECK("tt_head_wgrad");
+    head_wgrad_reduce_kernel<256><<<dim3(nred), dim3(256), 0, s>>>(part_w, part_b, slabs, dW, db);
+  } else {
+    head_wgrad_kernel<128><<<dim3(wg_blocks(N) * slabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
+                                                                                    db ? part_b : nullptr);
+    TT_LAUNCH_CHECK("tt_head_wgrad");
+    head_wgrad_reduce_kernel<128><<<dim3(nred), dim3(256), 0, s>>>(part_w, part_b, slabs, dW, db);
+  }
   TT_LAUNCH_CHECK("tt_head_wgrad reduce");
   return TT_OK;
 }

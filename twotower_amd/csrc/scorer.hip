@@ -317,6 +317,10 @@ struct NoHook {
 // packs both to bf16.  Slots 0-7 (G rows 0-15, the B operand of the Acc chain's first half) run
 // beside the next tile's S chain, slots 8-15 beside the first half of this tile's Acc chain,
 // which needs them only from its second half: the vector work is split between both MFMA runs.
+#ifndef TT_FWD_DEFER_PAIR
+#define TT_FWD_DEFER_PAIR 1
+#endif
+constexpr bool kDeferPair = TT_FWD_DEFER_PAIR != 0;
 template <int MODE, bool PRECISE>
 struct MapState {
   // scalar f32 only: packed f32 VALU beside MFMAs costs +22-26 cycles per instruction
@@ -341,8 +345,25 @@ struct MapState {
     }
   }
 
-  // slot v: element v's exponent and exp; odd slots also add the pair to the row sum and pack it
+  // slot v: element v's exponent and exp; a pair's row-sum add and bf16 pack follow its second
+  // exp (TT_FWD_DEFER_PAIR: one slot later, so no dependent VALU sits right behind a transcendental
+  // -- that needs a wait state, an s_nop per pair; pairs 6-7 and 14-15 stay immediate: they
+  // complete an MFMA operand (G rows 0-15, 16-31) that the next step may read).  The adds keep
+  // their order: bit-identical either way.
+  __device__ __forceinline__ void pair(int p, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
+    if constexpr (MODE == FWD) {
+      ls += e[p] + e[p + 1];
+      asm volatile("" : "+v"(ls));  // keeps the sum in this step (not sunk to the unit's end)
+    }
+#pragma unroll
+    for (int w = p; w <= p + 1; ++w) {
+      const __bf16 h = (__bf16)e[w];
+      bh[w >> 3][w & 7] = h;
+      if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
+    }
+  }
   __device__ __forceinline__ void slot(int v, const f32x16& xa, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
+    if (kDeferPair && (v & 1) == 0 && (v & 7) != 0) pair(v - 2, bh, bl);  // before this slot's exp
     const float y = __builtin_fmaf(xa[v], c2, -sub[v]);
 #ifdef TT_ABLATE_EXP
     e[v] = y;
@@ -350,19 +371,7 @@ struct MapState {
     e[v] = __builtin_amdgcn_exp2f(y);
 #endif
     asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
-    if (v & 1) {
-      const int p = v & ~1;
-      if constexpr (MODE == FWD) {
-        ls += e[p] + e[p + 1];
-        asm volatile("" : "+v"(ls));  // keeps the sum in this step (not sunk to the unit's end)
-      }
-#pragma unroll
-      for (int w = p; w <= p + 1; ++w) {
-        const __bf16 h = (__bf16)e[w];
-        bh[w >> 3][w & 7] = h;
-        if constexpr (PRECISE) bl[w >> 3][w & 7] = (__bf16)(e[w] - (float)h);
-      }
-    }
+    if ((v & 1) && (!kDeferPair || (v & 7) == 7)) pair(v & ~1, bh, bl);
   }
 };
 
@@ -494,9 +503,12 @@ constexpr int kSdFor = TT_SD < H / 8 ? TT_SD : H / 8;  // <= NSTEP: never past t
 // 0 splits them 8 + 8 between the S chain and the first half of the Acc chain.  Same arithmetic
 // in the same order either way.
 #ifndef TT_FWD_MAP_S
-#define TT_FWD_MAP_S 0
+#define TT_FWD_MAP_S 1
 #endif
 constexpr bool kMapInS = TT_FWD_MAP_S != 0;
+#ifndef TT_FWD_UNROLL4
+#define TT_FWD_UNROLL4 1
+#endif
 
 #ifdef TT_S_BUILTIN  // diagnostic: the S chain through the builtin (compiler-placed accumulators)
 __device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
@@ -891,8 +903,12 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   }
   constexpr int NSTEP = NK + 2 * NHT;
   if (MODE == FWD) TT_KTRACE_K(1, 1);
-  for (int64_t t = 0; t < ntiles; ++t) {
-    const int buf = (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
+  // One stage.  bufc: the ring slot (t & 3) as a compile-time constant when the loop is unrolled
+  // over the ring (TT_FWD_UNROLL4), so every LDS operand address is a per-lane offset plus an
+  // immediate (no per-read address add); -1: the slot computed at run time.
+  auto stage = [&](int64_t t, auto bufc) {
+    constexpr int bc = decltype(bufc)::value;
+    const int buf = bc >= 0 ? bc : (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
     const int64_t frow = stage_row(t + 3);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
     const lds_char_t* ntl = lds + nbuf * T::STAGE_B;
@@ -935,7 +951,17 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     static_assert(NJ == 2, "two units per stage");
     unit(std::integral_constant<int, 0>{}, xa, xb);
     unit(std::integral_constant<int, 1>{}, xb, xa);
+  };
+#if TT_FWD_UNROLL4
+  for (int64_t t = 0; t < ntiles; t += 4) {  // wave-uniform conditions: the ring slot of each call is constant
+    stage(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) stage(t + 1, std::integral_constant<int, 1>{});
+    if (t + 2 < ntiles) stage(t + 2, std::integral_constant<int, 2>{});
+    if (t + 3 < ntiles) stage(t + 3, std::integral_constant<int, 3>{});
   }
+#else
+  for (int64_t t = 0; t < ntiles; ++t) stage(t, std::integral_constant<int, -1>{});
+#endif
 #else
   f32x16 xa = ntiles > 0 ? s_chain<H>(lds, r32, hh, cf) : f32x16{};
   for (int64_t t = 0; t < ntiles; ++t) {
@@ -1272,176 +1298,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   TT_KTRACE(3);
-}
-
-// ------------------------------------------------------------------------------------------
-// Stored-P backward with two waves per SIMD (8-wave workgroups, 128 candidates).  Waves w and
-// w + 4 (one SIMD) own the same 32 candidates and split every 64-row query stage: wave w takes
-// its first 32-row tile, wave w + 4 the second, so each wave issues 16 MFMAs, 2 P loads and 4
-// fill pieces per stage.  In the one-wave engine every vector-memory instruction stalls the
-// only wave of its SIMD (40-75 cycles each while all waves issue them); here the
-// partner's MFMAs run through those stalls.  The pair's dD^T accumulators (the same 32
-// candidates over disjoint queries) are added through LDS at the end: acc(w) + acc(w + 4).
-// Per stage t (steps 0..NS-1 of this wave's tile): P(t+3) and fills(t+2) are issued before the
-// stage barrier at step NS - kDd, which waits for fills(t+1) (vmcnt: this stage's 2 + NPC ops may
-// stay in flight) in every wave; after it the operand reads run ahead into stage t+1.  fills(t+2)
-// go into buffer (t+2) & 3, last read in stage t-2, which every wave left behind at the barrier
-// of stage t-1.
-template <int H>
-__global__ __launch_bounds__(2 * NT, 2) void score_ddp2_kernel(const __bf16* __restrict__ R, int64_t nR, int64_t nC,
-                                                              int S, int64_t rows_per_split, const char* __restrict__ P,
-                                                              int64_t p_nqt, float* __restrict__ acc_part) {
-  using T = Tile<__bf16, H>;
-  constexpr int NHT = H / 32;
-  constexpr int NS = 2 * NHT;                   // MFMA steps per 32-row tile (and per stage)
-  constexpr int NW2 = 2 * NW;                   // waves per workgroup
-  constexpr int NPC = T::STAGE_B / 1024 / NW2;  // fill pieces per stage per wave
-  static_assert(NPC * 1024 * NW2 == T::STAGE_B && T::BJ == 64 && T::NSTAGE == 4, "8 waves over 64-row stages");
-  constexpr int kDd = kSdFor<H> < NS ? kSdFor<H> : NS;
-  constexpr int BAR = NS - kDd;  // the stage barrier: before the first read of stage t+1
-  static_assert(BAR >= 4, "the stage's VMEM issue slots sit before the barrier");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const lds_char_t* lds = (const lds_char_t*)smem;
-
-  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wc = wid & (NW - 1), jt = wid / NW;  // candidate tile of the pair, query tile of the stage
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int split = blockIdx.x % S;
-  const int64_t cb = blockIdx.x / S;
-  const int64_t ct = cb * NW + wc;
-  const int64_t row_begin = (int64_t)split * rows_per_split;
-  const int64_t row_end = min(nR, row_begin + rows_per_split);
-  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
-
-  unsigned fo[NPC];
-#pragma unroll
-  for (int c = 0; c < NPC; ++c) {
-    const int p = (c * NW2 + wid) * 1024 + lane * 16;
-    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
-    fo[c] = (unsigned)(row * T::ROWB + ((slot ^ T::swz(row)) << 4));
-  }
-  LdsOffs<H> lo;
-  lo.init(lane);
-  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
-  auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
-  auto fill = [&](int c, int b, int64_t r0) {
-    glds_dwordx4_s(fo[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW2 * 1024);
-  };
-  const char* pcol = P + ct * p_nqt * 2048;
-  const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
-  struct PSet {
-    bf16x8 v[2];
-  };
-  PSet pf[5];
-  auto pload = [&](PSet& dst, int64_t t, int k) {
-    const char* b = pcol + (stage_row(t) / 32 + jt) * 2048;
-    if (k == 0) dst.v[0] = p_load<0>(b, pvo);
-    else dst.v[1] = p_load<1>(b, pvo);
-  };
-  auto tie = [&](PSet& x) {
-    asm volatile("" : "+v"(x.v[0]));
-    asm volatile("" : "+v"(x.v[1]));
-  };
-  // prologue in steady-state issue order: P(0); [P(1), fills(0)]; [P(2), fills(1)]
-  pload(pf[0], 0, 0);
-  pload(pf[0], 0, 1);
-#pragma unroll
-  for (int k = 1; k < 3; ++k) {
-    pload(pf[k], k, 0);
-    pload(pf[k], k, 1);
-#pragma unroll
-    for (int c = 0; c < NPC; ++c) fill(c, k - 1, stage_row(k - 1));
-  }
-  f32x16 acc[NHT];
-#pragma unroll
-  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  // fills(0) and P(0), P(1) landed: P(2) and fills(1) may be in flight
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + NPC) : "memory");
-  __syncthreads();
-  tie(pf[0]);
-
-  auto opnd = [&](const lds_char_t* stile, int i) {  // A operand of step i of this wave's tile of a stage
-    const int s2 = i / NHT, ht = i % NHT;
-    const lds_char_t* tb = stile + jt * 32 * T::ROWB;
-    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
-    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
-    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
-    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-  };
-  bf16x8 ring[kDd];
-#pragma unroll
-  for (int k = 0; k < kDd; ++k) ring[k] = opnd(lds, k);
-  auto stage = [&](int64_t t, PSet& cur, PSet& ahead, PSet& next) {
-    const int buf = (int)(t & 3), fbuf = (buf + 2) & 3;
-    const int64_t frow = stage_row(t + 2);
-    const lds_char_t* tile = lds + buf * T::STAGE_B;
-    const lds_char_t* ntile = lds + ((buf + 1) & 3) * T::STAGE_B;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      if (i == BAR) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + NPC) : "memory");
-        asm volatile("s_barrier" ::: "memory");
-        tie(next);
-      }
-      const int s2 = i / NHT, ht = i % NHT;
-      acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[i % kDd], cur.v[s2], acc[ht], 0, 0, 0);
-      const int j = i + kDd;
-      ring[i % kDd] = j < NS ? opnd(tile, j) : opnd(ntile, j - NS);
-      // this stage's VMEM, all before the barrier: P(t+3) at steps 0 and BAR / 2, fills(t+2) between
-      if (i == 0) pload(ahead, t + 3, 0);
-      if (i == BAR / 2) pload(ahead, t + 3, 1);
-#pragma unroll
-      for (int c = 0; c < NPC; ++c)
-        if (i == 1 + c * (BAR - 1) / NPC + (1 + c * (BAR - 1) / NPC == BAR / 2 ? 1 : 0)) fill(c, fbuf, frow);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // full rounds of five stages, then the rest as nested conditionals (score_ddp_kernel: no register
-  // set is dead on any path while its load is in flight)
-  int64_t t = 0;
-  for (; t + 5 <= ntiles; t += 5) {
-    stage(t, pf[0], pf[3], pf[1]);
-    stage(t + 1, pf[1], pf[4], pf[2]);
-    stage(t + 2, pf[2], pf[0], pf[3]);
-    stage(t + 3, pf[3], pf[1], pf[4]);
-    stage(t + 4, pf[4], pf[2], pf[0]);
-  }
-  if (t < ntiles) {
-    stage(t, pf[0], pf[3], pf[1]);
-    if (t + 1 < ntiles) {
-      stage(t + 1, pf[1], pf[4], pf[2]);
-      if (t + 2 < ntiles) {
-        stage(t + 2, pf[2], pf[0], pf[3]);
-        if (t + 3 < ntiles) stage(t + 3, pf[3], pf[1], pf[4]);
-      }
-    }
-  }
-  drain_dma();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int k = 0; k < 5; ++k) tie(pf[k]);
-  __syncthreads();  // every wave's LDS-DMA landed and its reads of the ring done: the ring is free
-  // pair sum through LDS (the ring's first 4 x 32 KB): acc(w) + acc(w + 4), in that order
-  lds_f32x4_t* xch = (lds_f32x4_t*)((lds_char_t*)smem) + wc * (NHT * 4 * kWave);
-  if (jt == 1) {
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        xch[(ht * 4 + g) * kWave + lane] = f32x4{acc[ht][4 * g], acc[ht][4 * g + 1], acc[ht][4 * g + 2], acc[ht][4 * g + 3]};
-  }
-  __syncthreads();
-  if (jt == 0) {
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 o = xch[(ht * 4 + g) * kWave + lane];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[ht][4 * g + u] += o[u];
-      }
-    write_partials<DD, H>(acc, 0.f, split, nC, ct * 32 + r32, hh, acc_part, nullptr);
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2064,18 +1920,6 @@ int64_t p_nct_for(int64_t M) { return (M + 255) / 256 * 8; }  // also the 256-ca
 #define TT_DDP_CW256 1  // CW = 2 runs the loop ~15 % faster but doubles the split partials (S = 4): net slower (round 2)
 #endif
 int ddp_cw(int H) { return H == 256 ? TT_DDP_CW256 : 1; }
-// H = 256 stored-P backward at two waves per SIMD (score_ddp2_kernel); TT_DDP_W2=0 (read at load)
-// selects the one-wave engine
-#ifndef TT_DDP_W2_DEFAULT
-#define TT_DDP_W2_DEFAULT 1
-#endif
-bool ddp_w2() {
-  static const bool on = [] {
-    const char* e = std::getenv("TT_DDP_W2");
-    return (e ? std::strcmp(e, "0") != 0 : TT_DDP_W2_DEFAULT != 0) && TT_DDP_CW256 == 1;
-  }();
-  return on;
-}
 Plan ddp_plan(int64_t B, int64_t M, int H) {
   return plan_for(B, M, Tile<__bf16, 64>::BJ, wg_per_cu(H, TT_BF16, DD), 32 * NW * ddp_cw(H));
 }
@@ -2269,15 +2113,7 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
     TT_DDP(32, 1)
     TT_DDP(64, 1)
     TT_DDP(128, 1)
-    case 256:
-      if (ddp_w2()) {
-        score_ddp2_kernel<256><<<dim3(p.grid), dim3(2 * NT), Tile<__bf16, 256>::LDS_BYTES, s>>>(
-            Qs, B, M, p.S, p.rows_per_split, P, p_nqt, acc_part);
-        break;
-      }
-      score_ddp_kernel<256, TT_DDP_CW256><<<dim3(p.grid), dim3(NT), Tile<__bf16, 256>::LDS_BYTES, s>>>(
-          Qs, B, M, p.S, p.rows_per_split, P, p_nqt, acc_part);
-      break;
+    TT_DDP(256, TT_DDP_CW256)
 #undef TT_DDP
     default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
   }

@@ -371,7 +371,8 @@ def tower_ff(x, W1, b1, W2, b2):
     return TowerFF.apply(x, W1, b1, W2, b2)
 
 
-HEAD_WIDTH = 256  # the head GEMM kernels are specialised for E = H = 256
+HEAD_WIDTH = 256  # the width the scorer-side fusions (operand prep, fused L2 backward) are specialised for
+HEAD_WIDTHS = (128, 256)  # E = H widths of the hand-written tower head (C2: 128; C3 / C5: 256)
 
 
 def _planes(W: torch.Tensor, transpose: bool) -> torch.Tensor:
@@ -381,12 +382,15 @@ def _planes(W: torch.Tensor, transpose: bool) -> torch.Tensor:
     return buf
 
 
-def _head_gemm(A: torch.Tensor, planes: torch.Tensor, epi: int, bias=None, mask=None, norms=None) -> torch.Tensor:
+def _head_gemm(A: torch.Tensor, planes: torch.Tensor, epi: int, bias=None, mask=None, norms=None,
+               N: int | None = None) -> torch.Tensor:
+    """out (rows, N) = epi(A W^T) for the split planes of W (N x K); N defaults to K (square heads)."""
     rows, K = A.shape
-    out = torch.empty(rows, HEAD_WIDTH, dtype=_FLOAT, device=A.device)
+    N = K if N is None else N
+    out = torch.empty(rows, N, dtype=_FLOAT, device=A.device)
     nws = _lib.lib().tt_head_gemm_ws_size(rows, epi)
     ws = torch.empty(nws, dtype=torch.uint8, device=A.device) if nws else None
-    call("tt_head_gemm", ptr(A), rows, A.stride(0), K, ptr(planes), HEAD_WIDTH, epi, ptr(bias), ptr(mask), ptr(out),
+    call("tt_head_gemm", ptr(A), rows, A.stride(0), K, ptr(planes), N, epi, ptr(bias), ptr(mask), ptr(out),
          ptr(norms), ptr(ws), nws, stream_of(A))
     return out
 
@@ -437,7 +441,7 @@ def fused_head_backward():
 
 
 class TowerHead(torch.autograd.Function):
-    """F.normalize(Linear-ReLU-Linear(x)) for E = H = 256 (encoders.py:38-42,77) on the split-bf16
+    """F.normalize(Linear-ReLU-Linear(x)) for E = H in {128, 256} (encoders.py:38-42,77) on the split-bf16
     MFMA GEMMs with fused epilogues: bias + ReLU (+ the ReLU bitmask), bias + row L2 normalise
     (forward); the ReLU mask fused into dh = dy W2 (backward).  Weight gradients on K-split
     library GEMMs, bias gradients on tt_colsum."""
@@ -447,14 +451,15 @@ class TowerHead(torch.autograd.Function):
         require_gpu(x, W1, W2)
         ctx.bag_token = x._tt_bag_token if _SOLE_HEAD and _SOLE_HEAD[-1] is x else None
         x = _contig_f32(x, "x")
-        rows = x.shape[0]
-        nb = _lib.lib().tt_head_planes_bytes(HEAD_WIDTH, HEAD_WIDTH)
+        rows, width = x.shape  # E = H = width (HEAD_WIDTHS)
+        nb = _lib.lib().tt_head_planes_bytes(width, width)
         planes = torch.empty(4 * nb, dtype=torch.uint8, device=x.device)  # W1, W2, W1^T, W2^T
-        call("tt_head_split_ff", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), ptr(planes), stream_of(x))
+        call("tt_head_split_ff2", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), width, width, ptr(planes),
+             stream_of(x))
         mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
         h = _head_gemm(x, planes[:nb], 0, bias=b1, mask=mask)
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
-        req = _SCORER_PREP[-1] if _SCORER_PREP else None
+        req = _SCORER_PREP[-1] if _SCORER_PREP and width == HEAD_WIDTH else None
         if req is not None and 0 < req[0] < rows:
             nq, dt = req  # normalise pass fused with the in-batch scorer's operand prep
             out = _head_gemm(h, planes[nb:2 * nb], 4, bias=b2)
