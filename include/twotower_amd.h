@@ -93,6 +93,12 @@ int tt_bag_plan(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_
 int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,
                             int64_t V, int E, const void* plan, size_t plan_bytes,
                             float* grad_table, tt_stream_t stream);
+/* Where the plan's sorted output lies inside `plan` (byte offsets from the plan pointer rounded
+ * up to 256 B): offs[0] the sorted row keys (nseq*L uint32), offs[1] their sequence indices
+ * (nseq*L int32), offs[2] seg_start (V + 1 int32: row r's entries are [seg_start[r],
+ * seg_start[r + 1]), r = V the masked tail).  The sort is the stable sort of the (row, seq) pairs
+ * by row, so these are fixed by the ids: what the parity tests compare with a CPU stable sort. */
+int tt_bag_plan_layout(int64_t nseq, int L, int64_t V, int E, int64_t* offs);
 int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,
                                   int64_t V, int E, const void* plan, size_t plan_bytes,
                                   float* table, float* exp_avg, float* exp_avg_sq,

@@ -40,6 +40,24 @@ def bag_mean_bwd(d_pooled: np.ndarray, denom: np.ndarray, ids: np.ndarray, V: in
     return G
 
 
+def bag_plan(ids: np.ndarray, V: int, padding_idx: int | None = 0):
+    """The grouping bag_mean_bwd's scatter-add sums by: every token (s, t) of a kept id (0 < id < V,
+    id != padding_idx; masked tokens take key V) as the pair (id, s), stably sorted by id, and
+    seg_start[r] = the first sorted position whose key is >= r (r = 0..V).  Row r's gradient is
+    the sum of g_seq[s] over its segment, in ascending s: the sorted form of nn.Embedding's dense
+    backward (embeddings.py:30,40 via train.py:138).  Returns (keys, seqs, seg_start)."""
+    ids = np.asarray(ids, dtype=np.int64)
+    nseq, L = ids.shape
+    keep = (ids > 0) & (ids < V)
+    if padding_idx is not None:
+        keep &= ids != padding_idx
+    keys = np.where(keep, ids, V).reshape(-1)
+    seqs = np.repeat(np.arange(nseq, dtype=np.int64), L)
+    order = np.argsort(keys, kind="stable")
+    ks = keys[order]
+    return ks, seqs[order], np.searchsorted(ks, np.arange(V + 1), side="left")
+
+
 # ----------------------------------------------------------------------------------------------
 # Tower head: Linear(E,H) - ReLU - Linear(H,H) (encoders.py:38-42), F.normalize (encoders.py:77)
 def l2norm_fwd(x: np.ndarray):

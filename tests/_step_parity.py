@@ -17,10 +17,11 @@ bf16 scorers: the check is factored at the scorer's boundary, because a max-norm
 weight gradient is a sum over ~25k rows that cancels to a few % of its terms, which multiplies any
 per-row operand error by that cancellation.  (a) The scorer: the float64 loss on the HIP tower
 outputs rounded to bf16 (the operands the scorer multiplies), its operand gradients against the
-HIP scorer's gradients (hooked on q, p, n) at grad_tol, the scorer's measured bf16 error being
-~1.6e-5 (profiles/r02_scorer_error_table.jsonl); (b) the towers: the HIP scorer's own operand
-gradients back-propagated through the float64 towers (straight through the rounding) against the
-HIP parameter gradients at the fp32 bar, 1e-5.  Together they cover every step of the gradient.
+HIP scorer's (the same loss kernels run on the tower outputs as leaves) at grad_tol, the scorer's
+measured bf16 error being ~1.6e-5 (profiles/r02_scorer_error_table.jsonl); (b) the towers: the
+HIP scorer's own operand gradients back-propagated through the float64 towers (straight through
+the rounding) against the HIP parameter gradients at the fp32 bar, 1e-5.  Together they cover
+every step of the gradient.
 
 ReLU ties: a hidden pre-activation within rounding of zero may take the other branch in any fp32
 evaluation (ATen's or ours) than in float64, and one flipped element moves its bias gradient by
@@ -114,10 +115,6 @@ def run(V: int, E: int, L: int, B: int, loss: str, compute_dtype: str = "fp32", 
 
     # 1a. HIP gradients, plain autograd path (dense table gradient)
     q, p, n = model(*batch)
-    g_ops = {}
-    if compute_dtype != "fp32":
-        for i, t in enumerate((q, p, n)):
-            t.register_hook(lambda g, i=i: g_ops.__setitem__(i, g.detach().clone()))
     lh = hip_loss(q, p, n)
     lh.backward()
     torch.cuda.synchronize()
@@ -126,6 +123,12 @@ def run(V: int, E: int, L: int, B: int, loss: str, compute_dtype: str = "fp32", 
     loss_hip = float(lh)
     del q, p, n, lh
     model.zero_grad(set_to_none=True)
+    g_ops = {}
+    if compute_dtype != "fp32":  # the scorer's operand gradients: the same loss kernels on the same
+        leaves = [t.clone().requires_grad_(True) for t in qpn_hip]  # tower outputs, as leaves
+        hip_loss(*leaves).backward()
+        g_ops = {i: t.grad for i, t in enumerate(leaves)}
+        del leaves
 
     # 1b. float64 oracle on the same weights and batch, ReLU ties broken as the HIP forward broke them
     ref = RefTower(V, E, E).double().to(DEV)

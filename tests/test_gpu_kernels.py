@@ -4,6 +4,7 @@ rows / pooled values of single-token bags), fp32 loss and gradients within 1e-5 
 (max-abs normalised), bf16 scorer against the oracle on bf16-rounded inputs: 1e-4 for the
 hi/lo split of P (bf16_split) and the standard single-rounding bf16 form at about 1.5x their
 measured errors (BF16_SPLIT_GRAD_TOL, BF16_GRAD_TOL below)."""
+import ctypes
 import os
 
 import numpy as np
@@ -615,6 +616,58 @@ def test_planned_backward_equals_one_shot(E):
     t2, m2, v2 = tbl.clone(), m.clone(), v.clone()
     ops.bag_mean_backward_adamw_planned(dp, den, ops.BagPlan(ids, V, E, 0), t2, m2, v2, args)
     assert torch.equal(t1, t2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
+def _plan_out(plan, n):
+    """(sorted keys, their sequence indices, seg_start) read out of a BagPlan's buffer."""
+    offs = (ctypes.c_int64 * 3)()
+    ops.call("tt_bag_plan_layout", plan.nseq, plan.L, plan.V, plan.E, offs)
+    torch.cuda.synchronize()
+    base = (-plan.buf.data_ptr()) % 256
+    raw = plan.buf.cpu().numpy()
+
+    def arr(o, count):
+        return raw[base + o: base + o + 4 * count].view(np.int32)
+
+    return arr(offs[0], n).astype(np.int64), arr(offs[1], n).astype(np.int64), arr(offs[2], plan.V + 1)
+
+
+@pytest.mark.parametrize("case", ["edge-2pass", "one-pass", "c3-uniform", "zipf-hot", "three-pass-i64",
+                                  "all-masked", "padding-idx-7"])
+def test_plan_sort_equals_stable_sort(case):
+    """tt_bag_plan's hand-written LSD counting sort: its sorted keys, sequence indices and row
+    starts equal the oracle's stable sort (oracle.reference_math.bag_plan), bit for bit, for 1,
+    2 and 3 digit passes (V 1000 / 3001, 200000 / 2^23 + 5), ragged and all-padding batches, a
+    Zipf-hot id set, int64 ids and a non-zero padding index."""
+    rng = np.random.default_rng(31)
+    pad = 0
+    if case == "edge-2pass":
+        V, ids = 3001, edge_ids(300, 40, 3001, rng, torch.int32)
+    elif case == "one-pass":
+        V, ids = 1000, edge_ids(257, 33, 1000, rng, torch.int64)
+    elif case == "c3-uniform":
+        V, ids = 200_000, cuda(rng.integers(0, 200_000, size=(2048, 64)), torch.int32)
+    elif case == "zipf-hot":
+        V = 200_000
+        z = np.minimum(rng.zipf(1.2, size=(3000, 64)), V - 1)
+        ids = cuda(z, torch.int32)
+    elif case == "three-pass-i64":
+        V = (1 << 23) + 5
+        ids = cuda(rng.integers(0, V + 3, size=(600, 50)), torch.int64)  # ids >= V are masked
+    elif case == "all-masked":
+        V, ids = 5000, torch.zeros(64, 16, dtype=torch.int32, device=DEV)
+    else:
+        V, pad = 3001, 7
+        ids = edge_ids(300, 40, 3001, rng, torch.int32)
+        ids[5:50, 3] = 7
+    plan = ops.BagPlan(ids, V, 64, pad)
+    plan.wait()
+    n = ids.numel()
+    keys, seqs, starts = _plan_out(plan, n)
+    wk, ws, wst = O.bag_plan(ids.cpu().numpy(), V, pad)
+    assert np.array_equal(keys, wk)
+    assert np.array_equal(seqs, ws)
+    assert np.array_equal(starts, wst)
 
 
 @pytest.mark.parametrize("E,denom", [(256, True), (64, True), (48, False), (256, False)])

@@ -34,6 +34,31 @@ def test_bag_tiny_backward(golden):
     assert np.all(grads["table"][0] == 0)               # padding row never receives gradient
 
 
+def test_bag_plan_groups_the_golden_backward(golden):
+    """The plan restatement (stable (row, seq) sort + segment starts): summing g_seq over each
+    row's segment, in segment order, gives the golden table gradient of the reference."""
+    g = golden("bag_tiny")
+    p = params_of(g)
+    out, cache = O.tower_fwd(p, g["ids"])
+    grads = O.tower_bwd(p, g["g_out"], cache)
+    V = g["table"].shape[0]
+    keys, seqs, starts = O.bag_plan(g["ids"], V)
+    assert np.all(np.diff(keys) >= 0) and starts[0] == 0 and starts[V] == np.sum(keys < V)
+    for r in range(V):
+        seg = seqs[starts[r]:(starts[r + 1] if r < V else len(keys))]
+        assert np.all(np.diff(seg) >= 0) and np.all(keys[starts[r]:starts[r] + len(seg)] == r)
+    # the gradient from the plan: d_pooled / denom summed per segment
+    ids = np.asarray(g["ids"], np.int64)
+    _, denom = O.bag_mean_fwd(g["table"], ids)
+    dp = O.bag_mean_bwd(np.eye(ids.shape[0]), denom, ids, V)  # row r: sum over its tokens of e_s / denom
+    for r in range(1, V):
+        want = np.zeros(ids.shape[0])
+        for s_ in seqs[starts[r]:starts[r + 1]]:
+            want[s_] += 1.0 / denom[s_]
+        np.testing.assert_allclose(dp[r], want)
+    assert rel(grads["table"], g["g_table"]) < 1e-5
+
+
 def test_interior_zero_is_masked():
     """encoders.py:62 masks every id 0, not only trailing ones: [3,0,5,0] == [3,5,0,0]."""
     t = np.random.default_rng(0).standard_normal((8, 4))

@@ -5,6 +5,7 @@
   async_ar    dist.all_reduce(async_op=True) + work.wait()
   side_ar     all_reduce issued on a side stream forked from / joined back to the capture stream
   gather      dist.all_gather_into_tensor on the current stream
+  unjoined    a side stream forked from the capture and never joined (no collective)
   step_gather the bench's DP TrainStep (--dp gather) captured through TrainStep(graph=True)
 
 Usage: python tools/dbg/capture_probe.py MODE   (prints one JSON line; segfaults are the finding)"""
@@ -44,6 +45,10 @@ def body():
             out.copy_(x)
             dist.all_reduce(out)
         torch.cuda.current_stream().wait_stream(s)
+    elif mode == "unjoined":  # a forked stream never joined back: an error, or a crash?
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            out.copy_(x)
     elif mode == "gather":
         dist.all_gather_into_tensor(out, x)
     else:
@@ -67,8 +72,13 @@ if mode == "step_gather":
 else:
     side = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        body()
+    try:
+        with torch.cuda.graph(g):
+            body()
+    except RuntimeError as e:
+        res["error"] = str(e)[:300]
+        print(json.dumps(res), flush=True)
+        raise SystemExit(0)
     res["captured"] = True
     for _ in range(2):
         out.zero_()

@@ -194,6 +194,218 @@ __device__ __forceinline__ int piece_len(int len) {
   return t > kPieceT ? t : kPieceT;
 }
 
+// ---------------------------------------------------------------------------------------
+// The plan's sort, hand-written: a least-significant-digit counting sort of the row keys in P
+// passes of D <= 11 bits (C3: keys in [0, 200000], 18 bits = 2 passes of 9; C2: 2 of 8), each
+// pass three launches with no inter-workgroup waiting:
+//   count   one workgroup per tile of kSortTile consecutive entries: the tile's digit histogram
+//           (LDS), written digit-major, cnt[d * ntiles + tile];
+//   scan    one workgroup per digit: exclusive scan of its row over the tiles, in place, and the
+//           row total;
+//   scatter one workgroup per tile: digit base (exclusive scan of the totals + the tile's row
+//           offset) + the entry's rank among the tile's entries of its digit, in entry order, so
+//           every pass is stable and the result is THE stable sort of (key, seq) by key.
+// Pass 0 reads the ids directly (the key and the sequence index are formed on the fly), so no
+// keys/values arrays are staged.  The in-tile rank: entry j of a tile sits at wave j / 256,
+// step (j / 64) % 4, lane j % 64; a wave forms each step's same-digit lane set with D ballots,
+// and keeps its running per-digit counts in its own LDS row; the wave offsets per digit are an
+// exclusive scan over the waves' rows.  Bytes per pass: keys (+ values) read twice, written once.
+constexpr int kSortThreads = 512;
+constexpr int kSortWaves = kSortThreads / kWave;
+constexpr int kSortIPT = 4;  // entries per thread per tile
+constexpr int kSortTile = kSortThreads * kSortIPT;
+constexpr int kSortMaxD = 11;
+
+template <typename IdT>
+struct SortSrc {  // pass 0: ids (keys == nullptr); later passes: the previous pass's output
+  const IdT* ids;
+  int64_t L, ld, V, padding_idx;
+  const uint32_t* keys;
+  const int32_t* vals;
+  __device__ __forceinline__ void load(int64_t i, uint32_t& key, int32_t& val) const {
+    if (keys) {
+      key = keys[i];
+      val = vals[i];
+      return;
+    }
+    const int64_t seq = i / L, t = i - seq * L;
+    const int64_t id = (int64_t)ids[seq * ld + t];
+    const bool valid = id > 0 && id < V && id != padding_idx;
+    key = valid ? (uint32_t)id : (uint32_t)V;
+    val = (int32_t)seq;
+  }
+};
+
+// Exclusive scan of one int per thread over a kSortThreads workgroup; *total = the sum.
+__device__ __forceinline__ int32_t sort_block_excl_scan(int32_t x, int32_t* wsum, int32_t* total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  int32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  int32_t before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < kSortWaves; ++k) {
+    const int32_t s = wsum[k];
+    before += k < w ? s : 0;
+    all += s;
+  }
+  __syncthreads();  // wsum may be reused by the caller
+  if (total) *total = all;
+  return before + inc - x;
+}
+
+template <typename IdT>
+__global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<IdT> src, int64_t n, int shift,
+                                                                       int D, int64_t ntiles,
+                                                                       int32_t* __restrict__ cnt) {
+  __shared__ int32_t h[1 << kSortMaxD];
+  const int nd = 1 << D;
+  for (int d = threadIdx.x; d < nd; d += kSortThreads) h[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll
+  for (int k = 0; k < kSortIPT; ++k) {
+    const int64_t i = base + k * kSortThreads + threadIdx.x;
+    if (i < n) {
+      uint32_t key;
+      int32_t val;
+      src.load(i, key, val);
+      atomicAdd(&h[(key >> shift) & (nd - 1)], 1);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nd; d += kSortThreads) cnt[(int64_t)d * ntiles + blockIdx.x] = h[d];
+}
+
+// One workgroup per digit: cnt[d][0..ntiles) -> its exclusive scan, total[d] = the row sum.
+__global__ __launch_bounds__(kSortThreads) void plan_sort_scan_kernel(int32_t* __restrict__ cnt, int64_t ntiles,
+                                                                      int32_t* __restrict__ total) {
+  __shared__ int32_t wsum[kSortWaves];
+  int32_t* row = cnt + (int64_t)blockIdx.x * ntiles;
+  int32_t carry = 0;
+  for (int64_t t0 = 0; t0 < ntiles; t0 += kSortThreads) {
+    const int64_t t = t0 + threadIdx.x;
+    const int32_t x = t < ntiles ? row[t] : 0;
+    int32_t sum;
+    const int32_t ex = sort_block_excl_scan(x, wsum, &sum);
+    if (t < ntiles) row[t] = carry + ex;
+    carry += sum;
+  }
+  if (threadIdx.x == 0) total[blockIdx.x] = carry;
+}
+
+template <typename IdT, int D>
+__global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc<IdT> src, int64_t n, int shift,
+                                                                         int64_t ntiles,
+                                                                         const int32_t* __restrict__ cnt,
+                                                                         const int32_t* __restrict__ total,
+                                                                         uint32_t* __restrict__ keys_out,
+                                                                         int32_t* __restrict__ vals_out) {
+  constexpr int ND = 1 << D;
+  constexpr int DPT = (ND + kSortThreads - 1) / kSortThreads;  // digits per thread in the base scan
+  __shared__ int32_t hw[kSortWaves][ND];  // per-wave running counts, then per-wave digit offsets
+  __shared__ int32_t wsum[kSortWaves];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  for (int d = threadIdx.x; d < kSortWaves * ND; d += kSortThreads) (&hw[0][0])[d] = 0;
+  __syncthreads();
+
+  const int64_t wbase = (int64_t)blockIdx.x * kSortTile + (int64_t)w * (kWave * kSortIPT);
+  const uint64_t lt = (uint64_t(1) << lane) - 1;
+  uint32_t key[kSortIPT];
+  int32_t val[kSortIPT], rk[kSortIPT];
+#pragma unroll
+  for (int k = 0; k < kSortIPT; ++k) {
+    const int64_t i = wbase + k * kWave + lane;
+    const bool ok = i < n;
+    key[k] = 0;
+    val[k] = 0;
+    if (ok) src.load(i, key[k], val[k]);
+    const int d = (int)((key[k] >> shift) & (ND - 1));
+    uint64_t peers = __ballot(ok);
+#pragma unroll
+    for (int b = 0; b < D; ++b) {
+      const bool bit = (d >> b) & 1;
+      const uint64_t bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    const int below = __popcll(peers & lt);
+    const int32_t prior = ok ? hw[w][d] : 0;
+    rk[k] = prior + below;
+    if (ok && below == 0) hw[w][d] = prior + __popcll(peers);  // the lowest peer lane writes
+  }
+  __syncthreads();
+  // digit base of this tile = (sum of the totals of the smaller digits) + the tile's row offset;
+  // then the per-wave offsets: base + the counts of the earlier waves for that digit
+  int32_t tv[DPT], part = 0;
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const int d = threadIdx.x * DPT + j;
+    tv[j] = d < ND ? total[d] : 0;
+    part += tv[j];
+  }
+  int32_t run = sort_block_excl_scan(part, wsum, nullptr);
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const int d = threadIdx.x * DPT + j;
+    if (d < ND) {
+      int32_t off = run + cnt[(int64_t)d * ntiles + blockIdx.x];
+#pragma unroll
+      for (int v = 0; v < kSortWaves; ++v) {
+        const int32_t c = hw[v][d];
+        hw[v][d] = off;
+        off += c;
+      }
+    }
+    run += tv[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSortIPT; ++k) {
+    const int64_t i = wbase + k * kWave + lane;
+    if (i < n) {
+      const int d = (int)((key[k] >> shift) & (ND - 1));
+      const int64_t pos = (int64_t)hw[w][d] + rk[k];
+      keys_out[pos] = key[k];
+      vals_out[pos] = val[k];
+    }
+  }
+}
+
+// seg_start from the sorted keys, one thread per boundary i in [0, n]: every row r with
+// key[i - 1] < r <= key[i] starts at i (the first sorted position with key >= r).  The rows are
+// written once each; thread 0 also resets the piece counter bag_plan_pieces_kernel allocates from.
+__global__ __launch_bounds__(kBlock) void bag_plan_starts_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                                 int64_t V, int32_t* __restrict__ seg_start,
+                                                                 int32_t* __restrict__ n_pieces) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i == 0) *n_pieces = 0;
+  if (i > n) return;
+  const int64_t lo = i > 0 ? (int64_t)keys[i - 1] + 1 : 0;
+  const int64_t hi = i < n ? (int64_t)keys[i] : V;
+  for (int64_t r = lo; r <= hi; ++r) seg_start[r] = (int32_t)i;
+}
+
+// Row r's pieces ([st, en) its sorted range): nch[r] = their number (0 = short row); a long row
+// takes its slots from one counter (piece_off[V]), in token order.
+__device__ __forceinline__ void plan_row_pieces(int64_t r, int32_t st, int32_t en, int64_t V, int32_t* nch,
+                                                int32_t* piece_off, int32_t* piece_beg, int32_t* piece_end) {
+  const int len = en - st;
+  const int np = len > kPieceT ? (len + piece_len(len) - 1) / piece_len(len) : 0;
+  nch[r] = np;
+  if (np == 0) return;
+  const int k0 = atomicAdd(piece_off + V, np), t = piece_len(len);
+  piece_off[r] = k0;
+  for (int k = 0; k < np; ++k) {
+    piece_beg[k0 + k] = st + k * t;
+    piece_end[k0 + k] = min(st + (k + 1) * t, en);
+  }
+}
+
 // Segment bounds and pieces of every row from the sorted keys, one thread per row r <= V:
 // seg_start[r] = the first sorted position with key >= r (lower bound), so row r's tokens are
 // [seg_start[r], seg_start[r + 1]) (seg_end aliases seg_start + 1; r = V: the masked tail).  A
@@ -228,16 +440,22 @@ __global__ __launch_bounds__(kBlock) void bag_plan_bounds_kernel(const uint32_t*
     return;
   }
   const int64_t en = threadIdx.x + 1 < kBlock ? (int64_t)lb[threadIdx.x + 1] : lower_bound(r + 1, st);
-  const int len = (int)(en - st);
-  const int np = len > kPieceT ? (len + piece_len(len) - 1) / piece_len(len) : 0;
-  nch[r] = np;
-  if (np == 0) return;
-  const int k0 = atomicAdd(piece_off + V, np), t = piece_len(len);
-  piece_off[r] = k0;
-  for (int k = 0; k < np; ++k) {
-    piece_beg[k0 + k] = (int32_t)st + k * t;
-    piece_end[k0 + k] = min((int32_t)st + (k + 1) * t, (int32_t)en);
+  plan_row_pieces(r, (int32_t)st, (int32_t)en, V, nch, piece_off, piece_beg, piece_end);
+}
+
+// The pieces of every row r < V from seg_start (bag_plan_starts_kernel); nch[V] = 0.
+__global__ __launch_bounds__(kBlock) void bag_plan_pieces_kernel(const int32_t* __restrict__ seg_start, int64_t V,
+                                                                 int32_t* __restrict__ nch,
+                                                                 int32_t* __restrict__ piece_off,
+                                                                 int32_t* __restrict__ piece_beg,
+                                                                 int32_t* __restrict__ piece_end) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r > V) return;
+  if (r == V) {
+    nch[V] = 0;
+    return;
   }
+  plan_row_pieces(r, seg_start[r], seg_start[r + 1], V, nch, piece_off, piece_beg, piece_end);
 }
 
 // One wave per piece (LPR lanes x NV float4 per row, RPI pieces per wave): partial = sum of its
@@ -622,7 +840,31 @@ BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes
 }
 
 
-size_t sort_tmp_bytes(int64_t n, int64_t V) {
+// The hand-written sort's shape: P passes of D bits over ntiles tiles; its workspace holds the
+// digit-major tile counts and the digit totals.  TT_PLAN_SORT=rocprim selects the rocPRIM onesweep
+// sort instead (same output: the stable sort is unique), for A/B runs and the equality test.
+struct SortShape {
+  int P, D;
+  int64_t ntiles;
+};
+SortShape sort_shape(int64_t n, int64_t V) {
+  const int bits = end_bit_for(V);
+  const int P = (bits + kSortMaxD - 1) / kSortMaxD;
+  return SortShape{P, (bits + P - 1) / P, (n + kSortTile - 1) / kSortTile};
+}
+size_t own_sort_bytes(int64_t n, int64_t V) {
+  const SortShape sh = sort_shape(n, V);
+  return align_up(((size_t)sh.ntiles + 1) * ((size_t)1 << sh.D) * 4, 256);
+}
+bool use_rocprim_sort() {
+  static const bool r = [] {
+    const char* e = std::getenv("TT_PLAN_SORT");
+    return e && std::strcmp(e, "rocprim") == 0;
+  }();
+  return r;
+}
+
+size_t rocprim_sort_bytes(int64_t n, int64_t V) {
   size_t bytes = 0;
   hipError_t e = rocprim::radix_sort_pairs<PlanSortConfig>(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0,
@@ -632,6 +874,12 @@ size_t sort_tmp_bytes(int64_t n, int64_t V) {
     return 0;
   }
   return bytes;
+}
+
+// both sorts fit (the layout does not depend on TT_PLAN_SORT)
+size_t sort_tmp_bytes(int64_t n, int64_t V) {
+  const size_t a = rocprim_sort_bytes(n, V), b = own_sort_bytes(n, V);
+  return a > b ? a : b;
 }
 
 template <typename IdT>
@@ -731,16 +979,58 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     TT_HIP(hipMemsetAsync(w.piece_off, 0, (size_t)(V + 1) * 4, s), "memset piece_off");
     return TT_OK;
   }
-  bag_plan_keys_kernel<IdT><<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
-      ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in, w.piece_off + V);
-  TT_LAUNCH_CHECK("bag_plan_keys");
-  size_t tmp = w.sort_bytes;
-  TT_HIP(rocprim::radix_sort_pairs<PlanSortConfig>(w.sort_tmp, tmp, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
-                                   (size_t)n, 0, end_bit_for(V), s, false),
-         "rocprim::radix_sort_pairs");
-  bag_plan_bounds_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
-      w.keys_out, n, V, w.seg_start, w.nch, w.piece_off, w.piece_beg, w.piece_end);
-  TT_LAUNCH_CHECK("bag_plan_bounds");
+  if (use_rocprim_sort()) {
+    bag_plan_keys_kernel<IdT><<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
+        ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in, w.piece_off + V);
+    TT_LAUNCH_CHECK("bag_plan_keys");
+    size_t tmp = w.sort_bytes;
+    TT_HIP(rocprim::radix_sort_pairs<PlanSortConfig>(w.sort_tmp, tmp, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
+                                     (size_t)n, 0, end_bit_for(V), s, false),
+           "rocprim::radix_sort_pairs");
+    bag_plan_bounds_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
+        w.keys_out, n, V, w.seg_start, w.nch, w.piece_off, w.piece_beg, w.piece_end);
+    TT_LAUNCH_CHECK("bag_plan_bounds");
+    return TT_OK;
+  }
+  // hand-written LSD counting sort: pass p writes (keys_out, vals_out) when P - 1 - p is even,
+  // (keys_in, vals_in) otherwise, so the last pass lands in the _out arrays
+  const SortShape sh = sort_shape(n, V);
+  const int nd = 1 << sh.D;
+  int32_t* cnt = static_cast<int32_t*>(w.sort_tmp);
+  int32_t* total = cnt + (size_t)nd * sh.ntiles;
+  SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr};
+  for (int p = 0; p < sh.P; ++p) {
+    const bool to_out = ((sh.P - 1 - p) & 1) == 0;
+    uint32_t* ko = to_out ? w.keys_out : w.keys_in;
+    int32_t* vo = to_out ? w.vals_out : w.vals_in;
+    const int shift = p * sh.D;
+    plan_sort_count_kernel<IdT><<<dim3((unsigned)sh.ntiles), dim3(kSortThreads), 0, s>>>(src, n, shift, sh.D,
+                                                                                       sh.ntiles, cnt);
+    TT_LAUNCH_CHECK("plan_sort_count");
+    plan_sort_scan_kernel<<<dim3((unsigned)nd), dim3(kSortThreads), 0, s>>>(cnt, sh.ntiles, total);
+    TT_LAUNCH_CHECK("plan_sort_scan");
+    switch (sh.D) {
+#define TT_SC(DD)                                                                                         \
+  case DD:                                                                                                \
+    plan_sort_scatter_kernel<IdT, DD><<<dim3((unsigned)sh.ntiles), dim3(kSortThreads), 0, s>>>(src, n, shift, \
+                                                                                             sh.ntiles, cnt, \
+                                                                                             total, ko, vo);  \
+    break;
+      TT_SC(1) TT_SC(2) TT_SC(3) TT_SC(4) TT_SC(5) TT_SC(6) TT_SC(7) TT_SC(8) TT_SC(9) TT_SC(10) TT_SC(11)
+#undef TT_SC
+      default: TT_REQUIRE(false, "plan sort: digit width %d", sh.D);
+    }
+    TT_LAUNCH_CHECK("plan_sort_scatter");
+    src.keys = ko;
+    src.vals = vo;
+  }
+  bag_plan_starts_kernel<<<dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(w.keys_out, n, V,
+                                                                                           w.seg_start,
+                                                                                           w.piece_off + V);
+  TT_LAUNCH_CHECK("bag_plan_starts");
+  bag_plan_pieces_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
+      w.seg_start, V, w.nch, w.piece_off, w.piece_beg, w.piece_end);
+  TT_LAUNCH_CHECK("bag_plan_pieces");
   return TT_OK;
 }
 
@@ -847,6 +1137,15 @@ extern "C" int tt_bag_plan(const void* ids, int ids_dtype, int64_t nseq, int L, 
   if (rc) return rc;
   return plan_impl(ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, plan, plan_bytes,
                    reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_bag_plan_layout(int64_t nseq, int L, int64_t V, int E, int64_t* offs) {
+  TT_REQUIRE(offs != nullptr && V > 0 && E > 0 && nseq >= 0 && L >= 0, "tt_bag_plan_layout: bad arguments");
+  const BwdWs z = plan_layout(reinterpret_cast<void*>(256), nseq, L, V, E);  // offsets from a 256-B base
+  offs[0] = reinterpret_cast<char*>(z.keys_out) - reinterpret_cast<char*>(256);
+  offs[1] = reinterpret_cast<char*>(z.vals_out) - reinterpret_cast<char*>(256);
+  offs[2] = reinterpret_cast<char*>(z.seg_start) - reinterpret_cast<char*>(256);
+  return TT_OK;
 }
 
 extern "C" int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom, int64_t nseq, int L, int64_t V,
