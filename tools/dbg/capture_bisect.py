@@ -35,7 +35,8 @@ loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype="fp32", cro
 opt = tt.optim.AdamW(model.parameters(), fused_tables=True, tables=[emb], capturable=True, table_sync=sync)
 step = tt.TrainStep(model, loss_fn, opt, graph=False)
 batch = tt.data.synthetic_triplets(256, 16, 5000, seed=1, device="cuda")
-first = float(step.eager(*batch))
+for _ in range(int(os.environ.get("TT_BISECT_WARMUP", "1"))):
+    first = float(step.eager(*batch))
 torch.cuda.synchronize()
 print(f"eager step ok: loss {first:.6f}", flush=True)
 
@@ -47,10 +48,6 @@ with torch.cuda.graph(g):
         side.active = True
     with ops.deferred_loss_mean(), step._scorer_prep_open():
         loss = loss_fn(*model(*batch))
-    if mode == "fwd":  # the plan's side stream joins in the backward: join it here
-        from twotower_amd import _lib
-
-        torch.cuda.current_stream().wait_stream(_lib.side_stream(torch.device("cuda", 0)))
     if mode in ("fwd_bwd", "full"):
         opt.zero_grad(set_to_none=True)
         seed = torch.full((), step.sync.loss_scale() if step.sync is not None else 1.0, device="cuda")
@@ -64,6 +61,10 @@ with torch.cuda.graph(g):
     if side is not None:
         side.active = False
         side.join()
+    if mode != "full":  # the plan's side stream is joined by the optimizer: join it here
+        from twotower_amd import _lib
+
+        torch.cuda.current_stream().wait_stream(_lib.side_stream(torch.device("cuda", 0)))
 print("capture ended", flush=True)
 g.replay()
 torch.cuda.synchronize()

@@ -5,6 +5,8 @@
   async_ar    dist.all_reduce(async_op=True) + work.wait()
   side_ar     all_reduce issued on a side stream forked from / joined back to the capture stream
   gather      dist.all_gather_into_tensor on the current stream
+  side_async_ar  async all-reduce + wait on a forked comm stream, joined by an event
+  multi       all-gather on the capture stream, then a comm-stream async all-reduce
   unjoined    a side stream forked from the capture and never joined (no collective)
   step_gather the bench's DP TrainStep (--dp gather) captured through TrainStep(graph=True)
 
@@ -45,6 +47,23 @@ def body():
             out.copy_(x)
             dist.all_reduce(out)
         torch.cuda.current_stream().wait_stream(s)
+    elif mode == "side_async_ar":  # GradSync.launch's pattern: async all-reduce on a comm stream
+        side.wait_stream(torch.cuda.current_stream())
+        out.copy_(x)
+        with torch.cuda.stream(side):
+            dist.all_reduce(out, async_op=True).wait()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        out.record_stream(side)
+        torch.cuda.current_stream().wait_event(ev)
+    elif mode == "multi":  # all-gather on the capture stream, then the comm-stream all-reduce
+        tmp = torch.empty_like(x)
+        dist.all_gather_into_tensor(tmp, x)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            out.copy_(tmp)
+            dist.all_reduce(out, async_op=True).wait()
+        torch.cuda.current_stream().wait_stream(side)
     elif mode == "unjoined":  # a forked stream never joined back: an error, or a crash?
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):

@@ -222,13 +222,19 @@ struct SortSrc {  // pass 0: ids (keys == nullptr); later passes: the previous p
   int64_t L, ld, V, padding_idx;
   const uint32_t* keys;
   const int32_t* vals;
+  double inv_L;  // 1 / L: the entry -> (sequence, position) split without a 64-bit division
   __device__ __forceinline__ void load(int64_t i, uint32_t& key, int32_t& val) const {
     if (keys) {
       key = keys[i];
       val = vals[i];
       return;
     }
-    const int64_t seq = i / L, t = i - seq * L;
+    // i < 2^31: i * (1 / L) in double is within one of the quotient; fixed up exactly (no
+    // 64-bit integer division, which gfx950 emulates in ~40 instructions)
+    int64_t seq = (int64_t)((double)i * inv_L);
+    seq -= seq * L > i ? 1 : 0;
+    seq += (seq + 1) * L <= i ? 1 : 0;
+    const int64_t t = i - seq * L;
     const int64_t id = (int64_t)ids[seq * ld + t];
     const bool valid = id > 0 && id < V && id != padding_idx;
     key = valid ? (uint32_t)id : (uint32_t)V;
@@ -307,24 +313,33 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
                                                                          uint32_t* __restrict__ keys_out,
                                                                          int32_t* __restrict__ vals_out) {
   constexpr int ND = 1 << D;
-  constexpr int DPT = (ND + kSortThreads - 1) / kSortThreads;  // digits per thread in the base scan
-  __shared__ int32_t hw[kSortWaves][ND];  // per-wave running counts, then per-wave digit offsets
+  constexpr int DPT = (ND + kSortThreads - 1) / kSortThreads;  // digits per thread in the digit scans
+  __shared__ int32_t hw[kSortWaves][ND];  // per-wave running counts, then per-wave tile offsets
+  __shared__ int32_t gdst[ND];            // where digit d's run of this tile starts in the output
+  __shared__ int32_t tst[ND];             // ... and in the tile's sorted order
+  __shared__ uint32_t sk[kSortTile];      // the tile in sorted order (staged so the global
+  __shared__ int32_t sv[kSortTile];       // writes of a digit's run are consecutive lanes)
   __shared__ int32_t wsum[kSortWaves];
   const int w = threadIdx.x >> 6, lane = lane_id();
   for (int d = threadIdx.x; d < kSortWaves * ND; d += kSortThreads) (&hw[0][0])[d] = 0;
   __syncthreads();
 
-  const int64_t wbase = (int64_t)blockIdx.x * kSortTile + (int64_t)w * (kWave * kSortIPT);
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int64_t wbase = base + (int64_t)w * (kWave * kSortIPT);
+  const int tile_n = (int)(n - base < kSortTile ? n - base : kSortTile);
   const uint64_t lt = (uint64_t(1) << lane) - 1;
   uint32_t key[kSortIPT];
   int32_t val[kSortIPT], rk[kSortIPT];
 #pragma unroll
   for (int k = 0; k < kSortIPT; ++k) {
     const int64_t i = wbase + k * kWave + lane;
-    const bool ok = i < n;
     key[k] = 0;
     val[k] = 0;
-    if (ok) src.load(i, key[k], val[k]);
+    if (i < n) src.load(i, key[k], val[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kSortIPT; ++k) {
+    const bool ok = wbase + k * kWave + lane < n;
     const int d = (int)((key[k] >> shift) & (ND - 1));
     uint64_t peers = __ballot(ok);
 #pragma unroll
@@ -339,39 +354,58 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
     if (ok && below == 0) hw[w][d] = prior + __popcll(peers);  // the lowest peer lane writes
   }
   __syncthreads();
-  // digit base of this tile = (sum of the totals of the smaller digits) + the tile's row offset;
-  // then the per-wave offsets: base + the counts of the earlier waves for that digit
-  int32_t tv[DPT], part = 0;
+  // per digit: the waves' offsets inside the tile's run, the run's length, its global start
+  // (exclusive scan of the digit totals + this tile's row offset) and its tile-sorted start
+  int32_t tv[DPT], tl[DPT], part = 0, tpart = 0;
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
     const int d = threadIdx.x * DPT + j;
     tv[j] = d < ND ? total[d] : 0;
+    tl[j] = 0;
+    if (d < ND) {
+#pragma unroll
+      for (int v = 0; v < kSortWaves; ++v) {
+        const int32_t c = hw[v][d];
+        hw[v][d] = tl[j];
+        tl[j] += c;
+      }
+    }
     part += tv[j];
+    tpart += tl[j];
   }
   int32_t run = sort_block_excl_scan(part, wsum, nullptr);
+  int32_t trun = sort_block_excl_scan(tpart, wsum, nullptr);
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
     const int d = threadIdx.x * DPT + j;
     if (d < ND) {
-      int32_t off = run + cnt[(int64_t)d * ntiles + blockIdx.x];
-#pragma unroll
-      for (int v = 0; v < kSortWaves; ++v) {
-        const int32_t c = hw[v][d];
-        hw[v][d] = off;
-        off += c;
-      }
+      gdst[d] = run + cnt[(int64_t)d * ntiles + blockIdx.x];
+      tst[d] = trun;
     }
     run += tv[j];
+    trun += tl[j];
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kSortIPT; ++k) {
-    const int64_t i = wbase + k * kWave + lane;
-    if (i < n) {
+    if (wbase + k * kWave + lane < n) {
       const int d = (int)((key[k] >> shift) & (ND - 1));
-      const int64_t pos = (int64_t)hw[w][d] + rk[k];
-      keys_out[pos] = key[k];
-      vals_out[pos] = val[k];
+      const int lp = tst[d] + hw[w][d] + rk[k];
+      sk[lp] = key[k];
+      sv[lp] = val[k];
+    }
+  }
+  __syncthreads();
+  // the tile in sorted order: consecutive lanes write consecutive positions of each digit's run
+#pragma unroll
+  for (int k = 0; k < kSortIPT; ++k) {
+    const int s = k * kSortThreads + threadIdx.x;
+    if (s < tile_n) {
+      const uint32_t kk = sk[s];
+      const int d = (int)((kk >> shift) & (ND - 1));
+      const int64_t pos = (int64_t)gdst[d] + (s - tst[d]);
+      keys_out[pos] = kk;
+      vals_out[pos] = sv[s];
     }
   }
 }
@@ -998,7 +1032,7 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   const int nd = 1 << sh.D;
   int32_t* cnt = static_cast<int32_t*>(w.sort_tmp);
   int32_t* total = cnt + (size_t)nd * sh.ntiles;
-  SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr};
+  SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr, L > 0 ? 1.0 / (double)L : 0.0};
   for (int p = 0; p < sh.P; ++p) {
     const bool to_out = ((sh.P - 1 - p) & 1) == 0;
     uint32_t* ko = to_out ? w.keys_out : w.keys_in;

@@ -239,20 +239,20 @@ class GradSync:
         return small, large
 
     def _reduce(self, small, large) -> None:
-        works = []
+        # synchronous collectives: they queue on the communicator's stream behind each other
+        # either way, and an async_op collective waited on a forked stream crashes HIP graph
+        # capture at its end on this image (tools/dbg/capture_probe.py side_async_ar: segfault in
+        # hipStreamEndCapture; the same all-reduce without async_op captures and replays)
         if small:
             flat = torch.cat([p.grad.reshape(-1) for p in small])
-            works.append((dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True), flat, small))
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            off = 0
+            for p in small:
+                n = p.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
         for p in large:
-            works.append((dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None, None))
-        for work, flat, members in works:
-            work.wait()
-            if flat is not None:
-                off = 0
-                for p in members:
-                    n = p.numel()
-                    p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                    off += n
+            dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group)
 
     def sync(self) -> None:
         if not is_active(self.group):

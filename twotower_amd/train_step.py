@@ -34,7 +34,9 @@ class TrainStep:
         # (optim.AdamW): the all-reduce then overlaps the table update
         # (set on the optimizer only for the duration of this step's optimizer.step(): a plain loop
         # that calls GradSync.sync() itself must not see a second all-reduce)
-        self._sync_in_step = self.sync is not None and hasattr(optimizer, "_grad_sync")
+        # (TT_GRADSYNC_IN_STEP=0, diagnostic: the all-reduce as GradSync.sync() after backward)
+        self._sync_in_step = (self.sync is not None and hasattr(optimizer, "_grad_sync")
+                              and os.environ.get("TT_GRADSYNC_IN_STEP", "1") != "0")
         # a single-device bf16 in-batch loss: the tied towers' head prepares its operands
         # (TT_SCORER_PREP=0: the loss's own prep pass, for comparison)
         # Opened only around this step's own forward (_scorer_prep_open): set on the model for
