@@ -15,6 +15,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -307,6 +308,24 @@ def parse():
     return ap.parse_args()
 
 
+def dp_capture_canary(cfg, scorer_dtype: str, table_sync: str) -> str:
+    """Run tools/dp_capture_canary.py as a child of this rank (its own RCCL world on the job's
+    MASTER_PORT + 101, every rank's child together); "ok" if this rank's child captured and
+    replayed the small N-rank step."""
+    env = dict(os.environ)
+    env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29561")) + 101)
+    cmd = [sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "dp_capture_canary.py"),
+           "--d", str(cfg["d"]), "--loss", cfg["loss"], "--negatives", str(cfg["negatives"]), "--dtype", scorer_dtype,
+           "--table-sync", table_sync]
+    try:
+        r = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
+    except subprocess.TimeoutExpired:
+        return "timeout"
+    if r.returncode == 0 and "canary ok" in r.stdout:
+        return "ok"
+    return f"failed (rc {r.returncode})"
+
+
 def setup_dist(backend: str, force: bool = False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -350,10 +369,16 @@ def main():
 
         def loss_fn(q, p, n):
             return mn(q, p, n.view(q.shape[0], K, q.shape[1]))
-    # one rank: the step is one HIP graph.  N ranks: eager by default -- capturing the step with
-    # its RCCL collectives segfaulted in hipStreamEndCapture on this image ("graph
-    # capture with RCCL"); --graph on still asks for it
+    # the step is one HIP graph; N ranks (nccl) only after every rank's child process has captured
+    # and replayed a small N-rank step through the same paths (tools/dp_capture_canary.py), so a
+    # capture that fails or crashes on the box's ROCm/RCCL stack leaves this run eager
+    canary = None
     use_graph = args.graph == "on" or (args.graph == "auto" and not dp)
+    if dp and args.graph == "auto" and args.dist_backend == "nccl":
+        canary = dp_capture_canary(cfg, scorer_dtype, args.table_sync)
+        agree = torch.tensor([1 if canary == "ok" else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+        use_graph = bool(agree.item())
     # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
     # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
     opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
@@ -476,7 +501,7 @@ def main():
                    "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
                    "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
                    "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if dp else "local"),
-                   "hip_graph": use_graph},
+                   "hip_graph": use_graph, "graph_canary": canary},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "gather_hbm": gather_hbm_evidence(args.config, gather, V, d),
         "roofline": roofline,

@@ -235,3 +235,26 @@ def test_owner_backward_takes_each_ranks_seed(seeds):
             want = want.numpy()
             err = np.abs(got.astype(np.float64) - want).max() / max(np.abs(want).max(), 1e-30)
             assert err < 2e-3, (seeds, r, float(err))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("table_sync,loss_name", [("gather", "in_batch"), ("shard", "in_batch"),
+                                                  ("shard", "multiple_negatives")])
+def test_dp_graph_replay_equals_eager_one_rank_rccl(table_sync, loss_name):
+    """The N-rank step captured in one HIP graph (its RCCL collectives included: candidate
+    all-gathers, the table exchange, the gradient all-reduce on the communication stream) replays
+    exactly what the eager N-rank step computes: one RCCL rank with every exchange forced on
+    (tests/_dp_graph_check.py, own process), five steps, losses and parameters bit for bit."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MASTER_PORT=str(_free_port()))
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "_dp_graph_check.py"), table_sync, loss_name], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["graph_kept"], res
+    assert res["eager"] == res["graph"], res
+    assert res["max_param_diff"] == 0.0, res

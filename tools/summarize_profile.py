@@ -19,7 +19,8 @@ from collections import defaultdict
 # kernel-name pattern -> the C-ABI op (bench.py 'abi') it belongs to
 OPS = [
     (r"bag_fwd", "tt_bag_mean_fwd"),
-    (r"bag_plan_keys|bag_bwd_mark|bag_piece_count|bag_piece_list|radix_sort|onesweep|rocprim", "tt_bag_plan"),
+    (r"bag_plan_keys|bag_plan_bounds|bag_plan_starts|bag_plan_pieces|plan_sort_|bag_bwd_mark|bag_piece_count"
+     r"|bag_piece_list|radix_sort|onesweep|rocprim", "tt_bag_plan"),
     (r"bag_scale_rows|bag_piece_sum|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>"
      r"|bag_bwd_reduce_sliced_kernel<\d+, \d+, true", "tt_bag_mean_bwd_adamw_planned"),
     (r"bag_bwd_reduce", "tt_bag_mean_bwd_planned"),
@@ -38,6 +39,7 @@ OPS = [
     (r"relu_bwd", "tt_relu_bwd"),
     (r"head_gemm|head_normalize", "tt_head_gemm"),
     (r"head_wgrad", "tt_head_wgrad"),
+    (r"l2_prep_kernel", "tt_inbatch_l2_prep"),
     (r"split_planes", "tt_head_split_ff"),
     (r"Cijk_", "hipBLASLt GEMM (tower FF)"),
 ]

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -40,6 +41,8 @@ class AdamW(torch.optim.Optimizer):
         self._backward_done = None
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
+        # moment tensors already in the sharded layout (by identity; weak, so loaded state replaces them)
+        self._sharded_moments: dict[int, weakref.ref] = {}
         # capturable: id(step tensor) -> (hyper-parameters, that tensor) of the args formed one step
         # ahead by the previous step's tail launch; see _step_device
         self._ahead: dict[int, tuple] = {}
@@ -87,16 +90,32 @@ class AdamW(torch.optim.Optimizer):
             like = p if sh is None else p.new_empty(sh.Vs, sh.E)  # sharded table: this rank's rows only
             st["exp_avg"] = torch.zeros_like(like, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(like, memory_format=torch.preserve_format)
+            if sh is not None:
+                self._mark_sharded(st["exp_avg"])
         else:
             if capturable and st["step"].device != p.device:
                 st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
             sh = self._shards.get(id(p))
-            if sh is not None and st["exp_avg"].shape[0] == sh.V:  # full-table state loaded: keep own rows
+            # full-table moments loaded (load_state_dict): keep this rank's rows.  Told apart from
+            # the moments this optimizer sharded itself by identity, not by shape: at one rank the
+            # shard has the table's own row count (a shape test re-sharded them on every step,
+            # which a captured step then replayed from stale copies)
+            if sh is not None and not self._is_sharded(st["exp_avg"]):
                 for k in ("exp_avg", "exp_avg_sq"):
+                    if st[k].shape[0] != sh.V:
+                        raise ValueError(f"sharded table state: {k} has {st[k].shape[0]} rows, expected {sh.V}")
                     full = torch.zeros(sh.Vp, sh.E, dtype=st[k].dtype, device=st[k].device)
                     full[:sh.V] = st[k]
                     st[k] = sh.rows(full).clone()
+                self._mark_sharded(st["exp_avg"])
         return st
+
+    def _mark_sharded(self, t: torch.Tensor) -> None:
+        self._sharded_moments[id(t)] = weakref.ref(t)
+
+    def _is_sharded(self, t: torch.Tensor) -> bool:
+        r = self._sharded_moments.get(id(t))
+        return r is not None and r() is t
 
     def state_dict(self):
         """torch's layout; a row-sharded table (data parallel "shard" sync) reports its full-size
