@@ -5,11 +5,14 @@ import torch
 import twotower_amd as tt
 from twotower_amd import ops
 
-B, L, V, E = 8192, 64, 200_000, 256
+# shape: c3 (default: 3 x 8192 sequences of 64 ids over 200k rows) or c5 (6 x 8192 over 1M rows)
+shape = sys.argv[1] if len(sys.argv) > 1 else "c3"
+B, L, V, E = 8192, 64, (1_000_000 if shape == "c5" else 200_000), 256
+K = 4 if shape == "c5" else 1
 idsets = {}
 for name, z in (("uniform", None), ("zipf1.0", 1.0)):
-    q, p, n = tt.data.synthetic_triplets(B, L, V, seed=0, device="cuda", zipf_s=z)
-    idsets[name] = torch.cat([q, p, n]).to(torch.int32).contiguous()
+    parts = tt.data.synthetic_triplets(B, L, V, seed=0, device="cuda", zipf_s=z, negatives=K)
+    idsets[name] = torch.cat(list(parts)).to(torch.int32).contiguous()
 
 
 def t(fn, it=10, reps=10):
@@ -39,4 +42,4 @@ for name, ids in idsets.items():
     def plan():
         pl = ops.BagPlan(ids, V, E, 0)
         pl.wait()
-    print(f"tt_bag_plan {name}: {t(plan):.1f} us")
+    print(f"tt_bag_plan {shape} {name} maxd {os.environ.get('TT_PLAN_MAXD', 'default')}: {t(plan):.1f} us")

@@ -215,6 +215,10 @@ constexpr int kSortWaves = kSortThreads / kWave;
 constexpr int kSortIPT = 4;  // entries per thread per tile
 constexpr int kSortTile = kSortThreads * kSortIPT;
 constexpr int kSortMaxD = 11;
+#ifndef TT_PLAN_DEFAULT_D
+#define TT_PLAN_DEFAULT_D 9
+#endif
+constexpr int kSortDefaultD = TT_PLAN_DEFAULT_D;
 
 template <typename IdT>
 struct SortSrc {  // pass 0: ids (keys == nullptr); later passes: the previous pass's output
@@ -881,12 +885,22 @@ struct SortShape {
   int P, D;
   int64_t ntiles;
 };
+// Widest digit (TT_PLAN_MAXD, 1..11): wider digits mean fewer passes but a digits x tiles count
+// matrix that grows as 2^D (its transposed 4-byte accesses, not the entries' bytes, bound a pass)
+int sort_max_digit() {
+  static const int d = [] {
+    const char* e = std::getenv("TT_PLAN_MAXD");
+    const int v = e ? std::atoi(e) : kSortDefaultD;
+    return v < 1 ? 1 : (v > kSortMaxD ? kSortMaxD : v);
+  }();
+  return d;
+}
 SortShape sort_shape(int64_t n, int64_t V) {
-  const int bits = end_bit_for(V);
-  const int P = (bits + kSortMaxD - 1) / kSortMaxD;
+  const int bits = end_bit_for(V), maxd = sort_max_digit();
+  const int P = (bits + maxd - 1) / maxd;
   return SortShape{P, (bits + P - 1) / P, (n + kSortTile - 1) / kSortTile};
 }
-size_t own_sort_bytes(int64_t n, int64_t V) {
+size_t own_sort_bytes(int64_t n, int64_t V) {  // TT_PLAN_MAXD is read once per process: sizes agree
   const SortShape sh = sort_shape(n, V);
   return align_up(((size_t)sh.ntiles + 1) * ((size_t)1 << sh.D) * 4, 256);
 }
