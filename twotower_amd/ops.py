@@ -205,13 +205,20 @@ class BagMeanPool(torch.autograd.Function):
         if ids.dim() != 2:
             raise ValueError(f"ids must be (batch, seq_len), got shape {tuple(ids.shape)}")
         ids = ids.contiguous()
-        pooled, denom = bag_mean_forward(weight, ids)
         ctx.plan = None
-        if want_plan and scatter_mode == _lib.TT_SCATTER_SORTED:
+        plan_now = want_plan and scatter_mode == _lib.TT_SCATTER_SORTED
+        # TT_PLAN_FORK=early: the sort forked before the gather, beside it (measurement switch)
+        early = plan_now and os.environ.get("TT_PLAN_FORK", "after") == "early"
+        if early:
+            deferred = getattr(weight, "_tt_deferred", None)
+            group = deferred.gather_group if deferred is not None else None
+            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
+        pooled, denom = bag_mean_forward(weight, ids)
+        if plan_now and not early:
             # forked after the gather: the sort runs beside the towers and the scorer (forked
             # before it, beside the gather, the step took 22 us longer: 0.887 vs 0.864 ms; again
             # after the weight-gradient fix, 0.8825 vs 0.8785: the gather holds the CUs and the
-            # sort still ends beside the scorer)
+            # sort still ends beside the scorer -- both with the round-2 rocPRIM sort)
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
             ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
