@@ -308,12 +308,32 @@ def parse():
     return ap.parse_args()
 
 
-def dp_capture_canary(cfg, scorer_dtype: str, table_sync: str) -> str:
-    """Run tools/dp_capture_canary.py as a child of this rank (its own RCCL world on the job's
-    MASTER_PORT + 101, every rank's child together); "ok" if this rank's child captured and
-    replayed the small N-rank step."""
+def child_world_env(dev) -> dict:
+    """Environment for a child process of every rank that forms its own process group of the same
+    ranks: a free port chosen by rank 0 and broadcast, and its own store (under torch.distributed.run
+    TORCHELASTIC_USE_AGENT_STORE=True would make every child a client of the agent's store on the
+    job's port, where nothing serves the new one)."""
+    import socket
+
+    port = 0
+    if dist.get_rank() == 0:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+    t = torch.tensor([port], dtype=torch.int64, device=dev)
+    if dist.get_world_size() > 1:
+        dist.broadcast(t, 0)
     env = dict(os.environ)
-    env["MASTER_PORT"] = str(int(os.environ.get("MASTER_PORT", "29561")) + 101)
+    env["MASTER_PORT"] = str(int(t.item()))
+    env["TORCHELASTIC_USE_AGENT_STORE"] = "False"
+    return env
+
+
+def dp_capture_canary(cfg, scorer_dtype: str, table_sync: str, dev) -> str:
+    """Run tools/dp_capture_canary.py as a child of this rank (its own RCCL world of the same
+    ranks, every rank's child together); "ok" if this rank's child captured and replayed the small
+    N-rank step."""
+    env = child_world_env(dev)
     cmd = [sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "dp_capture_canary.py"),
            "--d", str(cfg["d"]), "--loss", cfg["loss"], "--negatives", str(cfg["negatives"]), "--dtype", scorer_dtype,
            "--table-sync", table_sync]
@@ -375,7 +395,7 @@ def main():
     canary = None
     use_graph = args.graph == "on" or (args.graph == "auto" and not dp)
     if dp and args.graph == "auto" and args.dist_backend == "nccl":
-        canary = dp_capture_canary(cfg, scorer_dtype, args.table_sync)
+        canary = dp_capture_canary(cfg, scorer_dtype, args.table_sync, dev)
         agree = torch.tensor([1 if canary == "ok" else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(agree, op=dist.ReduceOp.MIN)
         use_graph = bool(agree.item())

@@ -187,3 +187,25 @@ def _sync_modes(rank):
 def test_table_sync_mode_selection():
     assert D.table_sync_mode("auto") == "local"  # no process group
     _run(_sync_modes)
+
+
+def test_child_world_env_under_torchrun():
+    """bench.py's capture canary runs a child per rank that forms its own process group of the
+    same ranks: under torch.distributed.run (agent store on the job's port) the children must get
+    their own port and store (bench.child_world_env); 2 ranks, gloo, CPU."""
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ)
+    env.pop("TT_DIST_FORCE", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(here, "_child_world_check.py")],
+                       env=env, capture_output=True, text=True, timeout=240, cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.stdout.count("child ok") == 2, r.stdout[-2000:] + r.stderr[-2000:]
