@@ -121,6 +121,18 @@ def gather_hbm_evidence(config: str, gather: dict | None, V: int, d: int) -> dic
     return out
 
 
+def sleep_cycles_per_ms(dev) -> float:
+    """torch.cuda._sleep's spin rate on this device (cycles per ms), from one timed spin."""
+    n = 2_000_000
+    torch.cuda._sleep(n // 10)  # first launch
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    torch.cuda._sleep(n)
+    en.record()
+    torch.cuda.synchronize(dev)
+    return n / max(st.elapsed_time(en), 1e-3)
+
+
 def normalise_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     """Device time of the head's plain L2-normalise pass on (rows, d): tt_head_gemm with the
     normalise (epi 1) minus without it (epi 4), HIP events on the launch stream."""
@@ -136,6 +148,7 @@ def normalise_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     for epi in (1, 4, 1, 4):
         tt_ops._head_gemm(h, planes, epi, bias=b, norms=norms)
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(sleep_cycles_per_ms(dev) * 4.0))  # the host queues all reps first
         st.record()
         for _ in range(reps):
             tt_ops._head_gemm(h, planes, epi, bias=b, norms=norms)
@@ -159,6 +172,7 @@ def l2_backward_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     for _ in range(2):
         tt_ops.call("tt_l2norm_bwd", *args())
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(int(sleep_cycles_per_ms(dev) * 4.0))  # the host queues all reps first
         st.record()
         for _ in range(reps):
             tt_ops.call("tt_l2norm_bwd", *args())
@@ -430,9 +444,14 @@ def main():
     # Per-op device times for the rooflines: HIP events around every C-ABI call on its launch
     # stream, over an eager pass of the same step (events cannot be timed inside a graph replay;
     # the kernels and their inputs are the same).
+    # Each eager step is queued behind a spin kernel (torch.cuda._sleep) long enough for the host to
+    # enqueue the whole step first: the GPU then runs the step back to back and an op's events span
+    # its kernels only, not the host's launch gaps (an eager step costs more host time than GPU time).
+    prime = sleep_cycles_per_ms(dev) * 8.0
     _lib.TIMER.reset()
     _lib.TIMER.enabled = True
     for k in range(args.timing_steps):
+        torch.cuda._sleep(int(prime))
         step.eager(*batches[k % len(batches)])
     torch.cuda.synchronize()
     _lib.TIMER.enabled = False

@@ -1493,11 +1493,20 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
 // One block of kL2PrepWaves waves: the grid keeps prep_qd_kernel's block counts (the candidate
 // blocks' maxima are what the engines fold), but 16-wave blocks put 4x the rows in flight: with
 // 4-wave blocks the pass ran 20 us for 63 MB (each wave walked 4-8 rows in dependent rounds).
-constexpr int kL2PrepWaves = 16;
+// Round 3: 8-wave blocks with four rows' loads in flight per wave (the candidate blocks' waves
+// each take their four rows in one round; the grid fits the chip in one round of blocks):
+// 16.9 vs 20.1 us in the step (profiles/r03r_prep_ab.txt); TT_L2PREP_WAVES / _U for A/B.
+#ifndef TT_L2PREP_WAVES
+#define TT_L2PREP_WAVES 8
+#endif
+#ifndef TT_L2PREP_U
+#define TT_L2PREP_U 4
+#endif
+constexpr int kL2PrepWaves = TT_L2PREP_WAVES;
 __device__ __forceinline__ void l2_prep_rows(float* __restrict__ x, int64_t rows, __bf16* __restrict__ xb,
                                              float* __restrict__ norms, float* __restrict__ pnorms, int64_t b0,
                                              int64_t nb, float& mx) {
-  constexpr int H = 4 * kWave, U = 2;
+  constexpr int H = 4 * kWave, U = TT_L2PREP_U;
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   const int64_t step = nb * kL2PrepWaves;
   for (int64_t r0 = b0 * kL2PrepWaves + wid; r0 < rows; r0 += U * step) {
