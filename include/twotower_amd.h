@@ -354,7 +354,7 @@ int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const 
  * instead of torch.cat). */
 int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int count, void* dst, tt_stream_t stream);
 
-/* ---- tower head GEMMs, E = H in {128, 256} (MeanPoolingTower feed_forward + F.normalize,
+/* ---- tower head GEMMs, H in {128, 256}, E in {64, 128, 256} (MeanPoolingTower feed_forward + F.normalize,
  * twotower/encoders.py:38-42,77): fp32 GEMMs run on the bf16 MFMA with each operand split
  * into three bf16 terms (six cross products, fp32-equivalent).
  * tt_head_split: W (N x K fp32, or its transpose) -> three bf16 planes [3][N][K]
@@ -386,6 +386,13 @@ int tt_head_split_ff2(const float* W1, const float* W2, int E, int H, void* plan
 size_t tt_head_wgrad_ws_size(int64_t rows, int N);
 int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
                   size_t ws_bytes, tt_stream_t stream);
+/* tt_head_wgrad_ex: the rectangular form, dW = G^T X (NG x NX) and db = colsum G for G (rows x NG),
+ * X (rows x NX): NG = H in {128, 256}, NX in {64, 128, 256} -- the first Linear of a tower whose
+ * embedding width E differs from H (C1's char tower: E 64, H 128; encoders.py:38-42).
+ * tt_head_wgrad(.., N, ..) = tt_head_wgrad_ex(.., N, N, ..). */
+size_t tt_head_wgrad_ex_ws_size(int64_t rows, int NG, int NX);
+int tt_head_wgrad_ex(const float* G, const float* X, int64_t rows, int NG, int NX, float* dW, float* db, void* ws,
+                     size_t ws_bytes, tt_stream_t stream);
 /* tt_head_wgrad2: both weight gradients of a Linear-ReLU-Linear head in one launch, as slab
  * partials in ws (tt_head_wgrad2_ws_size bytes): problem 1 (G1, X1), problem 2 (G2, X2), each
  * rows x N fp32 (N in {128, 256}); tt_head_wgrad2_reduce then writes dW1 = G1^T X1, db1 = colsum G1, dW2, db2

@@ -77,9 +77,9 @@ def _hip_hidden_positive(model, ids: torch.Tensor) -> torch.Tensor:
 
     ff = model.query_tower.feed_forward
     x, _ = ops.bag_mean_forward(model.query_tower.embedding.embedding.weight, ids)
-    if x.shape[1] == ff[0].out_features and x.shape[1] in ops.HEAD_WIDTHS:
+    if ff[0].out_features in ops.HEAD_WIDTHS and x.shape[1] in ops.EMB_WIDTHS:
         mask = torch.empty(ops._lib.lib().tt_head_relu_mask_bytes(x.shape[0]) // 4, dtype=torch.int32, device=x.device)
-        h = ops._head_gemm(x, ops._planes(ff[0].weight, False), 0, bias=ff[0].bias, mask=mask)
+        h = ops._head_gemm(x, ops._planes(ff[0].weight, False), 0, bias=ff[0].bias, mask=mask, N=ff[0].out_features)
     else:
         h = torch.relu(torch.addmm(ff[0].bias, x, ff[0].weight.T))
     return h > 0

@@ -88,6 +88,8 @@ _SIGNATURES = {
     "tt_head_relu_mask_bytes": (_c_sz, [_c_i64]),
     "tt_head_wgrad_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _c_sz, _vp]),
+    "tt_head_wgrad_ex_ws_size": (_c_sz, [_c_i64, _c_int, _c_int]),
+    "tt_head_wgrad_ex": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_int, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_head_wgrad2_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad2": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_int, _vp, _c_sz, _vp]),
     "tt_head_wgrad2_reduce": (_c_int, [_vp, _c_int, _vp, _vp, _vp, _vp, _vp]),

@@ -30,11 +30,13 @@ constexpr int kWaves = 4;
 constexpr int kTileRows = 32;
 constexpr int kMaxSlices = 4;                       // N <= 256: the ReLU mask is sized for 4 slices
 
-// A head GEMM shape: out (rows x N) = A (rows x K) W^T, K, N in {128, 256} (MeanPoolingTower with
-// E = H = d: C2's d = 128, C3 / C5's d = 256).
+// A head GEMM shape: out (rows x N) = A (rows x K) W^T, K, N in {64, 128, 256} (MeanPoolingTower:
+// E = H = d at C2 (128) and C3 / C5 (256); C1's char tower E = 64 -> H = 128, whose first Linear
+// is K = 64 and whose dx GEMM is N = 64).
 template <int K, int N>
 struct HeadShape {
-  static_assert((K == 128 || K == 256) && (N == 128 || N == 256), "head GEMM shapes: K, N in {128, 256}");
+  static_assert((K == 64 || K == 128 || K == 256) && (N == 64 || N == 128 || N == 256),
+                "head GEMM shapes: K, N in {64, 128, 256}");
   static constexpr int kSlices = N / kColsWG;       // column slices (workgroups per row group)
   static constexpr int kRowB = K * 2;               // one bf16 row of W (bytes)
   static constexpr int kCH = K / 8;                 // 16-B chunks per row
@@ -400,7 +402,7 @@ struct WgradProblem2 {
   int nblk;  // blocks of the first problem (4 * slabs); 0: one problem
 };
 
-template <int N>
+template <int NG, int NX>
 __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ X,
                                                             int64_t rows, int64_t slab_rows,
                                                             float* __restrict__ part_w, float* __restrict__ part_b,
@@ -420,9 +422,12 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
   }
   // blocks b, b+8, ... share an XCD (round-robin dispatch): they take the NB output blocks of
   // one slab, so its G / X rows come from HBM once and from that XCD's L2 after
-  constexpr int NB1 = N / kWgBlk, NB = NB1 * NB1;  // output blocks per slab (4 at N = 256, 1 at 128)
+  // output blocks per slab: (NG / 128) x (NX / 128) (4 at 256 x 256, 1 at 128 x 128); an X narrower
+  // than a block (C1's E = 64) takes one block whose columns past NX are zero and never stored
+  constexpr int NBI = NG / kWgBlk, NBJ = NX < kWgBlk ? 1 : NX / kWgBlk, NB = NBI * NBJ;
+  constexpr int XW = NX < kWgBlk ? NX : kWgBlk;  // valid columns of an X block
   const int blk = (bid >> 3) % NB, slab = (bid >> 3) / NB * 8 + (bid & 7);
-  const int bi = blk % NB1, bj = blk / NB1;  // output block rows i in [128 bi, +128), cols j in [128 bj, +128)
+  const int bi = blk % NBI, bj = blk / NBI;  // output block rows i in [128 bi, +128), cols j in [128 bj, +XW)
   const int tid = threadIdx.x, lane = lane_id(), wid = tid >> 6;
   const int64_t r_begin = (int64_t)slab * slab_rows;
   const int64_t r_end = r_begin + slab_rows < rows ? r_begin + slab_rows : rows;
@@ -433,7 +438,8 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
   // loader: float4 column group lc (4 columns) of rows lr and lr + 8 of each chunk
   const int lc = tid & 31, lr = tid >> 5;
   const float* gsrc = G + 128 * bi + 4 * lc;
-  const float* xsrc = X + 128 * bj + 4 * lc;
+  const bool xok = 4 * lc < XW;
+  const float* xsrc = X + 128 * bj + (xok ? 4 * lc : 0);
   constexpr int kRing = 3;  // chunks in flight (registers); the loop is unrolled by it
   f32x4 raw[kRing][4];     // per chunk: G row lr, G row lr+8, X row lr, X row lr+8
   auto load_chunk = [&](int ch, f32x4 (&r)[4]) {
@@ -441,8 +447,8 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
     for (int h = 0; h < 2; ++h) {
       int64_t row = r_begin + (int64_t)ch * kWgChunk + lr + 8 * h;
       row = row < rows ? row : 0;
-      r[h] = *reinterpret_cast<const f32x4*>(gsrc + row * N);  // rows past the end: zeroed when staged
-      r[2 + h] = *reinterpret_cast<const f32x4*>(xsrc + row * N);
+      r[h] = *reinterpret_cast<const f32x4*>(gsrc + row * NG);  // rows past the end: zeroed when staged
+      r[2 + h] = *reinterpret_cast<const f32x4*>(xsrc + row * NX);
     }
   };
   f32x4 colsum = {0.f, 0.f, 0.f, 0.f};
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
     for (int q = 0; q < 4; ++q) {
       rv[q] = r[q];
       asm volatile("" : "+v"(rv[q]));  // keeps the use (and its vmcnt wait) here, not hoisted
-      rv[q] = ok[q & 1] ? rv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+      rv[q] = ok[q & 1] && (q < 2 || xok) ? rv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // q: 0,1 = G rows lr, lr+8; 2,3 = X rows lr, lr+8
@@ -542,7 +548,7 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
 
   // partial dW of this slab: acc[ti][tj][v] = (i, j) with i = 128 bi + 32 (2 wi + ti) + (v & 3) +
   // 8 (v >> 2) + 4 kh, j = 128 bj + 32 (2 wj + tj) + (lane & 31)
-  float* pw = part_w + (size_t)slab * N * N;
+  float* pw = part_w + (size_t)slab * NG * NX;
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -551,10 +557,11 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
       for (int v = 0; v < 16; ++v) {
         const int i = 128 * bi + 32 * (2 * wi + ti) + (v & 3) + 8 * (v >> 2) + 4 * kh;
         const int j = 128 * bj + 32 * (2 * wj + tj) + (lane & 31);
+        if (NX < kWgBlk && 32 * (2 * wj + tj) >= XW) continue;  // zero columns past a narrow X
 #ifdef TT_WABL_NOSTORE
         if (acc[ti][tj][v] == 12345.678f)
 #endif
-        pw[i * N + j] = acc[ti][tj][v];
+        pw[i * NX + j] = acc[ti][tj][v];
       }
   if (bj == 0 && part_b) {  // fold the 8 row groups (lr) of each column group in LDS, fixed order
     __syncthreads();
@@ -565,7 +572,7 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
       f32x4 t = red[tid];
 #pragma unroll
       for (int g = 1; g < 8; ++g) t += red[g * 32 + tid];
-      *reinterpret_cast<f32x4*>(part_b + (size_t)slab * N + 128 * bi + 4 * tid) = t;
+      *reinterpret_cast<f32x4*>(part_b + (size_t)slab * NG + 128 * bi + 4 * tid) = t;
     }
   }
 }
@@ -581,7 +588,7 @@ struct WgradReduce2 {
   int nblk;  // blocks of the first problem; 0: one problem
 };
 
-template <int N>
+template <int NG, int NX>
 __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __restrict__ part_w,
                                                                 const float* __restrict__ part_b, int slabs,
                                                                 float* __restrict__ dW, float* __restrict__ db,
@@ -603,10 +610,10 @@ __global__ __launch_bounds__(256) void head_wgrad_reduce_kernel(const float* __r
   const int per = (slabs + kRedQ - 1) / kRedQ;
   const int s0 = qq * per, s1 = min(slabs, s0 + per);
   const bool is_b = bid == nb - 1;  // the last block folds db (N / 4 float4 columns)
-  const bool ob = is_b && o < N / 4;
-  const f32x4 t = is_b ? (db && ob ? sum_slabs(reinterpret_cast<const f32x4*>(part_b) + o, N / 4, s0, s1)
+  const bool ob = is_b && o < NG / 4;
+  const f32x4 t = is_b ? (db && ob ? sum_slabs(reinterpret_cast<const f32x4*>(part_b) + o, NG / 4, s0, s1)
                                    : f32x4{0.f, 0.f, 0.f, 0.f})
-                       : sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, N * N / 4, s0, s1);
+                       : sum_slabs(reinterpret_cast<const f32x4*>(part_w) + i, NG * NX / 4, s0, s1);
   red[qq][o] = t;
   __syncthreads();
   if (qq == 0) {
@@ -625,19 +632,21 @@ using namespace tt;
 
 namespace tt {
 namespace {
-bool head_width_ok(int n) { return n == 128 || n == 256; }
+bool head_width_ok(int n) { return n == 128 || n == 256; }        // H (and E = H)
+bool emb_width_ok(int n) { return n == 64 || head_width_ok(n); }   // E of the first Linear
 // weight-gradient slabs: one round of 256 workgroups over the two problems of tt_head_wgrad2
 // (4 output blocks per slab at N = 256, 1 at N = 128); 64 / 256 for the one-problem form
 int wg_slabs2(int N) { return N == 256 ? 32 : 128; }
-int wg_slabs1(int N) { return N == 256 ? 64 : 256; }
-int wg_blocks(int N) { return (N / kWgBlk) * (N / kWgBlk); }
+int wg_blocks2(int NG, int NX) { return (NG / kWgBlk) * (NX < kWgBlk ? 1 : NX / kWgBlk); }
+int wg_blocks(int N) { return wg_blocks2(N, N); }
+int wg_slabs_ex(int NG, int NX) { return 256 / wg_blocks2(NG, NX); }
 }  // namespace
 }  // namespace tt
 
 extern "C" size_t tt_head_planes_bytes(int N, int K) { return (size_t)3 * N * K * 2; }
 
 extern "C" int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_stream_t stream) {
-  TT_REQUIRE(head_width_ok(N) && head_width_ok(K), "tt_head_split: N, K in {128, 256} (got %dx%d)", N, K);
+  TT_REQUIRE(emb_width_ok(N) && emb_width_ok(K), "tt_head_split: N, K in {64, 128, 256} (got %dx%d)", N, K);
   TT_REQUIRE(W && planes, "null pointer");
   SplitJobs jobs{};
   jobs.W[0] = W;
@@ -651,7 +660,8 @@ extern "C" int tt_head_split(const float* W, int N, int K, int transpose, void* 
 }
 
 extern "C" int tt_head_split_ff2(const float* W1, const float* W2, int E, int H, void* planes, tt_stream_t stream) {
-  TT_REQUIRE(head_width_ok(E) && head_width_ok(H), "tt_head_split_ff2: E, H in {128, 256} (got E=%d H=%d)", E, H);
+  TT_REQUIRE(emb_width_ok(E) && head_width_ok(H), "tt_head_split_ff2: E in {64, 128, 256}, H in {128, 256} (got E=%d H=%d)",
+             E, H);
   TT_REQUIRE(W1 && W2 && planes, "null pointer");
   // W1 (H x E), W2 (H x H), W1^T (E x H), W2^T (H x H), each as three bf16 planes, in that order
   const int64_t a = 3LL * H * E, b = 3LL * H * H;
@@ -709,7 +719,7 @@ int launch_head_gemm(const float* A, int64_t rows, int64_t lda, const __bf16* P,
 extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* planes, int N, int epi,
                             const float* bias, uint32_t* relu_mask, float* out, float* norms, void* ws,
                             size_t ws_bytes, tt_stream_t stream) {
-  TT_REQUIRE(head_width_ok(K) && head_width_ok(N), "tt_head_gemm: K, N in {128, 256} (got K=%d N=%d)", K, N);
+  TT_REQUIRE(emb_width_ok(K) && emb_width_ok(N) && (K > 64 || N > 64), "tt_head_gemm: K, N in {64, 128, 256}, not both 64 (got K=%d N=%d)", K, N);
   TT_REQUIRE(rows >= 0 && lda >= K, "bad shape rows=%lld lda=%lld", (long long)rows, (long long)lda);
   if (rows == 0) return TT_OK;
   TT_REQUIRE(rows < (int64_t(1) << 31), "rows=%lld too large", (long long)rows);
@@ -731,10 +741,20 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
   const __bf16* P = static_cast<const __bf16*>(planes);
   float* part = static_cast<float*>(ws);
   int rc;
-  if (K == 256 && N == 256) rc = launch_head_gemm<256, 256>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
-  else if (K == 128 && N == 128) rc = launch_head_gemm<128, 128>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
-  else if (K == 256) rc = launch_head_gemm<256, 128>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
-  else rc = launch_head_gemm<128, 256>(A, rows, lda, P, epi, bias, relu_mask, out, part, s);
+  TT_REQUIRE(N > 64 || (epi != EPI_BIAS_L2 && epi != EPI_BIAS_RELU), "tt_head_gemm: N = 64 only for the dx GEMMs (epi 3, 5)");
+  TT_REQUIRE(K > 64 || epi == EPI_BIAS_RELU, "tt_head_gemm: K = 64 only for the first Linear (epi 0)");
+#define TT_HG(KK, NN) \
+  if (K == KK && N == NN) rc = launch_head_gemm<KK, NN>(A, rows, lda, P, epi, bias, relu_mask, out, part, s)
+  TT_HG(256, 256);
+  else TT_HG(128, 128);
+  else TT_HG(256, 128);
+  else TT_HG(128, 256);
+  else TT_HG(64, 128);
+  else TT_HG(64, 256);
+  else TT_HG(128, 64);
+  else TT_HG(256, 64);
+  else rc = TT_ERR_UNSUPPORTED;
+#undef TT_HG
   if (rc) return rc;
   if (epi == EPI_BIAS_L2 && !defer_l2) {
     if (N == 256) head_normalize_kernel<256><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(out, rows, part, norms);
@@ -777,11 +797,11 @@ extern "C" int tt_head_wgrad2(const float* G1, const float* X1, const float* G2,
   constexpr int64_t kQuant = 3 * kWgChunk;
   const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + slabs * kQuant - 1) / (slabs * kQuant) * kQuant);
   if (N == 256)
-    head_wgrad_kernel<256><<<dim3(2 * nb), dim3(256), 2 * kWgBuf, s>>>(G1, X1, rows, slab_rows, pw1, pb1,
-                                                                      WgradProblem2{G2, X2, pw2, pb2, nb});
+    head_wgrad_kernel<256, 256><<<dim3(2 * nb), dim3(256), 2 * kWgBuf, s>>>(G1, X1, rows, slab_rows, pw1, pb1,
+                                                                           WgradProblem2{G2, X2, pw2, pb2, nb});
   else
-    head_wgrad_kernel<128><<<dim3(2 * nb), dim3(256), 2 * kWgBuf, s>>>(G1, X1, rows, slab_rows, pw1, pb1,
-                                                                      WgradProblem2{G2, X2, pw2, pb2, nb});
+    head_wgrad_kernel<128, 128><<<dim3(2 * nb), dim3(256), 2 * kWgBuf, s>>>(G1, X1, rows, slab_rows, pw1, pb1,
+                                                                           WgradProblem2{G2, X2, pw2, pb2, nb});
   TT_LAUNCH_CHECK("tt_head_wgrad2");
   return TT_OK;
 }
@@ -801,11 +821,11 @@ extern "C" int tt_head_wgrad2_reduce(const void* ws, int N, float* dW1, float* d
   const int nb = N * N / 4 / 64 + 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (N == 256)
-    head_wgrad_reduce_kernel<256><<<dim3(2 * nb), dim3(256), 0, s>>>(pw1, pb1, slabs, dW1, db1,
-                                                                    WgradReduce2{pw2, pb2, dW2, db2, nb});
+    head_wgrad_reduce_kernel<256, 256><<<dim3(2 * nb), dim3(256), 0, s>>>(pw1, pb1, slabs, dW1, db1,
+                                                                         WgradReduce2{pw2, pb2, dW2, db2, nb});
   else
-    head_wgrad_reduce_kernel<128><<<dim3(2 * nb), dim3(256), 0, s>>>(pw1, pb1, slabs, dW1, db1,
-                                                                    WgradReduce2{pw2, pb2, dW2, db2, nb});
+    head_wgrad_reduce_kernel<128, 128><<<dim3(2 * nb), dim3(256), 0, s>>>(pw1, pb1, slabs, dW1, db1,
+                                                                         WgradReduce2{pw2, pb2, dW2, db2, nb});
   TT_LAUNCH_CHECK("tt_head_wgrad2_reduce");
   return TT_OK;
 }
@@ -824,46 +844,67 @@ extern "C" int tt_head_wgrad2_parts(int N, int k, int64_t* offset, int64_t* stri
   return slabs;
 }
 
-extern "C" size_t tt_head_wgrad_ws_size(int64_t rows, int N) {
+namespace tt {
+namespace {
+template <int NG, int NX>
+void launch_wgrad(const float* G, const float* X, int64_t rows, int64_t slab_rows, int slabs, float* part_w,
+                  float* part_b, float* dW, float* db, hipStream_t s) {
+  head_wgrad_kernel<NG, NX><<<dim3(wg_blocks2(NG, NX) * slabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows,
+                                                                                          part_w, db ? part_b : nullptr);
+  const int nred = NG * NX / 4 / 64 + 1;
+  head_wgrad_reduce_kernel<NG, NX><<<dim3(nred), dim3(256), 0, s>>>(part_w, part_b, slabs, dW, db);
+}
+}  // namespace
+}  // namespace tt
+
+// dW = G^T X (NG x NX) and db = colsum G (NG): NG = H in {128, 256}, NX in {64, 128, 256} (the
+// first Linear's input width E, or H).
+extern "C" size_t tt_head_wgrad_ex_ws_size(int64_t rows, int NG, int NX) {
   (void)rows;
-  if (!head_width_ok(N)) return 0;
-  return (size_t)wg_slabs1(N) * N * (N + 1) * sizeof(float);
+  if (!head_width_ok(NG) || !emb_width_ok(NX)) return 0;
+  return (size_t)wg_slabs_ex(NG, NX) * NG * (NX + 1) * sizeof(float);
 }
 
-extern "C" int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
-                             size_t ws_bytes, tt_stream_t stream) {
-  TT_REQUIRE(head_width_ok(N), "tt_head_wgrad: N in {128, 256} (got %d)", N);
+extern "C" int tt_head_wgrad_ex(const float* G, const float* X, int64_t rows, int NG, int NX, float* dW, float* db,
+                                void* ws, size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(head_width_ok(NG) && emb_width_ok(NX), "tt_head_wgrad_ex: NG in {128, 256}, NX in {64, 128, 256} (got %dx%d)",
+             NG, NX);
   TT_REQUIRE(rows >= 0, "bad rows %lld", (long long)rows);
   TT_REQUIRE(dW && (rows == 0 || (G && X)), "null pointer");
-  TT_REQUIRE(ws && ws_bytes >= tt_head_wgrad_ws_size(rows, N), "workspace too small (%zu < %zu)", ws_bytes,
-             tt_head_wgrad_ws_size(rows, N));
+  TT_REQUIRE(ws && ws_bytes >= tt_head_wgrad_ex_ws_size(rows, NG, NX), "workspace too small (%zu < %zu)", ws_bytes,
+             tt_head_wgrad_ex_ws_size(rows, NG, NX));
   TT_REQUIRE(((reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(dW) |
                reinterpret_cast<uintptr_t>(db) | reinterpret_cast<uintptr_t>(ws)) & 15) == 0,
              "buffers must be 16-byte aligned");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (rows == 0) {  // the kernel's clamped loads need row 0 to exist
-    TT_HIP(hipMemsetAsync(dW, 0, (size_t)N * N * sizeof(float), s), "memset dW");
-    if (db) TT_HIP(hipMemsetAsync(db, 0, (size_t)N * sizeof(float), s), "memset db");
+    TT_HIP(hipMemsetAsync(dW, 0, (size_t)NG * NX * sizeof(float), s), "memset dW");
+    if (db) TT_HIP(hipMemsetAsync(db, 0, (size_t)NG * sizeof(float), s), "memset db");
     return TT_OK;
   }
-  const int slabs = wg_slabs1(N);
+  const int slabs = wg_slabs_ex(NG, NX);
   float* part_w = static_cast<float*>(ws);
-  float* part_b = part_w + (size_t)slabs * N * N;
+  float* part_b = part_w + (size_t)slabs * NG * NX;
   // slab rows: a multiple of the chunk, every slab launched (empty slabs write zero partials)
   constexpr int64_t kQuant = 3 * kWgChunk;  // whole ring turns (kRing chunks) per slab
   const int64_t slab_rows = std::max<int64_t>(kQuant, (rows + slabs * kQuant - 1) / (slabs * kQuant) * kQuant);
-  const int nred = N * N / 4 / 64 + 1;
-  if (N == 256) {
-    head_wgrad_kernel<256><<<dim3(wg_blocks(N) * slabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
-                                                                                    db ? part_b : nullptr);
-    TT_LAUNCH_CHECK("tt_head_wgrad");
-    head_wgrad_reduce_kernel<256><<<dim3(nred), dim3(256), 0, s>>>(part_w, part_b, slabs, dW, db);
-  } else {
-    head_wgrad_kernel<128><<<dim3(wg_blocks(N) * slabs), dim3(256), 2 * kWgBuf, s>>>(G, X, rows, slab_rows, part_w,
-                                                                                    db ? part_b : nullptr);
-    TT_LAUNCH_CHECK("tt_head_wgrad");
-    head_wgrad_reduce_kernel<128><<<dim3(nred), dim3(256), 0, s>>>(part_w, part_b, slabs, dW, db);
-  }
-  TT_LAUNCH_CHECK("tt_head_wgrad reduce");
+#define TT_WG(A, B) \
+  if (NG == A && NX == B) launch_wgrad<A, B>(G, X, rows, slab_rows, slabs, part_w, part_b, dW, db, s)
+  TT_WG(256, 256);
+  else TT_WG(128, 128);
+  else TT_WG(128, 64);
+  else TT_WG(256, 64);
+  else TT_WG(256, 128);
+  else TT_WG(128, 256);
+#undef TT_WG
+  TT_LAUNCH_CHECK("tt_head_wgrad_ex");
   return TT_OK;
+}
+
+extern "C" size_t tt_head_wgrad_ws_size(int64_t rows, int N) { return tt_head_wgrad_ex_ws_size(rows, N, N); }
+
+extern "C" int tt_head_wgrad(const float* G, const float* X, int64_t rows, int N, float* dW, float* db, void* ws,
+                             size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(head_width_ok(N), "tt_head_wgrad: N in {128, 256} (got %d)", N);
+  return tt_head_wgrad_ex(G, X, rows, N, N, dW, db, ws, ws_bytes, stream);
 }

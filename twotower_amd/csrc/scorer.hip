@@ -1304,15 +1304,20 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 // fp32 engine (exact f32 MFMA, 32x32x2).  The k order inside the X product is permuted
 // (k = 8*blk + 4*hh + u) so each lane reads one 16-byte chunk per four MFMAs; the Acc product
 // consumes X register t directly as its B operand (k = row of X held by register t).
-// Waves per SIMD the H = 128 fp32 engine is compiled for.  Two waves spill 80 B/lane of scratch
-// in the forward (256 VGPRs, no AGPRs); one wave keeps the whole forward in registers (217 VGPRs
-// + 64 AGPRs): C2 forward 222 -> 195 us, while the backward is faster at two waves (174 vs 182 us;
-// profiles/r02zl_f32_occupancy_ab.txt).
+// Waves per SIMD the H = 128 fp32 engine is compiled for.  Round 2: two waves spilled 80 B/lane of
+// scratch (256 VGPRs), so the forward ran at one (217 VGPRs + 64 AGPRs).  Round 3: the Acc chain's
+// LDS addresses come from four per-lane offsets plus immediates (TT_F32_AOFF; hipcc had held
+// 16 x NHT loop-invariant addresses in VGPRs across the loop), so both passes fit two waves with no
+// scratch (225 / 221 VGPRs): C2 forward 205 -> 175 us, backward 180 -> 160 us, bit-identical,
+// step 0.520 -> 0.469 ms (profiles/r03t_f32_variants.txt, r03t_c2_ab.txt).
 #ifndef TT_F32_MINW128_FWD
-#define TT_F32_MINW128_FWD 1
+#define TT_F32_MINW128_FWD 2
 #endif
 #ifndef TT_F32_MINW128_DD
 #define TT_F32_MINW128_DD 2
+#endif
+#ifndef TT_F32_AOFF
+#define TT_F32_AOFF 1
 #endif
 template <int MODE, int H>
 __global__ __launch_bounds__(NT, (H < 128 ? 2 : H > 128 ? 1 : MODE == FWD ? TT_F32_MINW128_FWD : TT_F32_MINW128_DD))
@@ -1357,6 +1362,12 @@ void score_f32_kernel(
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
   float l_run = 0.f;
   const int rx = T::swz(r32);
+#if TT_F32_AOFF
+  static_assert(T::SWM == 7, "the Acc chain's offsets assume the f32 tile's 3-bit row XOR");
+  unsigned aoff[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) aoff[u] = (u + 4 * hh) * T::ROWB + (((r32 >> 2) ^ (u + 4 * hh)) << 4) + (r32 & 3) * 4;
+#endif
   drain_dma();
   __syncthreads();
 
@@ -1379,9 +1390,16 @@ void score_f32_kernel(
     for (int ht = 0; ht < NHT; ++ht) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
+#if TT_F32_AOFF
+        // row = (v & 3) + 8 (v >> 2) + 4 hh and swz(row) = row & 7 = (v & 3) + 4 hh, so the XOR only
+        // touches the chunk's low three bits: four per-lane offsets (one per v & 3, kernel-constant)
+        // plus immediates, instead of 16 x NHT loop-invariant addresses held across the loop
+        const float a = *reinterpret_cast<const lds_float_t*>(tile + aoff[v & 3] + 8 * (v >> 2) * T::ROWB + 128 * ht);
+#else
         const int row = acc_row(v, hh);
         const float a = *reinterpret_cast<const lds_float_t*>(
             tile + row * T::ROWB + (((8 * ht + (r32 >> 2)) ^ T::swz(row)) << 4) + (r32 & 3) * 4);
+#endif
         acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, e[v], acc[ht], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);

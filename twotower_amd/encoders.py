@@ -85,7 +85,8 @@ class MeanPoolingTower(BaseTower):
         ff = self.feed_forward
         standard = (len(ff) == 3 and isinstance(ff[0], nn.Linear) and isinstance(ff[1], nn.ReLU)
                     and isinstance(ff[2], nn.Linear) and ff[0].bias is not None and ff[2].bias is not None)
-        if standard and ff[0].in_features == ff[0].out_features == ff[2].out_features in ops.HEAD_WIDTHS:
+        if (standard and ff[0].out_features == ff[2].out_features == ff[2].in_features in ops.HEAD_WIDTHS
+                and ff[0].in_features in ops.EMB_WIDTHS):
             # Linear-ReLU-Linear + F.normalize in two fused GEMM launches (encoders.py:38-42,77)
             return ops.tower_head(pooled.contiguous(), ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
         if standard and ff[0].out_features % 4 == 0 and ff[2].out_features % 4 == 0:

@@ -379,7 +379,8 @@ def tower_ff(x, W1, b1, W2, b2):
 
 
 HEAD_WIDTH = 256  # the width the scorer-side fusions (operand prep, fused L2 backward) are specialised for
-HEAD_WIDTHS = (128, 256)  # E = H widths of the hand-written tower head (C2: 128; C3 / C5: 256)
+HEAD_WIDTHS = (128, 256)  # H widths of the hand-written tower head (C2: 128; C3 / C5: 256)
+EMB_WIDTHS = (64, 128, 256)  # its first Linear's input widths E (C1's char tower: E 64, H 128)
 
 
 def _planes(W: torch.Tensor, transpose: bool) -> torch.Tensor:
@@ -448,28 +449,32 @@ def fused_head_backward():
 
 
 class TowerHead(torch.autograd.Function):
-    """F.normalize(Linear-ReLU-Linear(x)) for E = H in {128, 256} (encoders.py:38-42,77) on the split-bf16
-    MFMA GEMMs with fused epilogues: bias + ReLU (+ the ReLU bitmask), bias + row L2 normalise
-    (forward); the ReLU mask fused into dh = dy W2 (backward).  Weight gradients on K-split
-    library GEMMs, bias gradients on tt_colsum."""
+    """F.normalize(Linear(E,H)-ReLU-Linear(H,H)(x)) for H in {128, 256}, E in {64, 128, 256}
+    (encoders.py:38-42,77) on the split-bf16 MFMA GEMMs with fused epilogues: bias + ReLU (+ the
+    ReLU bitmask), bias + row L2 normalise (forward); the ReLU mask fused into dh = dy W2, dx = dh W1
+    (backward).  Weight and bias gradients on the split-bf16 MFMA kernels (tt_head_wgrad2 in one
+    launch for E = H, tt_head_wgrad_ex per Linear otherwise)."""
 
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2):
         require_gpu(x, W1, W2)
         ctx.bag_token = x._tt_bag_token if _SOLE_HEAD and _SOLE_HEAD[-1] is x else None
         x = _contig_f32(x, "x")
-        rows, width = x.shape  # E = H = width (HEAD_WIDTHS)
-        nb = _lib.lib().tt_head_planes_bytes(width, width)
-        planes = torch.empty(4 * nb, dtype=torch.uint8, device=x.device)  # W1, W2, W1^T, W2^T
-        call("tt_head_split_ff2", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), width, width, ptr(planes),
+        rows, E = x.shape
+        H = W1.shape[0]  # width = H (HEAD_WIDTHS), E in EMB_WIDTHS
+        width = H
+        n1, n2 = _lib.lib().tt_head_planes_bytes(H, E), _lib.lib().tt_head_planes_bytes(H, H)
+        planes = torch.empty(2 * (n1 + n2), dtype=torch.uint8, device=x.device)  # W1, W2, W1^T, W2^T
+        call("tt_head_split_ff2", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), E, H, ptr(planes),
              stream_of(x))
+        p_w1, p_w2 = planes[:n1], planes[n1:n1 + n2]
         mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
-        h = _head_gemm(x, planes[:nb], 0, bias=b1, mask=mask)
+        h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
         req = _SCORER_PREP[-1] if _SCORER_PREP and width == HEAD_WIDTH else None
         if req is not None and 0 < req[0] < rows:
             nq, dt = req  # normalise pass fused with the in-batch scorer's operand prep
-            out = _head_gemm(h, planes[nb:2 * nb], 4, bias=b2)
+            out = _head_gemm(h, p_w2, 4, bias=b2)
             ws = torch.empty(_lib.lib().tt_inbatch_ws_size(nq, rows - nq, HEAD_WIDTH, dt), dtype=torch.uint8,
                              device=x.device)
             call("tt_inbatch_l2_prep", ptr(out), nq, rows - nq, HEAD_WIDTH, dt, ptr(norm), ptr(ws), ws.numel(),
@@ -477,7 +482,7 @@ class TowerHead(torch.autograd.Function):
             ctx.l2_token = _L2Token(norm)
             out._tt_inbatch_prep = (nq, rows - nq, dt, ws, ctx.l2_token)
         else:
-            out = _head_gemm(h, planes[nb:2 * nb], 1, bias=b2, norms=norm)
+            out = _head_gemm(h, p_w2, 1, bias=b2, norms=norm)
         if req is None or not 0 < req[0] < rows:
             ctx.l2_token = None
         ctx.save_for_backward(x, h, mask, out, norm, planes)
@@ -492,7 +497,9 @@ class TowerHead(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, h, mask, out, norm, planes = ctx.saved_tensors
-        nb = planes.numel() // 4
+        E, H = x.shape[1], out.shape[1]
+        n1, n2 = _lib.lib().tt_head_planes_bytes(H, E), _lib.lib().tt_head_planes_bytes(H, H)
+        p_w1t, p_w2t = planes[n1 + n2:2 * n1 + n2], planes[2 * n1 + n2:]
         tok, ctx.l2_token = ctx.l2_token, None
         if tok is not None and tok.dy is not None:  # the loss applied F.normalize's backward (tt_inbatch_bwd_l2)
             if tok.dy.data_ptr() != dout.data_ptr() or tok.dy.shape != dout.shape:
@@ -504,9 +511,9 @@ class TowerHead(torch.autograd.Function):
             call("tt_l2norm_bwd", ptr(dout), ptr(out), ptr(norm), out.shape[0], out.shape[1], ptr(dy),
                  stream_of(out))
         side = ctx.side_grads
-        N = out.shape[1]
-        dW1, dW2 = (torch.empty(N, N, dtype=_FLOAT, device=dy.device) for _ in range(2))
-        db1, db2 = (torch.empty(N, dtype=_FLOAT, device=dy.device) for _ in range(2))
+        N = H
+        dW1, dW2 = torch.empty(H, E, dtype=_FLOAT, device=dy.device), torch.empty(H, H, dtype=_FLOAT, device=dy.device)
+        db1, db2 = (torch.empty(H, dtype=_FLOAT, device=dy.device) for _ in range(2))
         # The optimizer joins these (optim.AdamW), so the weight gradients may run on a side stream
         # beside what follows on this one: dx feeds the fused table scatter + AdamW, an
         # HBM-bound pass the MFMA-bound weight-gradient kernels overlap.  Autograd must hand the
@@ -526,15 +533,15 @@ class TowerHead(torch.autograd.Function):
             with torch.cuda.stream(aux):
                 head_wgrad(G, X, dW, db)
 
-        dh = _head_gemm(dy, planes[3 * nb:], 2, mask=mask)
+        dh = _head_gemm(dy, p_w2t, 2, mask=mask, N=H)
         tok, ctx.bag_token = ctx.bag_token, None
         dx = None
         if ctx.needs_input_grad[0] and tok is not None:  # dx / denom for the bag backward (epi 5)
-            dx = _head_gemm(dh, planes[2 * nb:3 * nb], 5, bias=tok.denom)
+            dx = _head_gemm(dh, p_w1t, 5, bias=tok.denom, N=E)
             tok.grad = dx
         elif ctx.needs_input_grad[0]:
-            dx = _head_gemm(dh, planes[2 * nb:3 * nb], 3)
-        two = os.environ.get("TT_WGRAD2", "1") != "0"
+            dx = _head_gemm(dh, p_w1t, 3, N=E)
+        two = os.environ.get("TT_WGRAD2", "1") != "0" and E == H  # one launch for both: square heads
         if not on_side:
             if two:
                 head_wgrad2_reduce(head_wgrad2(dh, x, dy, h), dW1, db1, dW2, db2)
@@ -569,13 +576,15 @@ class TowerHead(torch.autograd.Function):
 
 def head_wgrad(G: torch.Tensor, X: torch.Tensor, dW: torch.Tensor | None = None,
                db: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-    """(G^T X, G.sum(0)) for (rows, 256) fp32 G, X on the split-bf16 MFMA kernel (tt_head_wgrad)."""
-    rows, N = G.shape
-    dW = torch.empty(N, N, dtype=_FLOAT, device=G.device) if dW is None else dW
-    db = torch.empty(N, dtype=_FLOAT, device=G.device) if db is None else db
-    nws = _lib.lib().tt_head_wgrad_ws_size(rows, N)
+    """(G^T X, G.sum(0)) for fp32 G (rows, NG), X (rows, NX) on the split-bf16 MFMA kernel
+    (tt_head_wgrad_ex: NG in {128, 256}, NX in {64, 128, 256})."""
+    rows, NG = G.shape
+    NX = X.shape[1]
+    dW = torch.empty(NG, NX, dtype=_FLOAT, device=G.device) if dW is None else dW
+    db = torch.empty(NG, dtype=_FLOAT, device=G.device) if db is None else db
+    nws = _lib.lib().tt_head_wgrad_ex_ws_size(rows, NG, NX)
     ws = torch.empty(nws, dtype=torch.uint8, device=G.device)
-    call("tt_head_wgrad", ptr(G), ptr(X), rows, N, ptr(dW), ptr(db), ptr(ws), nws, stream_of(G))
+    call("tt_head_wgrad_ex", ptr(G), ptr(X), rows, NG, NX, ptr(dW), ptr(db), ptr(ws), nws, stream_of(G))
     return dW, db
 
 
