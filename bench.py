@@ -133,6 +133,23 @@ def sleep_cycles_per_ms(dev) -> float:
     return n / max(st.elapsed_time(en), 1e-3)
 
 
+def stamped_op_times(model, loss_fn, opt, batches, reps: int, dev) -> dict:
+    """Per-op device times (ms per call) of the replayed step: a TrainStep captured with every
+    C-ABI call bracketed by tt_stamp kernels (_lib.OpTimer.stamp_capture), replayed `reps` times,
+    the stamps read after each replay.  Returns _lib.OpTimer.summary()'s format."""
+    sstep = tt.TrainStep(model, loss_fn, opt, graph=True, eager_steps=1)
+    sstep(*batches[0])  # eager: lazy set-up
+    with _lib.TIMER.stamp_capture(dev):
+        sstep(*batches[1])  # captured (stamped) and replayed once
+    per: dict[str, list[float]] = {}
+    for k in range(reps):
+        sstep(*batches[k % len(batches)])
+        torch.cuda.synchronize()
+        for name, ts in _lib.TIMER.stamp_summary(dev).items():
+            per.setdefault(name, []).extend(ts)
+    return {n: {"calls": len(v), "mean_ms": sum(v) / len(v), "total_ms": sum(v)} for n, v in per.items()}
+
+
 def normalise_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     """Device time of the head's plain L2-normalise pass on (rows, d): tt_head_gemm with the
     normalise (epi 1) minus without it (epi 4), HIP events on the launch stream."""
@@ -441,21 +458,27 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    # Per-op device times for the rooflines: HIP events around every C-ABI call on its launch
-    # stream, over an eager pass of the same step (events cannot be timed inside a graph replay;
-    # the kernels and their inputs are the same).
-    # Each eager step is queued behind a spin kernel (torch.cuda._sleep) long enough for the host to
-    # enqueue the whole step first: the GPU then runs the step back to back and an op's events span
-    # its kernels only, not the host's launch gaps (an eager step costs more host time than GPU time).
-    prime = sleep_cycles_per_ms(dev) * 8.0
-    _lib.TIMER.reset()
-    _lib.TIMER.enabled = True
-    for k in range(args.timing_steps):
-        torch.cuda._sleep(int(prime))
-        step.eager(*batches[k % len(batches)])
-    torch.cuda.synchronize()
-    _lib.TIMER.enabled = False
-    ops_t = _lib.TIMER.summary()
+    # Per-op device times for the rooflines, after the timed region.
+    if use_graph and world == 1:
+        # From the replayed graph itself: a second capture of the same step with every C-ABI call
+        # bracketed by tt_stamp kernels on its launch stream (HIP events cannot be recorded inside
+        # a captured graph on ROCm); each replay rewrites the stamps.  Same kernels, same streams,
+        # same overlap as the timed replays, plus two one-wave stamp kernels per op.
+        ops_t, timing_source = stamped_op_times(model, loss_fn, opt, batches, args.timing_steps, dev), "graph_stamps"
+    else:
+        # Eager pass of the same step, HIP events around every C-ABI call on its launch stream.  Each
+        # eager step is queued behind a spin kernel (torch.cuda._sleep) long enough for the host to
+        # enqueue the whole step first: the GPU then runs the step back to back and an op's events
+        # span its kernels, not the host's launch gaps (an eager step costs more host time than GPU).
+        prime = sleep_cycles_per_ms(dev) * 8.0
+        _lib.TIMER.reset()
+        _lib.TIMER.enabled = True
+        for k in range(args.timing_steps):
+            torch.cuda._sleep(int(prime))
+            step.eager(*batches[k % len(batches)])
+        torch.cuda.synchronize()
+        _lib.TIMER.enabled = False
+        ops_t, timing_source = _lib.TIMER.summary(), "eager_events_primed"
     timing_steps = args.timing_steps
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -544,6 +567,9 @@ def main():
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "gather_hbm": gather_hbm_evidence(args.config, gather, V, d),
         "roofline": roofline,
+        # where the per-op times behind roofline / kernels come from: "graph_stamps" (a stamped
+        # capture of the same step, replayed) or "eager_events_primed" (N ranks: an eager pass)
+        "op_times": timing_source,
         "kernels": kernels,
         "cpu_baseline": cpu,
         "final_loss": float(loss.item()) if loss is not None else None,

@@ -349,6 +349,14 @@ int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float
  * id rows; an index outside [0, n_src) yields an all-padding row and sets *bad to 1 (caller zeroes). */
 int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n, int L,
                        int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream);
+
+/* ---- measurement (bench.py's per-op times from a replayed graph) ----
+ * tt_stamp: writes the device's constant-rate wall clock (tt_wall_clock_khz ticks per ms) to
+ *   *slot from a one-wave kernel on `stream`: stamps launched around an op time it in stream
+ *   order, also inside a captured HIP graph (where event timing is unavailable on ROCm).
+ * tt_wall_clock_khz: that clock's rate for `device` (hipDeviceAttributeWallClockRate), < 0 on error. */
+int tt_stamp(uint64_t* slot, tt_stream_t stream);
+int tt_wall_clock_khz(int device);
 /* tt_pack_blocks: `count` (<= 8) contiguous byte blocks copied into consecutive ranges of dst
  * in one launch (TrainStep's copy of a batch into the replayed graph's packed [q; p; n] input,
  * instead of torch.cat). */

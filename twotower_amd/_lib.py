@@ -89,6 +89,8 @@ _SIGNATURES = {
     "tt_head_wgrad_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_head_wgrad_ex_ws_size": (_c_sz, [_c_i64, _c_int, _c_int]),
+    "tt_stamp": (_c_int, [_vp, _vp]),
+    "tt_wall_clock_khz": (_c_int, [_c_int]),
     "tt_head_wgrad_ex": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_int, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_head_wgrad2_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad2": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_int, _vp, _c_sz, _vp]),
@@ -273,17 +275,59 @@ def check(rc: int, name: str) -> None:
 class OpTimer:
     """Optional HIP-event bracketing of every C-ABI call on the torch current stream (the stream
     the call launches on).  bench.py enables it over the timed region to get live per-op device
-    times for the roofline figures."""
+    times for the roofline figures.
+
+    Stamp mode (``stamp_capture``): while a graph is being captured, every C-ABI call is bracketed
+    by two tt_stamp kernels on its stream instead (HIP events cannot be recorded inside a captured
+    graph on ROCm); each replay of that graph then rewrites the stamps, and ``stamp_summary``
+    turns them into per-op device times of the replayed step."""
 
     def __init__(self):
         self.enabled = False
         self.events: dict[str, list] = {}
+        self.stamping = False
+        self.stamp_buf: torch.Tensor | None = None
+        self.stamps: list[tuple[str, int]] = []
 
     def reset(self):
         self.events = {}
 
+    @contextlib.contextmanager
+    def stamp_capture(self, device, slots: int = 4096):
+        """Around a graph capture: stamp every C-ABI call the capture records."""
+        self.stamp_buf = torch.zeros(slots, dtype=torch.int64, device=device)
+        self.stamps = []
+        self.stamping = True
+        try:
+            yield
+        finally:
+            self.stamping = False
+
+    def stamp_summary(self, device) -> dict[str, list[float]]:
+        """Per op, its device time (ms) summed over its calls in the last replay of the stamped graph."""
+        khz = lib().tt_wall_clock_khz(torch.device(device).index or 0)
+        if khz <= 0:
+            raise RuntimeError("tt_wall_clock_khz failed")
+        t = self.stamp_buf.cpu().tolist()
+        out: dict[str, list[float]] = {}
+        for name, i in self.stamps:
+            out.setdefault(name, []).append((t[i + 1] - t[i]) / khz)
+        return out
+
     def run(self, name: str, fn):
-        if not self.enabled or torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing():
+            if not self.stamping:
+                return fn()
+            i = 2 * len(self.stamps)
+            if i + 2 > self.stamp_buf.numel():
+                raise RuntimeError("OpTimer: stamp buffer full")
+            s = torch.cuda.current_stream().cuda_stream
+            check(lib().tt_stamp(self.stamp_buf.data_ptr() + 8 * i, s), "tt_stamp")
+            rc = fn()
+            check(lib().tt_stamp(self.stamp_buf.data_ptr() + 8 * (i + 1), s), "tt_stamp")
+            self.stamps.append((name, i))
+            return rc
+        if not self.enabled:
             return fn()
         start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         start.record()

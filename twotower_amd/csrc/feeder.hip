@@ -117,3 +117,30 @@ extern "C" int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_
   TT_LAUNCH_CHECK("tt_gather_rows_i32");
   return TT_OK;
 }
+
+// ------------------------------------------------------------------------------------------
+// Measurement: one device timestamp (the constant-rate wall clock, tt_wall_clock_khz ticks per
+// ms) written by a one-wave kernel, so that a captured graph can time the ops it replays: stamps
+// launched around an op on its stream run after the previous kernel of that stream and before the
+// next (bench.py's stamped replay).  Lane 0 stores through a vector store; nothing reads the slot
+// on the device.
+namespace {
+__global__ __launch_bounds__(64) void stamp_kernel(unsigned long long* __restrict__ slot) {
+  const unsigned long long t = wall_clock64();
+  if (threadIdx.x == 0) *slot = t;
+}
+}  // namespace
+
+extern "C" int tt_stamp(uint64_t* slot, tt_stream_t stream) {
+  TT_REQUIRE(slot && (reinterpret_cast<uintptr_t>(slot) & 7) == 0, "tt_stamp: 8-byte aligned slot");
+  stamp_kernel<<<dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+      reinterpret_cast<unsigned long long*>(slot));
+  TT_LAUNCH_CHECK("tt_stamp");
+  return TT_OK;
+}
+
+extern "C" int tt_wall_clock_khz(int device) {
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess) return -1;
+  return khz;
+}
