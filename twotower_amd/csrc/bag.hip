@@ -667,6 +667,12 @@ __device__ __forceinline__ void st4(float* p, int64_t i, f32x4 x) {
 // pair cut the update from 300 to 261 us (NS = 2: 277, NS = 8: 296 -- 128-B pieces of each row
 // stream worse; without NT no gain).  RPI = 64 / LPR rows per wave, one slice each; the
 // per-element sums are bag_bwd_reduce_kernel's, in the same order.
+// The row's bounds (nch, piece_off, seg_start, seg_end) loaded together instead of nch first: one
+// dependent memory round trip less before the gathers (round 3: apply 272 -> 267 us standalone,
+// step 0.8640 -> 0.8564 ms same box, bit-identical; profiles/r03v_reduce_bounds_ab.txt).
+#ifndef TT_REDUCE_SEG_EARLY
+#define TT_REDUCE_SEG_EARLY 1
+#endif
 template <int LPR, int U, bool FUSED, bool NT>
 __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_sliced_kernel(
     const int32_t* __restrict__ seg_start, const int32_t* __restrict__ seg_end,
@@ -684,9 +690,17 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_sliced_kernel(
   const int64_t row = row_lo + (rb * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   if (row >= V) return;
   const int col = slice * LPR + c;  // float4 index inside the row
+#if TT_REDUCE_SEG_EARLY
+  // the row's four bounds loaded together (piece_off holds V + 1 in-bounds entries, stale for rows
+  // without pieces and then unused): one memory round trip before the gathers' index loads
+  const int np = nch[row], po = piece_off[row], s0 = seg_start[row], e0 = seg_end[row];
+  const bool pieces = np > 0;
+  const int st = pieces ? po : s0, en = pieces ? po + np : e0;
+#else
   const int np = nch[row];
   const bool pieces = np > 0;
   const int st = pieces ? piece_off[row] : seg_start[row], en = pieces ? st + np : seg_end[row];
+#endif
   const float* src = pieces ? partial : gs;
   f32x4 pv, mv, vv;
   if constexpr (FUSED) {
