@@ -207,8 +207,15 @@ class BagMeanPool(torch.autograd.Function):
         ids = ids.contiguous()
         ctx.plan = None
         plan_now = want_plan and scatter_mode == _lib.TT_SCATTER_SORTED
-        # TT_PLAN_FORK=early: the sort forked before the gather, beside it (measurement switch)
-        early = plan_now and os.environ.get("TT_PLAN_FORK", "after") == "early"
+        # Where the sort forks onto its side stream (TT_PLAN_FORK=early | after | auto, default auto):
+        # before the gather, beside it, when the table fits the 256 MiB Infinity Cache (the gather
+        # then reads the cache, and the latency-bound sort beside it costs it little: C3 0.8381 vs
+        # 0.8419 ms/step), after it otherwise (an HBM-bound gather of a larger table: C5 1.8235
+        # early vs 1.8178 after; profiles/r03p_c3_plan_fork_ab.txt)
+        fork = os.environ.get("TT_PLAN_FORK", "auto")
+        if fork == "auto":
+            fork = "early" if weight.numel() * weight.element_size() <= 256 * 2 ** 20 else "after"
+        early = plan_now and fork == "early"
         if early:
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
