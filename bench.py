@@ -74,6 +74,15 @@ def scorer_pmc(config: str) -> dict | None:
     out = {f"mfma_busy_{k}": v for k, v in out.items() if v is not None}
     if "engines_mfma_busy" in d:
         out["mfma_busy_engines"] = d["engines_mfma_busy"]
+    # the clock each engine ran at while profiled: its known MFMA cycles per SIMD (C3 shape: B 8192,
+    # M 16384, H 256; 32 cycles per 32x32x16 bf16 MFMA; forward 4BMH, stored-P backward 2BMH
+    # executed) over busy fraction x duration -- the dense peak at that clock is 2.5 PF x f / 2.4 GHz
+    B, M, H = 8192, 16384, 256
+    for k, mult in (("fwd", 4), ("bwd", 2)):
+        p = d.get("passes", {}).get(k, {})
+        if p.get("mfma_busy") and p.get("engine_us"):
+            cycles = mult * B * M * H / 32768 / 1024 * 32
+            out[f"clock_ghz_{k}"] = round(cycles / (p["mfma_busy"] * p["engine_us"] * 1e-6) / 1e9, 3)
     out["source"] = os.path.relpath(files[-1], ROOT)
     return out
 
