@@ -467,8 +467,11 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    # Per-op device times for the rooflines, after the timed region.
-    if use_graph and world == 1:
+    # Per-op device times for the rooflines, after the timed region (--timing-steps 0: none, e.g.
+    # under rocprofv3, whose trace then holds the timed steps alone).
+    if args.timing_steps <= 0:
+        ops_t, timing_source = {}, None
+    elif use_graph and world == 1:
         # From the replayed graph itself: a second capture of the same step with every C-ABI call
         # bracketed by tt_stamp kernels on its launch stream (HIP events cannot be recorded inside
         # a captured graph on ROCm); each replay rewrites the stamps.  Same kernels, same streams,
