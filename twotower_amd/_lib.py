@@ -195,6 +195,10 @@ class SideGrads:
         if finalize is not None:
             self.finals.append(finalize)
 
+    def add_storage(self, grads) -> None:
+        """Register (param, gradient tensor) pairs whose storage a side launch will fill."""
+        self.grads.extend((p, g.data_ptr()) for p, g in grads)
+
     def defer(self, launch) -> None:
         """Queue a side-stream launch for later (launch_pending): its inputs are fixed by an event
         the caller recorded already, so only its place in the capture order moves."""

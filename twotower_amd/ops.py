@@ -568,7 +568,10 @@ class TowerHead(torch.autograd.Function):
             ws.record_stream(aux)
             for t in (dh, dy, x, h):
                 t.record_stream(aux)
-            params, grads = ctx.params, (dW1, db1, dW2, db2)
+            params = ctx.params
+            # the gradients' storage is registered now; the launch below holds no reference to the
+            # returned tensors (autograd hands them to .grad as they are only without extra references)
+            side.add_storage(zip(params, (dW1, db1, dW2, db2)))
 
             def launch():
                 aux.wait_event(ready)
@@ -576,7 +579,7 @@ class TowerHead(torch.autograd.Function):
                     head_wgrad2(dh, x, dy, h, ws)
                 done = torch.cuda.Event()
                 done.record(aux)
-                side.add(done, zip(params, grads), finalize=_Wgrad2Sums(ws, params))
+                side.add(done, (), finalize=_Wgrad2Sums(ws, params))
 
             # TT_WGRAD_DEFER=1 (A/B): captured after the optimizer queues the table update, so that
             # update is the dx GEMM's first child in the graph and stays on its hardware queue
