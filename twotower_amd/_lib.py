@@ -176,7 +176,6 @@ class SideGrads:
         self.grads: list[tuple] = []  # (param, gradient storage) pairs produced on the side
         self.uses: dict[int, int] = {}  # forward uses per parameter since the last join
         self.finals: list = []  # callables the join queues after its wait
-        self.pending: list = []  # side launches deferred until the optimizer's first update is queued
         self.active = False
 
     def use(self, param: torch.Tensor) -> None:
@@ -195,20 +194,6 @@ class SideGrads:
         if finalize is not None:
             self.finals.append(finalize)
 
-    def add_storage(self, grads) -> None:
-        """Register (param, gradient tensor) pairs whose storage a side launch will fill."""
-        self.grads.extend((p, g.data_ptr()) for p, g in grads)
-
-    def defer(self, launch) -> None:
-        """Queue a side-stream launch for later (launch_pending): its inputs are fixed by an event
-        the caller recorded already, so only its place in the capture order moves."""
-        self.pending.append(launch)
-
-    def launch_pending(self) -> None:
-        pending, self.pending = self.pending, []
-        for f in pending:
-            f()
-
     def run_finals(self) -> None:
         """Queue the pending finalize callables on the current stream (after its waits)."""
         finals, self.finals = self.finals, []
@@ -220,7 +205,6 @@ class SideGrads:
         whose gradient sums the caller forms itself (optim.AdamW: tt_adamw_multi_ex); a finalize
         that exposes ``grad_parts()`` (slab partials) for parameters all in claim is not run, and
         its {id(param): (part pointer, stride, slabs, owner)} are returned instead."""
-        self.launch_pending()
         for ev in self.events:
             (stream or torch.cuda.current_stream()).wait_event(ev)
         self.events.clear()

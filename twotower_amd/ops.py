@@ -563,30 +563,15 @@ class TowerHead(torch.autograd.Function):
         # which holds every CU once it runs (its last kernels ran 10-30x their own time).
         if two:
             ws = torch.empty(_lib.lib().tt_head_wgrad2_ws_size(dy.shape[0], N), dtype=torch.uint8, device=dy.device)
-            ready = torch.cuda.Event()
-            ready.record(main)  # dh, dy (and dx) written on this stream
+            aux.wait_stream(main)  # dh, dy written on this stream
             ws.record_stream(aux)
             for t in (dh, dy, x, h):
                 t.record_stream(aux)
-            params = ctx.params
-            # the gradients' storage is registered now; the launch below holds no reference to the
-            # returned tensors (autograd hands them to .grad as they are only without extra references)
-            side.add_storage(zip(params, (dW1, db1, dW2, db2)))
-
-            def launch():
-                aux.wait_event(ready)
-                with torch.cuda.stream(aux):
-                    head_wgrad2(dh, x, dy, h, ws)
-                done = torch.cuda.Event()
-                done.record(aux)
-                side.add(done, (), finalize=_Wgrad2Sums(ws, params))
-
-            # TT_WGRAD_DEFER=1 (A/B): captured after the optimizer queues the table update, so that
-            # update is the dx GEMM's first child in the graph and stays on its hardware queue
-            if os.environ.get("TT_WGRAD_DEFER", "0") == "1":
-                side.defer(launch)
-            else:
-                launch()
+            with torch.cuda.stream(aux):
+                head_wgrad2(dh, x, dy, h, ws)
+            done = torch.cuda.Event()
+            done.record(aux)
+            side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)), finalize=_Wgrad2Sums(ws, ctx.params))
             return dx, dW1, db1, dW2, db2
         wgrad_aside(dh, x, dW1, db1)
         wgrad_aside(dy, h, dW2, db2)

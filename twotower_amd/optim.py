@@ -273,7 +273,6 @@ class AdamW(torch.optim.Optimizer):
         for p, st, (ids, dp, den, plan) in fused:
             ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
                                                 self._adam_args(p))
-        self._side_grads.launch_pending()  # side launches deferred behind the table update (TT_WGRAD_DEFER)
         # data parallel, row-sharded tables: the chunk-pipelined exchange (its collectives are
         # issued before the tower all-reduce, so they lead on the communicator)
         for sh, parts, st, a in shards:
