@@ -812,6 +812,47 @@ def test_graph_step_equals_eager(loss_name):
         assert torch.equal(p1, p2), n_
 
 
+def test_stamped_graph_replay_times_every_op():
+    """bench.py's per-op times: a step captured under OpTimer.stamp_capture brackets every C-ABI
+    call with two tt_stamp kernels; each replay rewrites them (positive, ordered durations that sum
+    to less than the replay's own wall time) and the stamped step computes what an unstamped
+    graph step computes."""
+    import time
+    from twotower_amd import _lib
+    V, E, B, L = 5000, 256, 256, 20
+
+    def build():
+        torch.manual_seed(9)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+        model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        return model, opt, tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16")
+
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=k, device=DEV) for k in range(4)]
+    m1, o1, l1 = build()
+    s1 = tt.TrainStep(m1, l1, o1, graph=True, eager_steps=1)
+    m2, o2, l2 = build()
+    s2 = tt.TrainStep(m2, l2, o2, graph=True, eager_steps=1)
+    s1(*batches[0])
+    s2(*batches[0])
+    with _lib.TIMER.stamp_capture(DEV):
+        s2(*batches[1])  # captured with stamps
+    s1(*batches[1])
+    for b in batches[2:]:
+        s1(*b)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s2(*b)
+        torch.cuda.synchronize()
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        times = _lib.TIMER.stamp_summary(DEV)
+        assert {"tt_bag_mean_fwd", "tt_inbatch_fwd_prepped", "tt_bag_mean_bwd_adamw_planned"} <= set(times)
+        flat = [t for v in times.values() for t in v]
+        assert all(0.0 < t < wall_ms for t in flat)
+    for (n_, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p1, p2), n_
+
+
 @pytest.mark.parametrize("graph", [False, True])
 def test_step_side_stream_wgrad_equals_serial(graph):
     """E = H = 256 (TowerHead): TrainStep computes the head weight gradients on a side stream
