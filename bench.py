@@ -238,6 +238,12 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
     add("embedding bag forward (gather + masked mean)", "tt_bag_mean_fwd",
         nseq * L * id_bytes + nnz * d * 4 + nseq * d * 4 + nseq * 4, "GB/s", HBM_PEAK_GBS, "hbm",
         "ids N*L*4 + gathered rows nnz*E*4 + pooled N*E*4 + denom N*4 bytes")
+    # the same gather whose launch also splits the head's weights into bf16 planes (the encoders'
+    # default for the hand-written head): W1, W2 read twice (direct, transposed), 12 B of planes each
+    add("embedding bag forward (gather + masked mean) + head weight planes", "tt_bag_mean_fwd_split",
+        nseq * L * id_bytes + nnz * d * 4 + nseq * d * 4 + nseq * 4 + 2 * d * d * (8 + 12), "GB/s", HBM_PEAK_GBS,
+        "hbm", "ids N*L*4 + gathered rows nnz*E*4 + pooled N*E*4 + denom N*4 + W1, W2 (E = H) 2 x 4 B read "
+        "and 2 x 6 B of bf16 planes written per weight element")
     add("embedding bag backward fused with table AdamW (apply half: scale rows + per-row reduce + AdamW)",
         "tt_bag_mean_bwd_adamw_planned", nseq * d * 4 + nseq * 4 + 24 * V * d, "GB/s", HBM_PEAK_GBS, "hbm",
         "d_pooled N*E*4 + denom N*4 + AdamW p,m,v read+write 24*V*E bytes")
@@ -511,7 +517,7 @@ def main():
                                   tt_ops.get_inbatch_backward(),
                                   *(() if args.no_helpers else (lambda: normalise_ms((2 + K) * B, d, dev),
                                                                 lambda: l2_backward_ms((2 + K) * B, d, dev))))
-    gather = next((k for k in kernels if k["abi"] == "tt_bag_mean_fwd"), None)
+    gather = next((k for k in kernels if k["abi"] in ("tt_bag_mean_fwd", "tt_bag_mean_fwd_split")), None)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -53,6 +53,14 @@ const char* tt_last_error(void);
 int tt_bag_mean_fwd(const float* table, int64_t V, int E,
                     const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
                     float* pooled, float* denom, tt_stream_t stream);
+/* tt_bag_mean_fwd whose launch also forms the four weight plane sets of the tower head that
+ * consumes the pooled rows (W1 H x E, W2 H x H: tt_head_split_ff2's output in `planes`, bit for
+ * bit) in extra workgroups, so the split leaves the path between the gather and the first head
+ * GEMM (MeanPoolingTower, encoders.py:38-42).  E in {64, 128, 256}, H in {128, 256}. */
+int tt_bag_mean_fwd_split(const float* table, int64_t V, int E,
+                          const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                          float* pooled, float* denom, const float* W1, const float* W2, int H,
+                          void* planes, tt_stream_t stream);
 
 /* Backward of the above w.r.t. the table (autograd of encoders.py:67-72 +
  * embedding_dense_backward with padding_idx, reached from twotower/train.py:138):

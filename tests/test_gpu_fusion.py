@@ -209,3 +209,105 @@ def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dty
         assert torch.equal(a, b)
     for k in want:
         assert torch.equal(got[k], want[k]), k
+
+
+@pytest.mark.parametrize("E,H", [(256, 256), (128, 128), (64, 128), (128, 256)])
+def test_bag_forward_split_workgroups_equal_head_split(E, H):
+    """tt_bag_mean_fwd_split: the pooled rows and denominators equal tt_bag_mean_fwd's and the
+    planes equal tt_head_split_ff2's, bit for bit (one and 37 sequences)."""
+    rng = np.random.default_rng(E + H)
+    V = 700
+    table = torch.randn(V, E, device=DEV)
+    W1, W2 = torch.randn(H, E, device=DEV), torch.randn(H, H, device=DEV)
+    n1, n2 = ops._head_planes_bytes(E, H)
+    for B in (37, 1):
+        ids = _ids(B, 9, V, rng).to(torch.int32)
+        ref_p, ref_d = ops.bag_mean_forward(table, ids)
+        ref_planes = torch.empty(2 * (n1 + n2), dtype=torch.uint8, device=DEV)
+        ops.call("tt_head_split_ff2", ops.ptr(W1), ops.ptr(W2), E, H, ops.ptr(ref_planes), ops.stream_of(W1))
+        with ops.head_planes_in_gather(W1, W2):
+            p, d = ops.bag_mean_forward(table, ids)
+            planes = ops._PLANES_DONE[(W1.data_ptr(), W2.data_ptr())]
+        torch.cuda.synchronize()
+        assert not ops._PLANES_DONE
+        assert torch.equal(p, ref_p) and torch.equal(d, ref_d)
+        assert torch.equal(planes, ref_planes)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("tied,H", [(True, 256), (False, 256), (True, 128)])
+def test_head_planes_formed_in_gather_are_bit_identical(graph, tied, H, monkeypatch):
+    """The gather's launch forms the head's weight planes (ops.head_planes_in_gather): losses and
+    parameters after four TrainSteps (eager, and graph replays after one eager step) equal the
+    in-line split (TT_PLANES_IN_GATHER=0); the head takes them (no tt_head_split_ff2 launch on the
+    tied path; the untied towers pool and split as before)."""
+    V, B, L = 3000, 256, 24
+    rng = np.random.default_rng(11)
+    batches = [[_ids(B, L, V, rng) for _ in range(3)] for _ in range(4)]
+
+    def run():
+        torch.manual_seed(5)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=H)
+        model = tt.build_two_tower("mean", emb, hidden_dim=H, tied_weights=tied).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        st = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16"), opt,
+                          graph=graph, eager_steps=1)
+        losses = [st(*b).clone() for b in batches]
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().clone() for k, v in model.named_parameters()}
+
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
+    monkeypatch.setattr(ops, "call", spy)
+    monkeypatch.setenv("TT_PLANES_IN_GATHER", "1")
+    got_l, got = run()
+    if tied:
+        assert "tt_bag_mean_fwd_split" in seen and "tt_head_split_ff2" not in seen
+    assert not ops._PLANES_DONE and not ops._PLANES_REQ
+    monkeypatch.setenv("TT_PLANES_IN_GATHER", "0")
+    seen.clear()
+    want_l, want = run()
+    assert "tt_bag_mean_fwd_split" not in seen
+    for a, b in zip(got_l, want_l):
+        assert torch.equal(a, b)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+
+
+def test_single_tower_forward_takes_planes_from_its_gather():
+    """BaseTower.forward of a hand-written-head MeanPoolingTower (a tower called on its own):
+    one tt_bag_mean_fwd_split, no tt_head_split_ff2, same output and gradients as the in-line split."""
+    torch.manual_seed(2)
+    emb = tt.embeddings.build("lookup", vocab_size=500, embedding_dim=256)
+    tower = tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV).query_tower
+    ids = _ids(40, 10, 500, np.random.default_rng(4))
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
+    outs = []
+    for on in ("1", "0"):
+        import os
+        os.environ["TT_PLANES_IN_GATHER"] = on
+        try:
+            ops.call = spy
+            tower.zero_grad(set_to_none=True)
+            y = tower(ids)
+            y.square().sum().backward()
+        finally:
+            ops.call = real_call
+            os.environ.pop("TT_PLANES_IN_GATHER")
+        outs.append((y.detach().clone(), {k: v.grad.clone() for k, v in tower.named_parameters()}))
+        if on == "1":
+            assert "tt_bag_mean_fwd_split" in seen and "tt_head_split_ff2" not in seen
+    assert torch.equal(outs[0][0], outs[1][0])
+    for k in outs[1][1]:
+        assert torch.equal(outs[0][1][k], outs[1][1][k]), k

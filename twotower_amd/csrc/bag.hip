@@ -12,6 +12,7 @@
 // Layout: the table is V x E fp32 row-major (1 KiB rows at E = 256).  A wavefront owns a
 // sequence (forward) or a table row (backward).  Each lane moves 16 B per row-load so a
 // wave-instruction reads 64 x 16 B = 1 KiB: one E=256 row, two E=128 rows or four E=64 rows.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -30,13 +31,23 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 // (E = 4 * LPR * NV); RPI = 64 / LPR rows are in flight per wave-instruction and U such
 // instructions are issued before the adds, so each wave keeps U * 1 KiB of gathers in flight.
 // Token order is preserved per sub-row (sequential adds), sub-rows are folded at the end.
+// The first split_blocks workgroups (tt_bag_mean_fwd_split) form the tower head's weight planes
+// instead (SplitJobs, common.hpp: the bits of tt_head_split_ff2), one element of each job per
+// thread: the split rides in the gather's launch, off the path between it and the first head GEMM.
 template <typename IdT, int LPR, int NV, int U>
 __global__ __launch_bounds__(kBlock) void bag_fwd_kernel(
     const float* __restrict__ table, int64_t V, int E, const IdT* __restrict__ ids, int64_t nseq,
-    int L, int64_t ld, float* __restrict__ pooled, float* __restrict__ denom) {
+    int L, int64_t ld, float* __restrict__ pooled, float* __restrict__ denom, SplitJobs sj,
+    __bf16* __restrict__ planes, int split_blocks) {
+  if ((int)blockIdx.x < split_blocks) {  // workgroup-uniform
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+#pragma unroll
+    for (int job = 0; job < 4; ++job) split_planes_elem(sj, job, i, planes);
+    return;
+  }
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
-  const int64_t seq = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t seq = (int64_t)(blockIdx.x - split_blocks) * kWavesPerBlock + (threadIdx.x >> 6);
   if (seq >= nseq) return;  // wave-uniform
   const int sub = lane / LPR, c = lane % LPR;
   const IdT* rid = ids + seq * ld;
@@ -944,18 +955,32 @@ size_t sort_tmp_bytes(int64_t n, int64_t V) {
   return a > b ? a : b;
 }
 
+// planes != nullptr: the split workgroups of tt_bag_mean_fwd_split first (E in the templated set)
 template <typename IdT>
 int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nseq, int L, int64_t ld,
-               float* pooled, float* denom, hipStream_t s) {
-  const dim3 grid((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
-  switch (E) {
-    case 64: bag_fwd_kernel<IdT, 16, 1, 4><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
-    case 128: bag_fwd_kernel<IdT, 32, 1, 4><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
-    case 256: bag_fwd_kernel<IdT, 64, 1, 8><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
-    case 512: bag_fwd_kernel<IdT, 64, 2, 4><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
-    case 1024: bag_fwd_kernel<IdT, 64, 4, 2><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
-    default: bag_fwd_generic_kernel<IdT><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom); break;
+               float* pooled, float* denom, hipStream_t s, const SplitJobs& sj = SplitJobs{},
+               __bf16* planes = nullptr) {
+  int nsplit = 0;
+  if (planes) {
+    int64_t big = 0;
+    for (int j = 0; j < 4; ++j) big = std::max<int64_t>(big, (int64_t)sj.n[j] * sj.k[j]);
+    nsplit = (int)((big + kBlock - 1) / kBlock);
   }
+  const dim3 grid((unsigned)(nsplit + (nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+#define TT_FWD(LPR, NV, U) \
+  bag_fwd_kernel<IdT, LPR, NV, U><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom, sj, planes, nsplit)
+  switch (E) {
+    case 64: TT_FWD(16, 1, 4); break;
+    case 128: TT_FWD(32, 1, 4); break;
+    case 256: TT_FWD(64, 1, 8); break;
+    case 512: TT_FWD(64, 2, 4); break;
+    case 1024: TT_FWD(64, 4, 2); break;
+    default:
+      TT_REQUIRE(!planes, "tt_bag_mean_fwd_split: E %d", E);
+      bag_fwd_generic_kernel<IdT><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom);
+      break;
+  }
+#undef TT_FWD
   TT_LAUNCH_CHECK("tt_bag_mean_fwd");
   return TT_OK;
 }
@@ -1153,6 +1178,22 @@ extern "C" int tt_bag_mean_fwd(const float* table, int64_t V, int E, const void*
   if (ids_dtype == TT_IDS_I32)
     return launch_fwd(table, V, E, static_cast<const int32_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
   return launch_fwd(table, V, E, static_cast<const int64_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
+}
+
+extern "C" int tt_bag_mean_fwd_split(const float* table, int64_t V, int E, const void* ids, int ids_dtype,
+                                     int64_t nseq, int L, int64_t ld_ids, float* pooled, float* denom,
+                                     const float* W1, const float* W2, int H, void* planes, tt_stream_t stream) {
+  int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
+  if (rc) return rc;
+  TT_REQUIRE(table && pooled && denom && W1 && W2 && planes, "null pointer");
+  TT_REQUIRE((E == 64 || E == 128 || E == 256) && (H == 128 || H == 256),
+             "tt_bag_mean_fwd_split: E in {64, 128, 256}, H in {128, 256} (got E=%d H=%d)", E, H);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const SplitJobs sj = head_ff2_jobs(W1, W2, E, H);
+  __bf16* pl = static_cast<__bf16*>(planes);
+  if (ids_dtype == TT_IDS_I32)
+    return launch_fwd(table, V, E, static_cast<const int32_t*>(ids), nseq, L, ld_ids, pooled, denom, s, sj, pl);
+  return launch_fwd(table, V, E, static_cast<const int64_t*>(ids), nseq, L, ld_ids, pooled, denom, s, sj, pl);
 }
 
 extern "C" size_t tt_bag_mean_bwd_ws_size(int64_t nseq, int L, int64_t V, int E) {

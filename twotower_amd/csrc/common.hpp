@@ -91,6 +91,46 @@ __device__ __forceinline__ void adam_update(float& p, float g, float& m, float& 
 }
 
 
+// The tower head's weight planes (tt_head_split*, head.hip): each fp32 weight is cut into three
+// bf16 terms, x = a0 + a1 + a2 exactly.  Job j of SplitJobs writes the three planes of an n x k
+// matrix (W is n x k, or k x n when transposed) at planes_base + off[j]; element i = n * k + k'.
+// Shared by split_planes_kernel and the bag forward's split workgroups (tt_bag_mean_fwd_split),
+// so both produce the same bits.
+__device__ __forceinline__ void split3(float x, __bf16& a0, __bf16& a1, __bf16& a2) {
+  a0 = (__bf16)x;
+  const float r1 = x - (float)a0;
+  a1 = (__bf16)r1;
+  a2 = (__bf16)(r1 - (float)a1);
+}
+
+struct SplitJobs {
+  const float* W[4];
+  int transpose[4];
+  int n[4], k[4];
+  int64_t off[4];
+};
+
+__device__ __forceinline__ void split_planes_elem(const SplitJobs& jobs, int job, int i, __bf16* __restrict__ planes_base) {
+  const int nn = jobs.n[job], kk = jobs.k[job];
+  if (i >= nn * kk) return;
+  const float* W = jobs.W[job];
+  __bf16* planes = planes_base + jobs.off[job];
+  const int n = i / kk, k = i % kk;
+  const float x = jobs.transpose[job] ? W[k * nn + n] : W[n * kk + k];
+  __bf16 a0, a1, a2;
+  split3(x, a0, a1, a2);
+  planes[i] = a0;
+  planes[nn * kk + i] = a1;
+  planes[2 * nn * kk + i] = a2;
+}
+
+// The four plane sets of an E -> H Linear-ReLU-Linear head: W1 (H x E), W2 (H x H), W1^T (E x H),
+// W2^T (H x H), each three bf16 planes, consecutive in that order (tt_head_split_ff2).
+inline SplitJobs head_ff2_jobs(const float* W1, const float* W2, int E, int H) {
+  const int64_t a = 3LL * H * E, b = 3LL * H * H;
+  return SplitJobs{{W1, W2, W1, W2}, {0, 0, 1, 1}, {H, H, E, H}, {E, H, H, H}, {0, a, a + b, 2 * a + b}};
+}
+
 // Fixed-order sum of slab partials (tt_head_wgrad2_reduce, tt_adamw_multi_ex): slabs are cut
 // into kRedQ quarters; a quarter's slab s goes to partial s % 8 (8 loads in flight), the eight
 // partials fold in a fixed tree, and the callers add the quarters as (q0 + q1) + (q2 + q3).

@@ -47,36 +47,9 @@ struct HeadShape {
 
 enum Epi { EPI_BIAS_RELU = 0, EPI_BIAS_L2 = 1, EPI_RELU_MASK = 2, EPI_PLAIN = 3, EPI_ROWDIV = 5 };
 
-__device__ __forceinline__ void split3(float x, __bf16& a0, __bf16& a1, __bf16& a2) {
-  a0 = (__bf16)x;
-  const float r1 = x - (float)a0;
-  a1 = (__bf16)r1;
-  a2 = (__bf16)(r1 - (float)a1);
-}
-
-// blockIdx.y selects one of up to 4 (weight, transpose) jobs; job j writes its three planes of
-// an n x k matrix (W is n x k, or k x n when transposed) at planes_base + off[j].
-struct SplitJobs {
-  const float* W[4];
-  int transpose[4];
-  int n[4], k[4];
-  int64_t off[4];
-};
-
+// blockIdx.y selects one of up to 4 (weight, transpose) jobs (SplitJobs, common.hpp).
 __global__ __launch_bounds__(256) void split_planes_kernel(SplitJobs jobs, __bf16* __restrict__ planes_base) {
-  const int job = blockIdx.y;
-  const int nn = jobs.n[job], kk = jobs.k[job];
-  const int i = blockIdx.x * 256 + threadIdx.x;  // output index n * kk + k
-  if (i >= nn * kk) return;
-  const float* W = jobs.W[job];
-  __bf16* planes = planes_base + jobs.off[job];
-  const int n = i / kk, k = i % kk;
-  const float x = jobs.transpose[job] ? W[k * nn + n] : W[n * kk + k];
-  __bf16 a0, a1, a2;
-  split3(x, a0, a1, a2);
-  planes[i] = a0;
-  planes[nn * kk + i] = a1;
-  planes[2 * nn * kk + i] = a2;
+  split_planes_elem(jobs, blockIdx.y, blockIdx.x * 256 + threadIdx.x, planes_base);
 }
 
 // Workgroup b -> (row group g, column slice c).  Blocks b, b+8, ... share an XCD (round-robin
@@ -664,8 +637,7 @@ extern "C" int tt_head_split_ff2(const float* W1, const float* W2, int E, int H,
              E, H);
   TT_REQUIRE(W1 && W2 && planes, "null pointer");
   // W1 (H x E), W2 (H x H), W1^T (E x H), W2^T (H x H), each as three bf16 planes, in that order
-  const int64_t a = 3LL * H * E, b = 3LL * H * H;
-  const SplitJobs jobs{{W1, W2, W1, W2}, {0, 0, 1, 1}, {H, H, E, H}, {E, H, H, H}, {0, a, a + b, 2 * a + b}};
+  const SplitJobs jobs = head_ff2_jobs(W1, W2, E, H);
   const int big = std::max(H * E, H * H);
   split_planes_kernel<<<dim3(big / 256, 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
       jobs, static_cast<__bf16*>(planes));

@@ -38,6 +38,16 @@ def _table_of(embedding: nn.Module) -> torch.Tensor | None:
     return inner.weight if isinstance(inner, nn.Embedding) else None
 
 
+def _planes_in_gather(tower: nn.Module, ids: torch.Tensor):
+    """The gather feeding this tower's hand-written head also forms the head's weight planes
+    (ops.head_planes_in_gather)."""
+    if (ids.is_cuda and type(tower).encode_pooled is MeanPoolingTower.encode_pooled
+            and tower.hand_written_head()):
+        ff = tower.feed_forward
+        return ops.head_planes_in_gather(ff[0].weight, ff[2].weight)
+    return contextlib.nullcontext()
+
+
 def _sole_head(tower: nn.Module, pooled: torch.Tensor):
     """The pooled rows go to this tower's own fused head and nowhere else (MeanPoolingTower's
     encode_pooled, not overridden): its backward may then hand the bag backward d_pooled / denom
@@ -63,9 +73,10 @@ class BaseTower(nn.Module):
         raise NotImplementedError
 
     def forward(self, input_ids: torch.Tensor) -> torch.Tensor:
-        pooled = pool_mean(self.embedding, input_ids)
-        with _sole_head(self, pooled):
-            return self.encode_pooled(pooled)
+        with _planes_in_gather(self, input_ids):
+            pooled = pool_mean(self.embedding, input_ids)
+            with _sole_head(self, pooled):
+                return self.encode_pooled(pooled)
 
 
 class MeanPoolingTower(BaseTower):
@@ -81,12 +92,21 @@ class MeanPoolingTower(BaseTower):
         )
         self.log_params()
 
+    def _standard_ff(self) -> bool:
+        ff = self.feed_forward
+        return (len(ff) == 3 and isinstance(ff[0], nn.Linear) and isinstance(ff[1], nn.ReLU)
+                and isinstance(ff[2], nn.Linear) and ff[0].bias is not None and ff[2].bias is not None)
+
+    def hand_written_head(self) -> bool:
+        """The head runs on ops.tower_head (the hand-written split-bf16 GEMMs)."""
+        ff = self.feed_forward
+        return (self._standard_ff() and ff[0].out_features == ff[2].out_features == ff[2].in_features
+                in ops.HEAD_WIDTHS and ff[0].in_features in ops.EMB_WIDTHS)
+
     def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:
         ff = self.feed_forward
-        standard = (len(ff) == 3 and isinstance(ff[0], nn.Linear) and isinstance(ff[1], nn.ReLU)
-                    and isinstance(ff[2], nn.Linear) and ff[0].bias is not None and ff[2].bias is not None)
-        if (standard and ff[0].out_features == ff[2].out_features == ff[2].in_features in ops.HEAD_WIDTHS
-                and ff[0].in_features in ops.EMB_WIDTHS):
+        standard = self._standard_ff()
+        if self.hand_written_head():
             # Linear-ReLU-Linear + F.normalize in two fused GEMM launches (encoders.py:38-42,77)
             return ops.tower_head(pooled.contiguous(), ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
         if standard and ff[0].out_features % 4 == 0 and ff[2].out_features % 4 == 0:
@@ -176,14 +196,16 @@ class TwoTower(nn.Module):
             ids = [t if t.shape[1] == L else F.pad(t, (0, L - t.shape[1])) for t in inputs]
             dtype = torch.int64 if any(t.dtype == torch.int64 for t in ids) else ids[0].dtype
             all_ids = torch.cat([t.to(dtype) for t in ids], dim=0)
-        pooled = pool_mean(self.query_tower.embedding, all_ids)
         sizes = [t.shape[0] for t in inputs]
         nq = sizes[0]
         if self.query_tower is self.document_tower:
-            prep = ops.scorer_prep(nq, self.scorer_prep) if self.scorer_prep else contextlib.nullcontext()
-            with prep, _sole_head(self.query_tower, pooled):
-                # one head over all rows: its normalise pass may also prep the in-batch scorer
-                return list(torch.split(self.query_tower.encode_pooled(pooled), sizes, dim=0))
+            with _planes_in_gather(self.query_tower, all_ids):
+                pooled = pool_mean(self.query_tower.embedding, all_ids)
+                prep = ops.scorer_prep(nq, self.scorer_prep) if self.scorer_prep else contextlib.nullcontext()
+                with prep, _sole_head(self.query_tower, pooled):
+                    # one head over all rows: its normalise pass may also prep the in-batch scorer
+                    return list(torch.split(self.query_tower.encode_pooled(pooled), sizes, dim=0))
+        pooled = pool_mean(self.query_tower.embedding, all_ids)
         q = self.query_tower.encode_pooled(pooled[:nq])
         docs = self.document_tower.encode_pooled(pooled[nq:])
         return [q] + list(torch.split(docs, sizes[1:], dim=0))

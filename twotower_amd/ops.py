@@ -53,9 +53,51 @@ def bag_mean_forward(weight: torch.Tensor, ids: torch.Tensor) -> tuple[torch.Ten
     N, L = ids.shape
     pooled = torch.empty(N, E, dtype=_FLOAT, device=weight.device)
     denom = torch.empty(N, dtype=_FLOAT, device=weight.device)
+    req = _PLANES_REQ[-1] if _PLANES_REQ else None
+    if req is not None and req[0].shape[1] == E and req[0].device == weight.device:
+        # the consuming head's weight planes, formed by extra workgroups of this launch
+        W1, W2 = req
+        H = W1.shape[0]
+        n1, n2 = _head_planes_bytes(E, H)
+        planes = torch.empty(2 * (n1 + n2), dtype=torch.uint8, device=weight.device)  # W1, W2, W1^T, W2^T
+        call("tt_bag_mean_fwd_split", ptr(weight), V, E, ptr(ids), _lib.ids_dtype_code(ids), N, L, L, ptr(pooled),
+             ptr(denom), ptr(W1), ptr(W2), H, ptr(planes), stream_of(weight))
+        _PLANES_REQ[-1] = None  # one gather per request
+        _PLANES_DONE[(W1.data_ptr(), W2.data_ptr())] = planes
+        return pooled, denom
     call("tt_bag_mean_fwd", ptr(weight), V, E, ptr(ids), _lib.ids_dtype_code(ids), N, L, L, ptr(pooled), ptr(denom),
          stream_of(weight))
     return pooled, denom
+
+
+_PLANES_REQ: list = []  # (W1, W2) whose planes the next bag gather forms (open head_planes_in_gather), or None
+_PLANES_DONE: dict = {}  # (W1, W2 data_ptr) -> planes that gather formed, taken by that head's TowerHead
+
+
+def _head_planes_bytes(E: int, H: int) -> tuple[int, int]:
+    return _lib.lib().tt_head_planes_bytes(H, E), _lib.lib().tt_head_planes_bytes(H, H)
+
+
+@contextlib.contextmanager
+def head_planes_in_gather(W1: torch.Tensor, W2: torch.Tensor):
+    """While open, the next bag gather whose rows feed the tower head (W1, W2) also forms that
+    head's weight planes in its own launch (tt_bag_mean_fwd_split), and the head takes them
+    instead of launching tt_head_split_ff2 between the gather and its first GEMM (C3: that
+    launch sat on the step's critical path for 9-15 us).  The encoders open it around a
+    MeanPoolingTower's gather and head.  TT_PLANES_IN_GATHER=0 turns it off.  (Splitting on a
+    side stream before the gather instead was measured slower: +6 us on the plan's stream, +27 us
+    on a stream of its own -- the cross-queue wait in the replayed graph costs more than the
+    split; profiles/r03zf_planes_ab.txt.)"""
+    on = (os.environ.get("TT_PLANES_IN_GATHER", "1") != "0" and W1.is_cuda and W1.dtype == _FLOAT
+          and W2.dtype == _FLOAT and W1.is_contiguous() and W2.is_contiguous() and W1.shape[1] in EMB_WIDTHS
+          and W1.shape[0] in HEAD_WIDTHS and tuple(W2.shape) == (W1.shape[0], W1.shape[0]))
+    _PLANES_REQ.append((W1, W2) if on else None)
+    key = (W1.data_ptr(), W2.data_ptr())
+    try:
+        yield
+    finally:
+        _PLANES_REQ.pop()
+        _PLANES_DONE.pop(key, None)
 
 
 def bag_mean_backward(d_pooled: torch.Tensor, denom: torch.Tensor, ids: torch.Tensor, V: int,
@@ -470,10 +512,12 @@ class TowerHead(torch.autograd.Function):
         rows, E = x.shape
         H = W1.shape[0]  # width = H (HEAD_WIDTHS), E in EMB_WIDTHS
         width = H
-        n1, n2 = _lib.lib().tt_head_planes_bytes(H, E), _lib.lib().tt_head_planes_bytes(H, H)
-        planes = torch.empty(2 * (n1 + n2), dtype=torch.uint8, device=x.device)  # W1, W2, W1^T, W2^T
-        call("tt_head_split_ff2", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), E, H, ptr(planes),
-             stream_of(x))
+        n1, n2 = _head_planes_bytes(E, H)
+        planes = _PLANES_DONE.pop((W1.data_ptr(), W2.data_ptr()), None)  # formed by the gather (same stream)
+        if planes is None or planes.numel() != 2 * (n1 + n2):
+            planes = torch.empty(2 * (n1 + n2), dtype=torch.uint8, device=x.device)  # W1, W2, W1^T, W2^T
+            call("tt_head_split_ff2", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), E, H, ptr(planes),
+                 stream_of(x))
         p_w1, p_w2 = planes[:n1], planes[n1:n1 + n2]
         mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
         h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
