@@ -22,6 +22,14 @@ import os
 import torch
 import torch.distributed as dist
 
+# HIP-graph capture of the N-rank step (train_step.TrainStep): ProcessGroupNCCL's event cache hands
+# the end events of finished eager collectives to the collectives recorded during a capture while
+# its watchdog thread may still query them, and the query of an event last recorded in a capturing
+# stream fails ("operation not permitted on an event last recorded in a capturing stream": one run
+# of tests/_dp_graph_check.py, round 3).  Fresh events per collective; the variable is read when a
+# process group is created, so it is set here, before the caller creates one.
+os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+
 
 def is_active(group=None) -> bool:
     """Data-parallel exchanges on: more than one rank, or TT_DIST_FORCE=1 with any initialised
