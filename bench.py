@@ -255,8 +255,9 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
         nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
     pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
     mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
-    # bf16 single process: the backward reads the forward's stored probabilities (no S recompute)
-    stored_p = scorer_dtype == "bf16" and world == 1 and bwd_form == "stored" and B * M <= 2 ** 31
+    # single process, bf16 or fp32: the backward reads the forward's stored probabilities (no S recompute)
+    stored_p = world == 1 and bwd_form == "stored" and (
+        (scorer_dtype == "bf16" and B * M <= 2 ** 31) or (scorer_dtype == "fp32" and B * M <= 2 ** 30))
     fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
     bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd") if k in ops_t or
                    k == "tt_inbatch_bwd")
@@ -279,9 +280,9 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
         algo = 6.0 * B * M * d
         executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
         achieved = algo / (ms * 1e-3) / 1e12
-        form = ("bf16, backward from stored bf16 probabilities" if stored_p else
+        form = (f"{scorer_dtype}, backward from stored {scorer_dtype} probabilities" if stored_p else
                 {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
-                 "fp32": "fp32 MFMA"}[scorer_dtype])
+                 "fp32": "fp32 MFMA, recompute backward"}[scorer_dtype])
         kernels.append({
             "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
             "abi": fwd_key + "+" + bwd_key, "bound": "mfma", "mean_ms": round(ms, 4),

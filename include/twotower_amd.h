@@ -244,7 +244,9 @@ int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t 
  * argument of tt_inbatch_bwd is the same quantity, validated but not re-read).  In the default
  * backward form (TT_INBATCH_BWD_STORED) the TT_BF16 workspace also carries the forward's bf16
  * probabilities (about B * M * 2 bytes, kept while B * M <= 2^31) and a rescaled bf16 copy of q,
- * from which the backward forms P without recomputing S.
+ * from which the backward forms P without recomputing S; the TT_F32 workspace likewise carries
+ * fp32 probabilities (about B * M * 4 bytes, kept while B * M <= 2^30) and a rescaled fp32 copy
+ * of q (TT_BF16_SPLIT always recomputes).
  * tt_inbatch_set_backward(mode) selects the form process-wide and returns the previous one (an
  * unknown mode only reads it); the initial form is STORED unless the environment sets
  * TT_INBATCH_BWD=recompute.  The workspace size depends on the form: size it after selecting, and

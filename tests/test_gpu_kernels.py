@@ -326,6 +326,36 @@ def test_in_batch_stored_backward_vs_oracle_and_recompute(H, B, M, off):
     assert rel(dd, grads["recompute"][2]) < 4e-3 and torch.equal(dq, grads["recompute"][1])
 
 
+@pytest.mark.parametrize("H", [32, 64, 128, 256])
+@pytest.mark.parametrize("B,M,off", [(300, 700, 0), (129, 129, 0), (64, 256, 128), (1, 64, 0), (320, 330, 10),
+                                     (2500, 2600, 100)])
+def test_in_batch_fp32_stored_backward_vs_oracle_and_recompute(H, B, M, off):
+    """The fp32 stored-probability backward (score_f32_kernel<DD, H, true>: G^T from the forward's
+    fp32 P, the per-query factor folded into an fp32 copy of q) against the float64 oracle at the
+    fp32 bar (1e-5) and against the fp32 recompute backward (same products; the scaled copy adds
+    one fp32 rounding per term).  B, M off the 32- and 128-row tiles exercise the partial blocks."""
+    rng = np.random.default_rng(11 * H + B + M)
+    q, d = _unit(rng, B, H), _unit(rng, M, H)
+    g = 0.7
+    grads = {}
+    prev = ops.get_inbatch_backward()
+    try:
+        for form in ("stored", "recompute"):
+            ops.set_inbatch_backward(form)
+            Q, D = cuda(q).requires_grad_(True), cuda(d).requires_grad_(True)
+            loss = ops.InBatchSoftmaxLoss.apply(Q, D, 10.0, off, "fp32", None)
+            loss.backward(torch.tensor(g, device=DEV))
+            grads[form] = (loss.item(), Q.grad.clone(), D.grad.clone())
+    finally:
+        ops.set_inbatch_backward(prev)
+    rl, (rdq, rdd), _ = O.in_batch_fwd_bwd(q.astype(np.float64), d.astype(np.float64), 0.1, g=g, label_off=off)
+    loss, dq, dd = grads["stored"]
+    assert abs(loss - rl) < 1e-5 * max(1.0, abs(rl))
+    assert rel(dq, rdq) < 1e-5 and rel(dd, rdd) < 1e-5
+    assert torch.equal(dq, grads["recompute"][1])
+    assert rel(dd, grads["recompute"][2]) < 1e-5
+
+
 def test_in_batch_stored_backward_first_call_of_fresh_process():
     """Round 1's failure showed on the first (cold) call of a process only: run the first bf16
     in-batch forward + backward of a fresh process, with no host sync between the passes, at
@@ -846,7 +876,7 @@ def test_stamped_graph_replay_times_every_op():
         torch.cuda.synchronize()
         wall_ms = (time.perf_counter() - t0) * 1e3
         times = _lib.TIMER.stamp_summary(DEV)
-        assert {"tt_bag_mean_fwd", "tt_inbatch_fwd_prepped", "tt_bag_mean_bwd_adamw_planned"} <= set(times)
+        assert {"tt_bag_mean_fwd_split", "tt_inbatch_fwd_prepped", "tt_bag_mean_bwd_adamw_planned"} <= set(times)
         flat = [t for v in times.values() for t in v]
         assert all(0.0 < t < wall_ms for t in flat)
     for (n_, p1), p2 in zip(m1.named_parameters(), m2.parameters()):

@@ -726,7 +726,7 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
                                                 float c2, float inv_tau, int64_t label_off,
                                                 const DT* __restrict__ Qmat, const DT* __restrict__ Dmat,
                                                 float* __restrict__ lse, float* __restrict__ lse2,
-                                                float* __restrict__ dqu, __bf16* __restrict__ qs,
+                                                float* __restrict__ dqu, DT* __restrict__ qs,
                                                 int* __restrict__ xrows, int lane) {
   constexpr int H = 4 * kWave;
   l = __builtin_fmaf(-(float)n_pad, __builtin_amdgcn_exp2f(-sh), l);  // pad rows: X = 0 exactly
@@ -746,7 +746,7 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
     for (int u = 0; u < 4; ++u) {
       const int h = lane + kWave * u;
       if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
-      if (qs) qs[i * H + h] = (__bf16)0.f;  // its stored P underflowed: the backward combine adds the row
+      if (qs) qs[i * H + h] = (DT)0.f;  // its stored P underflowed: the backward combine adds the row
     }
     if (qs && xrows && lane == 0) {  // flagged for the backward combine (which adds flagged rows in row order)
       xrows[1 + i] = 1;
@@ -760,8 +760,11 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
   const float dot = wave_sum(dot4(qv, dv));
   if (qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
     const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
-    reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
-        bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
+    if constexpr (std::is_same_v<DT, float>)
+      reinterpret_cast<f32x4*>(qs + i * H)[lane] = f32x4{qv[0] * f, qv[1] * f, qv[2] * f, qv[3] * f};
+    else
+      reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
+          bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
   }
   if (lane == 0) {
     lse[i] = lse_i;
@@ -1319,14 +1322,22 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 #ifndef TT_F32_AOFF
 #define TT_F32_AOFF 1
 #endif
-template <int MODE, int H>
+// STOREP (round 3, the fp32 form of the stored-probability backward): the forward also writes each
+// 32 x 32 G tile to P, block (candidate tile ct, query tile qt) = 1,024 floats [candidate][query] at
+// (ct * p_nqt + qt) * 1024; the backward (MODE DD, R = the scaled query copy Qs) reads its G^T
+// tile from there (four 16-B loads per lane: lane (candidate r32, hh) takes queries 8k + 4hh + u)
+// instead of forming X = R C^T and its exp: half the backward's MFMAs, no transcendental.
+template <int MODE, int H, bool STOREP = false>
 __global__ __launch_bounds__(NT, (H < 128 ? 2 : H > 128 ? 1 : MODE == FWD ? TT_F32_MINW128_FWD : TT_F32_MINW128_DD))
 void score_f32_kernel(
     const float* __restrict__ R, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
     const float* __restrict__ dmax_part, int n_dmax,
-    const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part) {
+    const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part,
+    float* __restrict__ P = nullptr, int64_t p_nqt = 0) {
   using T = Tile<float, H>;
+  constexpr bool LOADP = STOREP && MODE == DD;  // G from P (no X chain, no map)
+  constexpr int FILLMODE = LOADP ? FWD : MODE;   // no lse2 row staging when G comes from P
   constexpr int NB = H / 8;
   constexpr int NHT = H / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1344,10 +1355,20 @@ void score_f32_kernel(
   const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
 
   const FillOffs<float, H> fo = make_fill_offs<float, H>();
-  if (ntiles > 0) stage_fill<float, H, MODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad, fo);
+  if (ntiles > 0) stage_fill<float, H, FILLMODE>(smem, 0, R, row_begin, row_end, lse2_rows, pad, fo);
+  // LOADP: this lane's G^T row of stored block (ct = my_col / 32, qt), as four float4
+  const f32x4* pcol = nullptr;
+  f32x4 pn[4];
+  if constexpr (LOADP) {
+    pcol = reinterpret_cast<const f32x4*>(P + ((my_col >> 5) * p_nqt + (row_begin >> 5)) * 1024 + r32 * 32 + 4 * hh);
+    if (ntiles > 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pn[k] = pcol[2 * k];
+    }
+  }
 
   f32x4 cf[NB];
-  {
+  if constexpr (!LOADP) {
     const bool ok = my_col < nC;
     const f32x4* src = reinterpret_cast<const f32x4*>(C + (ok ? my_col : 0) * H);
 #pragma unroll
@@ -1374,18 +1395,34 @@ void score_f32_kernel(
   for (int64_t t = 0; t < ntiles; ++t) {
     const int buf = (int)(t & 1);
     if (t + 1 < ntiles)
-      stage_fill<float, H, MODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad, fo);
+      stage_fill<float, H, FILLMODE>(smem, buf ^ 1, R, row_begin + (t + 1) * T::BJ, row_end, lse2_rows, pad, fo);
     const lds_char_t* tile = lds + buf * T::STAGE_B;
-    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
-    f32x16 x = f32x16{};
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const f32x4 a = *reinterpret_cast<const lds_f32x4_t*>(tile + r32 * T::ROWB + (((2 * b + hh) ^ rx) << 4));
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], cf[b][u], x, 0, 0, 0);
-    }
     float e[16];
-    map_tile<MODE>(x, e, c2, shift, lse4, hh, l_run);
+    if constexpr (LOADP) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[4 * k + u] = pn[k][u];
+      if (t + 1 < ntiles) {  // the next tile's G, in flight beside this tile's Acc chain
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pn[k] = pcol[(t + 1) * 256 + 2 * k];
+      }
+    } else {
+      const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
+      f32x16 x = f32x16{};
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const f32x4 a = *reinterpret_cast<const lds_f32x4_t*>(tile + r32 * T::ROWB + (((2 * b + hh) ^ rx) << 4));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], cf[b][u], x, 0, 0, 0);
+      }
+      map_tile<MODE>(x, e, c2, shift, lse4, hh, l_run);
+      if constexpr (STOREP) {  // forward: G of (candidate tile, this wave's query tile) to P
+        float* blk = P + (((row_begin >> 5) + t) * p_nqt + (my_col >> 5)) * 1024 + r32;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) blk[acc_row(v, hh) * 32] = e[v];
+      }
+    }
 #pragma unroll
     for (int ht = 0; ht < NHT; ++ht) {
 #pragma unroll
@@ -1642,7 +1679,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     const float* __restrict__ dmax_part, int n_dmax, const float* __restrict__ l_part,
     const float* __restrict__ acc_part, float inv_tau, int64_t label_off, const DT* __restrict__ Qmat,
     const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2, float* __restrict__ loss_rows,
-    float* __restrict__ dqu, __bf16* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr,
+    float* __restrict__ dqu, DT* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr,
     int S_loc = 0, const float* __restrict__ dmax_loc = nullptr, int n_dmax_loc = 0) {
   // S_loc > 0 (data-parallel forward in two launches): slots [0, S_loc) hold the local launch's
   // partials, formed with the local norm bound; they are rescaled to this launch's shift
@@ -1650,7 +1687,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   const int lane = lane_id();
   if (i >= B) {  // the zero tail of the scaled query copy (the stored-P backward's R rows)
     if (qs && i < B + kTailRows)
-      for (int h = lane; h < H; h += kWave) qs[i * H + h] = (__bf16)0.f;
+      for (int h = lane; h < H; h += kWave) qs[i * H + h] = (DT)0.f;
     return;
   }
   const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
@@ -1690,7 +1727,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
       const int h = lane + kWave * u;
       if (h >= H) break;
       if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
-      if (qs) qs[i * H + h] = (__bf16)0.f;  // its stored P underflowed: the backward combine adds the row
+      if (qs) qs[i * H + h] = (DT)0.f;  // its stored P underflowed: the backward combine adds the row
     }
     if (qs && xrows && lane == 0) {  // flagged for the backward combine (which adds flagged rows in row order)
       xrows[1 + i] = 1;
@@ -1705,7 +1742,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   dot = wave_sum(dot);
   if (qs) {
     const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
-    for (int h = lane; h < H; h += kWave) qs[i * H + h] = (__bf16)((float)qr[h] * f);
+    for (int h = lane; h < H; h += kWave) qs[i * H + h] = (DT)((float)qr[h] * f);
   }
   if (lane == 0) {
     lse[i] = lse_i;
@@ -1910,6 +1947,7 @@ struct Ws {
   __bf16* Qb;
   __bf16* Db;
   __bf16* Qs;   // stored-P backward: q~ scaled by 2^(shift - lse2) (+ zero tail)
+  float* Qs32;  // ... the fp32 form (fp32 scorer: q scaled in fp32, P fp32)
   char* P;      // stored-P backward: bf16 probabilities, p_nct x p_nqt blocks of 2 KiB
   int* xrows;   // stored-P backward: [count, flag per query row] of queries the forward redid exactly
   int64_t p_nqt;
@@ -1934,13 +1972,18 @@ std::atomic<int>& bwd_mode() {
   return m;
 }
 bool stored_p(int dtype, int64_t B, int64_t M) {
-  return dtype == TT_BF16 && bwd_mode().load(std::memory_order_relaxed) == 1 && B * M <= (int64_t(1) << 31);
+  if (bwd_mode().load(std::memory_order_relaxed) != 1) return false;
+  if (dtype == TT_BF16) return B * M <= (int64_t(1) << 31);
+  return dtype == TT_F32 && B * M <= (int64_t(1) << 30);  // fp32 P: up to 4 GiB
 }
 
 // P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
 // backward's 128-column blocks (every tile either engine touches exists)
 int64_t p_nqt_for(int64_t B) { return (B + 127) / 128 * 4; }
 int64_t p_nct_for(int64_t M) { return (M + 255) / 256 * 8; }  // also the 256-candidate backward blocks
+// fp32 P (score_f32_kernel<., ., true>): 32 x 32 blocks of 4 KiB, candidate tiles up to the
+// backward's 128-candidate blocks, query tiles as above
+int64_t p32_nct_for(int64_t M) { return (M + 127) / 128 * 4; }
 
 // candidate tiles per wave of the stored-P backward (score_ddp_kernel<H, CW>)
 #ifndef TT_DDP_CW256
@@ -1967,20 +2010,22 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   // never need per-lane redirection past the last row
   const size_t oq = take(bf ? (size_t)(B + kTailRows) * H * 2 : 0), od = take(bf ? (size_t)(M + kTailRows) * H * 2 : 0);
   const bool sp = stored_p(dtype, B, M);
-  const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * 2 : 0);
-  const size_t op = take(sp ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : 0);
+  const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * (bf ? 2 : 4) : 0);
+  const size_t op = take(sp ? (bf ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : (size_t)p_nqt_for(B) * p32_nct_for(M) * 4096)
+                            : 0);
   const size_t ox = take(sp ? (size_t)(B + 1) * 4 : 0);
   const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
-  if (sp) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
+  if (sp && bf) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
   const size_t oa = take(parts);
   Ws w{};
   char* b = static_cast<char*>(base);
   if (b) {
     w.Qb = reinterpret_cast<__bf16*>(b + oq);
     w.Db = reinterpret_cast<__bf16*>(b + od);
-    w.Qs = sp ? reinterpret_cast<__bf16*>(b + oqs) : nullptr;
+    w.Qs = sp && bf ? reinterpret_cast<__bf16*>(b + oqs) : nullptr;
+    w.Qs32 = sp && !bf ? reinterpret_cast<float*>(b + oqs) : nullptr;
     w.P = sp ? b + op : nullptr;
     w.xrows = sp ? reinterpret_cast<int*>(b + ox) : nullptr;
     w.p_nqt = p_nqt_for(B);
@@ -2004,7 +2049,11 @@ struct Skip {
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
                   const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
-  if (dtype == TT_F32) {
+  if (dtype == TT_F32 && MODE == FWD && w.P) {  // forward that also stores G (the fp32 stored-P backward)
+    score_f32_kernel<FWD, H, true><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
+        static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, reinterpret_cast<float*>(w.P), w.p_nqt);
+  } else if (dtype == TT_F32) {
     score_f32_kernel<MODE, H><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part);
@@ -2074,7 +2123,8 @@ namespace {
 int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, int H, const float* qnorm,
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
-             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr) {
+             hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr,
+             float* Qs32 = nullptr) {
   const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H, dtype, FWD));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
@@ -2087,11 +2137,12 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   w.p_nqt = p_nqt;
   int rc;
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
-  const dim3 grid((unsigned)((B + (Qs ? kTailRows : 0) + 3) / 4)), block(256);
+  const dim3 grid((unsigned)((B + (Qs || Qs32 ? kTailRows : 0) + 3) / 4)), block(256);
   if (dtype == TT_F32)
     fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                     acc_part, inv_tau, label_off, static_cast<const float*>(Cm),
-                                                    static_cast<const float*>(Rm), lse, lse2, loss_rows, dqu);
+                                                    static_cast<const float*>(Rm), lse, lse2, loss_rows, dqu, Qs32,
+                                                    Qs32 ? xrows : nullptr);
   else
     fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                      acc_part, inv_tau, label_off, static_cast<const __bf16*>(Cm),
@@ -2147,6 +2198,35 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
   TT_LAUNCH_CHECK("score_ddp");
   launch_bwd_combine<__bf16>(B, M, H, p.S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out, xrows,
                              Db, lse2, s);
+  TT_LAUNCH_CHECK("score_bwd_combine");
+  return TT_OK;
+}
+
+// Backward from the forward's stored fp32 probabilities: score_f32_kernel<DD, H, true> over Qs32
+// (q scaled by 2^(shift - lse2) in fp32) and P, then the fp32 combine (label terms from q, the
+// exact rows from q, d and lse2).
+int bwd_core_p32(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, const float* Qs32, const char* P,
+                 int64_t p_nqt, const float* q, const float* d, const float* dqu, const float* grad_loss,
+                 float grad_scale, const BwdOut& out, const char* pad, float* acc_part, const int* xrows,
+                 const float* lse2, hipStream_t s) {
+  const Plan p = plan_for(B, M, bj_for(TT_F32), wg_per_cu(H, TT_F32, DD));
+  float* Pf = reinterpret_cast<float*>(const_cast<char*>(P));
+  switch (H) {
+#define TT_DDP32(HH)                                                                                               \
+  case HH:                                                                                                         \
+    score_f32_kernel<DD, HH, true><<<dim3(p.grid), dim3(NT), Tile<float, HH>::LDS_BYTES, s>>>(                      \
+        Qs32, B, d, M, p.S, p.rows_per_split, 0.f, lse2, nullptr, nullptr, 0, pad, acc_part, nullptr, Pf, p_nqt);   \
+    break;
+    TT_DDP32(32)
+    TT_DDP32(64)
+    TT_DDP32(128)
+    TT_DDP32(256)
+#undef TT_DDP32
+    default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
+  }
+  TT_LAUNCH_CHECK("score_dd_p32");
+  launch_bwd_combine<float>(B, M, H, p.S, label_off, acc_part, q, dqu, grad_loss, grad_scale, inv_tau, out, xrows, d,
+                            lse2, s);
   TT_LAUNCH_CHECK("score_bwd_combine");
   return TT_OK;
 }
@@ -2229,7 +2309,7 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
   const bool sp = want_grad && w.P;
   return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
                   want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s, sp ? w.P : nullptr, w.p_nqt,
-                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr);
+                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr, sp ? w.Qs32 : nullptr);
 }
 }  // namespace
 }  // namespace tt
@@ -2276,6 +2356,9 @@ int inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
   // lse in log2 units (ws.lse2) and the pad rows were left in the workspace by the forward
   const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
   const void* Cm = bf ? (const void*)w.Db : (const void*)d;
+  if (w.P && !bf)
+    return bwd_core_p32(B, M, H, label_off, inv_tau, w.Qs32, w.P, w.p_nqt, q, d, dq_unscaled, grad_loss, grad_scale,
+                        out, w.pad, w.acc_part, w.xrows, w.lse2, s);
   if (w.P) return bwd_core_p(B, M, H, label_off, inv_tau, w.Qs, w.P, w.p_nqt, w.Qb, dq_unscaled, grad_loss, grad_scale,
                              out, w.acc_part, w.xrows, w.Db, w.lse2, s);
   return bwd_core(dtype, Rm, B, w.lse2, Cm, M, Rm, B, label_off, H, inv_tau, dq_unscaled, grad_loss, grad_scale, out,

@@ -776,15 +776,16 @@ _BWD_FORMS = {"recompute": _lib.TT_INBATCH_BWD_RECOMPUTE, "stored": _lib.TT_INBA
 
 
 def set_inbatch_backward(form: str) -> str:
-    """Select the single-process bf16 in-batch backward process-wide ("stored": G from the
-    forward's stored bf16 probabilities, the default; "recompute": recompute S = Q D^T) and return
-    the previous form.  Switch only between steps, never between a forward and its backward."""
+    """Select the single-process bf16 / fp32 in-batch backward process-wide ("stored": G from the
+    forward's stored probabilities, bf16 or fp32 as the scorer computes, the default; "recompute":
+    recompute S = Q D^T) and return the previous form.  Switch only between steps, never between a
+    forward and its backward."""
     prev = _lib.lib().tt_inbatch_set_backward(_BWD_FORMS[form])
     return {v: k for k, v in _BWD_FORMS.items()}[prev]
 
 
 def get_inbatch_backward() -> str:
-    """The current single-process bf16 in-batch backward form ("stored" or "recompute")."""
+    """The current single-process bf16 / fp32 in-batch backward form ("stored" or "recompute")."""
     return {v: k for k, v in _BWD_FORMS.items()}[_lib.lib().tt_inbatch_set_backward(-1)]
 
 
