@@ -1322,13 +1322,27 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 #ifndef TT_F32_AOFF
 #define TT_F32_AOFF 1
 #endif
+// Waves per SIMD of the fp32 backward from stored probabilities (no X chain: fewer registers), by H
+#ifndef TT_F32_MINW_LOADP128
+#define TT_F32_MINW_LOADP128 2
+#endif
+#ifndef TT_F32_MINW_LOADP256
+#define TT_F32_MINW_LOADP256 1
+#endif
+#ifndef TT_F32_MINW_LOADP64
+#define TT_F32_MINW_LOADP64 2
+#endif
+__host__ __device__ constexpr int f32_waves(int mode, int H, bool loadp) {
+  return loadp ? (H < 128 ? TT_F32_MINW_LOADP64 : H > 128 ? TT_F32_MINW_LOADP256 : TT_F32_MINW_LOADP128)
+               : (H < 128 ? 2 : H > 128 ? 1 : mode == FWD ? TT_F32_MINW128_FWD : TT_F32_MINW128_DD);
+}
 // STOREP (round 3, the fp32 form of the stored-probability backward): the forward also writes each
 // 32 x 32 G tile to P, block (candidate tile ct, query tile qt) = 1,024 floats [candidate][query] at
 // (ct * p_nqt + qt) * 1024; the backward (MODE DD, R = the scaled query copy Qs) reads its G^T
 // tile from there (four 16-B loads per lane: lane (candidate r32, hh) takes queries 8k + 4hh + u)
 // instead of forming X = R C^T and its exp: half the backward's MFMAs, no transcendental.
 template <int MODE, int H, bool STOREP = false>
-__global__ __launch_bounds__(NT, (H < 128 ? 2 : H > 128 ? 1 : MODE == FWD ? TT_F32_MINW128_FWD : TT_F32_MINW128_DD))
+__global__ __launch_bounds__(NT, f32_waves(MODE, H, STOREP && MODE == DD))
 void score_f32_kernel(
     const float* __restrict__ R, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ lse2_rows, const float* __restrict__ qnorm,
@@ -2018,6 +2032,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   if (sp && bf) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
+  if (sp && !bf) parts = std::max(parts, (size_t)plan_for(B, M, BJ, f32_waves(DD, H, true)).S * M * H * 4);
   const size_t oa = take(parts);
   Ws w{};
   char* b = static_cast<char*>(base);
@@ -2209,7 +2224,7 @@ int bwd_core_p32(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, 
                  int64_t p_nqt, const float* q, const float* d, const float* dqu, const float* grad_loss,
                  float grad_scale, const BwdOut& out, const char* pad, float* acc_part, const int* xrows,
                  const float* lse2, hipStream_t s) {
-  const Plan p = plan_for(B, M, bj_for(TT_F32), wg_per_cu(H, TT_F32, DD));
+  const Plan p = plan_for(B, M, bj_for(TT_F32), f32_waves(DD, H, true));
   float* Pf = reinterpret_cast<float*>(const_cast<char*>(P));
   switch (H) {
 #define TT_DDP32(HH)                                                                                               \
