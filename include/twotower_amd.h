@@ -266,6 +266,14 @@ int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, 
                    float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
                    const float* grad_loss, float grad_scale, float* dq, float* dd,
                    void* ws, size_t ws_bytes, tt_stream_t stream);
+/* tt_inbatch_bwd that also forms the mean of loss_rows (B floats) into *loss in one extra
+ * workgroup of its combine launch, with tt_mean's arithmetic (the same bits): for a caller whose
+ * forward passed loss = NULL because the loss is read only after the backward (train_step.TrainStep).
+ * loss and loss_rows are both set or both NULL (then this is tt_inbatch_bwd). */
+int tt_inbatch_bwd_mean(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+                        float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
+                        const float* grad_loss, float grad_scale, float* dq, float* dd,
+                        const float* loss_rows, float* loss, void* ws, size_t ws_bytes, tt_stream_t stream);
 
 /* ---- the same loss from explicit, prepared operands (bf16 / bf16_split only), for data
  * parallelism with candidate-owner gradients (cross-device negatives without a gradient

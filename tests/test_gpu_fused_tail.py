@@ -120,19 +120,22 @@ def test_pack_blocks_equals_cat(dtype, rows):
     assert torch.equal(dst, torch.cat(srcs, 0))
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp32"])
 @pytest.mark.parametrize("graph,B", [(False, 300), (True, 300), (True, 9000)])
-def test_trainstep_deferred_loss_mean_equals_own_launch(graph, B, monkeypatch):
-    """The loss mean formed by the backward combine's extra workgroup (tt_inbatch_bwd_l2_mean)
-    equals tt_mean's launch bit for bit, and so does everything after it.  B 300: short strided
-    tails; B 9000: past 8 x 1024 rows, the eight-load loop."""
-    V, E, L = 3000, 256, 12
+def test_trainstep_deferred_loss_mean_equals_own_launch(graph, B, dt, monkeypatch):
+    """The loss mean formed by the backward combine's extra workgroup (tt_inbatch_bwd_l2_mean;
+    fp32 at H = 128, no fused L2 backward: tt_inbatch_bwd_mean) equals tt_mean's launch bit for
+    bit, and so does everything after it.  B 300: short strided tails; B 9000: past 8 x 1024
+    rows, the eight-load loop."""
+    V, L = 3000, 12
+    E = 256 if dt == "bf16" else 128
 
     def run():
         torch.manual_seed(17)
         emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
         model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
         opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
-        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.05, compute_dtype="bf16"), opt,
+        step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.05, compute_dtype=dt), opt,
                             graph=graph, eager_steps=2)
         losses = [step(*tt.data.synthetic_triplets(B, L, V, seed=40 + k, device=DEV)).clone() for k in range(4)]
         torch.cuda.synchronize()

@@ -668,6 +668,31 @@ __device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
 }
 // sum over s < S of p[s * stride4], in split order (the same order as the generic path), with up
 // to four splits' loads in flight
+// sum over s < S of w_s p[s * stride] (w_s = f_loc for s < S_loc, else 1: the product is skipped,
+// x * 1 == x), added in the order s = 0, 1, ... as the plain loop does (the same bits), with four
+// loads in flight instead of one dependent round trip per split.
+// (-DTT_COMBINE_BATCHED=0: one load per step, the loop as it was before round 3's end; A/B)
+#ifndef TT_COMBINE_BATCHED
+#define TT_COMBINE_BATCHED 0
+#endif
+__device__ __forceinline__ float sum_parts1(const float* __restrict__ p, int64_t stride, int S, int S_loc = 0,
+                                            float f_loc = 1.f) {
+  float o = 0.f;
+#if !TT_COMBINE_BATCHED
+  for (int s = 0; s < S; ++s) o += s < S_loc ? f_loc * p[(int64_t)s * stride] : p[(int64_t)s * stride];
+  return o;
+#endif
+  for (int s0 = 0; s0 < S; s0 += 4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (s0 + u < S) o += s0 + u < S_loc ? f_loc * v[u] : v[u];
+  }
+  return o;
+}
+
 __device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t stride4, int S) {
   f32x4 o = {0.f, 0.f, 0.f, 0.f};
   for (int s0 = 0; s0 < S; s0 += 4) {
@@ -1707,8 +1732,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
   const float f_loc = S_loc > 0 ? __builtin_amdgcn_exp2f(col_shift(c2, qnorm[i], fold_dmax(dmax_loc, n_dmax_loc)) - sh)
                                 : 1.f;
-  float l = 0.f;
-  for (int s = 0; s < S; ++s) l += s < S_loc ? f_loc * l_part[(int64_t)s * B + i] : l_part[(int64_t)s * B + i];
+  float l = sum_parts1(l_part + i, B, S, S_loc, f_loc);
   if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
     const float loss_i = combine_row256<DT>(
         i, l,
@@ -1766,8 +1790,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   if (dqu) {
     const float inv_l = 1.f / l;
     for (int h = lane; h < H; h += kWave) {
-      float o = 0.f;
-      for (int s = 0; s < S; ++s) o += (s < S_loc ? f_loc : 1.f) * acc_part[((int64_t)s * B + i) * H + h];
+      const float o = sum_parts1(acc_part + i * H + h, B * H, S, S_loc, f_loc);
       dqu[i * H + h] = o * inv_l - (float)dl[h];
     }
   }
@@ -1811,8 +1834,17 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
                                                           float inv_tau, float* __restrict__ dq,
                                                           float* __restrict__ dd, const int* __restrict__ xrows = nullptr,
                                                           const DT* __restrict__ Dmat = nullptr,
-                                                          const float* __restrict__ lse2 = nullptr, float c2 = 0.f) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                          const float* __restrict__ lse2 = nullptr, float c2 = 0.f,
+                                                          const float* __restrict__ mean_x = nullptr,
+                                                          float* __restrict__ mean_out = nullptr) {
+  // one extra block, dispatched first (as in bwd_combine_l2_kernel): the forward's deferred loss mean
+  if (mean_out && blockIdx.x == 0) {
+    __shared__ float part[1024];
+    const float m = block256_mean_as_1024(mean_x, B, part);
+    if (threadIdx.x == 0) mean_out[0] = m;
+    return;
+  }
+  const int64_t r = (int64_t)(blockIdx.x - (mean_out ? 1 : 0)) * 4 + (threadIdx.x >> 6);
   const int lane = lane_id();
   const float scale = grad_loss[0] * grad_scale * inv_tau;
   if (H == 4 * kWave) {
@@ -1832,8 +1864,7 @@ __global__ __launch_bounds__(256) void bwd_combine_kernel(int64_t B, int64_t M, 
     for (int h0 = 0; h0 < H; h0 += kWave) {
       const int h = h0 + lane;
       float a = 0.f;
-      if (h < H)
-        for (int s = 0; s < S; ++s) a += acc_part[((int64_t)s * M + r) * H + h];
+      if (h < H) a = sum_parts1(acc_part + r * H + h, M * H, S);
       if (xrows)  // exact rows (stored-P backward; see add_exact_rows)
         for_exact_rows(xrows, B, lane, [&](int64_t i) {
           const float g = __builtin_amdgcn_exp2f(exact_row_dot(Qmat + i * H, Dmat + r * H, H, lane) * c2 - lse2[i]);
@@ -1918,8 +1949,9 @@ void launch_bwd_combine(int64_t B, int64_t M, int H, int S, int64_t label_off, c
     return;
   }
   const int64_t rows = std::max(B, M);
-  bwd_combine_kernel<DT><<<dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s>>>(
-      B, M, H, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.dq, out.dd, xrows, Db, lse2, c2);
+  bwd_combine_kernel<DT><<<dim3((unsigned)((rows + 3) / 4 + (out.loss ? 1 : 0))), dim3(256), 0, s>>>(
+      B, M, H, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.dq, out.dd, xrows, Db, lse2, c2,
+      out.loss_rows, out.loss);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2409,11 +2441,23 @@ extern "C" int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int
 extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
                               int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
                               float grad_scale, float* dq, float* dd, void* ws, size_t ws_bytes, tt_stream_t stream) {
+  return tt_inbatch_bwd_mean(q, d, B, M, H, dtype, inv_tau, label_off, lse, dq_unscaled, grad_loss, grad_scale, dq, dd,
+                             nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int tt_inbatch_bwd_mean(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+                                   float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
+                                   const float* grad_loss, float grad_scale, float* dq, float* dd,
+                                   const float* loss_rows, float* loss, void* ws, size_t ws_bytes, tt_stream_t stream) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
   TT_REQUIRE(q && d && lse && dq_unscaled && grad_loss && dq && dd && ws, "null pointer");
-  return inbatch_bwd(q, d, B, M, H, dtype, inv_tau, label_off, dq_unscaled, grad_loss, grad_scale, BwdOut{dq, dd}, ws,
-                     ws_bytes, reinterpret_cast<hipStream_t>(stream));
+  TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd_mean: loss and loss_rows together");
+  BwdOut out{dq, dd};
+  out.loss_rows = loss_rows;
+  out.loss = loss;
+  return inbatch_bwd(q, d, B, M, H, dtype, inv_tau, label_off, dq_unscaled, grad_loss, grad_scale, out, ws, ws_bytes,
+                     reinterpret_cast<hipStream_t>(stream));
 }
 
 // ---- explicit operands (data parallel with candidate-owner gradients; see twotower_amd.h)

@@ -813,9 +813,14 @@ def _inbatch_fwd(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale, want_
     return loss, lse, dqu, ws
 
 
-def _inbatch_bwd(meta, q, d, lse, dqu, ws, g, dq, dd):
+def _inbatch_bwd(meta, q, d, lse, dqu, ws, g, dq, dd, mean=None):
+    """mean = (loss_rows, loss): the forward deferred the loss mean; the combine launch forms it."""
     B, M, H, dt, inv_tau, label_off, grad_scale = meta
     g = g.to(_FLOAT).contiguous().reshape(1)
+    if mean is not None:
+        call("tt_inbatch_bwd_mean", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g),
+             grad_scale, ptr(dq), ptr(dd), ptr(mean[0]), ptr(mean[1]), ptr(ws), ws.numel(), stream_of(q))
+        return
     call("tt_inbatch_bwd", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g), grad_scale,
          ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(q))
 
@@ -852,9 +857,10 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         want_grad = bool(ctx.needs_input_grad[0])
         ctx.l2_token = prep[4] if prep is not None else None
         # inside TrainStep (deferred_loss_mean) the loss is read only after the step: its mean is
-        # formed by the backward's combine launch (tt_inbatch_bwd_l2_mean) instead of a launch of
-        # its own between the forward combine and the backward engine
-        defer = want_grad and prep is not None and _DEFER_MEAN[0] > 0 and os.environ.get("TT_DEFER_MEAN", "1") != "0"
+        # formed by the backward's combine launch (tt_inbatch_bwd_l2_mean, or tt_inbatch_bwd_mean
+        # when the head's L2 backward is not fused: fp32, H = 128) instead of a launch of its own
+        # between the forward combine and the backward engine
+        defer = want_grad and _DEFER_MEAN[0] > 0 and os.environ.get("TT_DEFER_MEAN", "1") != "0"
         loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad,
                                           prep[:4] if prep is not None else None, defer_mean=defer)
         if want_grad:
@@ -878,9 +884,7 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
                  ptr(ws), ws.numel(), stream_of(qd))
             tok.dy = grad
             return grad, None, None, None, None
-        if dm is not None:
-            call("tt_mean", ptr(dm[0]), dm[0].numel(), ptr(dm[1]), stream_of(qd))
-        _inbatch_bwd(ctx.meta, qd[:nq], qd[nq:], lse, dqu, ws, g, grad[:nq], grad[nq:])
+        _inbatch_bwd(ctx.meta, qd[:nq], qd[nq:], lse, dqu, ws, g, grad[:nq], grad[nq:], mean=dm)
         return grad, None, None, None, None
 
 
