@@ -671,9 +671,10 @@ __device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
 // sum over s < S of w_s p[s * stride] (w_s = f_loc for s < S_loc, else 1: the product is skipped,
 // x * 1 == x), added in the order s = 0, 1, ... as the plain loop does (the same bits), with four
 // loads in flight instead of one dependent round trip per split.
-// (-DTT_COMBINE_BATCHED=0: one load per step, the loop as it was before round 3's end; A/B)
+// (-DTT_COMBINE_BATCHED=0: one load per step, the loop before round 3's end; C2 0.4299 vs 0.4273
+// ms/step batched, same box, profiles/r03zp_c2_combine_ab.txt)
 #ifndef TT_COMBINE_BATCHED
-#define TT_COMBINE_BATCHED 0
+#define TT_COMBINE_BATCHED 1
 #endif
 __device__ __forceinline__ float sum_parts1(const float* __restrict__ p, int64_t stride, int S, int S_loc = 0,
                                             float f_loc = 1.f) {
