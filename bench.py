@@ -259,8 +259,8 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
     stored_p = world == 1 and bwd_form == "stored" and (
         (scorer_dtype == "bf16" and B * M <= 2 ** 31) or (scorer_dtype == "fp32" and B * M <= 2 ** 30))
     fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
-    bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd") if k in ops_t or
-                   k == "tt_inbatch_bwd")
+    bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd_mean", "tt_inbatch_bwd")
+                   if k in ops_t or k == "tt_inbatch_bwd")
     if fwd_key in ops_t and bwd_key in ops_t:
         # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
         # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
