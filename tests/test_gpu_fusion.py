@@ -15,10 +15,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _model(V, seed):
+def _model(V, seed, E=256):
     torch.manual_seed(seed)
-    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
-    return tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    return tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
 
 
 def _ids(B, L, V, rng):
@@ -39,16 +39,20 @@ def _step(model, loss_fn, batch):
 
 
 @pytest.mark.parametrize("B,L,dtype,bwd", [(8192, 64, "bf16", "stored"), (300, 12, "bf16", "stored"),
-                                           (129, 7, "bf16", "recompute"), (256, 16, "bf16_split", "stored")])
+                                           (129, 7, "bf16", "recompute"), (256, 16, "bf16_split", "stored"),
+                                           (4096, 32, "fp32", "stored"), (300, 12, "fp32", "stored"),
+                                           (129, 7, "fp32", "recompute")])
 def test_head_normalise_fused_with_scorer_prep_is_bit_identical(B, L, dtype, bwd, monkeypatch):
+    """bf16 at H = 256 (C3) and fp32 at H = 128 (C2, l2_prep128_kernel)."""
     V = 5000
+    E = 128 if dtype == "fp32" else 256
     rng = np.random.default_rng(B + L)
     batch = [_ids(B, L, V, rng) for _ in range(3)]
     loss_fn = tt.losses.build("in_batch", temperature=0.05, compute_dtype=dtype)
     assert tt.losses.scorer_prep_dtype(loss_fn) == dtype
     prev = ops.set_inbatch_backward(bwd)
     try:
-        model = _model(V, 7)
+        model = _model(V, 7, E)
         ref_out, ref_grads = _step(model, loss_fn, batch)
 
         seen = []
@@ -97,7 +101,23 @@ def test_scorer_prep_set_by_trainstep_and_ignored_by_other_losses():
         ops.call = real_call
     model2 = _model(100, 0)
     st2 = tt.TrainStep(model2, tt.losses.build("in_batch", compute_dtype="fp32"), tt.optim.AdamW(model2.parameters()))
-    assert st2._scorer_prep is None and model2.scorer_prep is None
+    assert st2._scorer_prep == "fp32" and model2.scorer_prep is None
+    ops.call = spy
+    try:  # fp32 at H = 256: no fused prep shape, the head normalises as usual
+        seen.clear()
+        st2(*batch)
+        assert "tt_inbatch_l2_prep" not in seen and "tt_inbatch_fwd" in seen
+    finally:
+        ops.call = real_call
+    model3 = _model(100, 0, 128)
+    st3 = tt.TrainStep(model3, tt.losses.build("in_batch", compute_dtype="fp32"), tt.optim.AdamW(model3.parameters()))
+    ops.call = spy
+    try:  # fp32 at H = 128 (C2): the head's normalise pass forms the scorer's norms
+        seen.clear()
+        st3(*batch)
+        assert "tt_inbatch_l2_prep" in seen and "tt_inbatch_fwd_prepped" in seen
+    finally:
+        ops.call = real_call
     # a head output carrying prepared operands into a triplet loss: ignored, same loss
     model.scorer_prep = "bf16"
     trip = tt.losses.build("triplet")

@@ -1684,6 +1684,55 @@ __global__ __launch_bounds__(64 * kL2PrepWaves) void l2_prep_kernel(float* __res
   }
 }
 
+// The same fusion for the fp32 scorer at H = 128 (C2): each row is normalised in place exactly as
+// head_normalize_kernel<128> does it (two floats per lane), and prep_rows' arithmetic for an fp32
+// scorer (no copies: the row norm from the normalised row as its 32 lanes of float4 would form it,
+// the per-block maximum) runs on the registers: lane L < 32 takes the float4 of lanes 2L and 2L + 1,
+// so the sum and its wave reduction are prep_qd_kernel's, bit for bit.  Blocks [0, gq) take the
+// query rows, [gq, gq + gd) the candidate rows (4 waves per block, grid-stride as prep_qd_kernel).
+__global__ __launch_bounds__(256) void l2_prep128_kernel(float* __restrict__ y, int64_t B, int64_t M, int gq,
+                                                         float* __restrict__ norms, float* __restrict__ qnorm,
+                                                         float* __restrict__ dmax_part, char* __restrict__ pad,
+                                                         float* __restrict__ lse2, int* __restrict__ xrows) {
+  constexpr int H = 128;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  __shared__ float wmax[4];
+  if (blockIdx.x == 0) {  // prep_qd_kernel's block-0 set-up (fp32: no operand copies)
+    if (xrows && threadIdx.x == 0) xrows[0] = 0;
+    for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
+      reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
+    for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
+  }
+  const bool isq = (int)blockIdx.x < gq;
+  const int64_t b0 = isq ? blockIdx.x : blockIdx.x - gq, nb = isq ? gq : gridDim.x - gq;
+  const int64_t rows = isq ? B : M, base = isq ? 0 : B;
+  if (isq && xrows)  // no query row redone exactly yet (see combine_row256)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gq * blockDim.x)
+      xrows[1 + i] = 0;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  float mx = 0.f;
+  for (int64_t r = b0 * 4 + wid; r < rows; r += nb * 4) {
+    f32x2* p = reinterpret_cast<f32x2*>(y + (base + r) * H) + lane;
+    f32x2 v = *p;
+    const float ss = wave_sum(__builtin_fmaf(v[1], v[1], v[0] * v[0]));  // head_normalize_kernel<128>
+    const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
+    v[0] *= inv;
+    v[1] *= inv;
+    *p = v;
+    if (lane == 0) norms[base + r] = nrm;
+    // prep_rows (H = 128): lane L < 32 holds elements 4L .. 4L + 3, i.e. lanes 2L and 2L + 1 here
+    const int src = (2 * lane) & (kWave - 1);
+    const f32x4 v4 = {__shfl(v[0], src), __shfl(v[1], src), __shfl(v[0], src + 1), __shfl(v[1], src + 1)};
+    const float n = sqrtf(wave_sum(lane < 32 ? sumsq4(v4) : 0.f));
+    if (isq && lane == 0) qnorm[r] = n;
+    mx = fmaxf(mx, n);
+  }
+  if (isq) return;
+  if (lane == 0) wmax[wid] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) dmax_part[b0] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+}
+
 // One matrix: optional bf16 copy (with a kTailRows zero tail written by block 0), optional row
 // norms, optional per-block max norm (max_parts[b], gridDim.x <= kMaxPrepBlocks values).
 __global__ __launch_bounds__(256) void prep_rows_kernel(const float* __restrict__ x, int64_t rows, int H,
@@ -2340,7 +2389,7 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
   TT_REQUIRE(q && d && lse && loss_rows && ws, "null pointer");  // loss NULL: the caller forms the mean (tt_mean)
   TT_REQUIRE(!want_grad || dq_unscaled, "want_grad needs dq_unscaled");
   TT_REQUIRE(((reinterpret_cast<uintptr_t>(q) | reinterpret_cast<uintptr_t>(d)) & 15) == 0, "q/d must be 16-byte aligned");
-  TT_REQUIRE(!prepped || dtype != TT_F32, "prepared operands are bf16 copies (dtype bf16 / bf16_split)");
+  TT_REQUIRE(!prepped || dtype != TT_F32 || H == 2 * kWave, "prepared fp32 operands: H = 128 (tt_inbatch_l2_prep)");
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   const bool bf = dtype != TT_F32;
@@ -2372,13 +2421,19 @@ extern "C" int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t
 extern "C" int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dtype, float* norms, void* ws,
                                   size_t ws_bytes, tt_stream_t stream) {
   TT_REQUIRE(B > 0 && M > 0, "B=%lld M=%lld must be positive", (long long)B, (long long)M);
-  TT_REQUIRE(H == 4 * kWave, "tt_inbatch_l2_prep: H = %d only (got %d)", 4 * kWave, H);
-  TT_REQUIRE(dtype == TT_BF16 || dtype == TT_BF16_SPLIT, "tt_inbatch_l2_prep: dtype bf16 / bf16_split (got %d)", dtype);
+  TT_REQUIRE((H == 4 * kWave && (dtype == TT_BF16 || dtype == TT_BF16_SPLIT)) || (H == 2 * kWave && dtype == TT_F32),
+             "tt_inbatch_l2_prep: H = 256 with bf16 / bf16_split or H = 128 with fp32 (got H=%d dtype=%d)", H, dtype);
   TT_REQUIRE(y && norms && ws, "null pointer");
   TT_REQUIRE((reinterpret_cast<uintptr_t>(y) & 15) == 0, "y must be 16-byte aligned");
   const Ws w = carve_user(ws, B, M, H, dtype);
   TT_REQUIRE(w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu", w.total + 256, ws_bytes);
   const int gq = prep_blocks_q(B), gd = prep_blocks_d(M);
+  if (dtype == TT_F32) {
+    l2_prep128_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        y, B, M, gq, norms, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows);
+    TT_LAUNCH_CHECK("score_l2_prep128");
+    return TT_OK;
+  }
   l2_prep_kernel<<<dim3((unsigned)(gq + gd)), dim3(64 * kL2PrepWaves), 0, reinterpret_cast<hipStream_t>(stream)>>>(
       y, B, M, gq, norms, w.Qb, w.Db, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows);
   TT_LAUNCH_CHECK("score_l2_prep");

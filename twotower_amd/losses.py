@@ -103,14 +103,15 @@ def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *arg
 
 
 def scorer_prep_dtype(loss_fn) -> str | None:
-    """The compute dtype when ``loss_fn`` is a single-device bf16 in-batch loss (as built by
-    ``build("in_batch", compute_dtype="bf16" | "bf16_split", ...)``), whose operand prep a tied
-    TwoTower may fold into its head (ops.scorer_prep); else None."""
+    """The compute dtype when ``loss_fn`` is a single-device in-batch loss (as built by
+    ``build("in_batch", compute_dtype=..., ...)``), whose operand prep a tied TwoTower may fold
+    into its head's normalise pass (ops.scorer_prep; the head fuses it where tt_inbatch_l2_prep
+    has the shape: bf16 / bf16_split at H = 256, fp32 at H = 128); else None."""
     fn, kw = (loss_fn.func, loss_fn.keywords) if isinstance(loss_fn, partial) else (loss_fn, {})
     if fn is not in_batch_sampled_softmax_loss or kw.get("cross_device_negatives"):
         return None
     dt = kw.get("compute_dtype", "fp32")
-    return dt if dt in ("bf16", "bf16_split") else None
+    return dt if dt in ("bf16", "bf16_split", "fp32") else None
 
 
 def _owner_gradients() -> bool:

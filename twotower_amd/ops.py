@@ -455,6 +455,11 @@ def _head_gemm(A: torch.Tensor, planes: torch.Tensor, epi: int, bias=None, mask=
 _SCORER_PREP: list[tuple[int, int]] = []  # (query rows, compute dtype code) of an open scorer_prep()
 
 
+def _prep_fusable(width: int, dt: int) -> bool:
+    """tt_inbatch_l2_prep's shapes: H = 256 with bf16 operand copies (C3), H = 128 fp32 (C2)."""
+    return (width == HEAD_WIDTH and dt != _lib.TT_F32) or (width == 128 and dt == _lib.TT_F32)
+
+
 @contextlib.contextmanager
 def scorer_prep(nq: int, compute_dtype: str):
     """While open, a TowerHead over rows [q (nq rows); candidates] also prepares the in-batch
@@ -522,13 +527,13 @@ class TowerHead(torch.autograd.Function):
         mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
         h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
-        req = _SCORER_PREP[-1] if _SCORER_PREP and width == HEAD_WIDTH else None
+        req = _SCORER_PREP[-1] if _SCORER_PREP and _prep_fusable(width, _SCORER_PREP[-1][1]) else None
         if req is not None and 0 < req[0] < rows:
             nq, dt = req  # normalise pass fused with the in-batch scorer's operand prep
             out = _head_gemm(h, p_w2, 4, bias=b2)
-            ws = torch.empty(_lib.lib().tt_inbatch_ws_size(nq, rows - nq, HEAD_WIDTH, dt), dtype=torch.uint8,
+            ws = torch.empty(_lib.lib().tt_inbatch_ws_size(nq, rows - nq, width, dt), dtype=torch.uint8,
                              device=x.device)
-            call("tt_inbatch_l2_prep", ptr(out), nq, rows - nq, HEAD_WIDTH, dt, ptr(norm), ptr(ws), ws.numel(),
+            call("tt_inbatch_l2_prep", ptr(out), nq, rows - nq, width, dt, ptr(norm), ptr(ws), ws.numel(),
                  stream_of(x))
             ctx.l2_token = _L2Token(norm)
             out._tt_inbatch_prep = (nq, rows - nq, dt, ws, ctx.l2_token)
