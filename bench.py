@@ -208,6 +208,60 @@ def l2_backward_ms(rows: int, d: int, dev, reps: int = 20) -> float:
     return t
 
 
+def scorer_entry(ops_t: dict, timing_steps: int, B: int, M: int, d: int, world: int, scorer_dtype: str,
+                 bwd_form: str, normalise=lambda: 0.0, l2_backward=lambda: 0.0) -> dict | None:
+    """The in-batch scorer's roofline entry (B queries x M candidates, width d) from per-op
+    device times: both passes, the operand prep's cost beyond a plain normalise and the fused
+    backward's cost beyond a plain L2 backward."""
+    pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
+    mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
+    # single process, bf16 or fp32: the backward reads the forward's stored probabilities (no S recompute)
+    stored_p = world == 1 and bwd_form == "stored" and (
+        (scorer_dtype == "bf16" and B * M <= 2 ** 31) or (scorer_dtype == "fp32" and B * M <= 2 ** 30))
+    fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
+    bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd_mean", "tt_inbatch_bwd")
+                   if k in ops_t or k == "tt_inbatch_bwd")
+    if fwd_key not in ops_t or bwd_key not in ops_t:
+        return None
+    # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
+    # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
+    fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t[bwd_key]["mean_ms"]
+    l2_ms = None
+    if bwd_key in ("tt_inbatch_bwd_l2", "tt_inbatch_bwd_l2_mean"):
+        # the backward combine also runs the tower head's F.normalize backward: the scorer is
+        # charged what that pass costs beyond a plain tt_l2norm_bwd over the same rows
+        l2_ms = l2_backward()
+        bwd_ms = max(0.0, bwd_ms - l2_ms)
+    prep_ms = None
+    if fwd_key == "tt_inbatch_fwd_prepped" and "tt_inbatch_l2_prep" in ops_t:
+        # the operand prep runs inside the head's normalise pass (tt_inbatch_l2_prep): charge
+        # the scorer what that pass costs beyond the plain normalise, measured on the same rows
+        prep_ms = max(0.0, ops_t["tt_inbatch_l2_prep"]["mean_ms"] - normalise())
+    ms = fwd_ms + bwd_ms + (prep_ms or 0.0)
+    algo = 6.0 * B * M * d
+    executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
+    achieved = algo / (ms * 1e-3) / 1e12
+    form = (f"{scorer_dtype}, backward from stored {scorer_dtype} probabilities" if stored_p else
+            {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
+             "fp32": "fp32 MFMA, recompute backward"}[scorer_dtype])
+    return {
+        "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
+        "abi": fwd_key + "+" + bwd_key, "bound": "mfma", "mean_ms": round(ms, 4), "B": B, "M": M,
+        "pass_ms": {"forward": round(fwd_ms, 4), "backward": round(bwd_ms, 4),
+                    **({"operand_prep_in_head_normalise": round(prep_ms, 4)} if prep_ms is not None else {}),
+                    **({"plain_l2_backward_subtracted": round(l2_ms, 4)} if l2_ms is not None else {})},
+        "calls_per_step": ops_t[fwd_key]["calls"] / timing_steps, "achieved": round(achieved, 2),
+        "peak": pk, "unit": "TFLOP/s", "frac": round(achieved / pk, 4), "algorithmic": algo,
+        "executed": executed, "executed_rate": round(executed / (ms * 1e-3) / 1e12, 2),
+        "per_launch": "6*B*M*H algorithmic flops (2BMH S + 4BMH dQ, dD) over both passes",
+        "form": form,
+        # measured max-abs-normalised gradient error at C3 (tools/scorer_error_table.py --big,
+        # profiles/r02_scorer_error_table.jsonl): against float64 on the same bf16-rounded
+        # operands, and against float64 on the fp32 operands (what the reference computes)
+        "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
+    }
+
+
 def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dtype: str, nnz: float,
               tower_params: int, bwd_form: str, normalise=lambda: 0.0, l2_backward=lambda: 0.0):
     """Per-op rooflines from the per-op device times (HIP events on each C-ABI call's launch
@@ -253,52 +307,9 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
         side_stream=True)
     add("embedding bag backward (dense grad, apply half)", "tt_bag_mean_bwd_planned",
         nseq * d * 4 + nseq * 4 + V * d * 4, "GB/s", HBM_PEAK_GBS, "hbm", "d_pooled + denom + V*E*4 grad write")
-    pk = MFMA_PEAK_TFLOPS["fp32" if scorer_dtype == "fp32" else "bf16"]
-    mult = 2 if scorer_dtype == "bf16_split" else 1  # hi/lo P doubles the second product
-    # single process, bf16 or fp32: the backward reads the forward's stored probabilities (no S recompute)
-    stored_p = world == 1 and bwd_form == "stored" and (
-        (scorer_dtype == "bf16" and B * M <= 2 ** 31) or (scorer_dtype == "fp32" and B * M <= 2 ** 30))
-    fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
-    bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd_mean", "tt_inbatch_bwd")
-                   if k in ops_t or k == "tt_inbatch_bwd")
-    if fwd_key in ops_t and bwd_key in ops_t:
-        # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
-        # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
-        fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t[bwd_key]["mean_ms"]
-        l2_ms = None
-        if bwd_key in ("tt_inbatch_bwd_l2", "tt_inbatch_bwd_l2_mean"):
-            # the backward combine also runs the tower head's F.normalize backward: the scorer is
-            # charged what that pass costs beyond a plain tt_l2norm_bwd over the same rows
-            l2_ms = l2_backward()
-            bwd_ms = max(0.0, bwd_ms - l2_ms)
-        prep_ms = None
-        if fwd_key == "tt_inbatch_fwd_prepped" and "tt_inbatch_l2_prep" in ops_t:
-            # the operand prep runs inside the head's normalise pass (tt_inbatch_l2_prep): charge
-            # the scorer what that pass costs beyond the plain normalise, measured on the same rows
-            prep_ms = max(0.0, ops_t["tt_inbatch_l2_prep"]["mean_ms"] - normalise())
-        ms = fwd_ms + bwd_ms + (prep_ms or 0.0)
-        algo = 6.0 * B * M * d
-        executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
-        achieved = algo / (ms * 1e-3) / 1e12
-        form = (f"{scorer_dtype}, backward from stored {scorer_dtype} probabilities" if stored_p else
-                {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
-                 "fp32": "fp32 MFMA, recompute backward"}[scorer_dtype])
-        kernels.append({
-            "op": "in-batch scorer, forward + backward (prep, MFMA engines, combines)",
-            "abi": fwd_key + "+" + bwd_key, "bound": "mfma", "mean_ms": round(ms, 4),
-            "pass_ms": {"forward": round(fwd_ms, 4), "backward": round(bwd_ms, 4),
-                        **({"operand_prep_in_head_normalise": round(prep_ms, 4)} if prep_ms is not None else {}),
-                        **({"plain_l2_backward_subtracted": round(l2_ms, 4)} if l2_ms is not None else {})},
-            "calls_per_step": ops_t[fwd_key]["calls"] / timing_steps, "achieved": round(achieved, 2),
-            "peak": pk, "unit": "TFLOP/s", "frac": round(achieved / pk, 4), "algorithmic": algo,
-            "executed": executed, "executed_rate": round(executed / (ms * 1e-3) / 1e12, 2),
-            "per_launch": "6*B*M*H algorithmic flops (2BMH S + 4BMH dQ, dD) over both passes",
-            "form": form,
-            # measured max-abs-normalised gradient error at C3 (tools/scorer_error_table.py --big,
-            # profiles/r02_scorer_error_table.jsonl): against float64 on the same bf16-rounded
-            # operands, and against float64 on the fp32 operands (what the reference computes)
-            "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
-        })
+    sc = scorer_entry(ops_t, timing_steps, B, M, d, world, scorer_dtype, bwd_form, normalise, l2_backward)
+    if sc is not None:
+        kernels.append(sc)
         if scorer_dtype == "bf16" and world == 1:
             pmc = scorer_pmc(config)
             if pmc:
@@ -322,6 +333,96 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
                     "unit": dominant["unit"], "frac": dominant["frac"], "traffic": None, "op": dominant["op"]}
         roofline.update(pmc_traffic(dominant["abi"], config))
     return kernels, roofline
+
+
+class PlainLoop:
+    """The reference's hot loop body unchanged (twotower/train.py:103-154) around this package's
+    registry entries: eager ``model(q, p, n)`` (:120-122), ``loss_fn(q, p, n)`` (:133),
+    ``optimizer.zero_grad(); loss.backward(); optimizer.step()`` (:137-139) with the reference's
+    own ``torch.optim.AdamW(model.parameters(), lr)`` (:358-359: a dense V x E table gradient and
+    torch's foreach AdamW over it), and the per-batch monitors: two cosine-similarity means and the
+    loss, three ``.item()`` host syncs (:144-154).  What a user gets by swapping the registries
+    and nothing else."""
+
+    def __init__(self, model, loss_fn, lr: float = 1e-3):
+        self.model, self.loss_fn = model, loss_fn
+        self.optimizer = torch.optim.AdamW(model.parameters(), lr=lr)
+
+    def __call__(self, q, p, n=None):
+        ins = (q, p) if n is None else (q, p, n)
+        outs = self.model(*ins)
+        loss = self.loss_fn(*outs)
+        self.optimizer.zero_grad()
+        loss.backward()
+        self.optimizer.step()
+        with torch.no_grad():
+            pos = torch.nn.functional.cosine_similarity(outs[0], outs[1]).mean().item()
+            neg = (torch.nn.functional.cosine_similarity(outs[0][:, None, :], outs[2].view(
+                outs[0].shape[0], -1, outs[0].shape[1]), dim=-1).mean().item() if n is not None else 0.0)
+            _ = pos - neg
+        return torch.tensor(loss.item())
+
+    eager = __call__
+
+
+def time_steps(step, batches, steps: int, warmup: int) -> float:
+    """ms per step of `step` over `steps` calls after `warmup`, synchronised at both ends."""
+    for k in range(warmup):
+        step(*batches[k % len(batches)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(*batches[k % len(batches)])
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3
+
+
+def build_model(cfg, dev):
+    torch.manual_seed(1234)  # identical initial weights on every rank
+    emb = tt.embeddings.build("lookup", vocab_size=cfg["V"], embedding_dim=cfg["d"])
+    model = tt.build_two_tower("mean", emb, hidden_dim=cfg["d"], tied_weights=True).to(dev)
+    return emb, model
+
+
+def bxb_scorer(cfg, scorer_dtype: str, dev, reps: int, steps: int, helpers: bool) -> dict | None:
+    """The north_star's B x B scorer (B = 8192 queries against their own 8192 positives, d 256):
+    the (query, positive) pairs form of the same fused step (TwoTower(q, d) + the in-batch loss
+    over the positives, M = B), graph-replayed.  Per-op times from a stamped replay as for the
+    main line; the step's own time and pairs/s beside it (the C4 pairs form at one GPU)."""
+    if cfg["loss"] != "in_batch":
+        return None
+    B, L, V, d = cfg["B"], cfg["L"], cfg["V"], cfg["d"]
+    emb, model = build_model(cfg, dev)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+    loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype)
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=700 + k, device=dev)[:2] for k in range(4)]
+    step = tt.TrainStep(model, loss_fn, opt, graph=True)
+    ms = time_steps(step, batches, steps, 5)
+    ops_t = stamped_op_times(model, loss_fn, opt, batches, reps, dev)
+    e = scorer_entry(ops_t, reps, B, B, d, 1, scorer_dtype, tt_ops.get_inbatch_backward(),
+                     *((lambda: normalise_ms(2 * B, d, dev), lambda: l2_backward_ms(2 * B, d, dev)) if helpers else ()))
+    if e is None:
+        return None
+    e["op"] = "in-batch scorer, B x B (M = B: query, positive pairs), forward + backward"
+    e["step_ms"] = round(ms, 4)
+    e["step_pairs_per_s"] = round(B / (ms * 1e-3), 1)
+    e["workload"] = (f"pairs form of configs[2]: B {B} queries x their {B} positives, d {d}, L {L}, V {V}, "
+                     f"{scorer_dtype} scorer; TwoTower(q, d) + in_batch, fused table AdamW, HIP graph")
+    del step, opt, model, emb
+    return e
+
+
+def plain_loop_entry(cfg, loss_fn, batches, dev, steps: int, trainstep_ms: float) -> dict:
+    """PlainLoop timed on the bench's batches (fresh model, torch.optim.AdamW)."""
+    _, model = build_model(cfg, dev)
+    loop = PlainLoop(model, loss_fn)
+    ms = time_steps(loop, batches, steps, 3)
+    del loop, model
+    return {"ms_per_step": round(ms, 4), "pairs_per_s": round(cfg["B"] / (ms * 1e-3), 1), "steps": steps,
+            "trainstep_ms_per_step": round(trainstep_ms, 4), "slowdown_vs_trainstep": round(ms / trainstep_ms, 3),
+            "loop": "twotower/train.py:103-154 body unchanged: eager model(q,p,n), loss_fn, zero_grad/backward/"
+                    "step with torch.optim.AdamW(model.parameters(), lr=1e-3) (dense V x E table gradient), "
+                    "cosine monitors + 3 .item() syncs per step"}
 
 
 def parse():
@@ -352,6 +453,11 @@ def parse():
                          "tools/profile_round.sh sets it so every kernel in the trace belongs to a step")
     ap.add_argument("--zipf", type=float, default=None,
                     help="token ids ~ Zipf(s) over the vocabulary (text-like hot rows); default uniform")
+    ap.add_argument("--loop", default="trainstep", choices=["trainstep", "plain"],
+                    help="plain: time the reference's loop body unchanged (bench.PlainLoop: eager, torch.optim.AdamW, "
+                         "three .item() syncs) instead of TrainStep")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the B x B scorer entry and the plain-loop entry measured after the timed region")
     return ap.parse_args()
 
 
@@ -424,9 +530,7 @@ def main():
     scorer_dtype = args.scorer_dtype or cfg["dtype"]
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    torch.manual_seed(1234)  # identical initial weights on every rank
-    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=d)
-    model = tt.build_two_tower("mean", emb, hidden_dim=d, tied_weights=True).to(dev)
+    emb, model = build_model(cfg, dev)
     K = cfg["negatives"]
     if cfg["loss"] == "in_batch":
         loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype,
@@ -440,17 +544,23 @@ def main():
     # and replayed a small N-rank step through the same paths (tools/dp_capture_canary.py), so a
     # capture that fails or crashes on the box's ROCm/RCCL stack leaves this run eager
     canary = None
-    use_graph = args.graph == "on" or (args.graph == "auto" and not dp)
-    if dp and args.graph == "auto" and args.dist_backend == "nccl":
+    plain = args.loop == "plain"
+    use_graph = not plain and (args.graph == "on" or (args.graph == "auto" and not dp))
+    if dp and not plain and args.graph == "auto" and args.dist_backend == "nccl":
         canary = dp_capture_canary(cfg, scorer_dtype, args.table_sync, dev)
         agree = torch.tensor([1 if canary == "ok" else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(agree, op=dist.ReduceOp.MIN)
         use_graph = bool(agree.item())
-    # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
-    # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
-    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
-                         table_sync=args.table_sync)
-    step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
+    if plain:
+        if dp:
+            raise SystemExit("--loop plain runs one GPU (the reference loop has no data parallelism)")
+        opt, step = None, PlainLoop(model, loss_fn)
+    else:
+        # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
+        # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
+                             table_sync=args.table_sync)
+        step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
 
     batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + k, device=dev, zipf_s=args.zipf,
                                           negatives=max(K, 1))[:(2 if K == 0 else 3)]
@@ -520,6 +630,13 @@ def main():
                                                                 lambda: l2_backward_ms((2 + K) * B, d, dev))))
     gather = next((k for k in kernels if k["abi"] in ("tt_bag_mean_fwd", "tt_bag_mean_fwd_split")), None)
 
+    # After the timed region, one GPU: the north_star's B x B scorer (the pairs form of the same
+    # step, M = B) and the reference's loop body unchanged around these registries (PlainLoop)
+    bxb, plain_entry = None, None
+    if world == 1 and not dp and not plain and not args.no_extras:
+        bxb = bxb_scorer(cfg, scorer_dtype, dev, max(args.timing_steps, 1), args.steps, not args.no_helpers)
+        plain_entry = plain_loop_entry(cfg, loss_fn, batches, dev, 10, ms_per_step)
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         from oracle.cpu_step import host_cores, time_cpu_step  # CPU baseline only: the GPU path never uses it
@@ -582,7 +699,8 @@ def main():
                    "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
                    "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
                    "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if dp else "local"),
-                   "hip_graph": use_graph, "graph_canary": canary},
+                   "hip_graph": use_graph, "graph_canary": canary,
+                   "loop": "reference loop body unchanged (bench.PlainLoop)" if plain else "TrainStep"},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "gather_hbm": gather_hbm_evidence(args.config, gather, V, d),
         "roofline": roofline,
@@ -590,6 +708,10 @@ def main():
         # capture of the same step, replayed) or "eager_events_primed" (N ranks: an eager pass)
         "op_times": timing_source,
         "kernels": kernels,
+        # the north_star's "B x B scorer at B=8192, d=256": M = B, the pairs form of this step
+        "scorer_bxb": bxb,
+        # the reference's train.py loop body unchanged around these registries (no TrainStep)
+        "plain_loop": plain_entry,
         "cpu_baseline": cpu,
         "final_loss": float(loss.item()) if loss is not None else None,
     }

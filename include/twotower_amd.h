@@ -402,7 +402,7 @@ int tt_head_split(const float* W, int N, int K, int transpose, void* planes, tt_
 /* the four plane sets of one Linear-ReLU-Linear head in one launch, each tt_head_planes_bytes(256,
  * 256) long, in the order W1, W2, W1^T, W2^T (forward operands, then backward operands) */
 int tt_head_split_ff(const float* W1, const float* W2, void* planes, tt_stream_t stream);
-/* the same for an E -> H head (W1 H x E, W2 H x H; E, H in {128, 256}): W1 (3 H E bf16), W2
+/* the same for an E -> H head (W1 H x E, W2 H x H; E in {64, 128, 256}, H in {128, 256}): W1 (3 H E bf16), W2
  * (3 H H), W1^T (3 E H), W2^T (3 H H), consecutive.  tt_head_split_ff = tt_head_split_ff2(.., 256,
  * 256, ..). */
 int tt_head_split_ff2(const float* W1, const float* W2, int E, int H, void* planes, tt_stream_t stream);

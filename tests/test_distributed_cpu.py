@@ -209,3 +209,68 @@ def test_child_world_env_under_torchrun():
                        env=env, capture_output=True, text=True, timeout=240, cwd=os.path.dirname(here))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert r.stdout.count("child ok") == 2, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+# ---------------------------------------------------------------------------------------------
+# Quantities that size collectives must agree across ranks (ShardedRows' chunk count).
+def _agree_chunks(rank):
+    assert D._agree(8, None, torch.device("cpu"), "x") == 8
+    with pytest.raises(ValueError, match="disagree"):
+        D._agree(8 if rank == 0 else 4, None, torch.device("cpu"), "row chunks")
+    w = torch.nn.Parameter(torch.zeros(40, 4))
+    os.environ["TT_SHARD_CHUNKS"] = "4" if rank == 0 else "2"
+    with pytest.raises(ValueError, match="TT_SHARD_CHUNKS"):
+        D.ShardedRows(w)
+    os.environ["TT_SHARD_CHUNKS"] = "2"
+    assert D.ShardedRows(w).NC == 2
+
+
+def test_sharded_chunks_agree_across_ranks_gloo():
+    _run(_agree_chunks)
+
+
+# ---------------------------------------------------------------------------------------------
+# The N-rank HIP-graph capture is refused (TrainStep stays eager) where ProcessGroupNCCL's event
+# cache may be on: its watchdog aborts the process on a recycled event under capture (round 3).
+def test_capture_blocker_rules(monkeypatch):
+    monkeypatch.setattr(D.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(D.dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setitem(D._AT_IMPORT, "group_existed", False)
+    monkeypatch.setitem(D._AT_IMPORT, "event_cache", "0")
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    assert D.capture_blocker() is None  # group created after the import, the default left alone
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")  # the caller turned the cache back on
+    assert "TORCH_NCCL_CUDA_EVENT_CACHE" in D.capture_blocker()
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    monkeypatch.setitem(D._AT_IMPORT, "event_cache", "1")  # set before the import: setdefault kept it
+    assert D.capture_blocker() is not None
+    monkeypatch.setitem(D._AT_IMPORT, "group_existed", True)  # a group created before the import ...
+    assert "before twotower_amd.distributed was imported" in D.capture_blocker()
+    monkeypatch.setitem(D._AT_IMPORT, "event_cache", "0")  # ... with the cache off
+    assert D.capture_blocker() is None
+    monkeypatch.setattr(D.dist, "get_backend", lambda group=None: "gloo")
+    assert "gloo" in D.capture_blocker()
+
+
+def test_capture_error_classification():
+    from twotower_amd.train_step import _is_capture_error
+
+    assert _is_capture_error(RuntimeError("operation not permitted when stream is capturing"))
+    assert _is_capture_error(RuntimeError("hipErrorStreamCaptureUnsupported"))
+    assert not _is_capture_error(RuntimeError("mat1 and mat2 shapes cannot be multiplied"))
+
+
+def test_deferred_loss_mean_only_for_the_bare_in_batch_loss():
+    """TrainStep lets the in-batch loss leave its mean to the backward only when loss_fn returns
+    that loss itself (a wrapped loss read the unformed value)."""
+    import twotower_amd as tt
+
+    emb = tt.embeddings.build("lookup", vocab_size=50, embedding_dim=16)
+    model = tt.build_two_tower("mean", emb, hidden_dim=16, tied_weights=True)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    bare = tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16")
+    assert tt.TrainStep(model, bare, opt)._defer_mean
+    assert tt.TrainStep(model, tt.losses.in_batch_sampled_softmax_loss, opt)._defer_mean
+    assert not tt.TrainStep(model, lambda q, p, n: 0.5 * bare(q, p, n), opt)._defer_mean
+    assert not tt.TrainStep(model, tt.losses.build("in_batch", cross_device_negatives=True), opt)._defer_mean
+    assert not tt.TrainStep(model, tt.losses.build("triplet"), opt)._defer_mean

@@ -151,3 +151,27 @@ def test_trainstep_deferred_loss_mean_equals_own_launch(graph, B, dt, monkeypatc
     for a, b in zip(got[1], want[1]):
         assert torch.equal(a, b)
 
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainstep_wrapped_in_batch_loss_returns_its_value(graph):
+    """A loss_fn that wraps the in-batch loss (here 0.5 x it) reads the loss value inside the
+    forward: TrainStep must not defer its mean to the backward then (the value was
+    uninitialised memory).  Every returned loss equals 0.5 x the loss of a no-grad forward on the
+    same weights and batch, taken right before the step."""
+    V, L, B, E = 3000, 12, 300, 256
+    torch.manual_seed(5)
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+    bare = tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16")
+    step = tt.TrainStep(model, lambda q, p, n: 0.5 * bare(q, p, n), opt, graph=graph, eager_steps=1)
+    assert not step._defer_mean
+    for k in range(4):
+        batch = tt.data.synthetic_triplets(B, L, V, seed=60 + k, device=DEV)
+        with torch.no_grad():
+            want = 0.5 * bare(*model(*batch))
+        got = step(*batch).clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(got)
+        torch.testing.assert_close(got, want, rtol=1e-6, atol=0)

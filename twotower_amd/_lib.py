@@ -182,6 +182,15 @@ class SideGrads:
         self.finals: list = []  # callables the join queues after its wait
         self.active = False
 
+    def reset(self) -> None:
+        """Drop everything registered since the last join (a step abandoned before its join, e.g.
+        a failed HIP-graph capture: none of its side-stream work ran)."""
+        self.events.clear()
+        self.grads.clear()
+        self.uses.clear()
+        self.finals.clear()
+        self.active = False
+
     def use(self, param: torch.Tensor) -> None:
         self.uses[id(param)] = self.uses.get(id(param), 0) + 1
 

@@ -27,8 +27,43 @@ import torch.distributed as dist
 # its watchdog thread may still query them, and the query of an event last recorded in a capturing
 # stream fails ("operation not permitted on an event last recorded in a capturing stream": one run
 # of tests/_dp_graph_check.py, round 3).  Fresh events per collective; the variable is read when a
-# process group is created, so it is set here, before the caller creates one.
-os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+# process group is created, so it is set here, before the caller creates one.  That protects only
+# groups created after this import with the variable left alone: capture_blocker() tells the
+# others apart, and TrainStep then stays eager instead of capturing.
+_EVENT_CACHE_VAR = "TORCH_NCCL_CUDA_EVENT_CACHE"
+os.environ.setdefault(_EVENT_CACHE_VAR, "0")
+# what held when this module was imported: the value, and whether a process group already existed
+# (its ProcessGroupNCCL then read the variable before the default above could apply)
+_AT_IMPORT = {"event_cache": os.environ.get(_EVENT_CACHE_VAR),
+              "group_existed": dist.is_available() and dist.is_initialized()}
+
+
+def capture_blocker(group=None) -> str | None:
+    """Why the N-rank step must not be captured in a HIP graph on `group`, or None if it may be.
+
+    ProcessGroupNCCL with its CUDA event cache on hands the end events of eager collectives to
+    collectives recorded during a capture, and its watchdog thread then queries an event last
+    recorded in a capturing stream: an uncatchable abort (std::terminate in the watchdog).  The
+    cache is off only for a group created while TORCH_NCCL_CUDA_EVENT_CACHE=0; this module sets
+    that default at import, so a group created before the import, or with the variable set to
+    anything else, is refused here.  gloo groups are not captured at all (their collectives
+    stage through host memory)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    backend = dist.get_backend(group)
+    if backend == "gloo":
+        return "gloo collectives cannot be captured in a HIP graph"
+    if backend != "nccl":
+        return None
+    if _AT_IMPORT["group_existed"]:
+        if _AT_IMPORT["event_cache"] != "0":
+            return (f"the process group was created before twotower_amd.distributed was imported, without "
+                    f"{_EVENT_CACHE_VAR}=0 (ProcessGroupNCCL's event cache aborts the watchdog under graph capture)")
+        return None
+    if os.environ.get(_EVENT_CACHE_VAR) != "0" or _AT_IMPORT["event_cache"] != "0":
+        return (f"{_EVENT_CACHE_VAR} is {os.environ.get(_EVENT_CACHE_VAR)!r}, not '0' (ProcessGroupNCCL's event "
+                f"cache aborts the watchdog under graph capture)")
+    return None
 
 
 def is_active(group=None) -> bool:
@@ -91,6 +126,18 @@ def shard_chunks(V: int, world: int) -> int:
     return max(1, min(n, V // max(1, world)))
 
 
+def _agree(value: int, group, device, what: str) -> int:
+    """`value`, checked equal on every rank of `group` (MIN and MAX all-reduced): a quantity that
+    sizes collectives must not differ between ranks (a hang or corrupted rows otherwise)."""
+    dev = device if dist.get_backend(group) != "gloo" else "cpu"
+    t = torch.tensor([value, -value], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    lo, hi = int(t[0]), -int(t[1])
+    if lo != hi:
+        raise ValueError(f"ranks disagree on the {what}: {lo} .. {hi}")
+    return value
+
+
 class ShardedRows:
     """Row partition of a (V, E) table over the ranks of `group` for the sharded table optimizer.
 
@@ -106,7 +153,8 @@ class ShardedRows:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.V, self.E = weight.shape
-        self.NC = chunks or shard_chunks(self.V, self.world)
+        self.NC = _agree(chunks or shard_chunks(self.V, self.world), group, weight.device,
+                         "row chunks of the sharded table (TT_SHARD_CHUNKS)")
         self.R = -(-self.V // (self.NC * self.world))
         self.Cr = self.R * self.world
         self.Vp = self.NC * self.Cr

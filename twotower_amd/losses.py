@@ -90,6 +90,12 @@ def in_batch_sampled_softmax_loss(q_emb: torch.Tensor, d_emb: torch.Tensor, *arg
             d_emb = _candidates(d_emb, args[0])
         else:
             temperature = args[0]
+    if not cross_device_negatives and (not args or not isinstance(args[0], torch.Tensor)):
+        base = _packed(q_emb, d_emb)
+        if base is not None:  # (query, positive) pairs as [q; d] in one tensor (TwoTower(q, d)): the
+            # same packed path, so the head's operand prep and fused L2 backward apply to M = B too
+            return ops.InBatchSoftmaxLossPacked.apply(base, q_emb.shape[0], 1.0 / float(temperature),
+                                                      compute_dtype, None)
     label_off = 0
     if cross_device_negatives:
         from . import distributed

@@ -18,7 +18,7 @@ import os
 import torch
 
 from . import ops
-from .distributed import GradSync, is_active
+from .distributed import GradSync, capture_blocker, is_active
 from .losses import scorer_prep_dtype
 
 
@@ -44,6 +44,10 @@ class TrainStep:
         dt = scorer_prep_dtype(loss_fn)
         self._scorer_prep = (dt if dt is not None and hasattr(model, "scorer_prep") and not is_active(group)
                              and os.environ.get("TT_SCORER_PREP", "1") != "0" else None)
+        # The in-batch loss may leave its mean to the backward's combine launch only when the
+        # tensor loss_fn returns IS that loss (the bare registry partial): a wrapper (a scaled or
+        # summed loss, a .item() log inside loss_fn) reads the value before the backward forms it.
+        self._defer_mean = dt is not None
         self.graph = graph
         if graph and not all(g.get("capturable", False) for g in optimizer.param_groups):
             raise ValueError("TrainStep(graph=True) needs an optimizer built with capturable=True")
@@ -62,7 +66,8 @@ class TrainStep:
             side.join()
             side.active = True
         try:
-            with ops.deferred_loss_mean(), self._scorer_prep_open():  # the loss is read after the backward below
+            defer = ops.deferred_loss_mean() if self._defer_mean else contextlib.nullcontext()
+            with defer, self._scorer_prep_open():  # the loss is read after the backward below
                 ins = (queries, positive_docs) if negative_docs is None else (queries, positive_docs, negative_docs)
                 loss = self.loss_fn(*self.model(*ins))
             self.optimizer.zero_grad(set_to_none=True)
@@ -111,14 +116,30 @@ class TrainStep:
             if self._eager_left > 0:
                 self._eager_left -= 1
                 return self.eager(*inputs)
-            try:
-                hit = self._graphs[key] = self._capture(inputs)
-            except RuntimeError as e:  # e.g. a collective this backend cannot capture: stay eager
+            why = capture_blocker(self.group) if is_active(self.group) else None
+            err = None
+            if why is None:
+                try:
+                    hit = self._capture(inputs)
+                except RuntimeError as e:  # e.g. a collective this backend cannot capture
+                    if not _is_capture_error(e):
+                        raise  # a real error of the step itself: not hidden behind a fallback
+                    err = e
+            # every rank replays, or none does: a rank whose capture failed steps eagerly, and its
+            # collectives must not meet graph-replayed ones on the other ranks
+            ok = why is None and err is None
+            if is_active(self.group):
+                ok = _all_ranks(ok, self.group, inputs[0].device)
+            if not ok:
                 import warnings
 
-                warnings.warn(f"TrainStep: HIP graph capture failed ({e}); running the step eagerly")
+                self._discard_partial_step()
+                reason = why or (f"HIP graph capture failed ({err})" if err is not None
+                                 else "another rank's HIP graph capture failed")
+                warnings.warn(f"TrainStep: {reason}; running the step eagerly")
                 self.graph = False
                 return self.eager(*inputs)
+            self._graphs[key] = hit
         graph, static_all, static_loss = hit
         if all(t.shape[1:] == inputs[0].shape[1:] and t.dtype == inputs[0].dtype for t in inputs):
             if (all(t.device == static_all.device and t.is_contiguous() for t in inputs) and len(inputs) <= 8
@@ -132,6 +153,19 @@ class TrainStep:
         graph.replay()
         return static_loss
 
+    def _discard_partial_step(self) -> None:
+        """Forget what a failed capture queued for the optimizer: the factored table gradients the
+        bag backward handed over and the side-stream gradient events (none of that ran)."""
+        for g in self.optimizer.param_groups:
+            for p in g["params"]:
+                deferred = getattr(p, "_tt_deferred", None)
+                if deferred is not None:
+                    deferred.parts.clear()
+        side = getattr(self.optimizer, "_side_grads", None)
+        if side is not None:
+            side.reset()
+        self.optimizer.zero_grad(set_to_none=True)
+
     def _capture(self, inputs):
         # the static inputs are consecutive row blocks of one buffer, so the fused TwoTower
         # forward uses them in place (no concatenation inside the step)
@@ -144,6 +178,23 @@ class TrainStep:
         with torch.cuda.graph(graph):
             static_loss = self.eager(*static_in)
         return graph, static_all, static_loss
+
+
+def _is_capture_error(e: BaseException) -> bool:
+    """An error raised because the step was being captured (a call HIP or a backend refuses inside
+    stream capture), as opposed to an error of the step itself."""
+    msg = str(e).lower()
+    return any(k in msg for k in ("captur", "graph", "not permitted"))
+
+
+def _all_ranks(flag: bool, group, device) -> bool:
+    """True iff `flag` holds on every rank of `group` (MIN all-reduce, outside any capture)."""
+    import torch.distributed as dist
+
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                     device=device if dist.get_backend(group) != "gloo" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
 
 
 def _packed_like(inputs):
