@@ -295,9 +295,9 @@ int tt_inbatch_bwd_mean(const float* q, const float* d, int64_t B, int64_t M, in
  *   grad_loss[0] * grad_scale * inv_tau (every rank's loss seeded alike); dq = scale * dq_unscaled.
  * ws: tt_inbatch_ex_ws_size(B, M_all, nQ_all, M) bytes serve both passes (partials only). */
 /* tt_inbatch_l2_prep: F.normalize (encoders.py:77) of the B + M rows of y = [q; d] in place, as
- *   tt_head_gemm epi 1 does it (norms[r] = |row|; y the epi 4 output, H = 256), fused with the
- *   operand prep of tt_inbatch_fwd on the normalised rows, which it leaves in ws (dtype TT_BF16 or
- *   TT_BF16_SPLIT; ws sized by tt_inbatch_ws_size(B, M, H, dtype)).
+ *   tt_head_gemm epi 1 does it (norms[r] = |row|; y the epi 4 output), fused with the operand prep
+ *   of tt_inbatch_fwd on the normalised rows, which it leaves in ws (H = 256 with dtype TT_BF16 or
+ *   TT_BF16_SPLIT, H = 128 with TT_F32; ws sized by tt_inbatch_ws_size(B, M, H, dtype)).
  * tt_inbatch_fwd_prepped: tt_inbatch_fwd on q = y[:B], d = y[B:] with that workspace, without its
  *   prep pass (bit-identical results). */
 int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dtype, float* norms, void* ws, size_t ws_bytes,
@@ -307,10 +307,11 @@ int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B, int64_t M,
                            float* lse, float* loss_rows, float* loss, float* dq_unscaled,
                            void* ws, size_t ws_bytes, tt_stream_t stream);
 /* tt_inbatch_bwd fused with the tower head's F.normalize backward (encoders.py:77), for the fused
- *   TwoTower output qd = [q; d] ((B + M) x 256 fp32, the rows tt_inbatch_l2_prep normalised,
- *   norms[r] = their norms before it, bf16 / bf16_split operands in ws from the forward): dx
- *   ((B + M) x 256) = the gradient w.r.t. the rows before F.normalize, i.e. tt_inbatch_bwd's dq, dd
- *   followed by tt_l2norm_bwd, bit for bit, without writing dq and dd. */
+ *   TwoTower output qd = [q; d] ((B + M) x H fp32, the rows tt_inbatch_l2_prep normalised,
+ *   norms[r] = their norms before it; H = 256 with bf16 / bf16_split operands in ws from the
+ *   forward, or H = 128 with fp32 operands): dx ((B + M) x H) = the gradient w.r.t. the rows
+ *   before F.normalize, i.e. tt_inbatch_bwd's dq, dd followed by tt_l2norm_bwd, bit for bit,
+ *   without writing dq and dd. */
 int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau, int64_t label_off,
                       const float* lse, const float* dq_unscaled, const float* grad_loss, float grad_scale,
                       const float* norms, float* dx, void* ws, size_t ws_bytes, tt_stream_t stream);

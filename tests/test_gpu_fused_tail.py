@@ -75,8 +75,8 @@ def test_adamw_multi_ex_prepare_only():
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("graph,prepare", [(False, "0"), (True, "0"), (True, "1")])
-def test_trainstep_fused_tail_equals_three_launches(graph, prepare, monkeypatch):
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainstep_fused_tail_equals_three_launches(graph, monkeypatch):
     V, E, B, L = 4000, 256, 128, 16
 
     def run():
@@ -93,7 +93,6 @@ def test_trainstep_fused_tail_equals_three_launches(graph, prepare, monkeypatch)
                 [opt.state[p]["step"].item() for p in model.parameters()])
 
     monkeypatch.setenv("TT_FUSED_TAIL", "1")
-    monkeypatch.setenv("TT_FUSED_PREPARE", prepare)
     got = run()
     monkeypatch.setenv("TT_FUSED_TAIL", "0")
     want = run()

@@ -187,19 +187,24 @@ def test_bag_scaling_in_head_dx_epilogue_is_bit_identical(fused_tables, tied, mo
 
 
 @pytest.mark.parametrize("graph", [False, True])
-@pytest.mark.parametrize("dtype,bwd", [("bf16", "stored"), ("bf16", "recompute"), ("bf16_split", "stored")])
-def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dtype, bwd, monkeypatch):
-    """TrainStep runs the bf16 in-batch loss's backward combine fused with the tower head's
-    F.normalize backward (tt_inbatch_bwd_l2: dq, dd never written); parameters and losses after
-    four steps equal the unfused combine + tt_l2norm_bwd (TT_FUSED_L2_BWD=0) bit for bit."""
+@pytest.mark.parametrize("dtype,bwd,d,n_in", [("bf16", "stored", 256, 3), ("bf16", "recompute", 256, 3),
+                                              ("bf16_split", "stored", 256, 3), ("bf16", "stored", 256, 2),
+                                              ("fp32", "stored", 128, 3), ("fp32", "recompute", 128, 3),
+                                              ("fp32", "stored", 128, 2)])
+def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dtype, bwd, d, n_in, monkeypatch):
+    """TrainStep runs the in-batch loss's backward combine fused with the tower head's
+    F.normalize backward (tt_inbatch_bwd_l2: dq, dd never written; bf16 at H = 256, fp32 at H =
+    128), for the triplet form (q, p, n: M = 2B) and the pairs form (q, p: M = B); parameters and
+    losses after four steps equal the unfused combine + tt_l2norm_bwd (TT_FUSED_L2_BWD=0) bit for
+    bit."""
     V, B, L = 4000, 320, 20
     rng = np.random.default_rng(9)
-    batches = [[_ids(B, L, V, rng) for _ in range(3)] for _ in range(4)]
+    batches = [[_ids(B, L, V, rng) for _ in range(n_in)] for _ in range(4)]
 
     def run():
         torch.manual_seed(4)
-        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=256)
-        model = tt.build_two_tower("mean", emb, hidden_dim=256, tied_weights=True).to(DEV)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=d)
+        model = tt.build_two_tower("mean", emb, hidden_dim=d, tied_weights=True).to(DEV)
         opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
         step = tt.TrainStep(model, tt.losses.build("in_batch", temperature=0.05, compute_dtype=dtype), opt,
                             graph=graph, eager_steps=1)

@@ -258,6 +258,26 @@ def test_multiple_negatives_vs_oracle(H, N):
     assert rel(Q.grad, rdq) < 1e-5 and rel(P.grad, rdp) < 1e-5 and rel(Nn.grad, rdn) < 1e-5
 
 
+def test_multiple_negatives_packed_equals_separate():
+    """[q; p; negatives] as consecutive row blocks of one tensor (TwoTower's fused output) take
+    MultiNegLossPacked, which writes the three gradients into one tensor: the same loss and the
+    same gradients, bit for bit, as three separate tensors."""
+    rng = np.random.default_rng(11)
+    B, K, H = 300, 4, 256
+    x = cuda(rng.standard_normal(((2 + K) * B, H)).astype(np.float32))
+    base = x.clone().requires_grad_(True)
+    q, p, n = torch.split(base, [B, B, K * B])
+    loss = tt.losses.multiple_negatives_loss(q, p, n.view(B, K, H), temperature=0.1)
+    assert loss.grad_fn.name().startswith("MultiNegLossPacked")
+    loss.backward()
+    Q, P, N = (t.detach().clone().requires_grad_(True) for t in torch.split(x, [B, B, K * B]))
+    ref = tt.losses.multiple_negatives_loss(Q, P, N.view(B, K, H), temperature=0.1)
+    assert not ref.grad_fn.name().startswith("MultiNegLossPacked")
+    ref.backward()
+    assert torch.equal(loss, ref)
+    assert torch.equal(base.grad, torch.cat([Q.grad, P.grad, N.grad]))
+
+
 # ---------------------------------------------------------------------------------------------
 # in-batch scorer
 def test_in_batch_golden(golden):

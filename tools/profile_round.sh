@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 # otherwise land in the trace and be charged to the step
 # --timing-steps 0: no stamped replay or eager timing pass after the timed steps (they would add
 # a second capture's kernels and the stamp kernels to the trace)
-ARGS="${*:---steps 10 --warmup 3 --no-cpu-baseline} --no-helpers --timing-steps 0"
+ARGS="${*:---steps 10 --warmup 3 --no-cpu-baseline} --no-helpers --timing-steps 0 --no-extras"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace" -o run -- \
   python3 bench.py $ARGS > "$OUT/ktrace.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \

@@ -60,22 +60,59 @@ def op_of(name: str) -> str:
     return "other (torch/runtime)"
 
 
+MARKER = "stamp_kernel"  # bench.py brackets its timed steps with two tt_stamp launches (window_marker)
+
+
+def _window(rows, key):
+    """(lo, hi) of `key` between the first two marker dispatches (bench.py's timed region comes before
+    any stamped per-op timing), or None without markers."""
+    marks = sorted(key(r) for r in rows if MARKER in r["Kernel_Name"])
+    return (marks[0], marks[1]) if len(marks) >= 2 else None
+
+
+def trace_stats(path: str):
+    """Per-kernel (calls, total ns) from the kernel trace, restricted to the timed steps when bench
+    left its window markers; None if the trace has no markers (then the --stats summary is used)."""
+    files = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        return None
+    with open(files[0]) as fh:
+        rows = list(csv.DictReader(fh))
+    win = _window(rows, lambda r: int(r["Start_Timestamp"]))
+    if win is None:
+        return None
+    out = defaultdict(lambda: [0, 0])
+    for r in rows:
+        t = int(r["Start_Timestamp"])
+        if win[0] < t < win[1] and MARKER not in r["Kernel_Name"]:
+            out[r["Kernel_Name"]][0] += 1
+            out[r["Kernel_Name"]][1] += int(r["End_Timestamp"]) - t
+    return out
+
+
 def pmc(path: str, counter: str):
     rows = []
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for r in csv.DictReader(fh):
-                if r.get("Counter_Name") == counter:
-                    rows.append((r["Kernel_Name"], float(r["Counter_Value"])))
-    return rows
+            rows += [r for r in csv.DictReader(fh) if r.get("Counter_Name") == counter]
+    win = _window(rows, lambda r: int(r["Dispatch_Id"]))
+    if win is not None:  # the dispatches of the timed steps only
+        rows = [r for r in rows if win[0] < int(r["Dispatch_Id"]) < win[1] and MARKER not in r["Kernel_Name"]]
+    return [(r["Kernel_Name"], float(r["Counter_Value"])) for r in rows]
 
 
 def main(outdir: str, tag: str):
     os.makedirs("profiles", exist_ok=True)
     stats = glob.glob(os.path.join(outdir, "ktrace", "**", "*kernel_stats.csv"), recursive=True)[0]
     shutil.copy(stats, f"profiles/{tag}_kernel_stats.csv")
-    with open(stats) as fh:
-        ks = list(csv.DictReader(fh))
+    ts = trace_stats(os.path.join(outdir, "ktrace"))
+    if ts is not None:  # the timed steps alone: bench set-up and the warmup steps left out
+        ks = [{"Name": n, "Calls": c, "TotalDurationNs": t, "AverageNs": t / c} for n, (c, t) in ts.items()]
+        scope = "the timed steps only (between bench.py's two window markers; set-up and warmup excluded)"
+    else:
+        with open(stats) as fh:
+            ks = list(csv.DictReader(fh))
+        scope = "the whole run (incl. warmup and set-up; no window markers in the trace)"
     # steps profiled = calls of the bag forward kernel (one launch per step)
     steps = max(int(r["Calls"]) for r in ks if "bag_fwd" in r["Name"])
     fetch = defaultdict(list)
@@ -85,8 +122,8 @@ def main(outdir: str, tag: str):
     for n, v in pmc(os.path.join(outdir, "write"), "WRITE_SIZE"):
         write[n].append(v * 1024)
     lines = [f"# Profile {tag}", "", "Source: `tools/profile_round.sh` (rocprofv3 --kernel-trace --stats; separate "
-             "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes) over `bench.py` at its default workload.", "",
-             f"Steps covered by the trace (incl. warmup): {steps}", "",
+             "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes) over `bench.py`.", "",
+             f"Steps covered: {steps}, {scope}", "",
              "| kernel | op | calls/step | avg us | us/step | fetch MB/launch | write MB/launch |",
              "|---|---|---|---|---|---|---|"]
     per_op = defaultdict(lambda: {"us_per_step": 0.0, "fetch": 0.0, "write": 0.0})
@@ -109,8 +146,8 @@ def main(outdir: str, tag: str):
     open(f"profiles/{tag}_summary.md", "w").write("\n".join(lines) + "\n")
     traffic = {op: {"hbm_bytes_per_call": d["fetch"] + d["write"], "fetch_bytes": d["fetch"], "write_bytes": d["write"],
                     "device_us_per_step": d["us_per_step"]} for op, d in per_op.items()}
-    json.dump({"tag": tag, "note": "PMC FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->bytes; "
-               "per step = per call for ops launched once per step", "ops": traffic},
+    json.dump({"tag": tag, "scope": scope, "note": "PMC FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, "
+               "KiB->bytes; per step = per call for ops launched once per step", "ops": traffic},
               open(f"profiles/{tag}_pmc_traffic.json", "w"), indent=1)
     print("\n".join(lines))
 

@@ -16,7 +16,6 @@
 #include <cstdlib>
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
 
 #include "common.hpp"
 
@@ -159,23 +158,10 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_generic_kernel(
 // ---------------------------------------------------------------------------------------
 // Backward, sorted (deterministic) path, in two halves:
 //   plan  (ids only, may run as soon as the ids exist, e.g. beside the forward):
-//         keys = row id (V for masked tokens), vals = seq -> stable radix sort -> segment bounds;
+//         keys = row id (V for masked tokens), vals = seq -> stable LSD counting sort -> segment
+//         bounds;
 //   apply (needs d_pooled): gs[s] = dpooled[s] / denom[s] (the division autograd applies,
 //         encoders.py:72), then the per-row reduce (optionally fused with AdamW).
-template <typename IdT>
-__global__ __launch_bounds__(kBlock) void bag_plan_keys_kernel(
-    const IdT* __restrict__ ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx,
-    uint32_t* __restrict__ keys, int32_t* __restrict__ vals, int32_t* __restrict__ n_pieces) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i == 0) *n_pieces = 0;  // the piece counter bag_plan_bounds_kernel allocates from
-  if (i >= nseq * L) return;
-  const int64_t seq = i / L, t = i - seq * L;
-  const int64_t id = (int64_t)ids[seq * ld + t];
-  const bool valid = id > 0 && id < V && id != padding_idx;
-  keys[i] = valid ? (uint32_t)id : (uint32_t)V;
-  vals[i] = (int32_t)seq;
-}
-
 __global__ __launch_bounds__(kBlock) void bag_scale_rows_kernel(const float* __restrict__ dpooled,
                                                                 const float* __restrict__ denom, int64_t nseq,
                                                                 int E, float* __restrict__ gs) {
@@ -226,10 +212,7 @@ constexpr int kSortWaves = kSortThreads / kWave;
 constexpr int kSortIPT = 4;  // entries per thread per tile
 constexpr int kSortTile = kSortThreads * kSortIPT;
 constexpr int kSortMaxD = 11;
-#ifndef TT_PLAN_DEFAULT_D
-#define TT_PLAN_DEFAULT_D 9
-#endif
-constexpr int kSortDefaultD = TT_PLAN_DEFAULT_D;
+constexpr int kSortDefaultD = 9;
 
 template <typename IdT>
 struct SortSrc {  // pass 0: ids (keys == nullptr); later passes: the previous pass's output
@@ -303,21 +286,41 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
   for (int d = threadIdx.x; d < nd; d += kSortThreads) cnt[(int64_t)d * ntiles + blockIdx.x] = h[d];
 }
 
-// One workgroup per digit: cnt[d][0..ntiles) -> its exclusive scan, total[d] = the row sum.
-__global__ __launch_bounds__(kSortThreads) void plan_sort_scan_kernel(int32_t* __restrict__ cnt, int64_t ntiles,
-                                                                      int32_t* __restrict__ total) {
-  __shared__ int32_t wsum[kSortWaves];
-  int32_t* row = cnt + (int64_t)blockIdx.x * ntiles;
+// One WAVE per digit: cnt[d][0..ntiles) -> its exclusive scan, total[d] = the row sum.  Every
+// chunk of 64 tiles is loaded before the first scan step (up to kScanChunks loads in flight per
+// lane), then scanned with a carry.  Round 3 ran one 512-thread workgroup per digit (512 of them
+// at D = 9): 4.8 us alone but 42 us beside the gather, whose CUs those workgroups had to share;
+// 8-wave workgroups of 8 digits leave 1/8 of the workgroups to dispatch.
+constexpr int kScanWaves = 8;
+constexpr int kScanChunks = 16;  // chunks of 64 tiles held per lane: 1,024 tiles per round
+__global__ __launch_bounds__(kScanWaves * kWave) void plan_sort_scan_kernel(int32_t* __restrict__ cnt, int64_t ntiles,
+                                                                            int nd, int32_t* __restrict__ total) {
+  const int d = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
+  if (d >= nd) return;
+  const int lane = lane_id();
+  int32_t* row = cnt + (int64_t)d * ntiles;
   int32_t carry = 0;
-  for (int64_t t0 = 0; t0 < ntiles; t0 += kSortThreads) {
-    const int64_t t = t0 + threadIdx.x;
-    const int32_t x = t < ntiles ? row[t] : 0;
-    int32_t sum;
-    const int32_t ex = sort_block_excl_scan(x, wsum, &sum);
-    if (t < ntiles) row[t] = carry + ex;
-    carry += sum;
+  for (int64_t t0 = 0; t0 < ntiles; t0 += kScanChunks * kWave) {
+    int32_t x[kScanChunks];
+#pragma unroll
+    for (int c = 0; c < kScanChunks; ++c) {
+      const int64_t t = t0 + c * kWave + lane;
+      x[c] = t < ntiles ? row[t] : 0;
+    }
+#pragma unroll
+    for (int c = 0; c < kScanChunks; ++c) {
+      int32_t inc = x[c];
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int32_t y = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += y;
+      }
+      const int64_t t = t0 + c * kWave + lane;
+      if (t < ntiles) row[t] = carry + inc - x[c];
+      carry += __shfl(inc, kWave - 1, kWave);
+    }
   }
-  if (threadIdx.x == 0) total[blockIdx.x] = carry;
+  if (lane == 0) total[d] = carry;
 }
 
 template <typename IdT, int D>
@@ -425,18 +428,27 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
   }
 }
 
-// seg_start from the sorted keys, one thread per boundary i in [0, n]: every row r with
-// key[i - 1] < r <= key[i] starts at i (the first sorted position with key >= r).  The rows are
-// written once each; thread 0 also resets the piece counter bag_plan_pieces_kernel allocates from.
+// seg_start from the sorted keys, kStartsPT consecutive boundaries i in [0, n] per thread: every
+// row r with key[i - 1] < r <= key[i] starts at i (the first sorted position with key >= r).  The
+// rows are written once each; thread 0 also resets the piece counter bag_plan_pieces_kernel
+// allocates from.  (Round 3: one thread per boundary, 6,144 workgroups at C3, 4.8 us alone but
+// 25 us beside the gather; four per thread dispatch a quarter of the workgroups.)
+constexpr int kStartsPT = 4;
 __global__ __launch_bounds__(kBlock) void bag_plan_starts_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                                  int64_t V, int32_t* __restrict__ seg_start,
                                                                  int32_t* __restrict__ n_pieces) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i == 0) *n_pieces = 0;
-  if (i > n) return;
-  const int64_t lo = i > 0 ? (int64_t)keys[i - 1] + 1 : 0;
-  const int64_t hi = i < n ? (int64_t)keys[i] : V;
-  for (int64_t r = lo; r <= hi; ++r) seg_start[r] = (int32_t)i;
+  const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kStartsPT;
+  if (i0 == 0) *n_pieces = 0;
+  if (i0 > n) return;
+  int64_t prev = i0 > 0 ? (int64_t)keys[i0 - 1] : -1;
+#pragma unroll
+  for (int j = 0; j < kStartsPT; ++j) {
+    const int64_t i = i0 + j;
+    if (i > n) break;
+    const int64_t hi = i < n ? (int64_t)keys[i] : V;
+    for (int64_t r = prev + 1; r <= hi; ++r) seg_start[r] = (int32_t)i;
+    prev = hi;
+  }
 }
 
 // Row r's pieces ([st, en) its sorted range): nch[r] = their number (0 = short row); a long row
@@ -455,42 +467,6 @@ __device__ __forceinline__ void plan_row_pieces(int64_t r, int32_t st, int32_t e
   }
 }
 
-// Segment bounds and pieces of every row from the sorted keys, one thread per row r <= V:
-// seg_start[r] = the first sorted position with key >= r (lower bound), so row r's tokens are
-// [seg_start[r], seg_start[r + 1]) (seg_end aliases seg_start + 1; r = V: the masked tail).  A
-// long row takes its nch pieces' slots from one counter (n_pieces = piece_off[V], zeroed by the
-// keys kernel): the slot order across rows varies per run, a row's own pieces stay consecutive
-// and in token order, so every sum is deterministic.  One kernel instead of two memsets, a mark
-// pass, a piece count, a scan and a piece list.
-__global__ __launch_bounds__(kBlock) void bag_plan_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n,
-                                                                 int64_t V, int32_t* __restrict__ seg_start,
-                                                                 int32_t* __restrict__ nch,
-                                                                 int32_t* __restrict__ piece_off,
-                                                                 int32_t* __restrict__ piece_beg,
-                                                                 int32_t* __restrict__ piece_end) {
-  __shared__ int32_t lb[kBlock];
-  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  auto lower_bound = [&](int64_t key, int64_t lo) {
-    int64_t hi = n;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)keys[mid] < key) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
-  };
-  const int64_t st = r <= V ? lower_bound(r, 0) : n;
-  lb[threadIdx.x] = (int32_t)st;
-  __syncthreads();
-  if (r > V) return;
-  seg_start[r] = (int32_t)st;
-  if (r == V) {
-    nch[V] = 0;
-    return;
-  }
-  const int64_t en = threadIdx.x + 1 < kBlock ? (int64_t)lb[threadIdx.x + 1] : lower_bound(r + 1, st);
-  plan_row_pieces(r, (int32_t)st, (int32_t)en, V, nch, piece_off, piece_beg, piece_end);
-}
 
 // The pieces of every row r < V from seg_start (bag_plan_starts_kernel); nch[V] = 0.
 __global__ __launch_bounds__(kBlock) void bag_plan_pieces_kernel(const int32_t* __restrict__ seg_start, int64_t V,
@@ -817,25 +793,6 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_atomic_kernel(
 
 // ---------------------------------------------------------------------------------------
 // Host side
-// Onesweep configuration of the plan's radix sort (uint32 row keys, int32 sequence values): 9-bit
-// digits (two passes for V <= 256k) on 512 x 16-item blocks measured 27 % faster than the tuned
-// gfx950 default (1024 x 16, 8-bit) on the C3 plan, uniform and Zipf ids (tools/sweep_plan.sh).
-#ifndef TT_PLAN_BLOCK
-#define TT_PLAN_BLOCK 512
-#endif
-#ifndef TT_PLAN_ITEMS
-#define TT_PLAN_ITEMS 16
-#endif
-#ifndef TT_PLAN_BITS
-#define TT_PLAN_BITS 9
-#endif
-using PlanSortConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<TT_PLAN_BLOCK, TT_PLAN_ITEMS>,
-                                        rocprim::kernel_config<TT_PLAN_BLOCK, TT_PLAN_ITEMS>, TT_PLAN_BITS,
-                                        rocprim::block_radix_rank_algorithm::match>,
-    0>;  // onesweep at every size (no merge-sort fallback)
-
 int end_bit_for(int64_t V) {
   int b = 1;
   while ((int64_t(1) << b) <= V) ++b;  // keys in [0, V] (V = masked sentinel)
@@ -848,7 +805,7 @@ struct BwdWs {
   int32_t* vals_in;
   int32_t* vals_out;
   float* gs;
-  int32_t* seg_start;  // V + 1 (bag_plan_bounds_kernel)
+  int32_t* seg_start;  // V + 1 (bag_plan_starts_kernel)
   int32_t* seg_end;    // = seg_start + 1
   void* sort_tmp;
   size_t sort_bytes;
@@ -903,56 +860,22 @@ BwdWs carve(void* base, int64_t nseq, int L, int64_t V, int E, size_t sort_bytes
 }
 
 
-// The hand-written sort's shape: P passes of D bits over ntiles tiles; its workspace holds the
-// digit-major tile counts and the digit totals.  TT_PLAN_SORT=rocprim selects the rocPRIM onesweep
-// sort instead (same output: the stable sort is unique), for A/B runs and the equality test.
+// The sort's shape: P passes of D bits over ntiles tiles; its workspace holds the digit-major
+// tile counts and the digit totals.  The widest digit is kSortDefaultD: wider digits mean fewer
+// passes but a digits x tiles count matrix that grows as 2^D (its transposed 4-byte accesses, not
+// the entries' bytes, bound a pass; sweep in profiles/r03o_plan_digit_sweep.txt).
 struct SortShape {
   int P, D;
   int64_t ntiles;
 };
-// Widest digit (TT_PLAN_MAXD, 1..11): wider digits mean fewer passes but a digits x tiles count
-// matrix that grows as 2^D (its transposed 4-byte accesses, not the entries' bytes, bound a pass)
-int sort_max_digit() {
-  static const int d = [] {
-    const char* e = std::getenv("TT_PLAN_MAXD");
-    const int v = e ? std::atoi(e) : kSortDefaultD;
-    return v < 1 ? 1 : (v > kSortMaxD ? kSortMaxD : v);
-  }();
-  return d;
-}
 SortShape sort_shape(int64_t n, int64_t V) {
-  const int bits = end_bit_for(V), maxd = sort_max_digit();
+  const int bits = end_bit_for(V), maxd = kSortDefaultD;
   const int P = (bits + maxd - 1) / maxd;
   return SortShape{P, (bits + P - 1) / P, (n + kSortTile - 1) / kSortTile};
 }
-size_t own_sort_bytes(int64_t n, int64_t V) {  // TT_PLAN_MAXD is read once per process: sizes agree
+size_t sort_tmp_bytes(int64_t n, int64_t V) {
   const SortShape sh = sort_shape(n, V);
   return align_up(((size_t)sh.ntiles + 1) * ((size_t)1 << sh.D) * 4, 256);
-}
-bool use_rocprim_sort() {
-  static const bool r = [] {
-    const char* e = std::getenv("TT_PLAN_SORT");
-    return e && std::strcmp(e, "rocprim") == 0;
-  }();
-  return r;
-}
-
-size_t rocprim_sort_bytes(int64_t n, int64_t V) {
-  size_t bytes = 0;
-  hipError_t e = rocprim::radix_sort_pairs<PlanSortConfig>(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0,
-                                           end_bit_for(V), (hipStream_t)0, false);
-  if (e != hipSuccess) {
-    set_error("rocprim::radix_sort_pairs size query: %s", hipGetErrorString(e));
-    return 0;
-  }
-  return bytes;
-}
-
-// both sorts fit (the layout does not depend on TT_PLAN_SORT)
-size_t sort_tmp_bytes(int64_t n, int64_t V) {
-  const size_t a = rocprim_sort_bytes(n, V), b = own_sort_bytes(n, V);
-  return a > b ? a : b;
 }
 
 // planes != nullptr: the split workgroups of tt_bag_mean_fwd_split first (E in the templated set)
@@ -986,15 +909,9 @@ int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nse
 }
 
 // E in {256, 512, 1024}: the XCD-sliced reduce with non-temporal table/moment traffic (C3:
-// 261 us against 300 us for the whole-row kernel, tools/mb_bag_bwd.py).  TT_BAG_REDUCE=rows
-// selects the whole-row kernel (same sums in the same order) for comparison.
-bool use_sliced_reduce(int E) {
-  static const bool rows = [] {
-    const char* e = std::getenv("TT_BAG_REDUCE");
-    return e && std::strcmp(e, "rows") == 0;
-  }();
-  return !rows && (E == 256 || E == 512 || E == 1024);
-}
+// 261 us against 300 us for the whole-row kernel, tools/mb_bag_bwd.py; same sums in the same
+// order); the whole-row kernels for other widths.
+bool use_sliced_reduce(int E) { return E == 256 || E == 512 || E == 1024; }
 
 // Rows [row_lo, V) of the table (row_lo > 0: a row range of the dense gradient; `grad` then
 // points at row 0's position, so row r lands at grad + r * E).
@@ -1053,8 +970,8 @@ int launch_piece_sum(const BwdWs& w, int64_t V, int E, hipStream_t s) {
   return TT_OK;
 }
 
-// plan: keys/vals -> stable radix sort (key = row id, value = seq) -> segment bounds and the
-// pieces of long rows (bag_plan_bounds_kernel).
+// plan: keys/vals -> stable counting sort (key = row id, value = seq) -> segment starts and the
+// pieces of long rows (bag_plan_starts_kernel, bag_plan_pieces_kernel).
 template <typename IdT>
 int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, const BwdWs& w,
                hipStream_t s) {
@@ -1064,19 +981,6 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)(V + 1) * 4, s), "memset seg_start");
     TT_HIP(hipMemsetAsync(w.nch, 0, (size_t)(V + 1) * 4, s), "memset nch");
     TT_HIP(hipMemsetAsync(w.piece_off, 0, (size_t)(V + 1) * 4, s), "memset piece_off");
-    return TT_OK;
-  }
-  if (use_rocprim_sort()) {
-    bag_plan_keys_kernel<IdT><<<dim3((unsigned)((n + kBlock - 1) / kBlock)), block, 0, s>>>(
-        ids, nseq, L, ld, V, padding_idx, w.keys_in, w.vals_in, w.piece_off + V);
-    TT_LAUNCH_CHECK("bag_plan_keys");
-    size_t tmp = w.sort_bytes;
-    TT_HIP(rocprim::radix_sort_pairs<PlanSortConfig>(w.sort_tmp, tmp, w.keys_in, w.keys_out, w.vals_in, w.vals_out,
-                                     (size_t)n, 0, end_bit_for(V), s, false),
-           "rocprim::radix_sort_pairs");
-    bag_plan_bounds_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
-        w.keys_out, n, V, w.seg_start, w.nch, w.piece_off, w.piece_beg, w.piece_end);
-    TT_LAUNCH_CHECK("bag_plan_bounds");
     return TT_OK;
   }
   // hand-written LSD counting sort: pass p writes (keys_out, vals_out) when P - 1 - p is even,
@@ -1094,7 +998,8 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     plan_sort_count_kernel<IdT><<<dim3((unsigned)sh.ntiles), dim3(kSortThreads), 0, s>>>(src, n, shift, sh.D,
                                                                                        sh.ntiles, cnt);
     TT_LAUNCH_CHECK("plan_sort_count");
-    plan_sort_scan_kernel<<<dim3((unsigned)nd), dim3(kSortThreads), 0, s>>>(cnt, sh.ntiles, total);
+    plan_sort_scan_kernel<<<dim3((unsigned)((nd + kScanWaves - 1) / kScanWaves)), dim3(kScanWaves * kWave), 0, s>>>(
+        cnt, sh.ntiles, nd, total);
     TT_LAUNCH_CHECK("plan_sort_scan");
     switch (sh.D) {
 #define TT_SC(DD)                                                                                         \
@@ -1111,9 +1016,9 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     src.keys = ko;
     src.vals = vo;
   }
-  bag_plan_starts_kernel<<<dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(w.keys_out, n, V,
-                                                                                           w.seg_start,
-                                                                                           w.piece_off + V);
+  const int64_t nst = (n + 1 + kStartsPT - 1) / kStartsPT;
+  bag_plan_starts_kernel<<<dim3((unsigned)((nst + kBlock - 1) / kBlock)), block, 0, s>>>(w.keys_out, n, V, w.seg_start,
+                                                                                       w.piece_off + V);
   TT_LAUNCH_CHECK("bag_plan_starts");
   bag_plan_pieces_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
       w.seg_start, V, w.nch, w.piece_off, w.piece_beg, w.piece_end);

@@ -48,6 +48,17 @@ __device__ __forceinline__ f32x4 l2_bwd_row4(const f32x4& g, const f32x4& o, flo
   return y;
 }
 
+// The same for an H = 128 row held as elements (lane, lane + 64) of each lane (g0, g1 / o0, o1):
+// l2norm_bwd_kernel at H = 128 and the fp32 in-batch combine that fuses it (bwd_combine_l2_128_kernel)
+// both take it, so they agree bit for bit.
+__device__ __forceinline__ void l2_bwd_row2(float g0, float g1, float o0, float o1, float nrm, float& y0, float& y1) {
+  const float den = fmaxf(nrm, 1e-12f);
+  const float sx = wave_sum(__builtin_fmaf(g1, o1, g0 * o0)) * den;
+  const float coef = (nrm >= 1e-12f && nrm > 0.f) ? sx / ((den * den) * nrm) : 0.f;
+  y0 = __builtin_fmaf(-coef, o0 * den, g0 / den);
+  y1 = __builtin_fmaf(-coef, o1 * den, g1 / den);
+}
+
 template <typename IdT>
 __device__ __forceinline__ int64_t load_id(const IdT* p) { return (int64_t)(*p); }
 

@@ -45,6 +45,15 @@ __global__ __launch_bounds__(kBlock) void l2norm_bwd_kernel(const float* __restr
     reinterpret_cast<f32x4*>(dx + r * H)[lane] = l2_bwd_row4(g, o, nrm);
     return;
   }
+  if (H == 2 * kWave) {  // elements lane and lane + 64 (the fp32 in-batch combine's fused form)
+    const float* gr = dout + r * H;
+    const float* orow = out + r * H;
+    float y0, y1;
+    l2_bwd_row2(gr[lane], gr[lane + kWave], orow[lane], orow[lane + kWave], nrm, y0, y1);
+    dx[r * H + lane] = y0;
+    dx[r * H + lane + kWave] = y1;
+    return;
+  }
   // x = out * den; s_x = sum(dout * x)
   float sx = 0.f;
   for (int c = lane; c < H; c += kWave) sx += dout[r * H + c] * out[r * H + c];

@@ -1975,8 +1975,60 @@ __global__ __launch_bounds__(256) void bwd_combine_l2_kernel(int64_t B, int64_t 
   reinterpret_cast<f32x4*>(dx + r * H)[lane] = l2_bwd_row4(g, o, nrm);
 }
 
+// The same fusion for the fp32 scorer at H = 128 (C2): row r < B takes dq_r, row B + j takes dd_j,
+// each element formed exactly as bwd_combine_kernel's generic path forms it (split partials in
+// split order, the exact rows of the stored-P form, the label row), then l2_bwd_row2 (the
+// arithmetic of l2norm_bwd_kernel at H = 128) with y_r and norms[r].  Elements lane and lane + 64
+// of each row per lane.
+__global__ __launch_bounds__(256) void bwd_combine_l2_128_kernel(
+    int64_t B, int64_t M, int S, int64_t label_off, const float* __restrict__ acc_part, const float* __restrict__ Qmat,
+    const float* __restrict__ dqu, const float* __restrict__ grad_loss, float grad_scale, float inv_tau,
+    const float* __restrict__ y, const float* __restrict__ norms, float* __restrict__ dx, const int* __restrict__ xrows,
+    const float* __restrict__ Dmat, const float* __restrict__ lse2, float c2, const float* __restrict__ mean_x = nullptr,
+    float* __restrict__ mean_out = nullptr) {
+  constexpr int H = 2 * kWave;
+  if (mean_out && blockIdx.x == 0) {  // the forward's deferred loss mean, as bwd_combine_kernel
+    __shared__ float part[1024];
+    const float m = block256_mean_as_1024(mean_x, B, part);
+    if (threadIdx.x == 0) mean_out[0] = m;
+    return;
+  }
+  const int64_t r = (int64_t)(blockIdx.x - (mean_out ? 1 : 0)) * 4 + (threadIdx.x >> 6);
+  if (r >= B + M) return;
+  const int lane = lane_id();
+  const float scale = grad_loss[0] * grad_scale * inv_tau;
+  const float o0 = y[r * H + lane], o1 = y[r * H + lane + kWave];  // issued first: independent of g
+  const float nrm = norms[r];
+  float g[2];
+  if (r < B) {
+    g[0] = dqu[r * H + lane] * scale;
+    g[1] = dqu[r * H + lane + kWave] * scale;
+  } else {
+    const int64_t j = r - B, qi = j - label_off;
+    float a[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) a[u] = sum_parts1(acc_part + j * H + lane + u * kWave, M * H, S);
+    if (xrows)  // exact rows (stored-P backward; see add_exact_rows)
+      for_exact_rows(xrows, B, lane, [&](int64_t i) {
+        const float gi = __builtin_amdgcn_exp2f(exact_row_dot(Qmat + i * H, Dmat + j * H, H, lane) * c2 - lse2[i]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) a[u] += gi * Qmat[i * H + lane + u * kWave];
+      });
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (qi >= 0 && qi < B) a[u] -= Qmat[qi * H + lane + u * kWave];
+      g[u] = a[u] * scale;
+    }
+  }
+  float y0, y1;
+  l2_bwd_row2(g[0], g[1], o0, o1, nrm, y0, y1);
+  dx[r * H + lane] = y0;
+  dx[r * H + lane + kWave] = y1;
+}
+
 // Where the backward's combine goes: dq / dd (the loss gradients), or, with `dx` set, the fused
-// F.normalize backward above (y = [q; d] rows, norms of the tower head; H = 256, bf16 operands).
+// F.normalize backward above (y = [q; d] rows, norms of the tower head; H = 256 with bf16
+// operands, H = 128 with fp32).
 struct BwdOut {
   float* dq;
   float* dd;
@@ -1992,6 +2044,14 @@ void launch_bwd_combine(int64_t B, int64_t M, int H, int S, int64_t label_off, c
                         const float* dqu, const float* grad_loss, float grad_scale, float inv_tau, const BwdOut& out,
                         const int* xrows, const DT* Db, const float* lse2, hipStream_t s) {
   const float c2 = inv_tau * kLog2e;
+  if constexpr (std::is_same<DT, float>::value) {
+    if (out.dx) {  // fp32, H = 128 (tt_inbatch_bwd_l2_mean checks the shape)
+      bwd_combine_l2_128_kernel<<<dim3((unsigned)((B + M + 3) / 4 + (out.loss ? 1 : 0))), dim3(256), 0, s>>>(
+          B, M, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.y, out.norms, out.dx, xrows, Db,
+          lse2, c2, out.loss_rows, out.loss);
+      return;
+    }
+  }
   if (out.dx) {
     bwd_combine_l2_kernel<DT><<<dim3((unsigned)((B + M + 3) / 4 + (out.loss ? 1 : 0))), dim3(256), 0, s>>>(
         B, M, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.y, out.norms, out.dx, xrows, Db,
@@ -2485,8 +2545,8 @@ extern "C" int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int
                                       tt_stream_t stream) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
-  TT_REQUIRE(H == 4 * kWave && dtype != TT_F32, "tt_inbatch_bwd_l2: H = 256 with bf16 operands only (H=%d dtype=%d)",
-             H, dtype);
+  TT_REQUIRE((H == 4 * kWave && dtype != TT_F32) || (H == 2 * kWave && dtype == TT_F32),
+             "tt_inbatch_bwd_l2: H = 256 with bf16 operands or H = 128 fp32 (H=%d dtype=%d)", H, dtype);
   TT_REQUIRE(qd && lse && dq_unscaled && grad_loss && norms && dx && ws, "null pointer");
   TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd_l2_mean: loss and loss_rows together");
   BwdOut out{nullptr, nullptr, qd, norms, dx, loss_rows, loss};

@@ -55,6 +55,11 @@ def multiple_negatives_loss(q_emb: torch.Tensor, d_pos_emb: torch.Tensor, d_neg_
     """InfoNCE over [d+, d-_1..N] by cosine / temperature, label 0 (losses.py:47-85)."""
     if d_neg_embs.dim() == 2:
         d_neg_embs = d_neg_embs.unsqueeze(1)
+    B, K = d_neg_embs.shape[0], d_neg_embs.shape[1]
+    if d_neg_embs.is_contiguous() and d_pos_emb.shape[0] == q_emb.shape[0] == B:
+        base = _packed(q_emb, d_pos_emb, d_neg_embs.view(B * K, -1))
+        if base is not None:  # [q; p; negatives] in one tensor (TwoTower's fused output): one gradient tensor
+            return ops.MultiNegLossPacked.apply(base, B, K, 1.0 / float(temperature))
     return ops.MultiNegLoss.apply(q_emb, d_pos_emb, d_neg_embs, 1.0 / float(temperature))
 
 

@@ -134,11 +134,9 @@ class BagPlan:
         dev = ids.device
         self.V, self.E = V, E
         main = torch.cuda.current_stream(dev)
-        # TT_PLAN_ON_MAIN=1 (diagnostic): serialise the plan on the main stream
-        side = main if os.environ.get("TT_PLAN_ON_MAIN") == "1" else _lib.side_stream(dev)
+        side = _lib.side_stream(dev)
         side.wait_stream(main)
-        if side is not main:
-            ids.record_stream(side)  # allocated on the current stream, read on the side stream
+        ids.record_stream(side)  # allocated on the current stream, read on the side stream
         pad = -1 if padding_idx is None else int(padding_idx)
         with torch.cuda.stream(side):
             if gather_group is not None:
@@ -249,15 +247,12 @@ class BagMeanPool(torch.autograd.Function):
         ids = ids.contiguous()
         ctx.plan = None
         plan_now = want_plan and scatter_mode == _lib.TT_SCATTER_SORTED
-        # Where the sort forks onto its side stream (TT_PLAN_FORK=early | after | auto, default auto):
-        # before the gather, beside it, when the table fits the 256 MiB Infinity Cache (the gather
-        # then reads the cache, and the latency-bound sort beside it costs it little: C3 0.8381 vs
-        # 0.8419 ms/step), after it otherwise (an HBM-bound gather of a larger table: C5 1.8235
-        # early vs 1.8178 after; profiles/r03p_c3_plan_fork_ab.txt)
-        fork = os.environ.get("TT_PLAN_FORK", "auto")
-        if fork == "auto":
-            fork = "early" if weight.numel() * weight.element_size() <= 256 * 2 ** 20 else "after"
-        early = plan_now and fork == "early"
+        # Where the sort forks onto its side stream: before the gather, beside it, when the table
+        # fits the 256 MiB Infinity Cache (the gather then reads the cache, and the latency-bound
+        # sort beside it costs it little: C3 0.8381 vs 0.8419 ms/step), after it otherwise (an
+        # HBM-bound gather of a larger table: C5 1.8235 early vs 1.8178 after;
+        # profiles/r03p_c3_plan_fork_ab.txt, r03w_plan_fork_auto_ab.txt)
+        early = plan_now and weight.numel() * weight.element_size() <= 256 * 2 ** 20
         if early:
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
@@ -597,7 +592,7 @@ class TowerHead(torch.autograd.Function):
             tok.grad = dx
         elif ctx.needs_input_grad[0]:
             dx = _head_gemm(dh, p_w1t, 3, N=E)
-        two = os.environ.get("TT_WGRAD2", "1") != "0" and E == H  # one launch for both: square heads
+        two = E == H  # square heads: both weight gradients in one launch (tt_head_wgrad2)
         if not on_side:
             if two:
                 head_wgrad2_reduce(head_wgrad2(dh, x, dy, h), dW1, db1, dW2, db2)
@@ -775,6 +770,39 @@ class MultiNegLoss(torch.autograd.Function):
         return dq, dp, dnegs, None
 
 
+class MultiNegLossPacked(torch.autograd.Function):
+    """The same loss on one ((2 + K) B, H) tensor [q; p; negatives (B K rows, query-major)]
+    (TwoTower's fused output): the three gradients are written into one tensor, so autograd
+    runs no split backward (a cat of the three, 50 MB at C5, on the step's critical path)."""
+
+    @staticmethod
+    def forward(ctx, qpn, B, K, inv_tau):
+        require_gpu(qpn)
+        qpn = _contig_f32(qpn, "qpn")
+        H = qpn.shape[1]
+        if qpn.shape[0] != (2 + K) * B:
+            raise ValueError(f"packed multiple-negatives input must have (2 + K) B = {(2 + K) * B} rows")
+        rows = torch.empty(B, dtype=_FLOAT, device=qpn.device)
+        loss = torch.empty((), dtype=_FLOAT, device=qpn.device)
+        q, p, n = qpn[:B], qpn[B:2 * B], qpn[2 * B:]
+        call("tt_multi_neg_fwd", ptr(q), ptr(p), ptr(n), B, K, H, float(inv_tau), ptr(rows), ptr(loss), stream_of(qpn))
+        ctx.save_for_backward(qpn)
+        ctx.meta = (B, K, float(inv_tau))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (qpn,) = ctx.saved_tensors
+        B, K, inv_tau = ctx.meta
+        H = qpn.shape[1]
+        g = g.to(_FLOAT).contiguous().reshape(1)
+        grad = torch.empty_like(qpn)
+        q, p, n = qpn[:B], qpn[B:2 * B], qpn[2 * B:]
+        call("tt_multi_neg_bwd", ptr(q), ptr(p), ptr(n), B, K, H, inv_tau, ptr(g), ptr(grad[:B]), ptr(grad[B:2 * B]),
+             ptr(grad[2 * B:]), stream_of(qpn))
+        return grad, None, None, None
+
+
 # --------------------------------------------------------------------------------------------
 # in_batch_sampled_softmax_loss   (twotower/losses.py:88-118), fused MFMA scorer
 _BWD_FORMS = {"recompute": _lib.TT_INBATCH_BWD_RECOMPUTE, "stored": _lib.TT_INBATCH_BWD_STORED}
@@ -881,7 +909,7 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         tok, ctx.l2_token = ctx.l2_token, None
         B, M, H, dt, inv_tau, label_off, grad_scale = ctx.meta
         dm, ctx.deferred_mean = ctx.deferred_mean, None
-        if tok is not None and _FUSED_HEAD_BWD[0] > 0 and H == HEAD_WIDTH and dt != _lib.TT_F32:
+        if tok is not None and _FUSED_HEAD_BWD[0] > 0 and _l2_fusable(H, dt):
             # the head's F.normalize backward in the combine: grad is the head's dy (see _L2Token)
             gs = g.to(_FLOAT).contiguous().reshape(1)
             call("tt_inbatch_bwd_l2_mean", ptr(qd), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(gs),
@@ -891,6 +919,11 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
             return grad, None, None, None, None
         _inbatch_bwd(ctx.meta, qd[:nq], qd[nq:], lse, dqu, ws, g, grad[:nq], grad[nq:], mean=dm)
         return grad, None, None, None, None
+
+
+def _l2_fusable(H: int, dt: int) -> bool:
+    """tt_inbatch_bwd_l2's shapes: H = 256 with bf16 operands (C3), H = 128 fp32 (C2)."""
+    return (H == HEAD_WIDTH and dt != _lib.TT_F32) or (H == 128 and dt == _lib.TT_F32)
 
 
 _DEFER_MEAN = [0]  # > 0 while a caller (TrainStep) runs the backward before anyone reads the loss

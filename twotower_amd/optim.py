@@ -288,8 +288,8 @@ class AdamW(torch.optim.Optimizer):
         # form the head weight gradients from their side-stream slab partials themselves (the sums
         # of tt_head_wgrad2_reduce, bit for bit, also written to .grad; tt_adamw_multi_ex).  The
         # next step's scalars stay a launch of their own: formed by the same launch's last
-        # workgroup (TT_FUSED_PREPARE=1) they cost more than that launch, one same-address
-        # device-scope increment per workgroup (1,000 of them) serialising at the memory side.
+        # workgroup they cost more than that launch (round 2: one same-address device-scope
+        # increment per workgroup, 1,000 of them, serialising at the memory side).
         fuse = (os.environ.get("TT_FUSED_TAIL", "1") != "0" and len(dense) <= _lib.TT_ADAM_MAX_TENSORS
                 and len(slots) <= _lib.TT_ADAM_MAX_TENSORS and (dense or ahead))
         parts = self._side_grads.join(claim={i for i in dense_ids if i is not None} if fuse else None)
@@ -298,14 +298,10 @@ class AdamW(torch.optim.Optimizer):
             ticket = self._tickets.get(dev)
             if ticket is None:
                 ticket = self._tickets[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-            in_launch = ahead and os.environ.get("TT_FUSED_PREPARE", "0") == "1"
-            if in_launch:
-                join_shards()
-            ops.adamw_multi_ex(dense, [parts.get(i) if i is not None else None for i in dense_ids],
-                               slots if in_launch else [], lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd,
-                               ticket=ticket)
+            ops.adamw_multi_ex(dense, [parts.get(i) if i is not None else None for i in dense_ids], [], lr=lr,
+                               beta1=b1, beta2=b2, eps=eps, weight_decay=wd, ticket=ticket)
             join_shards()
-            if ahead and not in_launch:
+            if ahead:
                 ops.adam_prepare(slots, lr=lr, beta1=b1, beta2=b2, eps=eps, weight_decay=wd, increment=1, ahead=1)
         else:
             ops.adamw_multi(dense)

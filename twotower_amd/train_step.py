@@ -34,9 +34,7 @@ class TrainStep:
         # (optim.AdamW): the all-reduce then overlaps the table update
         # (set on the optimizer only for the duration of this step's optimizer.step(): a plain loop
         # that calls GradSync.sync() itself must not see a second all-reduce)
-        # (TT_GRADSYNC_IN_STEP=0, diagnostic: the all-reduce as GradSync.sync() after backward)
-        self._sync_in_step = (self.sync is not None and hasattr(optimizer, "_grad_sync")
-                              and os.environ.get("TT_GRADSYNC_IN_STEP", "1") != "0")
+        self._sync_in_step = self.sync is not None and hasattr(optimizer, "_grad_sync")
         # a single-device bf16 in-batch loss: the tied towers' head prepares its operands
         # (TT_SCORER_PREP=0: the loss's own prep pass, for comparison)
         # Opened only around this step's own forward (_scorer_prep_open): set on the model for
@@ -142,8 +140,7 @@ class TrainStep:
             self._graphs[key] = hit
         graph, static_all, static_loss = hit
         if all(t.shape[1:] == inputs[0].shape[1:] and t.dtype == inputs[0].dtype for t in inputs):
-            if (all(t.device == static_all.device and t.is_contiguous() for t in inputs) and len(inputs) <= 8
-                    and os.environ.get("TT_PACK_INPUT", "1") != "0"):  # TT_PACK_INPUT=0: torch.cat
+            if all(t.device == static_all.device and t.is_contiguous() for t in inputs) and len(inputs) <= 8:
                 ops.pack_blocks(inputs, static_all)  # one launch into the packed static buffer
             else:
                 torch.cat(inputs, 0, out=static_all)
@@ -184,7 +181,7 @@ def _is_capture_error(e: BaseException) -> bool:
     """An error raised because the step was being captured (a call HIP or a backend refuses inside
     stream capture), as opposed to an error of the step itself."""
     msg = str(e).lower()
-    return any(k in msg for k in ("captur", "graph", "not permitted"))
+    return any(k in msg for k in ("captur", "hipgraph", "cudagraph", "not permitted"))
 
 
 def _all_ranks(flag: bool, group, device) -> bool:
