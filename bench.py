@@ -453,9 +453,10 @@ def parse():
                          "size 1, TT_DIST_FORCE=1), e.g. to check the N-rank step under HIP-graph capture on one GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard"],
-                    help="N ranks: table update from gathered ids + row grads (gather) or row-sharded AdamW "
-                         "(shard); auto picks gather up to 4 ranks")
+    ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard", "owner"],
+                    help="N ranks: table update from gathered ids + row grads on every rank (gather), row-sharded "
+                         "AdamW after a gradient reduce-scatter (shard), or each rank's own rows from the gathered "
+                         "factored gradient (owner); auto picks gather up to 4 ranks")
     ap.add_argument("--timing-steps", type=int, default=10, help="eager steps timed per op after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=8192,

@@ -128,6 +128,18 @@ int tt_bag_mean_bwd_planned_rows(const float* d_pooled, const float* denom, int6
                                  int64_t V, int E, const void* plan, size_t plan_bytes,
                                  int64_t row_begin, int64_t row_end, float* grad_rows,
                                  tt_stream_t stream);
+/* tt_bag_mean_bwd_adamw_planned_rows: rows [row_begin, row_end) of tt_bag_mean_bwd_adamw_planned
+ *   (after tt_bag_mean_bwd_planned_prepare on the same stream): the same sums in the same order,
+ *   then AdamW on those rows, whose parameters and moments are table_rows / exp_avg_rows /
+ *   exp_avg_sq_rows ((row_end - row_begin) x E each).  The data-parallel "owner" table exchange
+ *   (optim.AdamW): the plan covers every rank's tokens (all-gathered ids, d_pooled / denom), and each
+ *   rank updates only the rows it owns, with its shard of the moments, before the rows are
+ *   all-gathered (twotower/train.py:138-139). */
+int tt_bag_mean_bwd_adamw_planned_rows(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                       int64_t V, int E, const void* plan, size_t plan_bytes,
+                                       int64_t row_begin, int64_t row_end, float* table_rows,
+                                       float* exp_avg_rows, float* exp_avg_sq_rows, const void* adam_args,
+                                       tt_stream_t stream);
 
 /* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
  * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;

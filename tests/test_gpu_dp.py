@@ -4,8 +4,9 @@ parameters after each step must equal a single process stepping on the global ba
 
 The DP step: each rank pools/scores its half, the in-batch candidates are all-gathered with
 rank-offset labels, the loss is pre-scaled by 1/world, tower gradients are all-reduced, and the
-table is updated either from the all-gathered factored gradient on every rank ("gather") or by
-reduce-scatter into row shards, AdamW per shard and all-gather ("shard").  Sum orders differ from the single process (two partial sums), so the bar is the
+table is updated from the all-gathered factored gradient on every rank ("gather"), by
+reduce-scatter into row shards, AdamW per shard and all-gather ("shard"), or from the all-gathered
+factored gradient on each row's owner only, then all-gather ("owner").  Sum orders differ from the single process (two partial sums), so the bar is the
 fp32 1e-5 relative tolerance on the parameter change.  AdamW normalises every element's update,
 which turns rounding-level differences of near-cancelled gradients (|g| ~ eps) into O(lr)
 parameter differences; with eps = 1 and no decay the first update is -lr g / (|g| + 1), so the
@@ -96,7 +97,8 @@ KEYS = {"table": "query_tower.embedding.embedding.weight", "W1": "query_tower.fe
 
 @pytest.mark.parametrize("loss_name,table_sync,groups", [("in_batch", "gather", False), ("in_batch", "shard", False),
                                                          ("triplet", "gather", False), ("triplet", "shard", False),
-                                                         ("triplet", "gather", True), ("in_batch", "shard", True)])
+                                                         ("triplet", "gather", True), ("in_batch", "shard", True),
+                                                         ("in_batch", "owner", False), ("triplet", "owner", True)])
 def test_dp_step_equals_global_batch(loss_name, table_sync, groups):
     """One step, eps 1, no decay: delta = -lr g / (|g| + 1), so g is recovered from the parameter
     change and compared with the float64 oracle on the global batch.  groups: the parameters in
@@ -239,7 +241,7 @@ def test_owner_backward_takes_each_ranks_seed(seeds):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("table_sync,loss_name", [("gather", "in_batch"), ("shard", "in_batch"),
-                                                  ("shard", "multiple_negatives")])
+                                                  ("shard", "multiple_negatives"), ("owner", "multiple_negatives")])
 def test_dp_graph_replay_equals_eager_one_rank_rccl(table_sync, loss_name):
     """The N-rank step captured in one HIP graph (its RCCL collectives included: candidate
     all-gathers, the table exchange, the gradient all-reduce on the communication stream) replays

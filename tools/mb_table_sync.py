@@ -80,7 +80,7 @@ for R in a.ranks:
     denom = (ids > 0).sum(1).float() + 1e-9
     res = {"config": a.config, "ranks": R, "tokens_per_rank": int((own > 0).sum())}
     # gather: plan over all ranks' ids + the replicated fused update
-    t_plan_all = timed(lambda: ops.BagPlan(ids, V, E, 0), a.iters)
+    t_plan_all = timed(lambda: ops.BagPlan(ids, V, E, 0).wait(), a.iters)
     plan = ops.BagPlan(ids, V, E, 0)
     plan.wait()
     res["gather_update_us"] = timed(
@@ -92,7 +92,7 @@ for R in a.ranks:
     plan1.wait()
     gbuf = torch.empty(V, E, device="cuda")
     Vs = -(-V // R)
-    res["plan_own_us"] = timed(lambda: ops.BagPlan(own, V, E, 0), a.iters)
+    res["plan_own_us"] = timed(lambda: ops.BagPlan(own, V, E, 0).wait(), a.iters)
     res["shard_dense_grad_us"] = timed(
         lambda: ops.bag_mean_backward_planned(d_pooled[:nown], denom[:nown], plan1, out=gbuf), a.iters)
     res["shard_adamw_us"] = timed(
@@ -101,7 +101,7 @@ for R in a.ranks:
     del plan1, gbuf
     # owner: the N ranks' ids remapped to this rank's Vs rows (rank 0 owns rows [0, Vs)), others padding
     own_ids = torch.where(ids < Vs, ids, torch.zeros_like(ids)).contiguous()
-    res["owner_plan_us"] = timed(lambda: ops.BagPlan(own_ids, Vs, E, 0), a.iters)
+    res["owner_plan_us"] = timed(lambda: ops.BagPlan(own_ids, Vs, E, 0).wait(), a.iters)
     plan_o = ops.BagPlan(own_ids, Vs, E, 0)
     plan_o.wait()
     res["owner_update_us"] = timed(

@@ -69,6 +69,8 @@ _SIGNATURES = {
                                               _vp, _vp]),
     "tt_bag_mean_bwd_adamw_planned": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _vp, _vp, _vp,
                                                _vp, _vp]),
+    "tt_bag_mean_bwd_adamw_planned_rows": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _c_i64,
+                                                    _c_i64, _vp, _vp, _vp, _vp, _vp]),
     "tt_adam_prepare": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _vp]),
     "tt_adam_prepare_ex": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64,
                                     _c_int, _c_int, _vp]),

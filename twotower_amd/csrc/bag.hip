@@ -1211,6 +1211,29 @@ extern "C" int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float*
                           reinterpret_cast<hipStream_t>(stream));
 }
 
+extern "C" int tt_bag_mean_bwd_adamw_planned_rows(const float* d_pooled, const float* denom, int64_t nseq, int L,
+                                                  int64_t V, int E, const void* plan, size_t plan_bytes,
+                                                  int64_t row_begin, int64_t row_end, float* table_rows,
+                                                  float* exp_avg_rows, float* exp_avg_sq_rows, const void* adam_args,
+                                                  tt_stream_t stream) {
+  TT_REQUIRE(V > 0 && E > 0 && nseq >= 0 && L >= 0, "bad shape");
+  TT_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= V, "rows [%lld, %lld) outside [0, %lld)",
+             (long long)row_begin, (long long)row_end, (long long)V);
+  TT_REQUIRE(table_rows && exp_avg_rows && exp_avg_sq_rows && adam_args && (nseq == 0 || d_pooled), "null pointer");
+  const BwdWs w = plan_layout(const_cast<void*>(plan), nseq, L, V, E);
+  TT_REQUIRE(plan != nullptr && w.total + 256 <= plan_bytes, "plan workspace too small: need %zu have %zu",
+             w.total + 256, plan_bytes);
+  BwdWs wa;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int rc = apply_prepare(d_pooled, denom, (nseq == 0 || L == 0) ? 0 : nseq, V, E, w, wa, s, false);
+  if (rc) return rc;
+  AdamArgs aa{};
+  // row r of the range updates table_rows / the moment rows at (r - row_begin) * E
+  const int64_t sh = row_begin * (int64_t)E;
+  return launch_reduce<true>(wa, row_end, E, nullptr, table_rows - sh, exp_avg_rows - sh, exp_avg_sq_rows - sh, aa,
+                             static_cast<const AdamArgs*>(adam_args), s, row_begin);
+}
+
 extern "C" int tt_bag_mean_bwd(const float* d_pooled, const float* denom, const void* ids, int ids_dtype,
                                int64_t nseq, int L, int64_t ld_ids, int64_t V, int E, int64_t padding_idx,
                                float* grad_table, int mode, void* ws, size_t ws_bytes, tt_stream_t stream) {

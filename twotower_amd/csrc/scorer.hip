@@ -384,6 +384,9 @@ struct MapState {
 // 16 chunks (+256 B) and tile jt adds 32 rows: immediates.  Acc chain: the transposed 4-row
 // blocks of rows r0 and r0 + 8 at chunk (4 ht + cbase) ^ swz = 4 (ht ^ (swz >> 2)) + (cbase ^
 // (swz & 3)) for ht = 0..3; ht >= 4 (+256 B), the second 16-row half and jt: immediates.
+#ifndef TT_LDS_HI
+#define TT_LDS_HI 1
+#endif
 template <int H>
 struct LdsOffs {
   using T = Tile<__bf16, H>;
@@ -391,6 +394,11 @@ struct LdsOffs {
   static constexpr int NA4 = (H / 32) < 4 ? (H / 32) : 4;
   unsigned s[NS8];
   unsigned a0[NA4], a1[NA4];
+#if TT_LDS_HI
+  // the same offsets + 64 KiB: a ds_read's offset field holds 16 bits, so reads of the ring slots
+  // at 64 KiB and above take these (lds_at) instead of a v_add_u32 per read address
+  unsigned sh[NS8], a0h[NA4], a1h[NA4];
+#endif
   __device__ __forceinline__ void init(int lane) {
     const int r32 = lane & 31, hh = lane >> 5, x = T::swz(r32);
 #pragma unroll
@@ -404,8 +412,36 @@ struct LdsOffs {
       a0[ht] = r0 * T::ROWB + bo + (((4 * ht + cbase) ^ x0) << 4);
       a1[ht] = (r0 + 8) * T::ROWB + bo + (((4 * ht + cbase) ^ x1) << 4);
     }
+#if TT_LDS_HI
+#pragma unroll
+    for (int k = 0; k < NS8; ++k) {
+      sh[k] = s[k] + 65536u;
+      asm volatile("" : "+v"(sh[k]));  // a register of its own, not rematerialised as an add per read
+    }
+#pragma unroll
+    for (int ht = 0; ht < NA4; ++ht) {
+      a0h[ht] = a0[ht] + 65536u;
+      a1h[ht] = a1[ht] + 65536u;
+      asm volatile("" : "+v"(a0h[ht]), "+v"(a1h[ht]));
+    }
+#endif
   }
 };
+
+// LDS address of a read at lane offset vo (vo_hi = vo + 64 KiB) from `tile`, a compile-time
+// constant offset from `base` once the stage loop is unrolled over its ring slots: tiles at 64 KiB
+// and above go through the +64 KiB offsets, so offset + immediate stays inside the 16-bit field.
+__device__ __forceinline__ const lds_char_t* lds_at(const lds_char_t* base, const lds_char_t* tile, unsigned vo,
+                                                    unsigned vo_hi) {
+#if TT_LDS_HI
+  const int off = (int)(tile - base);
+  if (off >= 65536) return base + (off - 65536) + vo_hi;
+#else
+  (void)base;
+  (void)vo_hi;
+#endif
+  return tile + vo;
+}
 
 template <int MODE, bool PRECISE, int H, class Hook = NoHook>
 __device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int jrow, const LdsOffs<H>& lo,
@@ -531,6 +567,7 @@ struct UnitSrc {
   const lds_char_t* s;  // S chain source: stage tile + 32-row X tile base (bytes)
   const lds_char_t* a;  // Acc chain source: stage tile + 32-row tile base (bytes)
   const lds_char_t* n;  // next unit's S chain source
+  const lds_char_t* base;  // LDS byte 0 (lds_at)
 };
 
 // Operand i of the step stream that starts at this unit: i in [0, NSTEP) is this unit's, i >= NSTEP
@@ -544,15 +581,24 @@ __device__ __forceinline__ bf16x8 unit_operand(int i, const UnitSrc<H>& u, const
 #ifdef TT_ABLATE_LDSREAD  // timing ablation (never in a real build): no operand reads
   return bf16x8{(__bf16)(float)w, (__bf16)(float)(lo.s[0] & 7), 0, 0, 0, 0, 0, (__bf16)(float)nxt};
 #endif
+#if TT_LDS_HI
+#define TT_LO_HI(f, i) lo.f##h[i]
+#else
+#define TT_LO_HI(f, i) lo.f[i]
+#endif
   if (w < NK) {
     const lds_char_t* tb = nxt ? u.n : u.s;
-    return *reinterpret_cast<const lds_bf16x8_t*>(tb + lo.s[w & 7] + (w >= 8 ? 256 : 0));
+    return *reinterpret_cast<const lds_bf16x8_t*>(lds_at(u.base, tb, lo.s[w & 7], TT_LO_HI(s, w & 7)) +
+                                                   (w >= 8 ? 256 : 0));
   }
   const lds_char_t* ta = nxt ? u.s : u.a;
   const int st = w - NK, s2 = st / NHT, ht = st % NHT;
   const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
-  const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(ta + lo.a0[ht & 3] + imm));
-  const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(ta + lo.a1[ht & 3] + imm));
+  const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4_t*)(lds_at(u.base, ta, lo.a0[ht & 3], TT_LO_HI(a0, ht & 3)) + imm));
+  const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4_t*)(lds_at(u.base, ta, lo.a1[ht & 3], TT_LO_HI(a1, ht & 3)) + imm));
+#undef TT_LO_HI
   return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
 }
 
@@ -910,7 +956,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   static_assert(NJ % 2 == 0, "X tiles alternate between two register sets");
   f32x16 xa, xb;
   {  // X tile 0 (its operand reads exposed once), into VGPRs like every later X tile
-    const UnitSrc<H> u0{lds, lds, lds};
+    const UnitSrc<H> u0{lds, lds, lds, lds};
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const bf16x8 a = unit_operand<H>(k, u0, lo);
@@ -926,7 +972,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   }
   bf16x8 ring[kSdFor<H>];
   {
-    UnitSrc<H> u0{lds + 32 * T::ROWB, lds, lds};  // the first unit's S source: tile 1 of stage 0
+    UnitSrc<H> u0{lds + 32 * T::ROWB, lds, lds, lds};  // the first unit's S source: tile 1 of stage 0
 #pragma unroll
     for (int k = 0; k < kSdFor<H>; ++k) ring[k] = unit_operand<H>(k, u0, lo);
   }
@@ -959,7 +1005,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
       auto src = [&](int k) {  // 32-row tile k of stage t (k >= NJ: of stage t+1)
         return k < NJ ? tile + k * 32 * T::ROWB : ntl + (k - NJ) * 32 * T::ROWB;
       };
-      const UnitSrc<H> u{src(jt + 1), src(jt), src(jt + 2)};
+      const UnitSrc<H> u{src(jt + 1), src(jt), src(jt + 2), lds};
       MapState<MODE, PRECISE> ms;
       ms.init(c2, shift, lse4 + jt * 8, hh);
       char* blk = STOREP ? pblk(t, jt) : nullptr;

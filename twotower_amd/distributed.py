@@ -82,15 +82,19 @@ def table_sync_mode(requested: str, group=None) -> str:
                   backward: ~31 MB per rank at C3) and run the fused scatter + AdamW on every rank
                   over all ranks' entries (replicated table and moments, no parameter exchange);
       "shard"  -- reduce-scatter the dense table gradient by row range, AdamW on own rows,
-                  all-gather the rows (2 x 205 MB x (N-1)/N per rank at C3).
+                  all-gather the rows (2 x 205 MB x (N-1)/N per rank at C3);
+      "owner"  -- all-gather the factored gradient as "gather" does, but each rank scatters and
+                  updates only the rows it owns (shard's row partition and moment shards), then
+                  the rows are all-gathered: (N-1) x 31 MB + 205 MB x (N-1)/N per rank at C3,
+                  1/N of the update's HBM traffic, no dense gradient.
     "auto": gather up to 4 ranks (its bytes grow with N; at N <= 4 a rank pair shares few xGMI
     links, where the dense exchange is link-bound), shard beyond."""
     if not is_active(group):
         return "local"
     if requested == "auto":
         return "gather" if dist.get_world_size(group) <= 4 else "shard"
-    if requested not in ("gather", "shard"):
-        raise ValueError(f"table_sync must be 'auto', 'gather' or 'shard', got {requested!r}")
+    if requested not in ("gather", "shard", "owner"):
+        raise ValueError(f"table_sync must be 'auto', 'gather', 'shard' or 'owner', got {requested!r}")
     return requested
 
 

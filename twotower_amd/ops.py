@@ -1168,6 +1168,20 @@ def bag_mean_backward_adamw_planned(d_pooled, denom, plan: BagPlan, table, exp_a
          plan.buf.numel(), ptr(table), ptr(exp_avg), ptr(exp_avg_sq), ptr(adam_args), stream_of(table))
 
 
+def bag_mean_backward_adamw_planned_rows(d_pooled, denom, plan: BagPlan, row_begin: int, row_end: int, table_rows,
+                                         exp_avg_rows, exp_avg_sq_rows, adam_args: torch.Tensor) -> None:
+    """Rows [row_begin, row_end) of the fused scatter + AdamW (after bag_mean_backward_planned_prepare on the
+    same stream): table_rows, exp_avg_rows, exp_avg_sq_rows are those rows ((row_end - row_begin, E))."""
+    d_pooled = _contig_f32(d_pooled, "d_pooled")
+    n = row_end - row_begin
+    for t, nm in ((table_rows, "table_rows"), (exp_avg_rows, "exp_avg_rows"), (exp_avg_sq_rows, "exp_avg_sq_rows")):
+        if tuple(t.shape) != (n, plan.E) or not t.is_contiguous() or t.dtype != _FLOAT:
+            raise ValueError(f"{nm} must be a contiguous float32 ({n}, {plan.E}) tensor")
+    call("tt_bag_mean_bwd_adamw_planned_rows", ptr(d_pooled), ptr(denom), plan.nseq, plan.L, plan.V, plan.E,
+         ptr(plan.buf), plan.buf.numel(), int(row_begin), int(row_end), ptr(table_rows), ptr(exp_avg_rows),
+         ptr(exp_avg_sq_rows), ptr(adam_args), stream_of(table_rows))
+
+
 def bag_mean_backward_adamw(d_pooled, denom, ids, table, exp_avg, exp_avg_sq, padding_idx, *, lr, beta1, beta2,
                             eps, weight_decay, step) -> None:
     """Sorted scatter of the pooled gradient fused with the table's AdamW step."""

@@ -57,10 +57,11 @@ class AdamW(torch.optim.Optimizer):
                     raise ValueError("fused table is not among the optimizer's parameters")
                 mode = distributed.table_sync_mode(table_sync, group)
                 # (None is the "no exchange" sentinel there: name the default group explicitly)
-                gg = (group if group is not None else torch.distributed.group.WORLD) if mode == "gather" else None
+                gg = ((group if group is not None else torch.distributed.group.WORLD) if mode in ("gather", "owner")
+                      else None)
                 w._tt_deferred = ops.DeferredTableGrad(pad, gather_group=gg)
                 self._tables.append(w)
-                if mode == "shard":
+                if mode in ("shard", "owner"):  # owner: shard's row partition, gather's inputs
                     self._shards[id(w)] = distributed.ShardedRows(w, group)
             # the dense parameters' gradients may then be computed on a side stream beside the
             # fused table update (ops.TowerHead); step() joins them after launching that update
@@ -199,7 +200,8 @@ class AdamW(torch.optim.Optimizer):
                 sh = self._shards.get(id(p))
                 if sh is not None:
                     args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
-                    self._shard_update(sh, (ids, dp, den, plan), st, args)
+                    upd = self._owner_update if deferred.gather_group is not None else self._shard_update
+                    upd(sh, (ids, dp, den, plan), st, args)
                     torch.cuda.current_stream(p.device).wait_stream(sh.comm_stream())
                     continue
                 args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
@@ -227,8 +229,11 @@ class AdamW(torch.optim.Optimizer):
                 parts = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
                 sh = self._shards.get(id(p))
-                if sh is not None:  # data parallel: chunked reduce-scatter, AdamW on own rows, all-gather
-                    shards.append((sh, parts, st, a))
+                if sh is not None and deferred.gather_group is not None:  # "owner": every rank's factored
+                    # gradient, this rank's rows updated, the rows all-gathered in chunks
+                    shards.append((sh, _gather_parts(parts, deferred.gather_group), st, a, self._owner_update))
+                elif sh is not None:  # data parallel: chunked reduce-scatter, AdamW on own rows, all-gather
+                    shards.append((sh, parts, st, a, self._shard_update))
                 else:
                     if deferred.gather_group is not None:  # data parallel: every rank's factored grad
                         parts = _gather_parts(parts, deferred.gather_group)
@@ -275,11 +280,11 @@ class AdamW(torch.optim.Optimizer):
                                                 self._adam_args(p))
         # data parallel, row-sharded tables: the chunk-pipelined exchange (its collectives are
         # issued before the tower all-reduce, so they lead on the communicator)
-        for sh, parts, st, a in shards:
-            self._shard_update(sh, parts, st, a)
+        for sh, parts, st, a, update in shards:
+            update(sh, parts, st, a)
 
         def join_shards():  # the chunk updates read this step's scalars on their own stream: the
-            for sh, _, _, _ in shards:  # next step's scalars (and the next forward) wait for them
+            for sh, _, _, _, _ in shards:  # next step's scalars (and the next forward) wait for them
                 torch.cuda.current_stream(sh.weight.device).wait_stream(sh.comm_stream())
         # data parallel: the tower-gradient all-reduce, issued after the table's collectives and
         # the table update, overlaps that update on a communication stream; the join waits for it
@@ -343,6 +348,36 @@ class AdamW(torch.optim.Optimizer):
                 ops.adamw_multi([(sh.own(stor, c), g, sh.shard_chunk(st["exp_avg"], c),
                                   sh.shard_chunk(st["exp_avg_sq"], c), args)])
                 distributed.all_gather_rows(stor[lo:hi], sh.own(stor, c), sh.group)
+
+
+    @staticmethod
+    def _owner_update(sh, parts, st, args) -> None:
+        """Row-owner table update ("owner" exchange): `parts` is every rank's factored gradient
+        (all-gathered ids in the plan, d_pooled / denom), so this rank forms the global gradient of
+        exactly the rows it owns and applies AdamW to them with its moment shard
+        (tt_bag_mean_bwd_adamw_planned_rows, the fused update's sums and order for those rows), chunk
+        by chunk; the communication stream all-gathers chunk c's owned slabs into every rank's table
+        while the current stream updates chunk c + 1.  No dense gradient and no reduce-scatter; the
+        caller joins sh.comm_stream() before the table or `args` are read again."""
+        _, dp, den, plan = parts
+        main = torch.cuda.current_stream(dp.device)
+        comm = sh.comm_stream()
+        stor = sh.storage()
+        ops.bag_mean_backward_planned_prepare(dp, den, plan)
+        for c in range(sh.NC):
+            lo = c * sh.Cr + sh.rank * sh.R
+            top = min(lo + sh.R, sh.V)
+            if lo < top:
+                n = top - lo
+                ops.bag_mean_backward_adamw_planned_rows(dp, den, plan, lo, top, stor[lo:top],
+                                                         sh.shard_chunk(st["exp_avg"], c)[:n],
+                                                         sh.shard_chunk(st["exp_avg_sq"], c)[:n], args)
+            ready = torch.cuda.Event()
+            ready.record(main)
+            comm.wait_event(ready)
+            with torch.cuda.stream(comm):
+                clo, chi = sh.chunk(c)
+                distributed.all_gather_rows(stor[clo:chi], sh.own(stor, c), sh.group)
 
 
 def _gather_parts(parts, group):
