@@ -1,0 +1,323 @@
+"""Microbenchmarks of the step's kernels on one GPU, one driver with a subcommand per op family
+(device times from HIP graph replay of back-to-back calls, or HIP events per C-ABI call).
+
+  python tools/mb.py bag_bwd [--zipf S]          fused table update (scale rows + per-row reduce +
+                                                 AdamW) at C3, against a dense AdamW, a device copy and
+                                                 the dense-gradient apply on the same buffers
+  python tools/mb.py plan [c3|c5]                the backward's sort plan (tt_bag_plan), uniform and Zipf
+  python tools/mb.py head                        the tower head GEMMs (24576 x 256 x 256) against hipBLASLt
+  python tools/mb.py scorer [B M H dtype ...]    in-batch scorer fwd / bwd (prep + engine + combine)
+  python tools/mb.py scorer_dp [dtype]           one rank's scorer passes at the N-rank shapes (N = 1..8,
+                                                 cross-device negatives, candidate-owner gradients)
+  python tools/mb.py split_fwd                   two-launch vs one-launch data-parallel forward
+  python tools/mb.py table_sync [c3|c5]          per-rank GPU cost of the table exchanges at N ranks
+                                                 (gather / shard / owner) and their link bytes
+  python tools/mb.py scorer_once B M H [dtype] [lib]   three scorer fwd + bwd calls, nothing else (for
+                                                 counter collection: tools/pmc_scorer.sh)
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import twotower_amd as tt  # noqa: E402
+from twotower_amd import _lib, ops  # noqa: E402
+from twotower_amd._lib import call, ptr  # noqa: E402
+
+DEV = "cuda"
+
+
+def graph_us(fn, iters: int = 10, reps: int = 5) -> float:
+    """Per-call device time of `fn` from the replay of a graph holding `iters` back-to-back calls."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        for _ in range(iters):
+            fn()
+    gr.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        gr.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / (iters * reps) * 1e3
+
+
+def event_us(fn, iters: int = 20) -> float:
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def adam_args():
+    step = torch.zeros(1, device=DEV)
+    args = torch.zeros(_lib.TT_ADAM_ARGS_BYTES // 4, device=DEV)
+    slot = _lib.AdamSlot(step.data_ptr(), args.data_ptr())
+    call("tt_adam_prepare", ctypes.byref(slot), 1, 1e-3, 0.9, 0.999, 1e-8, 0.01, torch.cuda.current_stream().cuda_stream)
+    return step, args
+
+
+def ids_for(B, L, V, K=1, seed=0, zipf=None):
+    q, p, n = tt.data.synthetic_triplets(B, L, V, seed=seed, device=DEV, zipf_s=zipf, negatives=K)
+    return torch.cat([q, p, n]).to(torch.int32).contiguous()
+
+
+# ------------------------------------------------------------------------------------------------
+def bag_bwd(a):
+    B, L, V, E = 8192, 64, 200_000, 256
+    ids = ids_for(B, L, V, zipf=a.zipf)
+    N = ids.shape[0]
+    g = torch.Generator(device=DEV).manual_seed(0)
+    table = torch.randn(V, E, device=DEV, generator=g) * 0.02
+    m, v = torch.zeros_like(table), torch.zeros_like(table)
+    d_pooled = torch.randn(N, E, device=DEV, generator=g)
+    denom = (ids > 0).sum(1).float() + 1e-9
+    plan = ops.BagPlan(ids, V, E, 0)
+    plan.wait()
+    _, args = adam_args()
+    us = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, denom, plan, table, m, v, args), 20)
+    algo = N * E * 4 + N * 4 + 24 * V * E
+    print(f"fused update (zipf={a.zipf}): {us:.1f} us, algorithmic {algo / us / 1e3:.0f} GB/s")
+    grad = torch.randn(V, E, device=DEV, generator=g)
+    dst = torch.empty_like(table)
+    dense = lambda: call("tt_adamw", ptr(table), ptr(grad), ptr(m), ptr(v), V * E, 1e-3, 0.9, 0.999, 1e-8,  # noqa
+                         0.01, 1, torch.cuda.current_stream().cuda_stream)
+    for name, fn, nb in (("dense AdamW over V x E", dense, 28 * V * E), ("device copy of the table",
+                                                                         lambda: dst.copy_(table), 8 * V * E)):
+        us = event_us(fn)
+        print(f"{name}: {us:.1f} us, {nb / us / 1e3:.0f} GB/s")
+    us = event_us(lambda: ops.bag_mean_backward_planned(d_pooled, denom, plan, out=dst))
+    print(f"dense-gradient apply: {us:.1f} us, {(N * E * 4 + N * 4 + V * E * 4) / us / 1e3:.0f} GB/s algorithmic")
+
+
+def plan(a):
+    shape = a.shape or "c3"
+    B, L, E = 8192, 64, 256
+    V, K = (1_000_000, 4) if shape == "c5" else (200_000, 1)
+    for name, z in (("uniform", None), ("zipf1.0", 1.0)):
+        ids = ids_for(B, L, V, K, zipf=z)
+        print(f"tt_bag_plan {shape} {name}: {graph_us(lambda: ops.BagPlan(ids, V, E, 0).wait()):.1f} us")
+
+
+def head(a):
+    N = 24576
+    x = torch.randn(N, 256, device=DEV)
+    W = torch.randn(256, 256, device=DEV) / 16
+    b = torch.randn(256, device=DEV)
+    P = ops._planes(W, False)
+    norms = torch.empty(N, device=DEV)
+    mask = torch.empty(N, 8, dtype=torch.int32, device=DEV)
+    for epi in range(4):
+        us = graph_us(lambda: ops._head_gemm(x, P, epi, bias=b, mask=mask, norms=norms), 20)
+        print(f"head_gemm epi {epi}: {us:.1f} us")
+    g2 = torch.randn(N, 256, device=DEV)
+    print(f"split planes: {graph_us(lambda: ops._planes(W, True), 20):.1f} us")
+    print(f"torch addmm (hipBLASLt): {graph_us(lambda: torch.addmm(b, x, W.t()), 20):.1f} us")
+    print(f"head_wgrad (dW + db): {graph_us(lambda: ops.head_wgrad(g2, x), 20):.1f} us")
+
+
+def scorer(a):
+    cases = [tuple(a.rest[i:i + 4]) for i in range(0, len(a.rest), 4)] or [
+        (8192, 16384, 256, "bf16"), (8192, 8192, 256, "bf16"), (4096, 8192, 128, "fp32")]
+    for B, M, H, dt in cases:
+        B, M, H = int(B), int(M), int(H)
+        g = torch.Generator(device=DEV).manual_seed(0)
+        q = torch.nn.functional.normalize(torch.randn(B, H, device=DEV, generator=g), dim=-1).requires_grad_(True)
+        d = torch.nn.functional.normalize(torch.randn(M, H, device=DEV, generator=g), dim=-1).requires_grad_(True)
+        for _ in range(3):
+            ops.in_batch_softmax_loss(q, d, 0.1, compute_dtype=dt).backward()
+        torch.cuda.synchronize()
+        _lib.TIMER.reset()
+        _lib.TIMER.enabled = True
+        for _ in range(20):
+            ops.in_batch_softmax_loss(q, d, 0.1, compute_dtype=dt).backward()
+        _lib.TIMER.enabled = False
+        s = _lib.TIMER.summary()
+        f, b = s["tt_inbatch_fwd"]["mean_ms"], s["tt_inbatch_bwd"]["mean_ms"]
+        print(json.dumps(dict(B=B, M=M, H=H, dt=dt, fwd_us=round(f * 1e3, 1), bwd_us=round(b * 1e3, 1),
+                              algo_tflops=round(6 * B * M * H / ((f + b) * 1e-3) / 1e12, 1))), flush=True)
+
+
+def scorer_dp(a):
+    B, H, T, P = 8192, 256, _lib.TT_INBATCH_TAIL_ROWS, _lib.TT_INBATCH_MAX_PARTS
+    M = 2 * B
+    dt = _lib.compute_dtype_code(a.shape or "bf16")
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=DEV).manual_seed(0)
+    unit = lambda n: torch.nn.functional.normalize(torch.randn(n, H, device=DEV, generator=g), dim=-1)  # noqa
+    for W in (1, 2, 4, 8):
+        q, d_all, q_all = unit(B), unit(W * M), unit(W * B)
+        qb = torch.empty(B + T, H, dtype=torch.bfloat16, device=DEV)
+        qn = torch.empty(B, device=DEV)
+        call("tt_inbatch_prep_rows", ptr(q), B, H, ptr(qb), ptr(qn), None, st)
+        db_all = torch.empty(W * M + T, H, dtype=torch.bfloat16, device=DEV)
+        parts = torch.empty(P, device=DEV)
+        call("tt_inbatch_prep_rows", ptr(d_all), W * M, H, ptr(db_all), None, ptr(parts), st)
+        qb_all = torch.empty(W * B + T, H, dtype=torch.bfloat16, device=DEV)
+        call("tt_inbatch_prep_rows", ptr(q_all), W * B, H, ptr(qb_all), None, None, st)
+        db = db_all[:M + T]
+        ws = torch.empty(_lib.lib().tt_inbatch_ex_ws_size(B, W * M, W * B, M, H, dt), dtype=torch.uint8, device=DEV)
+        lse, lse2, rows = (torch.empty(B, device=DEV) for _ in range(3))
+        loss = torch.empty((), device=DEV)
+        dqu, dq, dd = torch.empty(B, H, device=DEV), torch.empty(B, H, device=DEV), torch.empty(M, H, device=DEV)
+        lse2_all = torch.empty(W * B + T, device=DEV)
+        gl = torch.ones(1, device=DEV)
+
+        def fwd():
+            call("tt_inbatch_fwd_ex", ptr(qb), ptr(qn), B, ptr(db_all), ptr(parts), P, W * M, H, dt, 10.0, 0, 1,
+                 ptr(lse), ptr(lse2), ptr(rows), ptr(loss), ptr(dqu), ptr(ws), ws.numel(), st)
+
+        fwd()
+        lse2_all[:W * B] = lse2.repeat(W)
+        lse2_all[W * B:] = float("inf")
+
+        def bwd():
+            call("tt_inbatch_bwd_ex", ptr(qb_all), ptr(lse2_all), W * B, 0, ptr(db), M, B, 0, H, dt, 10.0, ptr(dqu),
+                 ptr(gl), 1.0 / B, ptr(dq), ptr(dd), ptr(ws), ws.numel(), st)
+
+        tf, tb = event_us(fwd, 10), event_us(bwd, 10)
+        fl = 4.0 * B * W * M * H
+        print(json.dumps({"world": W, "candidates": W * M, "fwd_us": round(tf, 1), "bwd_us": round(tb, 1),
+                          "fwd_tflops": round(fl / tf / 1e6, 1), "bwd_tflops": round(fl / tb / 1e6, 1)}), flush=True)
+
+
+def split_fwd(a):
+    B, M, H, T, P = 8192, 16384, 256, _lib.TT_INBATCH_TAIL_ROWS, _lib.TT_INBATCH_MAX_PARTS
+    dt = _lib.compute_dtype_code("bf16")
+    g = torch.Generator(device=DEV).manual_seed(0)
+    st = torch.cuda.current_stream().cuda_stream
+    for N in (2, 4, 8):
+        rank = N // 2
+        q = torch.nn.functional.normalize(torch.randn(B, H, device=DEV, generator=g), dim=-1)
+        d_all = torch.nn.functional.normalize(torch.randn(N * M, H, device=DEV, generator=g), dim=-1)
+        qb = torch.empty(B + T, H, dtype=torch.bfloat16, device=DEV)
+        qn = torch.empty(B, device=DEV)
+        call("tt_inbatch_prep_rows", ptr(q), B, H, ptr(qb), ptr(qn), None, st)
+        db_all = torch.zeros(N * M + T, H, dtype=torch.bfloat16, device=DEV)
+        parts_all = torch.zeros(N * P, device=DEV)
+        for r in range(N):
+            call("tt_inbatch_prep_rows", ptr(d_all[r * M:(r + 1) * M]), M, H, ptr(db_all[r * M:]), None,
+                 ptr(parts_all[r * P:]), st)
+        db = torch.zeros(M + T, H, dtype=torch.bfloat16, device=DEV)
+        db[:M] = db_all[rank * M:(rank + 1) * M]
+        parts = parts_all[rank * P:(rank + 1) * P].clone()
+        ws = torch.empty(_lib.lib().tt_inbatch_ex_ws_size(B, N * M, N * B, M, H, dt), dtype=torch.uint8, device=DEV)
+        lse, lse2, rows = (torch.empty(B, device=DEV) for _ in range(3))
+        loss = torch.empty((), device=DEV)
+        dqu = torch.empty(B, H, device=DEV)
+        one = lambda: call("tt_inbatch_fwd_ex", ptr(qb), ptr(qn), B, ptr(db_all), ptr(parts_all), N * P, N * M,  # noqa
+                           H, dt, 10.0, rank * M, 1, ptr(lse), ptr(lse2), ptr(rows), ptr(loss), ptr(dqu), ptr(ws),
+                           ws.numel(), st)
+
+        def two():
+            call("tt_inbatch_fwd_ex_local", ptr(qb), ptr(qn), B, ptr(db), ptr(parts), P, M, N * M, rank * M, H, dt,
+                 10.0, ptr(ws), ws.numel(), st)
+            call("tt_inbatch_fwd_ex_remote", ptr(qb), ptr(qn), B, ptr(db_all), ptr(parts_all), N * P, ptr(parts), P,
+                 M, N * M, rank * M, H, dt, 10.0, 1, ptr(lse), ptr(lse2), ptr(rows), ptr(loss), ptr(dqu), ptr(ws),
+                 ws.numel(), st)
+
+        t1, t2 = event_us(one, 10), event_us(two, 10)
+        print(f"N={N}: one launch {t1:.1f} us, two launches {t2:.1f} us")
+
+
+def table_sync(a):
+    """gather: every rank runs the fused scatter + AdamW over all N ranks' sequences; shard: this
+    rank's dense V x E gradient + AdamW on V/N rows (links: reduce-scatter + all-gather); owner: the
+    N ranks' ids remapped to this rank's rows (others padding) and the fused update over a V/N-row
+    table, plus the sort plan over all N ranks' ids (links: factored all-gather + row all-gather)."""
+    B, L, E = 8192, 64, 256
+    shape = a.shape or "c3"
+    V, K = (200_000, 1) if shape == "c3" else (1_000_000, 4)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    table = torch.randn(V, E, device=DEV, generator=g) * 0.02
+    m, v = torch.zeros_like(table), torch.zeros_like(table)
+    _, args = adam_args()
+    own = ids_for(B, L, V, K)
+    nown = own.shape[0]
+    for R in (1, 2, 4, 8):
+        ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r) for r in range(1, R)]).contiguous()
+        N = ids.shape[0]
+        d_pooled = torch.randn(N, E, device=DEV, generator=g)
+        denom = (ids > 0).sum(1).float() + 1e-9
+        res = {"config": shape, "ranks": R, "tokens_per_rank": int((own > 0).sum())}
+        res["plan_all_ranks_us"] = graph_us(lambda: ops.BagPlan(ids, V, E, 0).wait())
+        pl = ops.BagPlan(ids, V, E, 0)
+        pl.wait()
+        res["gather_update_us"] = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, denom, pl, table, m,
+                                                                                       v, args))
+        del pl
+        p1 = ops.BagPlan(own, V, E, 0)
+        p1.wait()
+        gbuf = torch.empty(V, E, device=DEV)
+        Vs = -(-V // R)
+        res["plan_own_us"] = graph_us(lambda: ops.BagPlan(own, V, E, 0).wait())
+        res["shard_dense_grad_us"] = graph_us(lambda: ops.bag_mean_backward_planned(d_pooled[:nown], denom[:nown], p1,
+                                                                                    out=gbuf))
+        res["shard_adamw_us"] = graph_us(lambda: call("tt_adamw", ptr(table), ptr(gbuf), ptr(m), ptr(v), Vs * E, 1e-3,
+                                                      0.9, 0.999, 1e-8, 0.01, 1,
+                                                      torch.cuda.current_stream().cuda_stream))
+        del p1, gbuf
+        own_ids = torch.where(ids < Vs, ids, torch.zeros_like(ids)).contiguous()
+        res["owner_plan_us"] = graph_us(lambda: ops.BagPlan(own_ids, Vs, E, 0).wait())
+        po = ops.BagPlan(own_ids, Vs, E, 0)
+        po.wait()
+        res["owner_update_us"] = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, denom, po, table[:Vs],
+                                                                                      m[:Vs], v[:Vs], args))
+        del po, own_ids
+        seq_b = L * 4 + E * 4 + 4  # ids + d_pooled + denom per sequence
+        res = {k: (round(x, 1) if isinstance(x, float) else x) for k, x in res.items()}
+        res["link_MB_per_rank"] = {"gather": round((R - 1) * nown * seq_b / 1e6, 1),
+                                   "shard": round(2 * (R - 1) / R * V * E * 4 / 1e6, 1),
+                                   "owner": round(((R - 1) * nown * seq_b + (R - 1) / R * V * E * 4) / 1e6, 1)}
+        print(json.dumps(res), flush=True)
+        del d_pooled, ids, denom
+        torch.cuda.empty_cache()
+
+
+def scorer_once(a):
+    B, M, H = int(a.shape), int(a.rest[0]), int(a.rest[1])
+    dt = a.rest[2] if len(a.rest) > 2 else "bf16"
+    g = torch.Generator(device=DEV).manual_seed(0)
+    q = torch.nn.functional.normalize(torch.randn(B, H, device=DEV, generator=g), dim=-1).requires_grad_(True)
+    d = torch.nn.functional.normalize(torch.randn(M, H, device=DEV, generator=g), dim=-1).requires_grad_(True)
+    for _ in range(3):
+        ops.in_batch_softmax_loss(q, d, 0.1, compute_dtype=dt).backward()
+    torch.cuda.synchronize()
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
+                                     "scorer_once"])
+    ap.add_argument("shape", nargs="?", default=None)
+    ap.add_argument("rest", nargs="*")
+    ap.add_argument("--zipf", type=float, default=None)
+    a = ap.parse_args()
+    if a.what == "scorer_once" and len(a.rest) > 3:  # a variant library (tools/build_variants.sh)
+        _lib.LIB_PATH = os.path.abspath(a.rest[3])
+    if a.what == "scorer" and a.shape is not None:
+        a.rest = [a.shape] + a.rest
+    globals()[a.what](a)
+
+
+if __name__ == "__main__":
+    main()

@@ -5,11 +5,11 @@ set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/pmc_scorer}; DT=${2:-bf16}
 mkdir -p $OUT
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ks -o run -- python3 tools/mb_scorer_one.py 8192 16384 256 $DT > $OUT/ks.log 2>&1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ks -o run -- python3 tools/mb.py scorer_once 8192 16384 256 $DT > $OUT/ks.log 2>&1
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
 P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES"
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 tools/mb_scorer_one.py 8192 16384 256 $DT > $OUT/p$i.log 2>&1
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 tools/mb.py scorer_once 8192 16384 256 $DT > $OUT/p$i.log 2>&1
 done

@@ -11,4 +11,5 @@ run() {
 }
 run gather --table-sync gather
 run shard --table-sync shard
+run owner --table-sync owner
 run c5 --config c5

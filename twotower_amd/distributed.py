@@ -301,7 +301,7 @@ class GradSync:
     def _reduce(self, small, large) -> None:
         # synchronous collectives: they queue on the communicator's stream behind each other
         # either way, and an async_op collective waited on a forked stream crashes HIP graph
-        # capture at its end on this image (tools/dbg/capture_probe.py side_async_ar: segfault in
+        # capture at its end on this image (tools/repro/capture_probe.py side_async_ar: segfault in
         # hipStreamEndCapture; the same all-reduce without async_op captures and replays)
         if small:
             flat = torch.cat([p.grad.reshape(-1) for p in small])

@@ -1013,7 +1013,7 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
         # bf16 rows travel as bytes (any backend), rank-major; the zero tail stays local.  From 4
         # ranks on (M a multiple of 64) the forward runs in two launches: this rank's own
         # candidates are scored while the other ranks' rows arrive.  Splitting costs 35-39 us on
-        # one GPU (tools/mb_split_fwd.py: the local launch leaves CUs to the collective); the
+        # one GPU (tools/mb.py split_fwd: the local launch leaves CUs to the collective); the
         # gather it hides grows with N (~0.1 ms at 4 ranks).  TT_INBATCH_OVERLAP=1 / 0 forces it.
         ov = os.environ.get("TT_INBATCH_OVERLAP", "auto")
         split = M % 64 == 0 and (ov == "1" or (ov == "auto" and world >= 4))
