@@ -232,15 +232,14 @@ def scorer_entry(ops_t: dict, timing_steps: int, B: int, M: int, d: int, world: 
     stored_p = world == 1 and bwd_form == "stored" and (
         (scorer_dtype == "bf16" and B * M <= 2 ** 31) or (scorer_dtype == "fp32" and B * M <= 2 ** 30))
     fwd_key = "tt_inbatch_fwd_prepped" if "tt_inbatch_fwd_prepped" in ops_t else "tt_inbatch_fwd"
-    bwd_key = next(k for k in ("tt_inbatch_bwd_l2_mean", "tt_inbatch_bwd_l2", "tt_inbatch_bwd_mean", "tt_inbatch_bwd")
-                   if k in ops_t or k == "tt_inbatch_bwd")
+    bwd_key = "tt_inbatch_bwd_l2" if "tt_inbatch_bwd_l2" in ops_t else "tt_inbatch_bwd"
     if fwd_key not in ops_t or bwd_key not in ops_t:
         return None
     # one entry for both passes: the forward also forms P.D (dQ's product), so a per-pass split
     # of the 2BMH + 4BMH algorithmic flops would credit the backward with work the forward did
     fwd_ms, bwd_ms = ops_t[fwd_key]["mean_ms"], ops_t[bwd_key]["mean_ms"]
     l2_ms = None
-    if bwd_key in ("tt_inbatch_bwd_l2", "tt_inbatch_bwd_l2_mean"):
+    if bwd_key == "tt_inbatch_bwd_l2":
         # the backward combine also runs the tower head's F.normalize backward: the scorer is
         # charged what that pass costs beyond a plain tt_l2norm_bwd over the same rows
         l2_ms = l2_backward()

@@ -273,19 +273,15 @@ int tt_inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, 
                    void* ws, size_t ws_bytes, tt_stream_t stream);
 /* dq = grad_loss[0]*grad_scale*inv_tau*dq_unscaled;
  * dd[j] = grad_loss[0]*grad_scale*inv_tau * sum_i (P_ij - [j == i+label_off]) q~_i.
- * grad_scale is 1/B for the reference's mean reduction. */
+ * grad_scale is 1/B for the reference's mean reduction.
+ * loss_rows, loss: both NULL, or the forward's per-row losses (B floats) and where to put their
+ * mean, formed in one extra workgroup of the combine launch with tt_mean's arithmetic (the same
+ * bits): for a caller whose forward passed loss = NULL because the loss is read only after the
+ * backward (train_step.TrainStep), so the mean's own launch leaves the forward-to-backward path. */
 int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
                    float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
                    const float* grad_loss, float grad_scale, float* dq, float* dd,
-                   void* ws, size_t ws_bytes, tt_stream_t stream);
-/* tt_inbatch_bwd that also forms the mean of loss_rows (B floats) into *loss in one extra
- * workgroup of its combine launch, with tt_mean's arithmetic (the same bits): for a caller whose
- * forward passed loss = NULL because the loss is read only after the backward (train_step.TrainStep).
- * loss and loss_rows are both set or both NULL (then this is tt_inbatch_bwd). */
-int tt_inbatch_bwd_mean(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
-                        float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
-                        const float* grad_loss, float grad_scale, float* dq, float* dd,
-                        const float* loss_rows, float* loss, void* ws, size_t ws_bytes, tt_stream_t stream);
+                   const float* loss_rows, float* loss, void* ws, size_t ws_bytes, tt_stream_t stream);
 
 /* ---- the same loss from explicit, prepared operands (bf16 / bf16_split only), for data
  * parallelism with candidate-owner gradients (cross-device negatives without a gradient
@@ -323,18 +319,11 @@ int tt_inbatch_fwd_prepped(const float* q, const float* d, int64_t B, int64_t M,
  *   norms[r] = their norms before it; H = 256 with bf16 / bf16_split operands in ws from the
  *   forward, or H = 128 with fp32 operands): dx ((B + M) x H) = the gradient w.r.t. the rows
  *   before F.normalize, i.e. tt_inbatch_bwd's dq, dd followed by tt_l2norm_bwd, bit for bit,
- *   without writing dq and dd. */
+ *   without writing dq and dd.  loss_rows, loss: as tt_inbatch_bwd (the deferred loss mean). */
 int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau, int64_t label_off,
                       const float* lse, const float* dq_unscaled, const float* grad_loss, float grad_scale,
-                      const float* norms, float* dx, void* ws, size_t ws_bytes, tt_stream_t stream);
-/* tt_inbatch_bwd_l2_mean: the same, and *loss = the mean of loss_rows (B floats, the forward's
- *   per-row losses) formed in one extra workgroup of the same launch, bit for bit tt_mean's
- *   result: for a step whose forward passed loss = NULL (TrainStep: the loss is read only after
- *   the step), so the mean's own launch leaves the forward-to-backward critical path. */
-int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau,
-                           int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
-                           float grad_scale, const float* norms, float* dx, const float* loss_rows, float* loss,
-                           void* ws, size_t ws_bytes, tt_stream_t stream);
+                      const float* norms, float* dx, const float* loss_rows, float* loss, void* ws,
+                      size_t ws_bytes, tt_stream_t stream);
 #define TT_INBATCH_TAIL_ROWS 64
 #define TT_INBATCH_MAX_PARTS 512
 int tt_inbatch_prep_rows(const float* x, int64_t rows, int H, void* xb, float* norms, float* max_parts,

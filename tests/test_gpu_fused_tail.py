@@ -122,8 +122,8 @@ def test_pack_blocks_equals_cat(dtype, rows):
 @pytest.mark.parametrize("dt", ["bf16", "fp32"])
 @pytest.mark.parametrize("graph,B", [(False, 300), (True, 300), (True, 9000)])
 def test_trainstep_deferred_loss_mean_equals_own_launch(graph, B, dt, monkeypatch):
-    """The loss mean formed by the backward combine's extra workgroup (tt_inbatch_bwd_l2_mean;
-    fp32 at H = 128, no fused L2 backward: tt_inbatch_bwd_mean) equals tt_mean's launch bit for
+    """The loss mean formed by the backward combine's extra workgroup (tt_inbatch_bwd_l2, or
+    tt_inbatch_bwd when the L2 backward is not fused) equals tt_mean's launch bit for
     bit, and so does everything after it.  B 300: short strided tails; B 9000: past 8 x 1024
     rows, the eight-load loop."""
     V, L = 3000, 12

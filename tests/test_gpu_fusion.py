@@ -223,11 +223,11 @@ def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dty
     try:
         monkeypatch.setattr(ops, "call", spy)
         got_l, got = run()
-        assert "tt_inbatch_bwd_l2_mean" in seen and "tt_l2norm_bwd" not in seen
+        assert "tt_inbatch_bwd_l2" in seen and "tt_l2norm_bwd" not in seen
         monkeypatch.setenv("TT_FUSED_L2_BWD", "0")
         seen.clear()
         want_l, want = run()
-        assert "tt_inbatch_bwd_l2_mean" not in seen and "tt_l2norm_bwd" in seen
+        assert "tt_inbatch_bwd_l2" not in seen and "tt_l2norm_bwd" in seen
     finally:
         ops.set_inbatch_backward(prev)
     for a, b in zip(got_l, want_l):

@@ -118,13 +118,9 @@ _SIGNATURES = {
     "tt_inbatch_fwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp, _vp, _vp,
                                 _vp, _c_sz, _vp]),
     "tt_inbatch_bwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
-                                _vp, _vp, _c_sz, _vp]),
-    "tt_inbatch_bwd_mean": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32,
-                                     _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+                                _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_bwd_l2": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32, _vp,
-                                   _vp, _vp, _c_sz, _vp]),
-    "tt_inbatch_bwd_l2_mean": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _vp, _vp, _vp, _c_f32,
-                                        _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
+                                   _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_l2_prep": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp, _c_sz, _vp]),
     "tt_inbatch_fwd_prepped": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp,
                                         _vp, _vp, _vp, _c_sz, _vp]),

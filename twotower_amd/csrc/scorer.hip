@@ -2091,7 +2091,7 @@ void launch_bwd_combine(int64_t B, int64_t M, int H, int S, int64_t label_off, c
                         const int* xrows, const DT* Db, const float* lse2, hipStream_t s) {
   const float c2 = inv_tau * kLog2e;
   if constexpr (std::is_same<DT, float>::value) {
-    if (out.dx) {  // fp32, H = 128 (tt_inbatch_bwd_l2_mean checks the shape)
+    if (out.dx) {  // fp32, H = 128 (tt_inbatch_bwd_l2 checks the shape)
       bwd_combine_l2_128_kernel<<<dim3((unsigned)((B + M + 3) / 4 + (out.loss ? 1 : 0))), dim3(256), 0, s>>>(
           B, M, S, label_off, acc_part, Qlab, dqu, grad_loss, grad_scale, inv_tau, out.y, out.norms, out.dx, xrows, Db,
           lse2, c2, out.loss_rows, out.loss);
@@ -2577,14 +2577,6 @@ int inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
 }  // namespace tt
 
 extern "C" int tt_inbatch_bwd_l2(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau,
-                                 int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
-                                 float grad_scale, const float* norms, float* dx, void* ws, size_t ws_bytes,
-                                 tt_stream_t stream) {
-  return tt_inbatch_bwd_l2_mean(qd, B, M, H, dtype, inv_tau, label_off, lse, dq_unscaled, grad_loss, grad_scale, norms,
-                                dx, nullptr, nullptr, ws, ws_bytes, stream);
-}
-
-extern "C" int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int H, int dtype, float inv_tau,
                                       int64_t label_off, const float* lse, const float* dq_unscaled,
                                       const float* grad_loss, float grad_scale, const float* norms, float* dx,
                                       const float* loss_rows, float* loss, void* ws, size_t ws_bytes,
@@ -2594,27 +2586,20 @@ extern "C" int tt_inbatch_bwd_l2_mean(const float* qd, int64_t B, int64_t M, int
   TT_REQUIRE((H == 4 * kWave && dtype != TT_F32) || (H == 2 * kWave && dtype == TT_F32),
              "tt_inbatch_bwd_l2: H = 256 with bf16 operands or H = 128 fp32 (H=%d dtype=%d)", H, dtype);
   TT_REQUIRE(qd && lse && dq_unscaled && grad_loss && norms && dx && ws, "null pointer");
-  TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd_l2_mean: loss and loss_rows together");
+  TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd_l2: loss and loss_rows together");
   BwdOut out{nullptr, nullptr, qd, norms, dx, loss_rows, loss};
   return inbatch_bwd(qd, qd + B * H, B, M, H, dtype, inv_tau, label_off, dq_unscaled, grad_loss, grad_scale, out, ws,
                      ws_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
-extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype, float inv_tau,
-                              int64_t label_off, const float* lse, const float* dq_unscaled, const float* grad_loss,
-                              float grad_scale, float* dq, float* dd, void* ws, size_t ws_bytes, tt_stream_t stream) {
-  return tt_inbatch_bwd_mean(q, d, B, M, H, dtype, inv_tau, label_off, lse, dq_unscaled, grad_loss, grad_scale, dq, dd,
-                             nullptr, nullptr, ws, ws_bytes, stream);
-}
-
-extern "C" int tt_inbatch_bwd_mean(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
+extern "C" int tt_inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int dtype,
                                    float inv_tau, int64_t label_off, const float* lse, const float* dq_unscaled,
                                    const float* grad_loss, float grad_scale, float* dq, float* dd,
                                    const float* loss_rows, float* loss, void* ws, size_t ws_bytes, tt_stream_t stream) {
   int rc = check_args(B, M, H, dtype, label_off);
   if (rc) return rc;
   TT_REQUIRE(q && d && lse && dq_unscaled && grad_loss && dq && dd && ws, "null pointer");
-  TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd_mean: loss and loss_rows together");
+  TT_REQUIRE(!loss == !loss_rows, "tt_inbatch_bwd: loss and loss_rows together");
   BwdOut out{dq, dd};
   out.loss_rows = loss_rows;
   out.loss = loss;

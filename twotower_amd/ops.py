@@ -850,12 +850,9 @@ def _inbatch_bwd(meta, q, d, lse, dqu, ws, g, dq, dd, mean=None):
     """mean = (loss_rows, loss): the forward deferred the loss mean; the combine launch forms it."""
     B, M, H, dt, inv_tau, label_off, grad_scale = meta
     g = g.to(_FLOAT).contiguous().reshape(1)
-    if mean is not None:
-        call("tt_inbatch_bwd_mean", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g),
-             grad_scale, ptr(dq), ptr(dd), ptr(mean[0]), ptr(mean[1]), ptr(ws), ws.numel(), stream_of(q))
-        return
     call("tt_inbatch_bwd", ptr(q), ptr(d), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(g), grad_scale,
-         ptr(dq), ptr(dd), ptr(ws), ws.numel(), stream_of(q))
+         ptr(dq), ptr(dd), ptr(mean[0]) if mean else None, ptr(mean[1]) if mean else None, ptr(ws), ws.numel(),
+         stream_of(q))
 
 
 class InBatchSoftmaxLoss(torch.autograd.Function):
@@ -890,8 +887,8 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         want_grad = bool(ctx.needs_input_grad[0])
         ctx.l2_token = prep[4] if prep is not None else None
         # inside TrainStep (deferred_loss_mean) the loss is read only after the step: its mean is
-        # formed by the backward's combine launch (tt_inbatch_bwd_l2_mean, or tt_inbatch_bwd_mean
-        # when the head's L2 backward is not fused: fp32, H = 128) instead of a launch of its own
+        # formed by the backward's combine launch (tt_inbatch_bwd_l2, or tt_inbatch_bwd when the head's L2
+        # backward is not fused) instead of a launch of its own
         # between the forward combine and the backward engine
         defer = want_grad and _DEFER_MEAN[0] > 0 and os.environ.get("TT_DEFER_MEAN", "1") != "0"
         loss, lse, dqu, ws = _inbatch_fwd(ctx, q, d, inv_tau, 0, compute_dtype, grad_scale, want_grad,
@@ -912,7 +909,7 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
         if tok is not None and _FUSED_HEAD_BWD[0] > 0 and _l2_fusable(H, dt):
             # the head's F.normalize backward in the combine: grad is the head's dy (see _L2Token)
             gs = g.to(_FLOAT).contiguous().reshape(1)
-            call("tt_inbatch_bwd_l2_mean", ptr(qd), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(gs),
+            call("tt_inbatch_bwd_l2", ptr(qd), B, M, H, dt, inv_tau, label_off, ptr(lse), ptr(dqu), ptr(gs),
                  grad_scale, ptr(tok.norms), ptr(grad), ptr(dm[0]) if dm else None, ptr(dm[1]) if dm else None,
                  ptr(ws), ws.numel(), stream_of(qd))
             tok.dy = grad
