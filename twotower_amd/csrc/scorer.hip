@@ -241,75 +241,7 @@ __device__ __forceinline__ void map_tile(const f32x16& x, float (&e)[16], float 
 // ------------------------------------------------------------------------------------------
 // bf16 engine (32x32x16 bf16 MFMA).  PRECISE splits G into hi + lo bf16 so the second product
 // carries ~16 mantissa bits; otherwise G is rounded once (flash-attention style).
-// Schedule per 64-row stage (two 32-row X tiles, one barrier): S(0); then per tile j the next
-// tile's S chain is issued beside tile j's elementwise map (independent: the VALU fills the
-// MFMA issue gaps), then tile j's Acc chain.
-template <int H>
-__device__ __forceinline__ f32x16 s_chain(const lds_char_t* tile, int row, int hh, const bf16x8 (&cf)[H / 16]) {
-  using T = Tile<__bf16, H>;
-  constexpr int NK = H / 16;
-  const int rowb = row * T::ROWB, x = T::swz(row);
-  f32x16 acc = f32x16{};
-  bf16x8 a[4];
-#pragma unroll
-  for (int k = 0; k < 4 && k < NK; ++k)
-    a[k] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * k + hh) ^ x) << 4));
-#pragma unroll
-  for (int kk = 0; kk < NK; ++kk) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
-    if (kk + 4 < NK)
-      a[kk & 3] = *reinterpret_cast<const lds_bf16x8_t*>(tile + rowb + (((2 * (kk + 4) + hh) ^ x) << 4));
-  }
-  return acc;
-}
-
-template <bool PRECISE>
-__device__ __forceinline__ void pack_g(const float (&e)[16], bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float v = e[8 * s2 + jj];
-      const __bf16 h = (__bf16)v;
-      bh[s2][jj] = h;
-      if constexpr (PRECISE) bl[s2][jj] = (__bf16)(v - (float)h);
-    }
-}
-
-// Acc^T[h][col] += tile^T[h][rows] * G[rows][col] for one 32-row X tile.  k order inside a
-// step follows the accumulator layout: element j of lane half h is row 16 s + 8 (j>>2) + 4 h
-// + (j&3) (cdna_hip_programming.md §3), read as two 4-row transposed blocks.
-template <bool PRECISE, int H>
-__device__ __forceinline__ void acc_chain(const lds_char_t* tile, int jt, int lane, const bf16x8 (&bh)[2],
-                                          const bf16x8 (&bl)[2], f32x16 (&acc)[H / 32]) {
-  using T = Tile<__bf16, H>;
-  constexpr int NHT = H / 32;
-  const int tg = lane >> 4, ti = lane & 15, tq = ti >> 2, tp = ti & 3;
-  const int r0 = jt * 32 + 4 * (tg >> 1) + tq;  // (+16 s2 leaves swz unchanged: it reads row & 15)
-  const int x0 = T::swz(r0), x1 = T::swz(r0 + 8);
-  const int cbase = 2 * (tg & 1) + (tp >> 1), bo = (tp & 1) * 8;
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const int rb0 = (r0 + 16 * s2) * T::ROWB + bo, rb1 = (r0 + 16 * s2 + 8) * T::ROWB + bo;
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht) {
-      const int ch = 4 * ht + cbase;
-      const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb0 + ((ch ^ x0) << 4)));
-      const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tile + rb1 + ((ch ^ x1) << 4)));
-      const bf16x8 a = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-      acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh[s2], acc[ht], 0, 0, 0);
-      if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl[s2], acc[ht], 0, 0, 0);
-    }
-  }
-}
-
-// S chain of the next X tile fused, step by step, with the map of the current one: each step is
-// one MFMA, the operand read for the step four ahead, and the exp (+ bf16 pack) of 16/NK
-// elements of the current tile, fenced by sched_barrier(0) so the compiler keeps that interleave
-// (at one wave per SIMD nothing else hides a clump of transcendentals or an unprefetched read).
-struct NoHook {
-  __device__ void operator()(int) const {}
-};
+// The schedule: 'Forward unit U(j)' below.
 
 // The softmax map of one 32x32 X tile (16 elements per lane), processed in "slots" of one
 // element: an even slot forms the pair's scaled exponent with one v_pk_fma_f32 and takes the
@@ -375,10 +307,6 @@ struct MapState {
   }
 };
 
-// S chain of the next X tile fused, step by step, with map slots 0-7 of the current one: each
-// step is one MFMA, the operand read for the step four ahead and its share of the slots,
-// fenced by sched_barrier(0) so the compiler keeps that interleave (at one wave per SIMD nothing
-// else hides a clump of transcendentals or an unprefetched read).
 // Per-lane LDS byte offsets of the operand reads, relative to a stage base (computed once per
 // kernel).  S chain: chunk (2k + hh) ^ swz(row) of row r32 for k = 0..min(NK,8)-1; k >= 8 adds
 // 16 chunks (+256 B) and tile jt adds 32 rows: immediates.  Acc chain: the transposed 4-row
@@ -441,79 +369,6 @@ __device__ __forceinline__ const lds_char_t* lds_at(const lds_char_t* base, cons
   (void)vo_hi;
 #endif
   return tile + vo;
-}
-
-template <int MODE, bool PRECISE, int H, class Hook = NoHook>
-__device__ __forceinline__ f32x16 s_chain_map(const lds_char_t* tile, int jrow, const LdsOffs<H>& lo,
-                                              const bf16x8 (&cf)[H / 16], const f32x16& xa,
-                                              MapState<MODE, PRECISE>& ms, bf16x8 (&bh)[2], bf16x8 (&bl)[2],
-                                              Hook hook = Hook{}) {
-  using T = Tile<__bf16, H>;
-  constexpr int NK = H / 16;
-  const lds_char_t* tb = tile + jrow * T::ROWB;  // + per-lane offset + immediates
-  auto rd = [&](int k) {
-    return *reinterpret_cast<const lds_bf16x8_t*>(tb + lo.s[k & 7] + (k >= 8 ? 256 : 0));
-  };
-  f32x16 acc = f32x16{};
-  bf16x8 a[4];
-#pragma unroll
-  for (int k = 0; k < 4 && k < NK; ++k) a[k] = rd(k);
-#pragma unroll
-  for (int kk = 0; kk < NK; ++kk) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kk & 3], cf[kk], acc, 0, 0, 0);
-#ifndef TT_ABLATE_SREAD
-    if (kk + 4 < NK) a[kk & 3] = rd(kk + 4);
-#endif
-#pragma unroll
-    for (int v = 8 * kk / NK; v < 8 * (kk + 1) / NK; ++v) ms.slot(v, xa, bh, bl);
-    hook(kk);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  return acc;
-}
-
-// Acc chain with the transposed operand reads of each step issued kApf steps ahead.
-#ifndef TT_APF
-#define TT_APF 2
-#endif
-constexpr int kApf = TT_APF;
-template <int MODE, bool PRECISE, int H, class Hook = NoHook>
-__device__ __forceinline__ void acc_chain_pipelined(const lds_char_t* tile, int jt, const LdsOffs<H>& lo,
-                                                    bf16x8 (&bh)[2], bf16x8 (&bl)[2], f32x16 (&acc)[H / 32],
-                                                    const f32x16& xa, MapState<MODE, PRECISE>& ms, float& l_run,
-                                                    Hook hook = Hook{}) {
-  using T = Tile<__bf16, H>;
-  constexpr int NHT = H / 32;
-  constexpr int NS = 2 * NHT;  // steps: (s2, ht)
-  const lds_char_t* tb = tile + jt * 32 * T::ROWB;
-  auto load = [&](int st) {
-#ifdef TT_ABLATE_ACCREAD
-    return bf16x8{(__bf16)(float)st, 0, 0, 0, 0, 0, 0, (__bf16)(float)lo.s[0]};
-#endif
-    const int s2 = st / NHT, ht = st % NHT;
-    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
-    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
-    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
-    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-  };
-  bf16x8 op[kApf + 1];
-#pragma unroll
-  for (int k = 0; k < kApf && k < NS; ++k) op[k] = load(k);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int st = 0; st < NS; ++st) {
-    if (st + kApf < NS) op[(st + kApf) % (kApf + 1)] = load(st + kApf);
-    const int s2 = st / NHT, ht = st % NHT;
-    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % (kApf + 1)], bh[s2], acc[ht], 0, 0, 0);
-    if constexpr (PRECISE) acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % (kApf + 1)], bl[s2], acc[ht], 0, 0, 0);
-    if (st < NHT) {  // map slots 8-15 (G rows 16-31, first used at step NHT)
-#pragma unroll
-      for (int v = 8 + 8 * st / NHT; v < 8 + 8 * (st + 1) / NHT; ++v) ms.slot(v, xa, bh, bl);
-    }
-    hook(st);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if constexpr (MODE == FWD) l_run += ms.ls;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -679,32 +534,75 @@ __device__ long long g_tt_ktrace[2 * 1024 * 4];  // [bwd, fwd] per workgroup (wa
 
 // Stored probabilities (forward, bf16 engine): the backward can take G from the forward instead of
 // recomputing S = R C^T.  P is a grid of 2 KiB blocks, block (ct, qt) = candidates [32 ct, +32) x
-// queries [32 qt, +32), at byte ((ct * nqt) + qt) * 2048: 32 candidate rows of 64 B, each row's 32
-// queries permuted so that the 8 of one backward B-operand lane are contiguous (position
-// 16 (q >> 4) + 8 ((q >> 2) & 1) + 4 ((q >> 3) & 1) + (q & 3)).  The values are this wave's bf16
-// G = 2^(x c2 - shift_q); the backward folds 2^(shift_q - lse2_q) into its query rows.
-// In the forward a lane holds one query and 16 candidates; adjacent query lanes swap halves (one
-// DPP move and one v_perm per register) so each lane stores 4-byte query pairs: 8 stores per tile,
-// each writing 4 whole 64-B rows.
-__device__ __forceinline__ unsigned p_pos(int q) { return 16 * (q >> 4) + 8 * ((q >> 2) & 1) + 4 * ((q >> 3) & 1) + (q & 3); }
+// queries [32 qt, +32), at byte ((ct * nqt) + qt) * 2048.  Inside a block, byte
+//   1024 s2 + 32 c + 16 hh + 2 j   holds   G[candidate c][query 16 s2 + 8 (j >> 2) + 4 hh + (j & 3)]
+// for j = 0..7: the 16-byte fragment the backward's lane (c, hh) takes as its B operand of k-step
+// s2 (the queries in the A operand's k order), so one backward load and one forward store are each
+// a contiguous 1 KiB per wave-instruction.  The values are this wave's bf16 G = 2^(x c2 - shift_q);
+// the backward folds 2^(shift_q - lse2_q) into its query rows.
+// In the forward a lane holds one query and 16 candidates (registers 4g .. 4g+3 of the tile are
+// candidates 8g + 4hh + 0..3), so the tile is transposed through a 2 KiB per-wave LDS image
+// [query][candidate] with 64-B rows (cdna_hip_programming.md §3, 'An accumulator tile as the next
+// MFMA's operand'): four ds_write_b64 per lane, read back with four ds_read_b64_tr_b16 (lane i of
+// a 16-lane group receives candidate i of four query rows), then two 16-B stores per lane.  The
+// image's 8-byte slots are XOR-swizzled by (row >> 1) & 7 so both the writes (16 contiguous lanes,
+// 32 banks) and the transposed reads (32-lane halves, 64 banks) are conflict-free.  Round 3 did the
+// transpose in registers (a DPP move and a v_perm per register, eight 4-byte stores per tile).
+struct PStore {
+  unsigned w[4];  // LDS byte offsets of this lane's four 8-byte writes (register groups g = 0..3)
+  unsigned r[2];  // LDS byte offsets of its transposed reads (query rows +0 / +8); s2 adds 1024 B
+  unsigned g;     // byte offset of its 16-B fragment in a P block (s2 adds 1024 B)
+  __device__ __forceinline__ void init(unsigned img, int lane) {
+    const int r32 = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = img + r32 * 64 + 8 * ((2 * k + hh) ^ ((r32 >> 1) & 7));
+    const int i = lane & 15, g16 = lane >> 4, slot = 4 * (g16 & 1) + (i & 3);
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2) {
+      const int q = 8 * j2 + 4 * (g16 >> 1) + (i >> 2);  // (+16 s2 leaves (q >> 1) & 7 unchanged)
+      r[j2] = img + q * 64 + 8 * (slot ^ ((q >> 1) & 7));
+    }
+    this->g = (unsigned)(r32 * 32 + hh * 16);
+  }
+};
 
-// Store k (0..7) of a tile: register k & 3 of bh[k >> 2].  The engine issues them one per
-// acc-chain step (k * NS / 8), bh[1]'s after the map has finished it.
-__device__ __forceinline__ void store_p_piece(char* __restrict__ blk, unsigned lane_off, bool odd, const bf16x8 (&bh)[2],
-                                              int k) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const unsigned sel = odd ? 0x03020706u : 0x05040100u;
-  const unsigned x = __builtin_bit_cast(u32x4, bh[k >> 2])[k & 3];
-  const unsigned y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);  // lane ^ 1
-  const unsigned v = __builtin_amdgcn_perm(y, x, sel);
-  const int row = 16 * (k >> 2) + 8 * ((k >> 1) & 1) + 2 * (k & 1);  // + 4 hh + odd (in lane_off)
+// Acc-chain step `st` of a unit's P transpose (NSA steps per unit; bh[1] is complete from step
+// `w1`): the writes, the transposed reads two steps later, the stores once the reads have had a
+// few MFMAs to return.  Two stores per tile (kPStores): the stage's vmcnt waits count them.
+constexpr int kPStores = 2;
+template <int NSA>
+__device__ __forceinline__ void p_transpose_step(int st, int w1, const PStore& ps, const lds_char_t* lds, char* blk,
+                                                 const bf16x8 (&bh)[2], bf16x4 (&pt)[2][2]) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) u32x2 lds_u32x2_t;
+  auto at = [&](int step) { return step < NSA ? step : NSA - 1; };
+  lds_char_t* img = (lds_char_t*)lds;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (st == at(k < 2 ? 0 : w1)) {
+      const bf16x4 v = bf16x4{bh[k >> 1][4 * (k & 1)], bh[k >> 1][4 * (k & 1) + 1], bh[k >> 1][4 * (k & 1) + 2],
+                              bh[k >> 1][4 * (k & 1) + 3]};
+      *reinterpret_cast<lds_u32x2_t*>(img + ps.w[k]) = __builtin_bit_cast(u32x2, v);
+    }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    if (st == at(w1 + 1 + s2))
+#pragma unroll
+      for (int j2 = 0; j2 < 2; ++j2)
+        pt[s2][j2] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(lds + ps.r[j2] + 1024 * s2));
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    if (st == at(w1 + 5 + 2 * s2)) {
+      const bf16x8 v = bf16x8{pt[s2][0][0], pt[s2][0][1], pt[s2][0][2], pt[s2][0][3],
+                              pt[s2][1][0], pt[s2][1][1], pt[s2][1][2], pt[s2][1][3]};
 #ifdef TT_ABLATE_PSTORE  // timing ablation (never in a real build): no P stores
-  asm volatile("" ::"v"(v), "v"(blk + lane_off + row * 64));
-  return;
+      asm volatile("" ::"v"(v), "v"(blk + ps.g + 1024 * s2));
+      continue;
 #endif
-  // default cache policy: the backward, right after, finds part of P still in the Infinity Cache
-  // (measured: non-temporal stores and loads cost the backward 10 us at C3)
-  *reinterpret_cast<unsigned*>(blk + lane_off + row * 64) = v;
+      // default cache policy: the backward, right after, finds part of P still in the Infinity Cache
+      // (measured: non-temporal stores and loads cost the backward 10 us at C3)
+      *reinterpret_cast<bf16x8*>(blk + ps.g + 1024 * s2) = v;
+    }
 }
 
 __device__ __forceinline__ f32x4 load4(const float* p, int lane) { return reinterpret_cast<const f32x4*>(p)[lane]; }
@@ -799,7 +697,8 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
                                                 const DT* __restrict__ Qmat, const DT* __restrict__ Dmat,
                                                 float* __restrict__ lse, float* __restrict__ lse2,
                                                 float* __restrict__ dqu, DT* __restrict__ qs,
-                                                int* __restrict__ xrows, int lane) {
+                                                int* __restrict__ xrows, int lane, __bf16* __restrict__ qsp = nullptr,
+                                                int64_t qsp_plane = 0) {
   constexpr int H = 4 * kWave;
   l = __builtin_fmaf(-(float)n_pad, __builtin_amdgcn_exp2f(-sh), l);  // pad rows: X = 0 exactly
   const DT* qr = Qmat + i * H;
@@ -819,8 +718,10 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
       const int h = lane + kWave * u;
       if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
       if (qs) qs[i * H + h] = (DT)0.f;  // its stored P underflowed: the backward combine adds the row
+      if (qsp)
+        for (int pl = 0; pl < 3; ++pl) qsp[pl * qsp_plane + i * H + h] = (__bf16)0.f;
     }
-    if (qs && xrows && lane == 0) {  // flagged for the backward combine (which adds flagged rows in row order)
+    if ((qs || qsp) && xrows && lane == 0) {  // flagged for the backward combine (adds flagged rows in row order)
       xrows[1 + i] = 1;
       atomicAdd(xrows, 1);
     }
@@ -837,6 +738,14 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
     else
       reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
           bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
+  }
+  if (qsp) {  // the split-bf16 backward's planes of the same fp32 products
+    const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
+    bf16x4 pl[3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { __bf16 a0, a1, a2; split3(qv[u] * f, a0, a1, a2); pl[0][u] = a0; pl[1][u] = a1; pl[2][u] = a2; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) reinterpret_cast<bf16x4*>(qsp + k * qsp_plane + i * H)[lane] = pl[k];
   }
   if (lane == 0) {
     lse[i] = lse_i;
@@ -897,15 +806,14 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   lo.init(lane);
   // stored probabilities: this wave's query tile qt, candidate tile of (stage t, tile jt)
   const int64_t p_qt = cb * NW + wid;
-  const bool hh_odd = (r32 & 1) != 0;
-  const unsigned p_lane = 64u * (4 * hh + (r32 & 1)) + 2u * p_pos(r32 & ~1);
+  PStore ps;  // its per-wave transpose image follows the ring and the lse rows
+  if constexpr (STOREP) ps.init(T::LDS_BYTES + wid * 2048, lane);
   auto pblk = [&](int64_t t, int jt) {
     const int64_t ct = (row_begin + t * T::BJ) / 32 + jt;
     return pstore + (ct * p_nqt + p_qt) * 2048;
   };
   (void)pblk;
-  (void)p_lane;
-  (void)hh_odd;
+  (void)ps;
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // scalar per wave
   auto piece = [&](int c, int b, int64_t r0) {  // piece c of the stage at row r0 into buffer b
@@ -946,7 +854,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPC) : "memory");
   __syncthreads();
 
-#ifndef TT_FWD_V1
   // Stage t = units U(2t) (jt 0) and U(2t+1) (jt 1); each unit's S chain scores the NEXT 32-row
   // X tile, so jt 1's reads tile 0 of stage t+1.  One barrier per stage, at the start of U(2t):
   // after it stage t+1 is visible (the fills of this wave landed: vmcnt; in every wave: barrier),
@@ -989,12 +896,12 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const lds_char_t* ntl = lds + nbuf * T::STAGE_B;
     const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
     TT_TRACE(0);
-    // every VMEM op of stage t-1 (NPC fills, 8 P stores per tile) may still be in flight; all older
+    // every VMEM op of stage t-1 (NPC fills, kPStores P stores per tile) may still be in flight; all older
     // ones, among them the fills of stage t+1 (issued during stage t-2), have landed
     if (t == 0)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
     else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + (STOREP ? 8 * NJ : 0)) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + (STOREP ? kPStores * NJ : 0)) : "memory");
     TT_TRACE(1);
 #ifndef TT_ABLATE_BARRIER
     asm volatile("s_barrier" ::: "memory");
@@ -1009,15 +916,14 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
       MapState<MODE, PRECISE> ms;
       ms.init(c2, shift, lse4 + jt * 8, hh);
       char* blk = STOREP ? pblk(t, jt) : nullptr;
+      bf16x4 pt[2][2];  // the transposed P fragments between their reads and stores
       auto hook = [&](int i, const bf16x8 (&bh)[2]) {
 #pragma unroll
         for (int c = 0; c < NPC; ++c)
           if (c * (NJ * NSTEP) / NPC == jt * NSTEP + i) piece(c, fbuf, frow);
-        if constexpr (STOREP) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (NK + k * (2 * NHT) / 8 == i) store_p_piece(blk, p_lane, hh_odd, bh, k);
-        }
+        // bh[1] is complete after the S chain (kMapInS) or after Acc step NHT - 1
+        if constexpr (STOREP)
+          if (i >= NK) p_transpose_step<2 * NHT>(i - NK, kMapInS ? 1 : NHT, ps, lds, blk, bh, pt);
       };
       fwd_unit<MODE, PRECISE, H>(u, lo, cf, xin, xout, ms, ring, acc, l_run, hook);
       TT_TRACE(3 + jt);
@@ -1036,86 +942,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   }
 #else
   for (int64_t t = 0; t < ntiles; ++t) stage(t, std::integral_constant<int, -1>{});
-#endif
-#else
-  f32x16 xa = ntiles > 0 ? s_chain<H>(lds, r32, hh, cf) : f32x16{};
-  for (int64_t t = 0; t < ntiles; ++t) {
-    const int buf = (int)(t & 3), nbuf = (buf + 1) & 3, fbuf = (buf + 3) & 3;
-    const int64_t frow = stage_row(t + 3);
-    const lds_char_t* tile = lds + buf * T::STAGE_B;
-    const lds_f32x4_t* lse4 = reinterpret_cast<const lds_f32x4_t*>(lds + T::LSE_OFF + buf * 256);
-    // spread the NPC pieces of stage t+3 over the NK + 2*NHT steps after the barrier
-    constexpr int NSTEP = NK + 2 * NHT;
-    auto hook_s = [&](int step) {
-#pragma unroll
-      for (int c = 0; c < NPC; ++c)
-        if (c * NSTEP / NPC == step) piece(c, fbuf, frow);
-    };
-    auto hook_a = [&](int step) {
-#pragma unroll
-      for (int c = 0; c < NPC; ++c)
-        if (c * NSTEP / NPC == NK + step) piece(c, fbuf, frow);
-    };
-#pragma unroll
-    for (int jt = 0; jt < NJ; ++jt) {
-      TT_TRACE(jt * 4);
-      f32x16 xb;
-      bf16x8 bh[2], bl[2];
-      if (jt + 1 < NJ) {
-        MapState<MODE, PRECISE> ms;
-        ms.init(c2, shift, lse4 + jt * 8, hh);
-        xb = s_chain_map<MODE, PRECISE, H>(tile, (jt + 1) * 32, lo, cf, xa, ms, bh, bl);
-        TT_TRACE(jt * 4 + 3);
-        if constexpr (STOREP) {
-          char* blk = pblk(t, jt);
-          auto hook_p = [&](int st) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (k * (2 * NHT) / 8 == st) store_p_piece(blk, p_lane, hh_odd, bh, k);
-          };
-          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_p);
-        } else {
-          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run);
-        }
-      } else {
-        // stage t+1 landed: all but this wave's two newest fills (t+2, t+3's predecessor t+2 is
-        // newest; t+1 is the third newest) have retired
-        if constexpr (STOREP) {
-          // vmcnt counts the P stores too (8 per tile): after fills(t+1) come at least the stores
-          // of tiles (t-1, 0), (t-1, 1), (t, 0) and fills(t+2); at t = 0 only fills(2) and (0, 0)'s
-          if (t == 0)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + 8) : "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + 24) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC) : "memory");
-        }
-        TT_TRACE(jt * 4 + 1);
-#ifndef TT_ABLATE_BARRIER  // timing ablations (tools/ablate_scorer.sh); never defined in a real build
-        __syncthreads();  // ... in every wave, and every wave is past stage t-1
-#endif
-        TT_TRACE(jt * 4 + 2);
-        // (after the last stage this scores a stale stage; the result is dropped)
-        MapState<MODE, PRECISE> ms;
-        ms.init(c2, shift, lse4 + jt * 8, hh);
-        xb = s_chain_map<MODE, PRECISE, H>(lds + nbuf * T::STAGE_B, 0, lo, cf, xa, ms, bh, bl, hook_s);
-        TT_TRACE(jt * 4 + 3);
-        if constexpr (STOREP) {
-          char* blk = pblk(t, jt);
-          auto hook_ap = [&](int st) {
-            hook_a(st);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (k * (2 * NHT) / 8 == st) store_p_piece(blk, p_lane, hh_odd, bh, k);
-          };
-          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_ap);
-        } else {
-          acc_chain_pipelined<MODE, PRECISE, H>(tile, jt, lo, bh, bl, acc, xa, ms, l_run, hook_a);
-        }
-      }
-      xa = xb;
-    }
-  }
 #endif
   if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
@@ -1145,37 +971,9 @@ __device__ __forceinline__ bf16x8 p_load(const char* sbase, unsigned voff) {
   r = i32x4{(int)voff, s2, imm_extra, (int)(uintptr_t)sbase};
   return __builtin_bit_cast(bf16x8, r);
 #endif
-  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "n"(32 * s2 + imm_extra)
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "n"(1024 * s2 + imm_extra)
                : "memory");
   return __builtin_bit_cast(bf16x8, r);
-}
-
-template <int H, class Hook>
-__device__ __forceinline__ void acc_chain_p(const lds_char_t* tile, int jt, const LdsOffs<H>& lo, const bf16x8 (&g)[2],
-                                            f32x16 (&acc)[H / 32], Hook hook) {
-  using T = Tile<__bf16, H>;
-  constexpr int NHT = H / 32;
-  constexpr int NS = 2 * NHT;
-  const lds_char_t* tb = tile + jt * 32 * T::ROWB;
-  auto load = [&](int st) {
-    const int s2 = st / NHT, ht = st % NHT;
-    const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
-    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
-    const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
-    return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-  };
-  bf16x8 op[kApf + 1];
-#pragma unroll
-  for (int k = 0; k < kApf && k < NS; ++k) op[k] = load(k);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int st = 0; st < NS; ++st) {
-    if (st + kApf < NS) op[(st + kApf) % (kApf + 1)] = load(st + kApf);
-    const int s2 = st / NHT, ht = st % NHT;
-    acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(op[st % (kApf + 1)], g[s2], acc[ht], 0, 0, 0);
-    hook(jt * NS + st);
-    __builtin_amdgcn_sched_barrier(0);
-  }
 }
 
 // CW = candidate tiles (of 32) per wave.  CW = 2 (H = 256): every transposed Qs operand read feeds
@@ -1219,9 +1017,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 #endif
     glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024);
   };
-  // a lane's fragment of a P block: candidate row r32, query positions (2 s2 + hh) * 8 .. + 8
+  // a lane's fragment of a P block: candidate r32, queries 16 s2 + 8 (j >> 2) + 4 hh + (j & 3) (PStore)
   const char* pcol = P + ct0 * p_nqt * 2048;
-  const unsigned pvo = (unsigned)(r32 * 64 + hh * 16);
+  const unsigned pvo = (unsigned)(r32 * 32 + hh * 16);
   // P fragments of stages t .. t+3 in five register sets (index t % 5): the loads of stage t+3
   // go into the set stage t-2 read, so no load is in flight into registers an MFMA of the
   // previous stage may still be reading (the asm loads are outside the compiler's hazard checks)
@@ -1534,14 +1332,312 @@ void score_f32_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Split-bf16 engine for fp32 operands (round 4; the fp32 stored-P forward and backward at
+// H = 64, 128, 256).  Each fp32 operand is cut into three bf16 terms, x = x0 + x1 + x2 exactly
+// (split3, the tower head's scheme), and a product x y is formed from the six cross terms of
+// order >= 2^-16 (x0y2, x1y1, x2y0, x0y1, x1y0, x0y0, smallest first) on the 32x32x16 bf16 MFMA
+// with fp32 accumulation: six 32-cycle MFMAs do the work of eight 64-cycle 32x32x2 f32 MFMAs,
+// 2.7x the fp32 MFMA rate at fp32-product accuracy (the dropped terms are below 2^-24 relative).
+//   forward:  X = R C^T from the candidate planes (an LDS ring of 32-row stages, three planes per
+//             stage in the bf16 engine's row layout) and the query planes (VGPRs, split at entry
+//             from the fp32 rows); G = 2^(X c2 - shift) in fp32 (score_f32_kernel's map), stored
+//             to P as fp32 in score_f32_kernel's block layout; then Acc^T += R^T G with G split
+//             into three planes (the B operand) and R^T read with ds_read_b64_tr_b16.
+//   backward: Acc^T = Qs^T G (= dD^T) from the scaled-query planes (fwd_combine writes them) and G
+//             loaded from P (asm loads two stages ahead) and split in registers.
+// One wave per SIMD (the one-round grids of these shapes hold one workgroup per CU): the stage
+// loop is a straight unrolled stream the compiler schedules; a three-stage ring with one barrier
+// per stage keeps two stages of fills in flight.
+template <int H>
+struct SplitTile {
+  using T = Tile<__bf16, H>;  // a plane's rows: the bf16 engine's layout (ROWB, swizzle, LdsOffs)
+  static constexpr int BJ = 32;
+  static constexpr int PLANE_B = BJ * T::ROWB;
+  static constexpr int STAGE_B = 3 * PLANE_B;
+  static constexpr int NPP = PLANE_B / 1024 / NW;  // fill pieces per wave per plane
+  static constexpr int NF = 3 * NPP;                // ... per stage
+  static constexpr int NSTAGE = 3;
+  static constexpr int LDS_BYTES = NSTAGE * STAGE_B;
+  static_assert(NPP >= 1 && NPP * 1024 * NW == PLANE_B, "a plane tile is a whole number of 1 KiB pieces per wave");
+  static_assert(BJ == Tile<float, H>::BJ, "the plan's row tiles (bj_for(TT_F32)) are this engine's stages");
+};
+
+__device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// acc += a b over the six cross terms (a, b: three planes each)
+__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8& b0, const bf16x8& b1, const bf16x8& b2,
+                                       f32x16 acc) {
+  acc = mfma_bf16(a[0], b2, acc);
+  acc = mfma_bf16(a[1], b1, acc);
+  acc = mfma_bf16(a[2], b0, acc);
+  acc = mfma_bf16(a[0], b1, acc);
+  acc = mfma_bf16(a[1], b0, acc);
+  return mfma_bf16(a[0], b0, acc);
+}
+
+// G planes of a 32x32 tile from its 16 fp32 values per lane: plane p, k-step s2, element j = G row
+// 16 s2 + 8 (j >> 2) + 4 hh + (j & 3) (the accumulator order: the B operand of the Acc chain).
+__device__ __forceinline__ void split_tile(const float (&e)[16], bf16x8 (&g)[3][2]) {
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    __bf16 a0, a1, a2;
+    split3(e[v], a0, a1, a2);
+    g[0][v >> 3][v & 7] = a0;
+    g[1][v >> 3][v & 7] = a1;
+    g[2][v >> 3][v & 7] = a2;
+  }
+}
+
+// Acc^T += R^T G for one 32-row stage tile (three planes at tile + p * PLANE_B).
+template <int H>
+__device__ __forceinline__ void split_acc_chain(const lds_char_t* tile, const LdsOffs<H>& lo, const bf16x8 (&g)[3][2],
+                                                f32x16 (&acc)[H / 32]) {
+  using ST = SplitTile<H>;
+  using T = typename ST::T;
+  constexpr int NHT = H / 32;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht) {
+      const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+      bf16x8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const lds_char_t* tb = tile + p * ST::PLANE_B + imm;
+        const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3]));
+        const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3]));
+        a[p] = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+      }
+      acc[ht] = mfma6(a, g[0][s2], g[1][s2], g[2][s2], acc[ht]);
+    }
+}
+
+// Per-lane source offsets of a plane tile's NPP fill pieces (the swizzle on the source side, as
+// make_fill_offs).
+template <int H>
+__device__ __forceinline__ void split_fill_offs(unsigned (&fo)[SplitTile<H>::NPP]) {
+  using T = typename SplitTile<H>::T;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < SplitTile<H>::NPP; ++c) {
+    const int p = (c * NW + wid) * 1024 + lane * 16;
+    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
+    fo[c] = (unsigned)(row * T::ROWB + ((slot ^ T::swz(row)) << 4));
+  }
+}
+
+// R: three bf16 planes of nR rows + a kTailRows zero tail each (plane stride `plane` elements), so
+// every stage is a full tile from one scalar base.  C: the fp32 query rows.  P: fp32 blocks of
+// score_f32_kernel's layout.
+template <int H>
+__global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
+    const __bf16* __restrict__ R, int64_t plane, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
+    int64_t rows_per_split, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part, int n_dmax,
+    float* __restrict__ acc_part, float* __restrict__ l_part, float* __restrict__ P, int64_t p_nqt) {
+  using ST = SplitTile<H>;
+  constexpr int NK = H / 16, NHT = H / 32, NF = ST::NF;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t my_col = cb * (32 * NW) + wid * 32 + r32;
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + ST::BJ - 1) / ST::BJ : 0;
+  const float dmax = fold_dmax(dmax_part, n_dmax);  // wave-uniform call
+  const float shift = my_col < nC ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
+
+  unsigned fo[ST::NPP];
+  split_fill_offs<H>(fo);
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
+  auto fill = [&](int b, int64_t t) {  // stage t into ring slot b (past the last stage: stage 0 again)
+    const int64_t r0 = t < ntiles ? row_begin + t * ST::BJ : row_begin;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int c = 0; c < ST::NPP; ++c)
+        glds_dwordx4_s(fo[c], R + p * plane + r0 * H, wbase + b * ST::STAGE_B + p * ST::PLANE_B + c * NW * 1024);
+  };
+  fill(0, 0);
+  fill(1, 1);
+
+  bf16x8 cf[3][NK];  // query planes: lane (r32, hh) holds elements 16 kk + 8 hh + 0..7 of its query
+  {
+    const bool ok = my_col < nC;
+    const f32x4* src = reinterpret_cast<const f32x4*>(C + (ok ? my_col : 0) * H);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const f32x4 u0 = src[4 * kk + 2 * hh], u1 = src[4 * kk + 2 * hh + 1];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = ok ? (j < 4 ? u0[j] : u1[j - 4]) : 0.f;
+        __bf16 a0, a1, a2;
+        split3(x, a0, a1, a2);
+        cf[0][kk][j] = a0;
+        cf[1][kk][j] = a1;
+        cf[2][kk][j] = a2;
+      }
+    }
+  }
+  LdsOffs<H> lo;
+  lo.init(lane);
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  float l_run = 0.f;
+  int buf = 0;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    // stage t landed in this wave: younger VMEM ops are fills(t+1) and stage t-1's 16 P stores
+    if (t == 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 16) : "memory");
+    asm volatile("s_barrier" ::: "memory");  // ... in every wave; every wave is past stage t-1
+    fill(buf == 0 ? 2 : buf - 1, t + 2);     // into stage t-1's slot
+    const lds_char_t* tile = lds + buf * ST::STAGE_B;
+    // S chain: X = R C^T
+    f32x16 x = f32x16{};
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      bf16x8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[p] = *reinterpret_cast<const lds_bf16x8_t*>(tile + p * ST::PLANE_B + lo.s[kk & 7] + (kk >= 8 ? 256 : 0));
+      x = mfma6(a, cf[0][kk], cf[1][kk], cf[2][kk], x);
+    }
+    // the map (score_f32_kernel's arithmetic) and the fp32 P store
+    float e[16];
+    float ls = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      e[v] = __builtin_amdgcn_exp2f(x[v] * c2 - shift);
+      ls += e[v];
+    }
+    l_run += ls;
+    float* blk = P + (((row_begin >> 5) + t) * p_nqt + (my_col >> 5)) * 1024 + r32;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) blk[acc_row(v, hh) * 32] = e[v];
+    bf16x8 g[3][2];
+    split_tile(e, g);
+    split_acc_chain<H>(tile, lo, g, acc);
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  drain_dma();  // no LDS-DMA may outlive the workgroup
+  write_partials<FWD, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+}
+
+// P fragment of one 32-query tile for lane (candidate r32, hh): queries 8k + 4 hh + u (k, u < 4)
+// of its candidate row, four 16-B asm loads (no compiler vmcnt waits: the stage barrier counts them).
+struct SplitPSet {
+  f32x4 v[4];
+};
+__device__ __forceinline__ void split_p_load(SplitPSet& d, const float* sbase, unsigned voff) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    i32x4 r;
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "n"(32 * k) : "memory");
+    d.v[k] = __builtin_bit_cast(f32x4, r);
+  }
+}
+__device__ __forceinline__ void split_p_tie(SplitPSet& d) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(d.v[k]));
+}
+
+// Backward from stored fp32 P: R = the scaled-query planes (nR = B rows + zero tail), columns =
+// candidates (nC = M), dD^T partials per query split.
+template <int H>
+__global__ __launch_bounds__(NT, 1) void score_split_ddp_kernel(const __bf16* __restrict__ R, int64_t plane, int64_t nR,
+                                                                int64_t nC, int S, int64_t rows_per_split,
+                                                                const float* __restrict__ P, int64_t p_nqt,
+                                                                float* __restrict__ acc_part) {
+  using ST = SplitTile<H>;
+  constexpr int NHT = H / 32, NF = ST::NF;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;
+  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t ct = cb * NW + wid;  // this wave's 32-candidate tile
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + ST::BJ - 1) / ST::BJ : 0;
+
+  unsigned fo[ST::NPP];
+  split_fill_offs<H>(fo);
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
+  auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * ST::BJ : row_begin; };
+  auto fill = [&](int b, int64_t t) {
+    const int64_t r0 = stage_row(t);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int c = 0; c < ST::NPP; ++c)
+        glds_dwordx4_s(fo[c], R + p * plane + r0 * H, wbase + b * ST::STAGE_B + p * ST::PLANE_B + c * NW * 1024);
+  };
+  const float* pcol = P + ct * p_nqt * 1024;
+  const unsigned pvo = (unsigned)(r32 * 128 + hh * 16);
+  auto pload = [&](SplitPSet& d, int64_t t) { split_p_load(d, pcol + (stage_row(t) >> 5) * 1024, pvo); };
+  SplitPSet pf[3];
+  fill(0, 0);
+  pload(pf[0], 0);
+  fill(1, 1);
+  pload(pf[1], 1);
+  LdsOffs<H> lo;
+  lo.init(lane);
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  // stage t: fills(t) and P(t) landed once at most fills(t+1) and P(t+1) are in flight
+  auto stage = [&](int64_t t, int b, SplitPSet& cur, SplitPSet& nxt2) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 4) : "memory");
+    asm volatile("s_barrier" ::: "memory");
+    split_p_tie(cur);
+    float e[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[4 * k + u] = cur.v[k][u];
+    bf16x8 g[3][2];
+    split_tile(e, g);
+    fill(b == 0 ? 2 : b - 1, t + 2);  // into stage t-1's slot; P(t+2) into the set stage t-1 split
+    pload(nxt2, t + 2);
+    split_acc_chain<H>(lds + b * ST::STAGE_B, lo, g, acc);
+  };
+  // unrolled by the ring's three slots: every register set is named, no copies across iterations
+  int64_t t = 0;
+  for (; t + 3 <= ntiles; t += 3) {
+    stage(t, 0, pf[0], pf[2]);
+    stage(t + 1, 1, pf[1], pf[0]);
+    stage(t + 2, 2, pf[2], pf[1]);
+  }
+  if (t < ntiles) {
+    stage(t, 0, pf[0], pf[2]);
+    if (t + 1 < ntiles) stage(t + 1, 1, pf[1], pf[0]);
+  }
+  drain_dma();  // no load may outlive the workgroup
+#pragma unroll
+  for (int k = 0; k < 3; ++k) split_p_tie(pf[k]);
+  write_partials<DD, H>(acc, 0.f, split, nC, ct * 32 + r32, hh, acc_part, nullptr);
+}
+
+// ------------------------------------------------------------------------------------------
 // Operand prep, one launch for both matrices: blocks [0, gq) take the q rows, blocks [gq, grid)
 // the d rows (grid-stride, one wave per row).  Optional fp32 -> bf16 (RNE) copy, the row L2
 // norms of q, and for d one max norm per block (dmax_part[b]; readers fold the <= kMaxPrepBlocks
 // values themselves: no zero-initialised accumulator, no atomics).  Block 0 also writes the pad
 // rows (kPadBytes - 16 zero bytes, then +inf for the backward lse2).
 
+// xp: the rows as three bf16 planes (split3; plane stride xp_plane elements) for the split-bf16
+// fp32 engine.
 __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t rows, int H, __bf16* __restrict__ xb,
-                                          float* __restrict__ norms, int64_t b0, int64_t nb, float& mx) {
+                                          float* __restrict__ norms, int64_t b0, int64_t nb, float& mx,
+                                          __bf16* __restrict__ xp = nullptr, int64_t xp_plane = 0) {
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   if (H == 4 * kWave) {  // one float4 per lane per row: four rows' loads in flight per wave
     constexpr int U = 4;
@@ -1561,6 +1657,13 @@ __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t r
         if (xb && r < rows)
           reinterpret_cast<bf16x4*>(xb + r * H)[lane] =
               bf16x4{(__bf16)v[u][0], (__bf16)v[u][1], (__bf16)v[u][2], (__bf16)v[u][3]};
+        if (xp && r < rows) {
+          bf16x4 pl[3];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { __bf16 a0, a1, a2; split3(v[u][e], a0, a1, a2); pl[0][e] = a0; pl[1][e] = a1; pl[2][e] = a2; }
+#pragma unroll
+          for (int k = 0; k < 3; ++k) reinterpret_cast<bf16x4*>(xp + k * xp_plane + r * H)[lane] = pl[k];
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1582,6 +1685,13 @@ __device__ __forceinline__ void prep_rows(const float* __restrict__ x, int64_t r
       ss += sumsq4(v);
       if (xb)
         reinterpret_cast<bf16x4*>(xb + r * H)[c] = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      if (xp) {
+        bf16x4 pl[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { __bf16 a0, a1, a2; split3(v[e], a0, a1, a2); pl[0][e] = a0; pl[1][e] = a1; pl[2][e] = a2; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) reinterpret_cast<bf16x4*>(xp + k * xp_plane + r * H)[c] = pl[k];
+      }
     }
     const float n = sqrtf(wave_sum(ss));
     if (lane == 0 && norms) norms[r] = n;
@@ -1594,8 +1704,9 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
                                                       __bf16* __restrict__ qb, __bf16* __restrict__ db,
                                                       float* __restrict__ qnorm, float* __restrict__ dmax_part,
                                                       char* __restrict__ pad, float* __restrict__ lse2,
-                                                      int* __restrict__ xrows) {
+                                                      int* __restrict__ xrows, __bf16* __restrict__ dp = nullptr) {
   __shared__ float wmax[4];
+  const int64_t dp_plane = (M + kTailRows) * H;  // dp: the candidate planes (split-bf16 fp32 forward)
   if (blockIdx.x == 0) {
     if (xrows && threadIdx.x == 0) xrows[0] = 0;
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
@@ -1607,6 +1718,9 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
         db[M * H + i] = (__bf16)0.f;
       }
     }
+    if (dp)
+      for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x)
+        for (int k = 0; k < 3; ++k) dp[k * dp_plane + M * H + i] = (__bf16)0.f;
   }
   float mx = 0.f;
   if ((int)blockIdx.x < gq) {
@@ -1617,7 +1731,7 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
     return;
   }
   const int b = blockIdx.x - gq, gd = gridDim.x - gq;
-  prep_rows(d, M, H, db, nullptr, b, gd, mx);
+  prep_rows(d, M, H, db, nullptr, b, gd, mx, dp, dp_plane);
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   if (lane == 0) wmax[wid] = mx;
   __syncthreads();
@@ -1739,15 +1853,21 @@ __global__ __launch_bounds__(64 * kL2PrepWaves) void l2_prep_kernel(float* __res
 __global__ __launch_bounds__(256) void l2_prep128_kernel(float* __restrict__ y, int64_t B, int64_t M, int gq,
                                                          float* __restrict__ norms, float* __restrict__ qnorm,
                                                          float* __restrict__ dmax_part, char* __restrict__ pad,
-                                                         float* __restrict__ lse2, int* __restrict__ xrows) {
+                                                         float* __restrict__ lse2, int* __restrict__ xrows,
+                                                         __bf16* __restrict__ dp) {
   constexpr int H = 128;
   typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   __shared__ float wmax[4];
+  const int64_t dp_plane = (M + kTailRows) * H;  // dp: the candidate planes (split-bf16 fp32 forward)
   if (blockIdx.x == 0) {  // prep_qd_kernel's block-0 set-up (fp32: no operand copies)
     if (xrows && threadIdx.x == 0) xrows[0] = 0;
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
+    if (dp)
+      for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x)
+        for (int k = 0; k < 3; ++k) dp[k * dp_plane + M * H + i] = (__bf16)0.f;
   }
   const bool isq = (int)blockIdx.x < gq;
   const int64_t b0 = isq ? blockIdx.x : blockIdx.x - gq, nb = isq ? gq : gridDim.x - gq;
@@ -1766,6 +1886,13 @@ __global__ __launch_bounds__(256) void l2_prep128_kernel(float* __restrict__ y, 
     v[1] *= inv;
     *p = v;
     if (lane == 0) norms[base + r] = nrm;
+    if (dp && !isq) {
+      bf16x2 pl[3];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) { __bf16 a0, a1, a2; split3(v[e], a0, a1, a2); pl[0][e] = a0; pl[1][e] = a1; pl[2][e] = a2; }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) reinterpret_cast<bf16x2*>(dp + k * dp_plane + r * H)[lane] = pl[k];
+    }
     // prep_rows (H = 128): lane L < 32 holds elements 4L .. 4L + 3, i.e. lanes 2L and 2L + 1 here
     const int src = (2 * lane) & (kWave - 1);
     const f32x4 v4 = {__shfl(v[0], src), __shfl(v[1], src), __shfl(v[0], src + 1), __shfl(v[1], src + 1)};
@@ -1815,14 +1942,20 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     const float* __restrict__ acc_part, float inv_tau, int64_t label_off, const DT* __restrict__ Qmat,
     const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2, float* __restrict__ loss_rows,
     float* __restrict__ dqu, DT* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr,
-    int S_loc = 0, const float* __restrict__ dmax_loc = nullptr, int n_dmax_loc = 0) {
+    int S_loc = 0, const float* __restrict__ dmax_loc = nullptr, int n_dmax_loc = 0,
+    __bf16* __restrict__ qsp = nullptr) {
   // S_loc > 0 (data-parallel forward in two launches): slots [0, S_loc) hold the local launch's
-  // partials, formed with the local norm bound; they are rescaled to this launch's shift
+  // partials, formed with the local norm bound; they are rescaled to this launch's shift.
+  // qsp: the scaled query rows as three bf16 planes (split-bf16 fp32 backward) instead of qs.
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = lane_id();
+  const int64_t qsp_plane = (B + kTailRows) * H;
   if (i >= B) {  // the zero tail of the scaled query copy (the stored-P backward's R rows)
     if (qs && i < B + kTailRows)
       for (int h = lane; h < H; h += kWave) qs[i * H + h] = (DT)0.f;
+    if (qsp && i < B + kTailRows)
+      for (int h = lane; h < H; h += kWave)
+        for (int pl = 0; pl < 3; ++pl) qsp[pl * qsp_plane + i * H + h] = (__bf16)0.f;
     return;
   }
   const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
@@ -1838,7 +1971,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
           return sum_parts4(p + (int64_t)S_loc * B * (H / 4), B * (H / 4), S - S_loc) +
                  f_loc * sum_parts4(p, B * (H / 4), S_loc);
         },
-        sh, n_pad, M, c2, inv_tau, label_off, Qmat, Dmat, lse, lse2, dqu, qs, xrows, lane);
+        sh, n_pad, M, c2, inv_tau, label_off, Qmat, Dmat, lse, lse2, dqu, qs, xrows, lane, qsp, qsp_plane);
     if (lane == 0) loss_rows[i] = loss_i;
     return;
   }
@@ -1862,8 +1995,10 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
       if (h >= H) break;
       if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
       if (qs) qs[i * H + h] = (DT)0.f;  // its stored P underflowed: the backward combine adds the row
+      if (qsp)
+        for (int pl = 0; pl < 3; ++pl) qsp[pl * qsp_plane + i * H + h] = (__bf16)0.f;
     }
-    if (qs && xrows && lane == 0) {  // flagged for the backward combine (which adds flagged rows in row order)
+    if ((qs || qsp) && xrows && lane == 0) {  // flagged for the backward combine (adds flagged rows in row order)
       xrows[1 + i] = 1;
       atomicAdd(xrows, 1);
     }
@@ -1877,6 +2012,16 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   if (qs) {
     const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
     for (int h = lane; h < H; h += kWave) qs[i * H + h] = (DT)((float)qr[h] * f);
+  }
+  if (qsp) {
+    const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
+    for (int h = lane; h < H; h += kWave) {
+      __bf16 a0, a1, a2;
+      split3((float)qr[h] * f, a0, a1, a2);
+      qsp[i * H + h] = a0;
+      qsp[qsp_plane + i * H + h] = a1;
+      qsp[2 * qsp_plane + i * H + h] = a2;
+    }
   }
   if (lane == 0) {
     lse[i] = lse_i;
@@ -2150,6 +2295,8 @@ struct Ws {
   __bf16* Db;
   __bf16* Qs;   // stored-P backward: q~ scaled by 2^(shift - lse2) (+ zero tail)
   float* Qs32;  // ... the fp32 form (fp32 scorer: q scaled in fp32, P fp32)
+  __bf16* Qsp;  // ... as three bf16 planes (the split-bf16 fp32 backward), plane stride (B + tail) H
+  __bf16* Dp;   // split-bf16 fp32 forward: the candidate planes, plane stride (M + tail) H
   char* P;      // stored-P backward: bf16 probabilities, p_nct x p_nqt blocks of 2 KiB
   int* xrows;   // stored-P backward: [count, flag per query row] of queries the forward redid exactly
   int64_t p_nqt;
@@ -2179,6 +2326,13 @@ bool stored_p(int dtype, int64_t B, int64_t M) {
   return dtype == TT_F32 && B * M <= (int64_t(1) << 30);  // fp32 P: up to 4 GiB
 }
 
+// The fp32 stored-P passes run the split-bf16 engines (score_split_*_kernel) at H = 64, 128, 256;
+// H = 32 keeps score_f32_kernel's stored-P form (a 32-row plane tile is under one 1 KiB piece per
+// wave).  One workgroup per CU.
+bool split_f32(int H, int dtype, int64_t B, int64_t M) {
+  return dtype == TT_F32 && (H == 64 || H == 128 || H == 256) && stored_p(dtype, B, M);
+}
+
 // P grid: query tiles up to the forward's 128-column blocks, candidate tiles up to the
 // backward's 128-column blocks (every tile either engine touches exists)
 int64_t p_nqt_for(int64_t B) { return (B + 127) / 128 * 4; }
@@ -2200,6 +2354,9 @@ Plan ddp_plan(int64_t B, int64_t M, int H) {
 // everything else is scratch reused by both passes.
 Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const int BJ = bj_for(dtype);
+  const bool spl = split_f32(H, dtype, B, M);
+  // (sized for the engines' largest split counts: the split-bf16 passes plan for one workgroup per
+  // CU, never more splits than the fp32 engine's two)
   const Plan pf = plan_for(M, B, BJ, wg_per_cu(H, dtype, FWD)), pd = plan_for(B, M, BJ, wg_per_cu(H, dtype, DD));
   const bool bf = dtype != TT_F32;
   size_t off = 0;
@@ -2212,7 +2369,8 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   // never need per-lane redirection past the last row
   const size_t oq = take(bf ? (size_t)(B + kTailRows) * H * 2 : 0), od = take(bf ? (size_t)(M + kTailRows) * H * 2 : 0);
   const bool sp = stored_p(dtype, B, M);
-  const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * (bf ? 2 : 4) : 0);
+  const size_t oqs = take(sp ? (size_t)(B + kTailRows) * H * (bf ? 2 : spl ? 6 : 4) : 0);
+  const size_t odp = take(spl ? (size_t)3 * (M + kTailRows) * H * 2 : 0);
   const size_t op = take(sp ? (bf ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : (size_t)p_nqt_for(B) * p32_nct_for(M) * 4096)
                             : 0);
   const size_t ox = take(sp ? (size_t)(B + 1) * 4 : 0);
@@ -2220,7 +2378,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   if (sp && bf) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
-  if (sp && !bf) parts = std::max(parts, (size_t)plan_for(B, M, BJ, f32_waves(DD, H, true)).S * M * H * 4);
+  if (sp && !bf) parts = std::max(parts, (size_t)plan_for(B, M, BJ, spl ? 1 : f32_waves(DD, H, true)).S * M * H * 4);
   const size_t oa = take(parts);
   Ws w{};
   char* b = static_cast<char*>(base);
@@ -2228,7 +2386,9 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.Qb = reinterpret_cast<__bf16*>(b + oq);
     w.Db = reinterpret_cast<__bf16*>(b + od);
     w.Qs = sp && bf ? reinterpret_cast<__bf16*>(b + oqs) : nullptr;
-    w.Qs32 = sp && !bf ? reinterpret_cast<float*>(b + oqs) : nullptr;
+    w.Qs32 = sp && !bf && !spl ? reinterpret_cast<float*>(b + oqs) : nullptr;
+    w.Qsp = spl ? reinterpret_cast<__bf16*>(b + oqs) : nullptr;
+    w.Dp = spl ? reinterpret_cast<__bf16*>(b + odp) : nullptr;
     w.P = sp ? b + op : nullptr;
     w.xrows = sp ? reinterpret_cast<int*>(b + ox) : nullptr;
     w.p_nqt = p_nqt_for(B);
@@ -2252,8 +2412,17 @@ struct Skip {
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
                   const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
-  if (dtype == TT_F32 && MODE == FWD && w.P) {  // forward that also stores G (the fp32 stored-P backward)
-    score_f32_kernel<FWD, H, true><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
+  if constexpr (H >= 64) {
+    if (dtype == TT_F32 && MODE == FWD && w.P && w.Dp) {  // split-bf16 forward storing fp32 G
+      score_split_fwd_kernel<H><<<dim3(p.grid), dim3(NT), SplitTile<H>::LDS_BYTES, s>>>(
+          w.Dp, (nR + kTailRows) * H, nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, w.qnorm,
+          w.dmax_part, n_dmax, w.acc_part, w.l_part, reinterpret_cast<float*>(w.P), w.p_nqt);
+      TT_LAUNCH_CHECK("score_split_fwd");
+      return TT_OK;
+    }
+  }
+  if (H < 64 && dtype == TT_F32 && MODE == FWD && w.P) {  // H = 32: score_f32_kernel's stored-P forward
+    score_f32_kernel<FWD, (H < 64 ? H : 32), true><<<dim3(p.grid), dim3(NT), Tile<float, H>::LDS_BYTES, s>>>(
         static_cast<const float*>(R), nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, reinterpret_cast<float*>(w.P), w.p_nqt);
   } else if (dtype == TT_F32) {
@@ -2265,7 +2434,7 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, nullptr, 0, sk.begin, sk.len, sk.split_base);
   } else if (MODE == FWD && w.P) {
-    score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
+    score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES + NW * 2048, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, w.P, w.p_nqt);
   } else {
@@ -2327,8 +2496,8 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
              const float* dmax_part, int n_dmax, float inv_tau, int64_t label_off, float* lse, float* lse2,
              float* loss_rows, float* loss, float* dqu, const char* pad, float* l_part, float* acc_part,
              hipStream_t s, char* P = nullptr, int64_t p_nqt = 0, __bf16* Qs = nullptr, int* xrows = nullptr,
-             float* Qs32 = nullptr) {
-  const Plan p = plan_for(M, B, bj_for(dtype), wg_per_cu(H, dtype, FWD));
+             float* Qs32 = nullptr, const __bf16* Dp = nullptr, __bf16* Qsp = nullptr) {
+  const Plan p = plan_for(M, B, bj_for(dtype), Dp ? 1 : wg_per_cu(H, dtype, FWD));
   const float c2 = inv_tau * kLog2e;
   Ws w{};
   w.qnorm = const_cast<float*>(qnorm);
@@ -2338,14 +2507,15 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   w.acc_part = acc_part;
   w.P = P;
   w.p_nqt = p_nqt;
+  w.Dp = const_cast<__bf16*>(Dp);
   int rc;
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
-  const dim3 grid((unsigned)((B + (Qs || Qs32 ? kTailRows : 0) + 3) / 4)), block(256);
+  const dim3 grid((unsigned)((B + (Qs || Qs32 || Qsp ? kTailRows : 0) + 3) / 4)), block(256);
   if (dtype == TT_F32)
     fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                     acc_part, inv_tau, label_off, static_cast<const float*>(Cm),
                                                     static_cast<const float*>(Rm), lse, lse2, loss_rows, dqu, Qs32,
-                                                    Qs32 ? xrows : nullptr);
+                                                    Qs32 || Qsp ? xrows : nullptr, 0, nullptr, 0, Qsp);
   else
     fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                      acc_part, inv_tau, label_off, static_cast<const __bf16*>(Cm),
@@ -2408,24 +2578,28 @@ int bwd_core_p(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, co
 // Backward from the forward's stored fp32 probabilities: score_f32_kernel<DD, H, true> over Qs32
 // (q scaled by 2^(shift - lse2) in fp32) and P, then the fp32 combine (label terms from q, the
 // exact rows from q, d and lse2).
-int bwd_core_p32(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, const float* Qs32, const char* P,
-                 int64_t p_nqt, const float* q, const float* d, const float* dqu, const float* grad_loss,
+int bwd_core_p32(int64_t B, int64_t M, int H, int64_t label_off, float inv_tau, const float* Qs32, const __bf16* Qsp,
+                 const char* P, int64_t p_nqt, const float* q, const float* d, const float* dqu, const float* grad_loss,
                  float grad_scale, const BwdOut& out, const char* pad, float* acc_part, const int* xrows,
                  const float* lse2, hipStream_t s) {
-  const Plan p = plan_for(B, M, bj_for(TT_F32), f32_waves(DD, H, true));
+  const Plan p = plan_for(B, M, bj_for(TT_F32), Qsp ? 1 : f32_waves(DD, H, true));
   float* Pf = reinterpret_cast<float*>(const_cast<char*>(P));
-  switch (H) {
-#define TT_DDP32(HH)                                                                                               \
+  const int64_t plane = (B + kTailRows) * H;
+  switch (Qsp ? H : -H) {
+#define TT_SPLIT_DDP(HH)                                                                                           \
   case HH:                                                                                                         \
-    score_f32_kernel<DD, HH, true><<<dim3(p.grid), dim3(NT), Tile<float, HH>::LDS_BYTES, s>>>(                      \
-        Qs32, B, d, M, p.S, p.rows_per_split, 0.f, lse2, nullptr, nullptr, 0, pad, acc_part, nullptr, Pf, p_nqt);   \
+    score_split_ddp_kernel<HH><<<dim3(p.grid), dim3(NT), SplitTile<HH>::LDS_BYTES, s>>>(                            \
+        Qsp, plane, B, M, p.S, p.rows_per_split, Pf, p_nqt, acc_part);                                              \
     break;
-    TT_DDP32(32)
-    TT_DDP32(64)
-    TT_DDP32(128)
-    TT_DDP32(256)
-#undef TT_DDP32
-    default: set_error("in-batch scorer: H=%d unsupported (32, 64, 128, 256)", H); return TT_ERR_UNSUPPORTED;
+    TT_SPLIT_DDP(64)
+    TT_SPLIT_DDP(128)
+    TT_SPLIT_DDP(256)
+#undef TT_SPLIT_DDP
+    case -32:  // H = 32: score_f32_kernel's stored-P backward (split_f32)
+      score_f32_kernel<DD, 32, true><<<dim3(p.grid), dim3(NT), Tile<float, 32>::LDS_BYTES, s>>>(
+          Qs32, B, d, M, p.S, p.rows_per_split, 0.f, lse2, nullptr, nullptr, 0, pad, acc_part, nullptr, Pf, p_nqt);
+      break;
+    default: set_error("in-batch scorer: fp32 stored-P backward at H=%d", H); return TT_ERR_UNSUPPORTED;
   }
   TT_LAUNCH_CHECK("score_dd_p32");
   launch_bwd_combine<float>(B, M, H, p.S, label_off, acc_part, q, dqu, grad_loss, grad_scale, inv_tau, out, xrows, d,
@@ -2504,7 +2678,7 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
     const int gq = prep_blocks_q(B);
     prep_qd_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, s>>>(q, B, d, M, H, gq, bf ? w.Qb : nullptr,
                                                                    bf ? w.Db : nullptr, w.qnorm, w.dmax_part, w.pad,
-                                                                   w.lse2, w.xrows);
+                                                                   w.lse2, w.xrows, w.Dp);
     TT_LAUNCH_CHECK("score_prep");
   }
   const void* Rm = bf ? (const void*)w.Db : (const void*)d;
@@ -2512,7 +2686,8 @@ int inbatch_fwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
   const bool sp = want_grad && w.P;
   return fwd_core(dtype, Rm, M, Cm, B, H, w.qnorm, w.dmax_part, gd, inv_tau, label_off, lse, w.lse2, loss_rows, loss,
                   want_grad ? dq_unscaled : nullptr, w.pad, w.l_part, w.acc_part, s, sp ? w.P : nullptr, w.p_nqt,
-                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr, sp ? w.Qs32 : nullptr);
+                  sp ? w.Qs : nullptr, sp ? w.xrows : nullptr, sp ? w.Qs32 : nullptr, sp ? w.Dp : nullptr,
+                  sp ? w.Qsp : nullptr);
 }
 }  // namespace
 }  // namespace tt
@@ -2536,7 +2711,7 @@ extern "C" int tt_inbatch_l2_prep(float* y, int64_t B, int64_t M, int H, int dty
   const int gq = prep_blocks_q(B), gd = prep_blocks_d(M);
   if (dtype == TT_F32) {
     l2_prep128_kernel<<<dim3((unsigned)(gq + gd)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        y, B, M, gq, norms, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows);
+        y, B, M, gq, norms, w.qnorm, w.dmax_part, w.pad, w.lse2, w.xrows, w.Dp);
     TT_LAUNCH_CHECK("score_l2_prep128");
     return TT_OK;
   }
@@ -2566,7 +2741,7 @@ int inbatch_bwd(const float* q, const float* d, int64_t B, int64_t M, int H, int
   const void* Rm = bf ? (const void*)w.Qb : (const void*)q;  // operands left by the forward
   const void* Cm = bf ? (const void*)w.Db : (const void*)d;
   if (w.P && !bf)
-    return bwd_core_p32(B, M, H, label_off, inv_tau, w.Qs32, w.P, w.p_nqt, q, d, dq_unscaled, grad_loss, grad_scale,
+    return bwd_core_p32(B, M, H, label_off, inv_tau, w.Qs32, w.Qsp, w.P, w.p_nqt, q, d, dq_unscaled, grad_loss, grad_scale,
                         out, w.pad, w.acc_part, w.xrows, w.lse2, s);
   if (w.P) return bwd_core_p(B, M, H, label_off, inv_tau, w.Qs, w.P, w.p_nqt, w.Qb, dq_unscaled, grad_loss, grad_scale,
                              out, w.acc_part, w.xrows, w.Db, w.lse2, s);
