@@ -424,6 +424,41 @@ def bxb_scorer(cfg, scorer_dtype: str, dev, reps: int, steps: int, helpers: bool
     return e
 
 
+def c4_pairs_entry(cfg, scorer_dtype: str, dev, world: int, rank: int, steps: int, warmup: int, table_sync: str,
+                   use_graph: bool) -> dict:
+    """BASELINE.json configs[3] as it is stated (N ranks): (query, positive) pairs, every rank's positives
+    all-gathered as the candidates, M = N * B (65,536 global negatives at N = 8), timed like the main
+    line (barrier + synchronize around the steps, max over ranks).  The main line at N ranks keeps the
+    triplet form of configs[2] (M = N * 2B), so both C4 forms are reported."""
+    B, L, V, d = cfg["B"], cfg["L"], cfg["V"], cfg["d"]
+    emb, model = build_model(cfg, dev)
+    opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True,
+                         table_sync=table_sync)
+    loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype=scorer_dtype, cross_device_negatives=True)
+    step = tt.TrainStep(model, loss_fn, opt, graph=use_graph)
+    batches = [tt.data.synthetic_triplets(B, L, V, seed=rank * 1000 + 500 + k, device=dev)[:2] for k in range(4)]
+    for k in range(warmup):
+        step(*batches[k % len(batches)])
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(*batches[k % len(batches)])
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item()) / steps * 1e3
+    del step, opt, model, emb
+    return {"value": round(B * world / (ms * 1e-3), 1), "unit": "pairs/s", "ms_per_step": round(ms, 4),
+            "steps": steps, "warmup": warmup, "M": B * world,
+            "workload": f"C4 pairs form (configs[3]): {world} x {B} (query, positive) pairs, candidates = every "
+                        f"rank's positives (M = {B * world}), d {d}, L {L}, V {V}, {scorer_dtype} scorer, "
+                        f"table_sync {table_sync}, {'HIP graph' if use_graph else 'eager'}"}
+
+
 def plain_loop_entry(cfg, loss_fn, batches, dev, steps: int, trainstep_ms: float) -> dict:
     """PlainLoop timed on the bench's batches (fresh model, torch.optim.AdamW)."""
     _, model = build_model(cfg, dev)
@@ -630,6 +665,11 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # N ranks: configs[3] as stated (pairs form, M = N B) beside the main line's triplet form
+    c4p = None
+    if world > 1 and args.config == "c3" and not plain and not args.no_extras:
+        c4p = c4_pairs_entry(cfg, scorer_dtype, dev, world, rank, max(args.steps, 1), max(args.warmup, 1),
+                             args.table_sync, use_graph)
     ms_per_step = elapsed / args.steps * 1e3
     value = B * world * args.steps / elapsed
 
@@ -728,6 +768,8 @@ def main():
         "scorer_bxb": bxb,
         # the reference's train.py loop body unchanged around these registries (no TrainStep)
         "plain_loop": plain_entry,
+        # N ranks: BASELINE configs[3] as stated (pairs form, M = N B; the main line is the triplet form)
+        "c4_pairs": c4p,
         "cpu_baseline": cpu,
         "final_loss": float(loss.item()) if loss is not None else None,
     }

@@ -350,10 +350,13 @@ def test_in_batch_stored_backward_vs_oracle_and_recompute(H, B, M, off):
 @pytest.mark.parametrize("B,M,off", [(300, 700, 0), (129, 129, 0), (64, 256, 128), (1, 64, 0), (320, 330, 10),
                                      (2500, 2600, 100)])
 def test_in_batch_fp32_stored_backward_vs_oracle_and_recompute(H, B, M, off):
-    """The fp32 stored-probability backward (score_f32_kernel<DD, H, true>: G^T from the forward's
-    fp32 P, the per-query factor folded into an fp32 copy of q) against the float64 oracle at the
-    fp32 bar (1e-5) and against the fp32 recompute backward (same products; the scaled copy adds
-    one fp32 rounding per term).  B, M off the 32- and 128-row tiles exercise the partial blocks."""
+    """The fp32 stored-probability passes against the float64 oracle at the fp32 bar (1e-5) and
+    against the fp32 recompute form (score_f32_kernel, exact f32 MFMA).  H = 64, 128, 256: the
+    split-bf16 engines (score_split_fwd_kernel / score_split_ddp_kernel: six bf16 cross products
+    per fp32 product, G^T from the forward's fp32 P, the per-query factor folded into three bf16
+    planes of the scaled q); H = 32: score_f32_kernel's stored form, whose dq is the recompute
+    form's bit for bit (same forward).  B, M off the 32- and 128-row tiles exercise the partial
+    blocks."""
     rng = np.random.default_rng(11 * H + B + M)
     q, d = _unit(rng, B, H), _unit(rng, M, H)
     g = 0.7
@@ -372,7 +375,10 @@ def test_in_batch_fp32_stored_backward_vs_oracle_and_recompute(H, B, M, off):
     loss, dq, dd = grads["stored"]
     assert abs(loss - rl) < 1e-5 * max(1.0, abs(rl))
     assert rel(dq, rdq) < 1e-5 and rel(dd, rdd) < 1e-5
-    assert torch.equal(dq, grads["recompute"][1])
+    if H == 32:
+        assert torch.equal(dq, grads["recompute"][1])
+    else:
+        assert rel(dq, grads["recompute"][1]) < 1e-5
     assert rel(dd, grads["recompute"][2]) < 1e-5
 
 

@@ -32,8 +32,10 @@ def load(paths):
 def exch(mode, r, bw_gbs):
     """(GPU work us, exposed link us) of one table exchange per rank and step."""
     link_us = r["link_MB_per_rank"][mode] * 1e6 / (bw_gbs * 1e9) * 1e6
+    # the one-GPU step already holds its own plan (plan_own_us): gather and owner sort every rank's
+    # tokens instead, counted here as exposed (the plan runs on a side stream beside the forward)
     if mode == "gather":  # factored all-gather (overlaps nothing: it follows the backward), then the
-        work = r["gather_update_us"]  # replicated update over every rank's tokens
+        work = r["gather_update_us"] + r["plan_all_ranks_us"] - r["plan_own_us"]  # replicated update
         return work, link_us
     if mode == "shard":  # dense gradient, then per chunk: reduce-scatter -> AdamW(own) -> all-gather,
         work = r["shard_dense_grad_us"] + r["shard_adamw_us"]  # pipelined behind the next chunk's rows
@@ -42,7 +44,7 @@ def exch(mode, r, bw_gbs):
     ag_factored = (r["link_MB_per_rank"]["gather"]) * 1e6 / (bw_gbs * 1e9) * 1e6
     ag_rows = link_us - ag_factored
     work = r["owner_update_us"]
-    return work, ag_factored + max(0.0, ag_rows - work * 7 / 8)
+    return work + r["owner_plan_us"] - r["plan_own_us"], ag_factored + max(0.0, ag_rows - work * 7 / 8)
 
 
 def main():
