@@ -3,19 +3,25 @@ Usage: pmc_report.py OUTDIR [JSON]: with JSON, also write the per-pass MFMA util
 engines' average durations there (bench.py reports them beside the scorer's algorithmic rate)."""
 import csv, glob, json, sys, collections, re
 out = sys.argv[1]
+
+
+def _pass(name: str) -> str:
+    """forward engines: score_bf16_kernel<0, ...> (Li0E), score_ws_kernel, score_split_fwd_kernel"""
+    return "fwd" if ("<0," in name or "Li0E" in name or "score_ws" in name or "split_fwd" in name) else "bwd"
+
 js = {"passes": {}}
 ks = list(csv.DictReader(open(glob.glob(f"{out}/ks/**/*kernel_stats.csv", recursive=True)[0])))
 for r in ks:
     n = re.sub(r"\(.*", "", r["Name"].replace("tt::(anonymous namespace)::", "").replace("void ", ""))[:60]
     print(f"{n:62s} calls {r['Calls']:>4s} avg {float(r['AverageNs'])/1e3:8.1f} us")
     if n.startswith("score_"):
-        js["passes"].setdefault("fwd" if "<0," in n or "Li0E" in n else "bwd", {})["engine_us"] = round(
+        js["passes"].setdefault(_pass(n), {})["engine_us"] = round(
             float(r["AverageNs"]) / 1e3, 2)
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if "score_" in r["Kernel_Name"]:
-            k = "fwd" if "Li0E" in r["Kernel_Name"] or "<0," in r["Kernel_Name"] else "bwd"
+            k = _pass(r["Kernel_Name"])
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in vals.items():
     a = {c: sum(v) / len(v) for c, v in d.items()}

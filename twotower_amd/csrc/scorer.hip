@@ -46,7 +46,7 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
 typedef __attribute__((address_space(3))) f32x4 lds_f32x4_t;
 typedef __attribute__((address_space(3))) float lds_float_t;
 
-__device__ __forceinline__ int acc_row(int v, int hh) { return (v & 3) + 8 * (v >> 2) + 4 * hh; }
+__host__ __device__ constexpr int acc_row(int v, int hh) { return (v & 3) + 8 * (v >> 2) + 4 * hh; }
 
 // ------------------------------------------------------------------------------------------
 // LDS tile image shared by both engines: BJ rows of H elements, row-major, 16-byte chunk c of
@@ -953,6 +953,221 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Warp-specialised forward with stored probabilities (round 4; bf16, H = 256): the same products
+// and sums as score_bf16_kernel<FWD, false, H, true>, bit for bit, by eight waves per workgroup
+// (two per SIMD) in two roles instead of four waves doing everything:
+//   S waves 0-3 (query tile w): X = R C^T for both 32-row tiles of stage t, the softmax map
+//     (row sums l, G = 2^(x c2 - shift) rounded to bf16), G written to a per-tile LDS image
+//     [query][candidate] (the PStore image: ds_write_b64, swizzled);
+//   A waves 4-7 (query tile w - 4), one stage behind: Acc^T += R^T G for stage t-1 with G read
+//     back from the image as the B operand (the S lane's own registers, two ds_read_b64 per
+//     k-step), P from the same image by ds_read_b64_tr_b16 and 16-B stores.
+// Each wave holds half the state (S: the query operand, X; A: the 128-register Acc^T), so two
+// fit a SIMD and one wave's map, LDS waits and stores run beside the other's MFMAs: the stage's
+// 64 MFMAs per SIMD are the same, its exposed latency is what the pairing removes (the four-wave
+// engine measures ~3,100 cycles per stage against a 2,048-cycle MFMA floor).
+// One barrier per iteration; iteration i: S on stage i, A on stage i - 1, fills of stage i + 2
+// into the ring slot of stage i - 2 (read by S in i - 2 and by A in i - 1).  LDS: the four-stage
+// ring (128 KiB) + G images [tile pair 4][iteration parity 2][tile 2] x 2 KiB = 160 KiB.
+// TT_WS_SPREAD=1: each wave's NPW fill pieces of a stage are issued one every few MFMAs of its
+// first tile (a burst right after the barrier stalls the issuing wave on the address queue);
+// TT_WS_PRIO: s_setprio 1 for the A waves (1), the S waves (2) or neither (0).
+#ifndef TT_WS_SPREAD
+#define TT_WS_SPREAD 1
+#endif
+#ifndef TT_WS_PRIO
+#define TT_WS_PRIO 0
+#endif
+template <int H>
+struct WsTile {
+  using T = Tile<__bf16, H>;
+  static constexpr int NWS = 8;
+  static constexpr int RING_B = T::NSTAGE * T::STAGE_B;
+  static constexpr int G_OFF = RING_B;
+  static constexpr int LDS_BYTES = RING_B + 4 * 2 * 2 * 2048;
+  static constexpr int NPW = T::STAGE_B / 1024 / NWS;  // fill pieces per wave per stage
+  static_assert(NPW >= 1 && NPW * 1024 * NWS == T::STAGE_B, "whole 1 KiB pieces per wave");
+};
+
+template <int H>
+__global__ __launch_bounds__(512, 1) void score_ws_kernel(
+    const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
+    int64_t rows_per_split, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part, int n_dmax,
+    float* __restrict__ acc_part, float* __restrict__ l_part, char* __restrict__ pstore, int64_t p_nqt) {
+  using W = WsTile<H>;
+  using T = typename W::T;
+  constexpr int NK = H / 16, NHT = H / 32, NPW = W::NPW;
+  static_assert(T::NSTAGE == 4 && T::BJ == 64, "four-slot ring of 64-row stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const lds_char_t* lds = (const lds_char_t*)smem;
+  lds_char_t* ldsw = (lds_char_t*)smem;
+  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool accw = wid >= 4;  // wave-uniform role
+  const int pw = wid & 3;      // query tile of the workgroup
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int split = blockIdx.x % S;
+  const int64_t cb = blockIdx.x / S;
+  const int64_t my_col = cb * 128 + pw * 32 + r32;
+  const int64_t row_begin = (int64_t)split * rows_per_split;
+  const int64_t row_end = min(nR, row_begin + rows_per_split);
+  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
+
+  // fills: piece c of a stage is bytes (c * 8 + wid) KiB of its image (source-side swizzle)
+  unsigned fo[NPW];
+#pragma unroll
+  for (int c = 0; c < NPW; ++c) {
+    const int p = (c * W::NWS + wid) * 1024 + lane * 16;
+    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
+    fo[c] = (unsigned)(row * T::ROWB + ((slot ^ T::swz(row)) << 4));
+  }
+  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
+  auto piece = [&](int64_t t, int c) {  // piece c of stage t (past the last: stage 0 again, into a slot nobody reads)
+    const int64_t r0 = t < ntiles ? row_begin + t * T::BJ : row_begin;
+    glds_dwordx4_s(fo[c], R + r0 * H, wbase + (unsigned)(t & 3) * T::STAGE_B + c * W::NWS * 1024);
+  };
+  auto fill = [&](int64_t t) {
+#pragma unroll
+    for (int c = 0; c < NPW; ++c) piece(t, c);
+  };
+  // step i (of 2 NHT = NK per tile) of the first tile carries piece c when i == c * NK / NPW + 1
+  auto spread = [&](int64_t t, int i) {
+#pragma unroll
+    for (int c = 0; c < NPW; ++c)
+      if (TT_WS_SPREAD && i == c * NK / NPW + 1) piece(t, c);
+  };
+  fill(0);
+  fill(1);
+
+  LdsOffs<H> lo;
+  lo.init(lane);
+  PStore ps;  // the G image offsets of this tile pair (+ parity * 4 KiB + tile * 2 KiB)
+  ps.init(W::G_OFF + pw * 8192, lane);
+  const int64_t p_qt = cb * 4 + pw;
+
+  if (TT_WS_PRIO == (accw ? 1 : 2)) __builtin_amdgcn_s_setprio(1);
+  if (!accw) {
+    // ---------------- S waves: X = R C^T, the map, G to the image ----------------
+    const float dmax = fold_dmax(dmax_part, n_dmax);
+    const float shift = my_col < nC ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
+    bf16x8 cf[NK];
+    {
+      const bool ok = my_col < nC;
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(C + (ok ? my_col : 0) * H);
+#pragma unroll
+      for (int kk = 0; kk < NK; ++kk) {
+        bf16x8 v = src[2 * kk + hh];
+        if (!ok) v = bf16x8{};
+        cf[kk] = v;
+      }
+    }
+    float l_run = 0.f;
+    for (int64_t it = 0; it <= ntiles; ++it) {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW) : "memory");  // fills(it) landed; G(it-1) written
+      asm volatile("s_barrier" ::: "memory");
+      if (!TT_WS_SPREAD || it == ntiles) fill(it + 2);
+      if (it == ntiles) break;
+      const lds_char_t* tile = lds + (unsigned)(it & 3) * T::STAGE_B;
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const lds_char_t* tb = tile + jt * 32 * T::ROWB;
+        f32x16 x = f32x16{};
+#pragma unroll
+        for (int kk = 0; kk < NK; ++kk) {
+          const bf16x8 a = *reinterpret_cast<const lds_bf16x8_t*>(tb + lo.s[kk & 7] + (kk >= 8 ? 256 : 0));
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cf[kk], x, 0, 0, 0);
+          if (jt == 0) spread(it + 2, kk);
+        }
+        // the map in MapState's arithmetic and order: pair sums, then the tile's sum into l
+        float e[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[v], c2, -shift));
+        float ls = 0.f;
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) ls += e[v] + e[v + 1];
+        l_run += ls;
+        const unsigned img = (unsigned)((it & 1) * 4096 + jt * 2048);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        typedef __attribute__((address_space(3))) u32x2 lds_u32x2_t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bf16x4 v = bf16x4{(__bf16)e[4 * k], (__bf16)e[4 * k + 1], (__bf16)e[4 * k + 2], (__bf16)e[4 * k + 3]};
+          *reinterpret_cast<lds_u32x2_t*>(ldsw + ps.w[k] + img) = __builtin_bit_cast(u32x2, v);
+        }
+      }
+    }
+    drain_dma();
+    l_run += __shfl_xor(l_run, 32);
+    if (my_col < nC && hh == 0) l_part[(int64_t)split * nC + my_col] = l_run;
+    return;
+  }
+  // ---------------- A waves: Acc^T += R^T G one stage behind, P stores ----------------
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  // B operand of k-step s2 = the S lane's bh[s2]: slots 4 s2 + hh and 4 s2 + 2 + hh of row r32
+  unsigned gb[2][2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2)
+      gb[s2][j2] = W::G_OFF + pw * 8192 + r32 * 64 + 8 * ((4 * s2 + 2 * j2 + hh) ^ ((r32 >> 1) & 7));
+  for (int64_t it = 0; it <= ntiles; ++it) {
+    // younger than fills(it): fills(it+1), and the 4 P stores of iteration it-1 (it >= 2)
+    if (it >= 2)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW + 4) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW) : "memory");
+    asm volatile("s_barrier" ::: "memory");
+    if (!TT_WS_SPREAD || it == 0) fill(it + 2);
+    if (it == 0) continue;
+    const int64_t t = it - 1;
+    const lds_char_t* tile = lds + (unsigned)(t & 3) * T::STAGE_B;
+    const unsigned img = (unsigned)((t & 1) * 4096);
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      const unsigned gi = img + jt * 2048;
+      bf16x8 g[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x4 lo4 = *reinterpret_cast<const lds_bf16x4_t*>(lds + gb[s2][0] + gi);
+        const bf16x4 hi4 = *reinterpret_cast<const lds_bf16x4_t*>(lds + gb[s2][1] + gi);
+        g[s2] = bf16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+      }
+      const lds_char_t* tb = tile + jt * 32 * T::ROWB;
+#pragma unroll
+      for (int st = 0; st < 2 * NHT; ++st) {
+        const int s2 = st / NHT, ht = st % NHT;
+        const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+        const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
+        const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
+        const bf16x8 a = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
+        acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, g[s2], acc[ht], 0, 0, 0);
+        if (jt == 0) spread(it + 2, st);
+      }
+      // P: the transposed fragments of this tile's image, two 16-B stores
+      char* blk = pstore + (((row_begin + t * T::BJ) / 32 + jt) * p_nqt + p_qt) * 2048;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x4 u0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(lds + ps.r[0] + gi + 1024 * s2));
+        const bf16x4 u1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(lds + ps.r[1] + gi + 1024 * s2));
+        *reinterpret_cast<bf16x8*>(blk + ps.g + 1024 * s2) =
+            bf16x8{u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      }
+    }
+  }
+  drain_dma();
+  if (my_col < nC) {
+    float* dst = acc_part + ((int64_t)split * nC + my_col) * H;
+#pragma unroll
+    for (int ht = 0; ht < NHT; ++ht)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<f32x4*>(dst + ht * 32 + 8 * g4 + 4 * hh) =
+            f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // bf16 backward from stored probabilities (single-rounded G): Acc^T = Qs^T P_tile for every
 // 32-row query tile, with Qs = q~ scaled per row by 2^(shift_q - lse2_q) (fwd_combine), so that
 // Qs^T P = q~^T G exactly as the recompute engine forms it, minus its S chain and softmax map.
@@ -1489,12 +1704,18 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
   float l_run = 0.f;
   int buf = 0;
-  for (int64_t t = 0; t < ntiles; ++t) {
+  // G of stage t goes to P by asm stores from register set t & 1, which stays untouched until the
+  // wait at the top of stage t + 2 has seen those stores complete (compiler-placed stores made
+  // hipcc wait for them before reusing their data registers, vmcnt(0) inside the S chain)
+  float ev[2][16];
+  auto stage = [&](int64_t t, float (&e)[16]) {
     // stage t landed in this wave: younger VMEM ops are fills(t+1) and stage t-1's 16 P stores
     if (t == 0)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 16) : "memory");
+#pragma unroll
+    for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(e[v]));  // stage t-2's stores have read them
     asm volatile("s_barrier" ::: "memory");  // ... in every wave; every wave is past stage t-1
     fill(buf == 0 ? 2 : buf - 1, t + 2);     // into stage t-1's slot
     const lds_char_t* tile = lds + buf * ST::STAGE_B;
@@ -1509,7 +1730,6 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
       x = mfma6(a, cf[0][kk], cf[1][kk], cf[2][kk], x);
     }
     // the map (score_f32_kernel's arithmetic) and the fp32 P store
-    float e[16];
     float ls = 0.f;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -1517,15 +1737,27 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
       ls += e[v];
     }
     l_run += ls;
-    float* blk = P + (((row_begin >> 5) + t) * p_nqt + (my_col >> 5)) * 1024 + r32;
+    float* blk = P + (((row_begin >> 5) + t) * p_nqt + (my_col >> 5)) * 1024 + 4 * hh * 32 + r32;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) blk[acc_row(v, hh) * 32] = e[v];
+    for (int v = 0; v < 16; ++v)
+      asm volatile("global_store_dword %0, %1, off offset:%2" ::"v"(blk), "v"(e[v]), "n"(acc_row(v, 0) * 128)
+                   : "memory");  // (+ 4 hh rows in blk: hh is per lane)
     bf16x8 g[3][2];
     split_tile(e, g);
     split_acc_chain<H>(tile, lo, g, acc);
     buf = buf == 2 ? 0 : buf + 1;
+  };
+  int64_t t = 0;
+  for (; t + 2 <= ntiles; t += 2) {
+    stage(t, ev[0]);
+    stage(t + 1, ev[1]);
   }
-  drain_dma();  // no LDS-DMA may outlive the workgroup
+  if (t < ntiles) stage(t, ev[0]);
+  drain_dma();  // no LDS-DMA or P store may outlive the workgroup
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(ev[k][v]));
   write_partials<FWD, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
 }
 
@@ -2409,6 +2641,16 @@ struct Skip {
   int split_base = 0;          // partial slot of split 0
 };
 
+// The warp-specialised stored-P forward (score_ws_kernel) at H = 256; TT_WS_FWD=0 (read at load)
+// runs the four-wave engine instead (A/B measurement: the same bits either way).
+bool ws_forward() {
+  static const bool on = [] {
+    const char* e = std::getenv("TT_WS_FWD");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
                   const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
@@ -2433,6 +2675,10 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, nullptr, 0, sk.begin, sk.len, sk.split_base);
+  } else if (MODE == FWD && w.P && H == 256 && ws_forward()) {
+    score_ws_kernel<(H == 256 ? H : 256)><<<dim3(p.grid), dim3(512), WsTile<256>::LDS_BYTES, s>>>(
+        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, w.qnorm,
+        w.dmax_part, n_dmax, w.acc_part, w.l_part, w.P, w.p_nqt);
   } else if (MODE == FWD && w.P) {
     score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES + NW * 2048, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
