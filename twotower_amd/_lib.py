@@ -154,7 +154,10 @@ def side_stream(device: torch.device, role: str = "plan") -> torch.cuda.Stream:
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), role)
     st = _SIDE.get(key)
     if st is None:
-        st = _SIDE[key] = torch.cuda.Stream(device=key[0])
+        # the plan's small sort kernels at high priority: beside the bandwidth-bound gather they
+        # otherwise wait for CU slots and stretch (TT_PLAN_PRIORITY=0: normal priority, A/B only)
+        prio = -1 if role == "plan" and os.environ.get("TT_PLAN_PRIORITY", "1") != "0" else 0
+        st = _SIDE[key] = torch.cuda.Stream(device=key[0], priority=prio)
     return st
 
 

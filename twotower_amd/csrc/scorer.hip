@@ -768,7 +768,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     const float* __restrict__ dmax_part, int n_dmax,
     const char* __restrict__ pad, float* __restrict__ acc_part, float* __restrict__ l_part,
     char* __restrict__ pstore = nullptr, int64_t p_nqt = 0, int64_t skip_begin = 0, int64_t skip_len = 0,
-    int split_base = 0) {
+    int split_base = 0, float* __restrict__ dmax_out = nullptr) {
   // skip_begin / skip_len: the streamed rows are R's rows with [skip_begin, skip_begin + skip_len)
   // left out (a data-parallel rank's remote candidates around its own block; stages never straddle
   // the gap: skip_begin % BJ == 0); split_base: the slot of split 0 in the partial buffers.
@@ -791,6 +791,8 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   if (MODE == FWD) TT_KTRACE_K(1, 0);
   const float dmax = MODE == FWD ? fold_dmax(dmax_part, n_dmax) : 0.f;  // wave-uniform call
   const float shift = (MODE == FWD && my_col < nC) ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
+  // the folded bound for the combine (one float instead of every row's wave folding the block maxima)
+  if (dmax_out && blockIdx.x == 0 && threadIdx.x == 0) *dmax_out = dmax;
 
   // Four-stage LDS ring.  After the barrier of stage t (which proves every wave is done with
   // stage t-1's buffer) the fill of stage t+3 goes into that buffer, one 1 KiB piece at a time
@@ -950,221 +952,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   if (MODE == FWD) TT_KTRACE_K(1, 3);
-}
-
-// ------------------------------------------------------------------------------------------
-// Warp-specialised forward with stored probabilities (round 4; bf16, H = 256): the same products
-// and sums as score_bf16_kernel<FWD, false, H, true>, bit for bit, by eight waves per workgroup
-// (two per SIMD) in two roles instead of four waves doing everything:
-//   S waves 0-3 (query tile w): X = R C^T for both 32-row tiles of stage t, the softmax map
-//     (row sums l, G = 2^(x c2 - shift) rounded to bf16), G written to a per-tile LDS image
-//     [query][candidate] (the PStore image: ds_write_b64, swizzled);
-//   A waves 4-7 (query tile w - 4), one stage behind: Acc^T += R^T G for stage t-1 with G read
-//     back from the image as the B operand (the S lane's own registers, two ds_read_b64 per
-//     k-step), P from the same image by ds_read_b64_tr_b16 and 16-B stores.
-// Each wave holds half the state (S: the query operand, X; A: the 128-register Acc^T), so two
-// fit a SIMD and one wave's map, LDS waits and stores run beside the other's MFMAs: the stage's
-// 64 MFMAs per SIMD are the same, its exposed latency is what the pairing removes (the four-wave
-// engine measures ~3,100 cycles per stage against a 2,048-cycle MFMA floor).
-// One barrier per iteration; iteration i: S on stage i, A on stage i - 1, fills of stage i + 2
-// into the ring slot of stage i - 2 (read by S in i - 2 and by A in i - 1).  LDS: the four-stage
-// ring (128 KiB) + G images [tile pair 4][iteration parity 2][tile 2] x 2 KiB = 160 KiB.
-// TT_WS_SPREAD=1: each wave's NPW fill pieces of a stage are issued one every few MFMAs of its
-// first tile (a burst right after the barrier stalls the issuing wave on the address queue);
-// TT_WS_PRIO: s_setprio 1 for the A waves (1), the S waves (2) or neither (0).
-#ifndef TT_WS_SPREAD
-#define TT_WS_SPREAD 1
-#endif
-#ifndef TT_WS_PRIO
-#define TT_WS_PRIO 0
-#endif
-template <int H>
-struct WsTile {
-  using T = Tile<__bf16, H>;
-  static constexpr int NWS = 8;
-  static constexpr int RING_B = T::NSTAGE * T::STAGE_B;
-  static constexpr int G_OFF = RING_B;
-  static constexpr int LDS_BYTES = RING_B + 4 * 2 * 2 * 2048;
-  static constexpr int NPW = T::STAGE_B / 1024 / NWS;  // fill pieces per wave per stage
-  static_assert(NPW >= 1 && NPW * 1024 * NWS == T::STAGE_B, "whole 1 KiB pieces per wave");
-};
-
-template <int H>
-__global__ __launch_bounds__(512, 1) void score_ws_kernel(
-    const __bf16* __restrict__ R, int64_t nR, const __bf16* __restrict__ C, int64_t nC, int S,
-    int64_t rows_per_split, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part, int n_dmax,
-    float* __restrict__ acc_part, float* __restrict__ l_part, char* __restrict__ pstore, int64_t p_nqt) {
-  using W = WsTile<H>;
-  using T = typename W::T;
-  constexpr int NK = H / 16, NHT = H / 32, NPW = W::NPW;
-  static_assert(T::NSTAGE == 4 && T::BJ == 64, "four-slot ring of 64-row stages");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const lds_char_t* lds = (const lds_char_t*)smem;
-  lds_char_t* ldsw = (lds_char_t*)smem;
-  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool accw = wid >= 4;  // wave-uniform role
-  const int pw = wid & 3;      // query tile of the workgroup
-  const int r32 = lane & 31, hh = lane >> 5;
-  const int split = blockIdx.x % S;
-  const int64_t cb = blockIdx.x / S;
-  const int64_t my_col = cb * 128 + pw * 32 + r32;
-  const int64_t row_begin = (int64_t)split * rows_per_split;
-  const int64_t row_end = min(nR, row_begin + rows_per_split);
-  const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + T::BJ - 1) / T::BJ : 0;
-
-  // fills: piece c of a stage is bytes (c * 8 + wid) KiB of its image (source-side swizzle)
-  unsigned fo[NPW];
-#pragma unroll
-  for (int c = 0; c < NPW; ++c) {
-    const int p = (c * W::NWS + wid) * 1024 + lane * 16;
-    const int row = p / T::ROWB, slot = (p % T::ROWB) >> 4;
-    fo[c] = (unsigned)(row * T::ROWB + ((slot ^ T::swz(row)) << 4));
-  }
-  const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
-  auto piece = [&](int64_t t, int c) {  // piece c of stage t (past the last: stage 0 again, into a slot nobody reads)
-    const int64_t r0 = t < ntiles ? row_begin + t * T::BJ : row_begin;
-    glds_dwordx4_s(fo[c], R + r0 * H, wbase + (unsigned)(t & 3) * T::STAGE_B + c * W::NWS * 1024);
-  };
-  auto fill = [&](int64_t t) {
-#pragma unroll
-    for (int c = 0; c < NPW; ++c) piece(t, c);
-  };
-  // step i (of 2 NHT = NK per tile) of the first tile carries piece c when i == c * NK / NPW + 1
-  auto spread = [&](int64_t t, int i) {
-#pragma unroll
-    for (int c = 0; c < NPW; ++c)
-      if (TT_WS_SPREAD && i == c * NK / NPW + 1) piece(t, c);
-  };
-  fill(0);
-  fill(1);
-
-  LdsOffs<H> lo;
-  lo.init(lane);
-  PStore ps;  // the G image offsets of this tile pair (+ parity * 4 KiB + tile * 2 KiB)
-  ps.init(W::G_OFF + pw * 8192, lane);
-  const int64_t p_qt = cb * 4 + pw;
-
-  if (TT_WS_PRIO == (accw ? 1 : 2)) __builtin_amdgcn_s_setprio(1);
-  if (!accw) {
-    // ---------------- S waves: X = R C^T, the map, G to the image ----------------
-    const float dmax = fold_dmax(dmax_part, n_dmax);
-    const float shift = my_col < nC ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
-    bf16x8 cf[NK];
-    {
-      const bool ok = my_col < nC;
-      const bf16x8* src = reinterpret_cast<const bf16x8*>(C + (ok ? my_col : 0) * H);
-#pragma unroll
-      for (int kk = 0; kk < NK; ++kk) {
-        bf16x8 v = src[2 * kk + hh];
-        if (!ok) v = bf16x8{};
-        cf[kk] = v;
-      }
-    }
-    float l_run = 0.f;
-    for (int64_t it = 0; it <= ntiles; ++it) {
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW) : "memory");  // fills(it) landed; G(it-1) written
-      asm volatile("s_barrier" ::: "memory");
-      if (!TT_WS_SPREAD || it == ntiles) fill(it + 2);
-      if (it == ntiles) break;
-      const lds_char_t* tile = lds + (unsigned)(it & 3) * T::STAGE_B;
-#pragma unroll
-      for (int jt = 0; jt < 2; ++jt) {
-        const lds_char_t* tb = tile + jt * 32 * T::ROWB;
-        f32x16 x = f32x16{};
-#pragma unroll
-        for (int kk = 0; kk < NK; ++kk) {
-          const bf16x8 a = *reinterpret_cast<const lds_bf16x8_t*>(tb + lo.s[kk & 7] + (kk >= 8 ? 256 : 0));
-          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, cf[kk], x, 0, 0, 0);
-          if (jt == 0) spread(it + 2, kk);
-        }
-        // the map in MapState's arithmetic and order: pair sums, then the tile's sum into l
-        float e[16];
-#pragma unroll
-        for (int v = 0; v < 16; ++v) e[v] = __builtin_amdgcn_exp2f(__builtin_fmaf(x[v], c2, -shift));
-        float ls = 0.f;
-#pragma unroll
-        for (int v = 0; v < 16; v += 2) ls += e[v] + e[v + 1];
-        l_run += ls;
-        const unsigned img = (unsigned)((it & 1) * 4096 + jt * 2048);
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-        typedef __attribute__((address_space(3))) u32x2 lds_u32x2_t;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bf16x4 v = bf16x4{(__bf16)e[4 * k], (__bf16)e[4 * k + 1], (__bf16)e[4 * k + 2], (__bf16)e[4 * k + 3]};
-          *reinterpret_cast<lds_u32x2_t*>(ldsw + ps.w[k] + img) = __builtin_bit_cast(u32x2, v);
-        }
-      }
-    }
-    drain_dma();
-    l_run += __shfl_xor(l_run, 32);
-    if (my_col < nC && hh == 0) l_part[(int64_t)split * nC + my_col] = l_run;
-    return;
-  }
-  // ---------------- A waves: Acc^T += R^T G one stage behind, P stores ----------------
-  f32x16 acc[NHT];
-#pragma unroll
-  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  // B operand of k-step s2 = the S lane's bh[s2]: slots 4 s2 + hh and 4 s2 + 2 + hh of row r32
-  unsigned gb[2][2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int j2 = 0; j2 < 2; ++j2)
-      gb[s2][j2] = W::G_OFF + pw * 8192 + r32 * 64 + 8 * ((4 * s2 + 2 * j2 + hh) ^ ((r32 >> 1) & 7));
-  for (int64_t it = 0; it <= ntiles; ++it) {
-    // younger than fills(it): fills(it+1), and the 4 P stores of iteration it-1 (it >= 2)
-    if (it >= 2)
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW + 4) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW) : "memory");
-    asm volatile("s_barrier" ::: "memory");
-    if (!TT_WS_SPREAD || it == 0) fill(it + 2);
-    if (it == 0) continue;
-    const int64_t t = it - 1;
-    const lds_char_t* tile = lds + (unsigned)(t & 3) * T::STAGE_B;
-    const unsigned img = (unsigned)((t & 1) * 4096);
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      const unsigned gi = img + jt * 2048;
-      bf16x8 g[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x4 lo4 = *reinterpret_cast<const lds_bf16x4_t*>(lds + gb[s2][0] + gi);
-        const bf16x4 hi4 = *reinterpret_cast<const lds_bf16x4_t*>(lds + gb[s2][1] + gi);
-        g[s2] = bf16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-      }
-      const lds_char_t* tb = tile + jt * 32 * T::ROWB;
-#pragma unroll
-      for (int st = 0; st < 2 * NHT; ++st) {
-        const int s2 = st / NHT, ht = st % NHT;
-        const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
-        const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3] + imm));
-        const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3] + imm));
-        const bf16x8 a = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-        acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, g[s2], acc[ht], 0, 0, 0);
-        if (jt == 0) spread(it + 2, st);
-      }
-      // P: the transposed fragments of this tile's image, two 16-B stores
-      char* blk = pstore + (((row_begin + t * T::BJ) / 32 + jt) * p_nqt + p_qt) * 2048;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x4 u0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(lds + ps.r[0] + gi + 1024 * s2));
-        const bf16x4 u1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(lds + ps.r[1] + gi + 1024 * s2));
-        *reinterpret_cast<bf16x8*>(blk + ps.g + 1024 * s2) =
-            bf16x8{u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-      }
-    }
-  }
-  drain_dma();
-  if (my_col < nC) {
-    float* dst = acc_part + ((int64_t)split * nC + my_col) * H;
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-        *reinterpret_cast<f32x4*>(dst + ht * 32 + 8 * g4 + 4 * hh) =
-            f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1649,7 +1436,8 @@ template <int H>
 __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
     const __bf16* __restrict__ R, int64_t plane, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
     int64_t rows_per_split, float c2, const float* __restrict__ qnorm, const float* __restrict__ dmax_part, int n_dmax,
-    float* __restrict__ acc_part, float* __restrict__ l_part, float* __restrict__ P, int64_t p_nqt) {
+    float* __restrict__ acc_part, float* __restrict__ l_part, float* __restrict__ P, int64_t p_nqt,
+    float* __restrict__ dmax_out = nullptr) {
   using ST = SplitTile<H>;
   constexpr int NK = H / 16, NHT = H / 32, NF = ST::NF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1664,6 +1452,7 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + ST::BJ - 1) / ST::BJ : 0;
   const float dmax = fold_dmax(dmax_part, n_dmax);  // wave-uniform call
   const float shift = my_col < nC ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
+  if (dmax_out && blockIdx.x == 0 && threadIdx.x == 0) *dmax_out = dmax;  // (as score_bf16_kernel)
 
   unsigned fo[ST::NPP];
   split_fill_offs<H>(fo);
@@ -2175,7 +1964,7 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
     const DT* __restrict__ Dmat, float* __restrict__ lse, float* __restrict__ lse2, float* __restrict__ loss_rows,
     float* __restrict__ dqu, DT* __restrict__ qs = nullptr, int* __restrict__ xrows = nullptr,
     int S_loc = 0, const float* __restrict__ dmax_loc = nullptr, int n_dmax_loc = 0,
-    __bf16* __restrict__ qsp = nullptr) {
+    __bf16* __restrict__ qsp = nullptr, const float* __restrict__ dmax_folded = nullptr) {
   // S_loc > 0 (data-parallel forward in two launches): slots [0, S_loc) hold the local launch's
   // partials, formed with the local norm bound; they are rescaled to this launch's shift.
   // qsp: the scaled query rows as three bf16 planes (split-bf16 fp32 backward) instead of qs.
@@ -2190,7 +1979,8 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
         for (int pl = 0; pl < 3; ++pl) qsp[pl * qsp_plane + i * H + h] = (__bf16)0.f;
     return;
   }
-  const float sh = col_shift(c2, qnorm[i], fold_dmax(dmax_part, n_dmax));
+  // dmax_folded: the engine's fold of the same block maxima (the same float)
+  const float sh = col_shift(c2, qnorm[i], dmax_folded ? *dmax_folded : fold_dmax(dmax_part, n_dmax));
   const float f_loc = S_loc > 0 ? __builtin_amdgcn_exp2f(col_shift(c2, qnorm[i], fold_dmax(dmax_loc, n_dmax_loc)) - sh)
                                 : 1.f;
   float l = sum_parts1(l_part + i, B, S, S_loc, f_loc);
@@ -2535,6 +2325,7 @@ struct Ws {
   float* qnorm;
   float* lse2;
   float* dmax_part;
+  float* dmax_fold;  // the stored-P forward engine's fold of dmax_part (one float), read by the combine
   char* pad;
   float* l_part;
   float* acc_part;
@@ -2606,7 +2397,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
   const size_t op = take(sp ? (bf ? (size_t)p_nqt_for(B) * p_nct_for(M) * 2048 : (size_t)p_nqt_for(B) * p32_nct_for(M) * 4096)
                             : 0);
   const size_t ox = take(sp ? (size_t)(B + 1) * 4 : 0);
-  const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4);
+  const size_t oqn = take((size_t)B * 4), ol2 = take((size_t)(B + kTailRows) * 4), omx = take(kMaxPrepBlocks * 4 + 4);
   const size_t opad = take(kPadBytes), ol = take((size_t)pf.S * B * 4);
   size_t parts = std::max((size_t)pf.S * B, (size_t)pd.S * M) * H * 4;
   if (sp && bf) parts = std::max(parts, (size_t)ddp_plan(B, M, H).S * M * H * 4);
@@ -2627,6 +2418,7 @@ Ws carve(void* base, int64_t B, int64_t M, int H, int dtype) {
     w.qnorm = reinterpret_cast<float*>(b + oqn);
     w.lse2 = reinterpret_cast<float*>(b + ol2);
     w.dmax_part = reinterpret_cast<float*>(b + omx);
+    w.dmax_fold = sp ? w.dmax_part + kMaxPrepBlocks : nullptr;
     w.pad = b + opad;
     w.l_part = reinterpret_cast<float*>(b + ol);
     w.acc_part = reinterpret_cast<float*>(b + oa);
@@ -2641,16 +2433,6 @@ struct Skip {
   int split_base = 0;          // partial slot of split 0
 };
 
-// The warp-specialised stored-P forward (score_ws_kernel) at H = 256; TT_WS_FWD=0 (read at load)
-// runs the four-wave engine instead (A/B measurement: the same bits either way).
-bool ws_forward() {
-  static const bool on = [] {
-    const char* e = std::getenv("TT_WS_FWD");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  return on;
-}
-
 template <int MODE, int H>
 int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t nC, const Plan& p, float c2,
                   const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
@@ -2658,7 +2440,7 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     if (dtype == TT_F32 && MODE == FWD && w.P && w.Dp) {  // split-bf16 forward storing fp32 G
       score_split_fwd_kernel<H><<<dim3(p.grid), dim3(NT), SplitTile<H>::LDS_BYTES, s>>>(
           w.Dp, (nR + kTailRows) * H, nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, w.qnorm,
-          w.dmax_part, n_dmax, w.acc_part, w.l_part, reinterpret_cast<float*>(w.P), w.p_nqt);
+          w.dmax_part, n_dmax, w.acc_part, w.l_part, reinterpret_cast<float*>(w.P), w.p_nqt, w.dmax_fold);
       TT_LAUNCH_CHECK("score_split_fwd");
       return TT_OK;
     }
@@ -2675,14 +2457,10 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
     score_bf16_kernel<MODE, true, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
         w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, nullptr, 0, sk.begin, sk.len, sk.split_base);
-  } else if (MODE == FWD && w.P && H == 256 && ws_forward()) {
-    score_ws_kernel<(H == 256 ? H : 256)><<<dim3(p.grid), dim3(512), WsTile<256>::LDS_BYTES, s>>>(
-        static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, w.qnorm,
-        w.dmax_part, n_dmax, w.acc_part, w.l_part, w.P, w.p_nqt);
   } else if (MODE == FWD && w.P) {
     score_bf16_kernel<FWD, false, H, true><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES + NW * 2048, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
-        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, w.P, w.p_nqt);
+        w.qnorm, w.dmax_part, n_dmax, w.pad, w.acc_part, w.l_part, w.P, w.p_nqt, 0, 0, 0, w.dmax_fold);
   } else {
     score_bf16_kernel<MODE, false, H><<<dim3(p.grid), dim3(NT), Tile<__bf16, H>::LDS_BYTES, s>>>(
         static_cast<const __bf16*>(R), nR, static_cast<const __bf16*>(C), nC, p.S, p.rows_per_split, c2, lse2,
@@ -2754,6 +2532,9 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
   w.P = P;
   w.p_nqt = p_nqt;
   w.Dp = const_cast<__bf16*>(Dp);
+  // the stored-P engines (bf16, split-bf16) fold dmax once into the slot after the block maxima
+  // (carve reserves it); the combine then reads that one float
+  w.dmax_fold = P && (dtype == TT_BF16 || Dp) ? const_cast<float*>(dmax_part) + kMaxPrepBlocks : nullptr;
   int rc;
   if ((rc = dispatch_engine<FWD>(H, dtype, Rm, M, Cm, B, p, c2, nullptr, w, n_dmax, s))) return rc;
   const dim3 grid((unsigned)((B + (Qs || Qs32 || Qsp ? kTailRows : 0) + 3) / 4)), block(256);
@@ -2761,12 +2542,12 @@ int fwd_core(int dtype, const void* Rm, int64_t M, const void* Cm, int64_t B, in
     fwd_combine_kernel<float><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                     acc_part, inv_tau, label_off, static_cast<const float*>(Cm),
                                                     static_cast<const float*>(Rm), lse, lse2, loss_rows, dqu, Qs32,
-                                                    Qs32 || Qsp ? xrows : nullptr, 0, nullptr, 0, Qsp);
+                                                    Qs32 || Qsp ? xrows : nullptr, 0, nullptr, 0, Qsp, w.dmax_fold);
   else
     fwd_combine_kernel<__bf16><<<grid, block, 0, s>>>(B, M, H, p.S, p.n_pad, c2, qnorm, dmax_part, n_dmax, l_part,
                                                      acc_part, inv_tau, label_off, static_cast<const __bf16*>(Cm),
                                                      static_cast<const __bf16*>(Rm), lse, lse2, loss_rows, dqu, Qs,
-                                                     xrows);
+                                                     xrows, 0, nullptr, 0, nullptr, w.dmax_fold);
   TT_LAUNCH_CHECK("score_fwd_combine");
   return loss ? launch_mean(loss_rows, B, loss, s) : TT_OK;
 }
