@@ -154,10 +154,9 @@ def side_stream(device: torch.device, role: str = "plan") -> torch.cuda.Stream:
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), role)
     st = _SIDE.get(key)
     if st is None:
-        # the plan's small sort kernels at high priority: beside the bandwidth-bound gather they
-        # otherwise wait for CU slots and stretch (TT_PLAN_PRIORITY=0: normal priority, A/B only)
-        prio = -1 if role == "plan" and os.environ.get("TT_PLAN_PRIORITY", "1") != "0" else 0
-        st = _SIDE[key] = torch.cuda.Stream(device=key[0], priority=prio)
+        # (normal priority: a high-priority plan stream made the C3 step 1.42 vs 0.82 ms, round 4,
+        # profiles/r04e_plan_priority_ab.txt)
+        st = _SIDE[key] = torch.cuda.Stream(device=key[0])
     return st
 
 

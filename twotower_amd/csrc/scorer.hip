@@ -1497,18 +1497,7 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   // wait at the top of stage t + 2 has seen those stores complete (compiler-placed stores made
   // hipcc wait for them before reusing their data registers, vmcnt(0) inside the S chain)
   float ev[2][16];
-  auto stage = [&](int64_t t, float (&e)[16]) {
-    // stage t landed in this wave: younger VMEM ops are fills(t+1) and stage t-1's 16 P stores
-    if (t == 0)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 16) : "memory");
-#pragma unroll
-    for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(e[v]));  // stage t-2's stores have read them
-    asm volatile("s_barrier" ::: "memory");  // ... in every wave; every wave is past stage t-1
-    fill(buf == 0 ? 2 : buf - 1, t + 2);     // into stage t-1's slot
-    const lds_char_t* tile = lds + buf * ST::STAGE_B;
-    // S chain: X = R C^T
+  auto s_chain3 = [&](const lds_char_t* tile) {  // X = R C^T over one stage tile's planes
     f32x16 x = f32x16{};
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
@@ -1518,7 +1507,10 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
         a[p] = *reinterpret_cast<const lds_bf16x8_t*>(tile + p * ST::PLANE_B + lo.s[kk & 7] + (kk >= 8 ? 256 : 0));
       x = mfma6(a, cf[0][kk], cf[1][kk], cf[2][kk], x);
     }
-    // the map (score_f32_kernel's arithmetic) and the fp32 P store
+    return x;
+  };
+  // the map (score_f32_kernel's arithmetic), the fp32 P store and the split of G for tile t
+  auto map_store = [&](int64_t t, const f32x16& x, float (&e)[16], bf16x8 (&g)[3][2]) {
     float ls = 0.f;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -1531,8 +1523,21 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
     for (int v = 0; v < 16; ++v)
       asm volatile("global_store_dword %0, %1, off offset:%2" ::"v"(blk), "v"(e[v]), "n"(acc_row(v, 0) * 128)
                    : "memory");  // (+ 4 hh rows in blk: hh is per lane)
-    bf16x8 g[3][2];
     split_tile(e, g);
+  };
+  auto stage = [&](int64_t t, float (&e)[16]) {
+    // stage t landed in this wave: younger VMEM ops are fills(t+1) and stage t-1's 16 P stores
+    if (t == 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 16) : "memory");
+#pragma unroll
+    for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(e[v]));  // stage t-2's stores have read them
+    asm volatile("s_barrier" ::: "memory");  // ... in every wave; every wave is past stage t-1
+    fill(buf == 0 ? 2 : buf - 1, t + 2);     // into stage t-1's slot
+    const lds_char_t* tile = lds + buf * ST::STAGE_B;
+    bf16x8 g[3][2];
+    map_store(t, s_chain3(tile), e, g);
     split_acc_chain<H>(tile, lo, g, acc);
     buf = buf == 2 ? 0 : buf + 1;
   };
