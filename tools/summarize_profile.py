@@ -24,8 +24,8 @@ OPS = [
     (r"bag_scale_rows|bag_piece_sum|bag_bwd_reduce_kernel<.*true>|bag_bwd_reduce_generic_kernel<true>"
      r"|bag_bwd_reduce_sliced_kernel<\d+, \d+, true", "tt_bag_mean_bwd_adamw_planned"),
     (r"bag_bwd_reduce", "tt_bag_mean_bwd_planned"),
-    (r"score_bf16_kernel<0|score_f32_kernel<0|prep_rows|prep_qd|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
-    (r"score_bf16_kernel<1|score_f32_kernel<1|score_ddp_kernel|to_log2|bwd_combine", "tt_inbatch_bwd"),
+    (r"score_bf16_kernel<0|score_f32_kernel<0|score_split_fwd|prep_rows|prep_qd|shift_kernel|fwd_combine", "tt_inbatch_fwd"),
+    (r"score_bf16_kernel<1|score_f32_kernel<1|score_ddp_kernel|score_split_ddp|to_log2|bwd_combine", "tt_inbatch_bwd"),
     (r"adamw_(vec4|scalar)", "tt_adamw"),
     (r"adamw_multi_ex", "tt_adamw_multi_ex"),
     (r"adamw_multi|adam_prepare", "tt_adamw_multi"),
@@ -39,7 +39,7 @@ OPS = [
     (r"relu_bwd", "tt_relu_bwd"),
     (r"head_gemm|head_normalize", "tt_head_gemm"),
     (r"head_wgrad", "tt_head_wgrad"),
-    (r"l2_prep_kernel", "tt_inbatch_l2_prep"),
+    (r"l2_prep_kernel|l2_prep128_kernel", "tt_inbatch_l2_prep"),
     (r"split_planes", "tt_head_split_ff"),
     (r"Cijk_", "hipBLASLt GEMM (tower FF)"),
 ]

@@ -252,9 +252,8 @@ class BagMeanPool(torch.autograd.Function):
         # sort beside it costs it little: C3 0.8381 vs 0.8419 ms/step), after it otherwise (an
         # HBM-bound gather of a larger table: C5 1.8235 early vs 1.8178 after;
         # profiles/r03p_c3_plan_fork_ab.txt, r03w_plan_fork_auto_ab.txt)
-        fork = os.environ.get("TT_PLAN_FORK", "auto")  # early | late | auto (A/B of the placement)
-        early = plan_now and (fork == "early" or (fork == "auto" and weight.numel() * weight.element_size()
-                                                  <= 256 * 2 ** 20))
+        # (round 4, same box: early 0.8256 vs late 0.8343 ms/step at C3, profiles/r04f_plan_fork_ab.txt)
+        early = plan_now and weight.numel() * weight.element_size() <= 256 * 2 ** 20
         if early:
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
