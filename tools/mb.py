@@ -12,6 +12,8 @@
   python tools/mb.py split_fwd                   two-launch vs one-launch data-parallel forward
   python tools/mb.py table_sync [c3|c5]          per-rank GPU cost of the table exchanges at N ranks
                                                  (gather / shard / owner) and their link bytes
+  python tools/mb.py l2prep                      the head's normalise fused with the scorer's operand prep,
+                                                 alone (C3 and B x B rows)
   python tools/mb.py scorer_once B M H [dtype] [lib]   three scorer fwd + bwd calls, nothing else (for
                                                  counter collection: tools/pmc_scorer.sh)
 """
@@ -293,6 +295,32 @@ def table_sync(a):
         torch.cuda.empty_cache()
 
 
+def l2prep(a):
+    """tt_inbatch_l2_prep alone (the head's normalise fused with the scorer's operand prep) at C3's
+    rows (B = 8192 queries + 16384 candidates, H = 256, bf16) and the B x B pairs form (8192 + 8192),
+    beside a plain row normalise (rows.hip tt_l2_normalize) of the same rows: the pass's own cost
+    without the concurrent sort plan of the step."""
+    H = 256
+    dt = _lib.compute_dtype_code("bf16")
+    st = torch.cuda.current_stream().cuda_stream
+    for B, M in ((8192, 16384), (8192, 8192)):
+        y0 = torch.randn(B + M, H, device=DEV)
+        y = y0.clone()
+        norms = torch.empty(B + M, device=DEV)
+        ws = torch.empty(_lib.lib().tt_inbatch_ws_size(B, M, H, dt), dtype=torch.uint8, device=DEV)
+
+        def prep():
+            y.copy_(y0)
+            call("tt_inbatch_l2_prep", ptr(y), B, M, H, dt, ptr(norms), ptr(ws), ws.numel(), st)
+
+        def copy_only():
+            y.copy_(y0)
+
+        t_prep, t_copy = graph_us(prep), graph_us(copy_only)
+        print(json.dumps({"B": B, "M": M, "l2_prep_us": round(t_prep - t_copy, 1), "copy_us": round(t_copy, 1),
+                          "bytes_MB": round((B + M) * H * (4 + 4 + 2) / 1e6, 1)}), flush=True)
+
+
 def scorer_once(a):
     B, M, H = int(a.shape), int(a.rest[0]), int(a.rest[1])
     dt = a.rest[2] if len(a.rest) > 2 else "bf16"
@@ -306,7 +334,7 @@ def scorer_once(a):
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
+    ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync", "l2prep",
                                      "scorer_once"])
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")

@@ -1738,10 +1738,10 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
-    if (qb) {
-      for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x) {
-        qb[B * H + i] = (__bf16)0.f;
-        db[M * H + i] = (__bf16)0.f;
+    if (qb) {  // H % 8 == 0: 16-B stores (B * H and M * H are multiples of 8 elements)
+      for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H / 8; i += blockDim.x) {
+        reinterpret_cast<bf16x8*>(qb + B * H)[i] = bf16x8{};
+        reinterpret_cast<bf16x8*>(db + M * H)[i] = bf16x8{};
       }
     }
     if (dp)
@@ -1844,9 +1844,9 @@ __global__ __launch_bounds__(64 * kL2PrepWaves) void l2_prep_kernel(float* __res
     for (int i = threadIdx.x; i < kPadBytes / 4; i += blockDim.x)
       reinterpret_cast<float*>(pad)[i] = (i >= (kPadBytes - 16) / 4) ? INFINITY : 0.f;
     for (int i = threadIdx.x; i < kTailRows; i += blockDim.x) lse2[B + i] = INFINITY;
-    for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H; i += blockDim.x) {
-      qb[B * H + i] = (__bf16)0.f;
-      db[M * H + i] = (__bf16)0.f;
+    for (int64_t i = threadIdx.x; i < (int64_t)kTailRows * H / 8; i += blockDim.x) {  // 16-B stores
+      reinterpret_cast<bf16x8*>(qb + B * H)[i] = bf16x8{};
+      reinterpret_cast<bf16x8*>(db + M * H)[i] = bf16x8{};
     }
   }
   float mx = 0.f;
