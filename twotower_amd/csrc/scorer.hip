@@ -611,10 +611,10 @@ __device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 // sum over s < S of p[s * stride4], in split order (the same order as the generic path), with up
-// to four splits' loads in flight
+// to eight splits' loads in flight (round 3: four; C2's forward has S = 8)
 // sum over s < S of w_s p[s * stride] (w_s = f_loc for s < S_loc, else 1: the product is skipped,
-// x * 1 == x), added in the order s = 0, 1, ... as the plain loop does (the same bits), with four
-// loads in flight instead of one dependent round trip per split.
+// x * 1 == x), added in the order s = 0, 1, ... as the plain loop does (the same bits), with up to
+// eight loads in flight instead of one dependent round trip per split.
 // (-DTT_COMBINE_BATCHED=0: one load per step, the loop before round 3's end; C2 0.4299 vs 0.4273
 // ms/step batched, same box, profiles/r03zp_c2_combine_ab.txt)
 #ifndef TT_COMBINE_BATCHED
@@ -627,12 +627,12 @@ __device__ __forceinline__ float sum_parts1(const float* __restrict__ p, int64_t
   for (int s = 0; s < S; ++s) o += s < S_loc ? f_loc * p[(int64_t)s * stride] : p[(int64_t)s * stride];
   return o;
 #endif
-  for (int s0 = 0; s0 < S; s0 += 4) {
-    float v[4];
+  for (int s0 = 0; s0 < S; s0 += 8) {  // up to 8 splits' loads in one round (S <= 8 by plan_for)
+    float v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride] : 0.f;
+    for (int u = 0; u < 8; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 8; ++u)
       if (s0 + u < S) o += s0 + u < S_loc ? f_loc * v[u] : v[u];
   }
   return o;
@@ -640,12 +640,13 @@ __device__ __forceinline__ float sum_parts1(const float* __restrict__ p, int64_t
 
 __device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t stride4, int S) {
   f32x4 o = {0.f, 0.f, 0.f, 0.f};
-  for (int s0 = 0; s0 < S; s0 += 4) {
-    f32x4 v[4];
+  for (int s0 = 0; s0 < S; s0 += 8) {  // up to 8 splits' loads in one round
+    f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 8; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) o += v[u];
+    for (int u = 0; u < 8; ++u)
+      if (s0 + u < S) o += v[u];
   }
   return o;
 }
