@@ -297,28 +297,29 @@ def table_sync(a):
 
 def l2prep(a):
     """tt_inbatch_l2_prep alone (the head's normalise fused with the scorer's operand prep) at C3's
-    rows (B = 8192 queries + 16384 candidates, H = 256, bf16) and the B x B pairs form (8192 + 8192),
-    beside a plain row normalise (rows.hip tt_l2_normalize) of the same rows: the pass's own cost
-    without the concurrent sort plan of the step."""
-    H = 256
-    dt = _lib.compute_dtype_code("bf16")
-    st = torch.cuda.current_stream().cuda_stream
-    for B, M in ((8192, 16384), (8192, 8192)):
+    rows (B = 8192 queries + 16384 candidates, H = 256, bf16), the B x B pairs form (8192 + 8192) and
+    C2 (4096 + 8192, H = 128, fp32: the split engine's candidate planes), net of the copy that resets
+    the rows: the pass's own cost without the concurrent sort plan of the step."""
+    for B, M, H, name in ((8192, 16384, 256, "bf16"), (8192, 8192, 256, "bf16"), (4096, 8192, 128, "fp32")):
+        dt = _lib.compute_dtype_code(name)
         y0 = torch.randn(B + M, H, device=DEV)
         y = y0.clone()
         norms = torch.empty(B + M, device=DEV)
         ws = torch.empty(_lib.lib().tt_inbatch_ws_size(B, M, H, dt), dtype=torch.uint8, device=DEV)
 
-        def prep():
+        def prep():  # the stream at call time: graph_us captures on a stream of its own
             y.copy_(y0)
-            call("tt_inbatch_l2_prep", ptr(y), B, M, H, dt, ptr(norms), ptr(ws), ws.numel(), st)
+            call("tt_inbatch_l2_prep", ptr(y), B, M, H, dt, ptr(norms), ptr(ws), ws.numel(),
+                 torch.cuda.current_stream().cuda_stream)
 
         def copy_only():
             y.copy_(y0)
 
         t_prep, t_copy = graph_us(prep), graph_us(copy_only)
-        print(json.dumps({"B": B, "M": M, "l2_prep_us": round(t_prep - t_copy, 1), "copy_us": round(t_copy, 1),
-                          "bytes_MB": round((B + M) * H * (4 + 4 + 2) / 1e6, 1)}), flush=True)
+        out_b = 2 if name == "bf16" else 6  # the bf16 copy, or the fp32 scorer's three candidate planes
+        print(json.dumps({"B": B, "M": M, "H": H, "dtype": name, "l2_prep_us": round(t_prep - t_copy, 1),
+                          "copy_us": round(t_copy, 1), "bytes_MB": round((B + M) * H * (4 + 4 + out_b) / 1e6, 1)}),
+              flush=True)
 
 
 def scorer_once(a):
