@@ -105,12 +105,32 @@ __device__ __forceinline__ void glds_dword_s(unsigned voff, const void* sbase, u
 __device__ __forceinline__ void drain_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // max_j |d_j| from the per-block maxima (every lane of the calling wave gets it).
-__device__ __forceinline__ float fold_dmax(const float* __restrict__ part, int n) {
+// n <= kMaxPrepBlocks: the loads are unrolled and predicated, so all of them are in flight at once
+// (a runtime-bounded loop waited one L2 round trip per 64 values: 8 in a row at 512 parts).  A
+// kernel that needs dmax late issues the loads early (load_dmax) and folds them where it is used.
+struct DmaxParts {
+  float v[kMaxPrepBlocks / kWave];
+};
+__device__ __forceinline__ DmaxParts load_dmax(const float* __restrict__ part, int n) {
+  DmaxParts d;
+#pragma unroll
+  for (int k = 0; k < kMaxPrepBlocks / kWave; ++k) {
+    const int i = lane_id() + k * kWave;
+    const float x = part[i < n ? i : 0];  // unconditional (clamped) load: no branch, no wait per load
+    d.v[k] = i < n ? x : 0.f;
+  }
+  return d;
+}
+__device__ __forceinline__ float fold_loaded(const DmaxParts& d) {
   float m = 0.f;
-  for (int i = lane_id(); i < n; i += kWave) m = fmaxf(m, part[i]);
+#pragma unroll
+  for (int k = 0; k < kMaxPrepBlocks / kWave; ++k) m = fmaxf(m, d.v[k]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   return m;
+}
+__device__ __forceinline__ float fold_dmax(const float* __restrict__ part, int n) {
+  return fold_loaded(load_dmax(part, n));
 }
 
 // Column shift for the forward: an upper bound of row i's logits in log2 units,
@@ -1347,10 +1367,11 @@ void score_f32_kernel(
 //             to P as fp32 in score_f32_kernel's block layout; then Acc^T += R^T G with G split
 //             into three planes (the B operand) and R^T read with ds_read_b64_tr_b16.
 //   backward: Acc^T = Qs^T G (= dD^T) from the scaled-query planes (fwd_combine writes them) and G
-//             loaded from P (asm loads two stages ahead) and split in registers.
-// One wave per SIMD (the one-round grids of these shapes hold one workgroup per CU): the stage
-// loop is a straight unrolled stream the compiler schedules; a three-stage ring with one barrier
-// per stage keeps two stages of fills in flight.
+//             loaded from P (asm loads two units ahead) and split in registers.
+// One wave per SIMD (the one-round grids of these shapes hold one workgroup per CU).  Both kernels
+// run software-pipelined unit streams (score_split_fwd_kernel, score_split_ddp_kernel): every
+// MFMA gap carries one operand piece read kSd steps ahead, and the map / split of the next tile
+// sits beside the current tile's MFMAs, pinned there by sched_barrier per MFMA.
 template <int H>
 struct SplitTile {
   using T = Tile<__bf16, H>;  // a plane's rows: the bf16 engine's layout (ROWB, swizzle, LdsOffs)
@@ -1359,7 +1380,7 @@ struct SplitTile {
   static constexpr int STAGE_B = 3 * PLANE_B;
   static constexpr int NPP = PLANE_B / 1024 / NW;  // fill pieces per wave per plane
   static constexpr int NF = 3 * NPP;                // ... per stage
-  static constexpr int NSTAGE = 3;
+  static constexpr int NSTAGE = 3;  // the backward's ring (the forward's: SplitFwdRing)
   static constexpr int LDS_BYTES = NSTAGE * STAGE_B;
   static_assert(NPP >= 1 && NPP * 1024 * NW == PLANE_B, "a plane tile is a whole number of 1 KiB pieces per wave");
   static_assert(BJ == Tile<float, H>::BJ, "the plan's row tiles (bj_for(TT_F32)) are this engine's stages");
@@ -1368,17 +1389,6 @@ struct SplitTile {
 __device__ __forceinline__ f32x16 mfma_bf16(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-// acc += a b over the six cross terms (a, b: three planes each)
-__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8& b0, const bf16x8& b1, const bf16x8& b2,
-                                       f32x16 acc) {
-  acc = mfma_bf16(a[0], b2, acc);
-  acc = mfma_bf16(a[1], b1, acc);
-  acc = mfma_bf16(a[2], b0, acc);
-  acc = mfma_bf16(a[0], b1, acc);
-  acc = mfma_bf16(a[1], b0, acc);
-  return mfma_bf16(a[0], b0, acc);
-}
-
 // G planes of a 32x32 tile from its 16 fp32 values per lane: plane p, k-step s2, element j = G row
 // 16 s2 + 8 (j >> 2) + 4 hh + (j & 3) (the accumulator order: the B operand of the Acc chain).
 __device__ __forceinline__ void split_tile(const float (&e)[16], bf16x8 (&g)[3][2]) {
@@ -1390,30 +1400,6 @@ __device__ __forceinline__ void split_tile(const float (&e)[16], bf16x8 (&g)[3][
     g[1][v >> 3][v & 7] = a1;
     g[2][v >> 3][v & 7] = a2;
   }
-}
-
-// Acc^T += R^T G for one 32-row stage tile (three planes at tile + p * PLANE_B).
-template <int H>
-__device__ __forceinline__ void split_acc_chain(const lds_char_t* tile, const LdsOffs<H>& lo, const bf16x8 (&g)[3][2],
-                                                f32x16 (&acc)[H / 32]) {
-  using ST = SplitTile<H>;
-  using T = typename ST::T;
-  constexpr int NHT = H / 32;
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int ht = 0; ht < NHT; ++ht) {
-      const int imm = s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
-      bf16x8 a[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const lds_char_t* tb = tile + p * ST::PLANE_B + imm;
-        const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a0[ht & 3]));
-        const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + lo.a1[ht & 3]));
-        a[p] = bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
-      }
-      acc[ht] = mfma6(a, g[0][s2], g[1][s2], g[2][s2], acc[ht]);
-    }
 }
 
 // Per-lane source offsets of a plane tile's NPP fill pieces (the swizzle on the source side, as
@@ -1430,9 +1416,86 @@ __device__ __forceinline__ void split_fill_offs(unsigned (&fo)[SplitTile<H>::NPP
   }
 }
 
+#ifndef TT_SPLIT_ABLATE
+#define TT_SPLIT_ABLATE 0  // timing ablations of score_split_fwd_kernel (bits: 1 P stores, 2 map, 4 operand reads, 8 fills)
+#endif
+// The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
+template <int H>
+struct SplitFwdRing {
+  static constexpr int NSLOT = 4 * SplitTile<H>::STAGE_B <= 128 * 1024 ? 4 : 3;
+  static constexpr int LDS_BYTES = NSLOT * SplitTile<H>::STAGE_B;
+};
+
+// Operand registers of one MFMA step: three planes of a 32x16 fragment, held as 8-byte halves
+// (an Acc operand arrives as two ds_read_b64_tr_b16 per plane).
+struct SplitOp {
+  bf16x4 h[3][2];
+  __device__ __forceinline__ bf16x8 a(int p) const {
+    return bf16x8{h[p][0][0], h[p][0][1], h[p][0][2], h[p][0][3], h[p][1][0], h[p][1][1], h[p][1][2], h[p][1][3]};
+  }
+};
+
+// Piece j (0..5) of the Acc chain's operand of step st (G rows 16 s2, h-tile ht): half j & 1 of
+// plane j >> 1, one ds_read_b64_tr_b16.
+template <int H>
+__device__ __forceinline__ void split_acc_piece(SplitOp& o, int st, int j, const lds_char_t* tile, const LdsOffs<H>& lo) {
+  using ST = SplitTile<H>;
+  using T = typename ST::T;
+  constexpr int NHT = H / 32;
+  const int s2 = st / NHT, ht = st % NHT, p = j >> 1;
+  const lds_char_t* tb = tile + p * ST::PLANE_B + s2 * 16 * T::ROWB + (ht >= 4 ? 256 : 0);
+  o.h[p][j & 1] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(tb + ((j & 1) ? lo.a1[ht & 3] : lo.a0[ht & 3])));
+}
+
+// Piece j (0..5) of the operand of step i of a forward unit: steps [0, NK) are the S chain's (plane
+// j, one ds_read_b128, j < 3) from s_tile, steps [NK, NSTEP) the Acc chain's (half j & 1 of plane
+// j >> 1, one ds_read_b64_tr_b16) from a_tile, steps >= NSTEP the next unit's S steps from n_tile.
+template <int H>
+__device__ __forceinline__ void split_fwd_piece(SplitOp& o, int i, int j, const lds_char_t* s_tile,
+                                                const lds_char_t* a_tile, const lds_char_t* n_tile,
+                                                const LdsOffs<H>& lo) {
+  using ST = SplitTile<H>;
+  using T = typename ST::T;
+  constexpr int NK = H / 16, NHT = H / 32, NSTEP = NK + 2 * NHT;
+  if (i >= NSTEP) {
+    i -= NSTEP;
+    s_tile = n_tile;
+  }
+  if (i < NK) {
+    if (j < 3) {
+      const bf16x8 v =
+          *reinterpret_cast<const lds_bf16x8_t*>(s_tile + j * ST::PLANE_B + lo.s[i & 7] + (i >= 8 ? 256 : 0));
+      o.h[j][0] = bf16x4{v[0], v[1], v[2], v[3]};
+      o.h[j][1] = bf16x4{v[4], v[5], v[6], v[7]};
+    }
+  } else {
+    split_acc_piece<H>(o, i - NK, j, a_tile, lo);
+  }
+}
+
+// The six cross terms of a split product, smallest first (x0y2, x1y1, x2y0, x0y1, x1y0, x0y0):
+// MFMA j takes plane kPa[j] of the A operand and plane kPb[j] of the B operand.
+constexpr int kPa[6] = {0, 1, 2, 0, 1, 0};
+constexpr int kPb[6] = {2, 1, 0, 1, 0, 0};
+
 // R: three bf16 planes of nR rows + a kTailRows zero tail each (plane stride `plane` elements), so
 // every stage is a full tile from one scalar base.  C: the fp32 query rows.  P: fp32 blocks of
 // score_f32_kernel's layout.
+//
+// Software-pipelined like the bf16 engine's fwd_unit: unit t is one stream of NSTEP MFMA steps
+// (six MFMAs each), steps [0, NK) the S chain of tile t+1 (into xb) beside the map
+// of tile t (xa: exp, row sum, P store, split of G into three planes, SPS = 16 / NK slots a step,
+// spread over the step's six MFMA gaps), steps [NK, NSTEP) the Acc chain of tile t.  Each step's
+// operand is read kSd steps ahead in six pieces, one per MFMA, across the chain and unit
+// boundaries.  Round 4's first form ran the S chain, the map and the Acc chain back to back
+// (0.48 MFMA busy at C2: the map and each chain's first operand reads exposed).
+//   Ring (NSLOT stages of 32 rows): unit t reads tiles t, t+1 and, in its last kSd steps, t+2.  At
+//   step NSTEP - kSd (the barrier point) fill(t+2) must have landed in every wave: wait, barrier.
+//   Four slots: the barrier point also frees tile t-1's slot, which takes fill(t+3) right there,
+//   one 1 KiB piece per MFMA gap (six LDS-DMA issues in a row cost ~480 cycles of MFMA idle).
+//   Three slots (H = 256): a second barrier at the unit's start frees it for fill(t+2).
+//   P stores: unit t's 16 stores come from register set e[t & 1]; the barrier point of unit t+1
+//   (its vmcnt wait sees them complete) releases that set to unit t+2.
 template <int H>
 __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
     const __bf16* __restrict__ R, int64_t plane, int64_t nR, const float* __restrict__ C, int64_t nC, int S,
@@ -1440,10 +1503,13 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
     float* __restrict__ acc_part, float* __restrict__ l_part, float* __restrict__ P, int64_t p_nqt,
     float* __restrict__ dmax_out = nullptr) {
   using ST = SplitTile<H>;
-  constexpr int NK = H / 16, NHT = H / 32, NF = ST::NF;
+  constexpr int NK = H / 16, NHT = H / 32, NSTEP = NK + 2 * NHT, NF = ST::NF;
+  constexpr int NSLOT = SplitFwdRing<H>::NSLOT;
+  constexpr int kSd = 2, SPS = 16 / NK;
+  static_assert(NSTEP % kSd == 0 && kSd <= 2 * NHT, "the barrier point follows the map's stores");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const lds_char_t* lds = (const lds_char_t*)smem;
-  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int split = blockIdx.x % S;
   const int64_t cb = blockIdx.x / S;
@@ -1451,9 +1517,17 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   const int64_t row_begin = (int64_t)split * rows_per_split;
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + ST::BJ - 1) / ST::BJ : 0;
-  const float dmax = fold_dmax(dmax_part, n_dmax);  // wave-uniform call
-  const float shift = my_col < nC ? col_shift(c2, qnorm[my_col], dmax) : 0.f;
-  if (dmax_out && blockIdx.x == 0 && threadIdx.x == 0) *dmax_out = dmax;  // (as score_bf16_kernel)
+  TT_KTRACE_K(1, 0);
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  float l_run = 0.f;
+  if (ntiles == 0) {  // (workgroup-uniform) no rows: zero partials
+    const float dmax = fold_dmax(dmax_part, n_dmax);
+    if (dmax_out && blockIdx.x == 0 && threadIdx.x == 0) *dmax_out = dmax;
+    write_partials<FWD, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+    return;
+  }
 
   unsigned fo[ST::NPP];
   split_fill_offs<H>(fo);
@@ -1466,16 +1540,30 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
       for (int c = 0; c < ST::NPP; ++c)
         glds_dwordx4_s(fo[c], R + p * plane + r0 * H, wbase + b * ST::STAGE_B + p * ST::PLANE_B + c * NW * 1024);
   };
+  auto fill_piece = [&](int b, int64_t t, int f) {  // piece f (plane f / NPP) of fill(b, t)
+    const int64_t r0 = t < ntiles ? row_begin + t * ST::BJ : row_begin;
+    const int p = f / ST::NPP, c = f % ST::NPP;
+    glds_dwordx4_s(fo[c], R + p * plane + r0 * H, wbase + b * ST::STAGE_B + p * ST::PLANE_B + c * NW * 1024);
+  };
+  auto slot_tile = [&](int b) { return lds + b * ST::STAGE_B; };
+  const DmaxParts dparts = load_dmax(dmax_part, n_dmax);  // (folded after tile 0's S chain)
+  const float qn = my_col < nC ? qnorm[my_col] : 0.f;
   fill(0, 0);
-  fill(1, 1);
 
   bf16x8 cf[3][NK];  // query planes: lane (r32, hh) holds elements 16 kk + 8 hh + 0..7 of its query
   {
     const bool ok = my_col < nC;
     const f32x4* src = reinterpret_cast<const f32x4*>(C + (ok ? my_col : 0) * H);
+    f32x4 u[2 * NK];
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
-      const f32x4 u0 = src[4 * kk + 2 * hh], u1 = src[4 * kk + 2 * hh + 1];
+      u[2 * kk] = src[4 * kk + 2 * hh];
+      u[2 * kk + 1] = src[4 * kk + 2 * hh + 1];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every query load issued before the first wait
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const f32x4 u0 = u[2 * kk], u1 = u[2 * kk + 1];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = ok ? (j < 4 ? u0[j] : u1[j - 4]) : 0.f;
@@ -1489,71 +1577,160 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   }
   LdsOffs<H> lo;
   lo.init(lane);
-  f32x16 acc[NHT];
-#pragma unroll
-  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  float l_run = 0.f;
-  int buf = 0;
-  // G of stage t goes to P by asm stores from register set t & 1, which stays untouched until the
-  // wait at the top of stage t + 2 has seen those stores complete (compiler-placed stores made
-  // hipcc wait for them before reusing their data registers, vmcnt(0) inside the S chain)
-  float ev[2][16];
-  auto s_chain3 = [&](const lds_char_t* tile) {  // X = R C^T over one stage tile's planes
-    f32x16 x = f32x16{};
+  // P: tile t's block of this wave's 32 queries at a wave-uniform base, the lane's column and
+  // half (4 hh rows) as a 32-bit offset, the register's row as the store's immediate
+  const float* pcol = P + (cb * NW + wid) * 1024;  // (= my_col >> 5: wave-uniform)
+  const int64_t pstride = p_nqt * 1024;          // floats from one candidate tile's blocks to the next
+  const unsigned pvo = (unsigned)((4 * hh * 32 + r32) * 4);
+
+  // Prologue: stage 0 and the query rows in flight together (an all-CU burst runs ~11 B/cycle/CU:
+  // every KiB waited for here costs ~50 ns); stage 1 is issued once the queries are split and
+  // lands beside tile 0's S chain, stage 2 after it.
+  fill(1, 1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");  // stage 0 landed (younger: stage 1)
+  asm volatile("s_barrier" ::: "memory");
+
+  f32x16 X[2];  // S chain results: X[t & 1] = tile t's
+  {             // tile 0's S chain (the prologue)
+    const lds_char_t* t0 = slot_tile(0);
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
-      bf16x8 a[3];
+      SplitOp o;
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        a[p] = *reinterpret_cast<const lds_bf16x8_t*>(tile + p * ST::PLANE_B + lo.s[kk & 7] + (kk >= 8 ? 256 : 0));
-      x = mfma6(a, cf[0][kk], cf[1][kk], cf[2][kk], x);
+      for (int j = 0; j < 3; ++j) split_fwd_piece<H>(o, kk, j, t0, t0, t0, lo);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        X[0] = mfma_bf16(o.a(kPa[j]), cf[kPb[j]][kk], kk == 0 && j == 0 ? f32x16{} : X[0]);
+      }
     }
-    return x;
-  };
-  // the map (score_f32_kernel's arithmetic), the fp32 P store and the split of G for tile t
-  auto map_store = [&](int64_t t, const f32x16& x, float (&e)[16], bf16x8 (&g)[3][2]) {
-    float ls = 0.f;
+  }
+  const float dmax = fold_loaded(dparts);  // wave-uniform
+  const float shift = my_col < nC ? col_shift(c2, qn, dmax) : 0.f;
+  if (dmax_out && blockIdx.x == 0 && threadIdx.x == 0) *dmax_out = dmax;  // (as score_bf16_kernel)
+  if constexpr (NSLOT == 4) {
+    fill(2, 2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");  // stage 1 landed (younger: stage 2)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage 1 landed
+  }
+  asm volatile("s_barrier" ::: "memory");
+  SplitOp ring[kSd];  // operands of the next kSd steps
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      e[v] = __builtin_amdgcn_exp2f(x[v] * c2 - shift);
-      ls += e[v];
+  for (int i = 0; i < kSd; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) split_fwd_piece<H>(ring[i], i, j, slot_tile(1), slot_tile(0), slot_tile(1), lo);
+
+  float ev[2][16];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) ev[k][v] = 0.f;
+
+  int sl = 0;  // ring slot of tile t
+  auto unit = [&](int64_t t, const f32x16& xa, f32x16& xb, float (&e)[16], float (&e_prev)[16]) {
+    const int s1 = sl + 1 == NSLOT ? 0 : sl + 1, s2n = s1 + 1 == NSLOT ? 0 : s1 + 1;
+    const lds_char_t* a_tile = slot_tile(sl);   // tile t (Acc chain)
+    const lds_char_t* s_tile = slot_tile(s1);   // tile t+1 (S chain)
+    const lds_char_t* n_tile = slot_tile(s2n);  // tile t+2 (next unit's first operands)
+    if constexpr (NSLOT == 3) {
+      asm volatile("s_barrier" ::: "memory");  // every wave is past tile t-1's Acc chain
+      fill(s2n, t + 2);
+    }
+    const float* pblk = pcol + ((row_begin >> 5) + t) * pstride;
+    TT_TRACE(0);
+#ifdef TT_SCORER_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace[t * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
+    float ls = 0.f;
+    bf16x8 g[3][2];
+    float r1[SPS], r2[SPS];
+#pragma unroll
+    for (int i = 0; i < NSTEP; ++i) {
+      if (i == NSTEP - kSd && !(TT_SPLIT_ABLATE & 8)) {  // the barrier point: fill(t+2) landed (younger: this unit's 16 P stores)
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#pragma unroll
+        for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(e_prev[v]));  // unit t-1's stores have read them
+        TT_TRACE(1);
+        asm volatile("s_barrier" ::: "memory");
+        TT_TRACE(3);
+      }
+      SplitOp nx;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const SplitOp& cur = ring[i % kSd];
+        if (i < NK) {
+          xb = mfma_bf16(cur.a(kPa[j]), cf[kPb[j]][i], i == 0 && j == 0 ? f32x16{} : xb);
+        } else {
+          const int st = i - NK, s2 = st / NHT, ht = st % NHT;
+          acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur.a(kPa[j]), g[kPb[j]][s2], acc[ht], 0, 0, 0);
+        }
+        if constexpr (NSLOT == 4) {  // fill(t+3) into tile t-1's slot, one piece per MFMA gap after the barrier
+          const int f = (i - (NSTEP - kSd)) * 6 + j;
+          if (f >= 0 && f < NF && !(TT_SPLIT_ABLATE & 8)) fill_piece(sl == 0 ? 3 : sl - 1, t + 3, f);
+        }
+#if TT_SPLIT_ABLATE & 4  // timing ablation (never in a real build): no operand reads
+        nx.h[j % 3][j / 3] = bf16x4{(__bf16)(float)i, (__bf16)(float)j, 0, 0};
+#else
+        split_fwd_piece<H>(nx, i + kSd, j, s_tile, a_tile, n_tile, lo);
+#endif
+        if (i < NK) {  // the map of tile t, slots [SPS i, SPS (i + 1))
+#pragma unroll
+          for (int q = 0; q < SPS; ++q) {
+            const int v = SPS * i + q;
+            if (j == 0) {
+#if TT_SPLIT_ABLATE & 2  // timing ablation: no exp, no split (below)
+              e[v] = xa[v];
+#else
+              e[v] = __builtin_amdgcn_exp2f(xa[v] * c2 - shift);
+#endif
+              asm volatile("" : "+v"(e[v]));
+            } else if (j == 1) {
+              ls += e[v];
+#if !(TT_SPLIT_ABLATE & 1)  // (timing ablation: no P stores)
+              asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(pvo), "v"(e[v]), "s"(pblk),
+                           "n"(acc_row(v, 0) * 128)
+                           : "memory");  // (+ 4 hh rows in pvo: hh is per lane)
+#endif
+            } else if (TT_SPLIT_ABLATE & 2) {
+              if (j == 2) g[0][v >> 3][v & 7] = g[1][v >> 3][v & 7] = g[2][v >> 3][v & 7] = (__bf16)e[v];
+            } else if (j == 2) {
+              const __bf16 h0 = (__bf16)e[v];
+              g[0][v >> 3][v & 7] = h0;
+              r1[q] = e[v] - (float)h0;
+              asm volatile("" : "+v"(r1[q]));
+            } else if (j == 3) {
+              const __bf16 h1 = (__bf16)r1[q];
+              g[1][v >> 3][v & 7] = h1;
+              r2[q] = r1[q] - (float)h1;
+              asm volatile("" : "+v"(r2[q]));
+            } else if (j == 4) {
+              g[2][v >> 3][v & 7] = (__bf16)r2[q];
+            }
+          }
+          if (j == 1) asm volatile("" : "+v"(ls));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      ring[i % kSd] = nx;
     }
     l_run += ls;
-    float* blk = P + (((row_begin >> 5) + t) * p_nqt + (my_col >> 5)) * 1024 + 4 * hh * 32 + r32;
-#pragma unroll
-    for (int v = 0; v < 16; ++v)
-      asm volatile("global_store_dword %0, %1, off offset:%2" ::"v"(blk), "v"(e[v]), "n"(acc_row(v, 0) * 128)
-                   : "memory");  // (+ 4 hh rows in blk: hh is per lane)
-    split_tile(e, g);
+    sl = s1;
   };
-  auto stage = [&](int64_t t, float (&e)[16]) {
-    // stage t landed in this wave: younger VMEM ops are fills(t+1) and stage t-1's 16 P stores
-    if (t == 0)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 16) : "memory");
-#pragma unroll
-    for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(e[v]));  // stage t-2's stores have read them
-    asm volatile("s_barrier" ::: "memory");  // ... in every wave; every wave is past stage t-1
-    fill(buf == 0 ? 2 : buf - 1, t + 2);     // into stage t-1's slot
-    const lds_char_t* tile = lds + buf * ST::STAGE_B;
-    bf16x8 g[3][2];
-    map_store(t, s_chain3(tile), e, g);
-    split_acc_chain<H>(tile, lo, g, acc);
-    buf = buf == 2 ? 0 : buf + 1;
-  };
+  TT_KTRACE_K(1, 1);
   int64_t t = 0;
   for (; t + 2 <= ntiles; t += 2) {
-    stage(t, ev[0]);
-    stage(t + 1, ev[1]);
+    unit(t, X[0], X[1], ev[0], ev[1]);
+    unit(t + 1, X[1], X[0], ev[1], ev[0]);
   }
-  if (t < ntiles) stage(t, ev[0]);
+  if (t < ntiles) unit(t, X[0], X[1], ev[0], ev[1]);
+  TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA or P store may outlive the workgroup
 #pragma unroll
   for (int k = 0; k < 2; ++k)
 #pragma unroll
     for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(ev[k][v]));
   write_partials<FWD, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+  TT_KTRACE_K(1, 3);
 }
 
 // P fragment of one 32-query tile for lane (candidate r32, hh): queries 8k + 4 hh + u (k, u < 4)
@@ -1577,13 +1754,26 @@ __device__ __forceinline__ void split_p_tie(SplitPSet& d) {
 
 // Backward from stored fp32 P: R = the scaled-query planes (nR = B rows + zero tail), columns =
 // candidates (nC = M), dD^T partials per query split.
+// Software-pipelined like the forward: unit t is the Acc chain of tile t (NSA steps of six MFMAs,
+// operands read kSd steps ahead in one piece per MFMA gap, across the unit boundary), with the
+// split of the next tile's G (P(t+1): two of its 16 values a step) beside it.  Round 4's first
+// form split a tile's G and then ran its chain (0.44 MFMA busy at C2).
+//   Ring (three 32-row stages): unit t reads tile t and, in its last kSd steps, tile t+1.  At step
+//   NSA - kSd (the barrier point) fill(t+1) must have landed in every wave: wait, barrier; that
+//   also frees tile t-1's slot, which takes fill(t+2), one 1 KiB piece per MFMA gap.
+//   P: four register sets; P(t+3) is issued at unit t's start (into the set P(t-1) left), two
+//   units ahead of its split.  VMEM order per unit: P(t+3), fill(t+2), so at unit t's start
+//   P(t+1) has landed once at most fill(t), P(t+2), fill(t+1) are in flight (2 NF + 4), and at
+//   its barrier point fill(t+1) has once at most P(t+3) is (4).
 template <int H>
 __global__ __launch_bounds__(NT, 1) void score_split_ddp_kernel(const __bf16* __restrict__ R, int64_t plane, int64_t nR,
                                                                 int64_t nC, int S, int64_t rows_per_split,
                                                                 const float* __restrict__ P, int64_t p_nqt,
                                                                 float* __restrict__ acc_part) {
   using ST = SplitTile<H>;
-  constexpr int NHT = H / 32, NF = ST::NF;
+  constexpr int NHT = H / 32, NSA = 2 * NHT, NF = ST::NF;
+  constexpr int kSd = 2, EPS = 16 / NSA;  // operand distance (steps), G values split per step
+  static_assert(NSA % kSd == 0 && NF <= 6 * kSd, "a fill's pieces fit the steps after the barrier point");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const lds_char_t* lds = (const lds_char_t*)smem;
   const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1594,63 +1784,131 @@ __global__ __launch_bounds__(NT, 1) void score_split_ddp_kernel(const __bf16* __
   const int64_t row_begin = (int64_t)split * rows_per_split;
   const int64_t row_end = min(nR, row_begin + rows_per_split);
   const int64_t ntiles = row_end > row_begin ? (row_end - row_begin + ST::BJ - 1) / ST::BJ : 0;
+  TT_KTRACE_K(0, 0);
+  f32x16 acc[NHT];
+#pragma unroll
+  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
+  if (ntiles == 0) {  // (workgroup-uniform) no rows: zero partials
+    write_partials<DD, H>(acc, 0.f, split, nC, ct * 32 + r32, hh, acc_part, nullptr);
+    return;
+  }
 
   unsigned fo[ST::NPP];
   split_fill_offs<H>(fo);
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
   auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * ST::BJ : row_begin; };
-  auto fill = [&](int b, int64_t t) {
-    const int64_t r0 = stage_row(t);
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int c = 0; c < ST::NPP; ++c)
-        glds_dwordx4_s(fo[c], R + p * plane + r0 * H, wbase + b * ST::STAGE_B + p * ST::PLANE_B + c * NW * 1024);
+  auto fill_piece = [&](int b, int64_t t, int f) {  // piece f (plane f / NPP) of stage t into slot b
+    const int p = f / ST::NPP, c = f % ST::NPP;
+    glds_dwordx4_s(fo[c], R + p * plane + stage_row(t) * H, wbase + b * ST::STAGE_B + p * ST::PLANE_B + c * NW * 1024);
   };
+  auto fill = [&](int b, int64_t t) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) fill_piece(b, t, f);
+  };
+  auto slot_tile = [&](int b) { return lds + b * ST::STAGE_B; };
   const float* pcol = P + ct * p_nqt * 1024;
   const unsigned pvo = (unsigned)(r32 * 128 + hh * 16);
   auto pload = [&](SplitPSet& d, int64_t t) { split_p_load(d, pcol + (stage_row(t) >> 5) * 1024, pvo); };
-  SplitPSet pf[3];
-  fill(0, 0);
-  pload(pf[0], 0);
-  fill(1, 1);
-  pload(pf[1], 1);
   LdsOffs<H> lo;
   lo.init(lane);
-  f32x16 acc[NHT];
-#pragma unroll
-  for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
-  // stage t: fills(t) and P(t) landed once at most fills(t+1) and P(t+1) are in flight
-  auto stage = [&](int64_t t, int b, SplitPSet& cur, SplitPSet& nxt2) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 4) : "memory");
-    asm volatile("s_barrier" ::: "memory");
-    split_p_tie(cur);
+
+  SplitPSet pf[4];
+  pload(pf[0], 0);
+  pload(pf[1], 1);
+  fill(0, 0);
+  pload(pf[2], 2);
+  fill(1, 1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NF + 4) : "memory");  // P(0), P(1), stage 0 landed
+  asm volatile("s_barrier" ::: "memory");
+  bf16x8 g[2][3][2];  // G planes: g[t & 1] = tile t's
+  {
+    split_p_tie(pf[0]);
     float e[16];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) e[4 * k + u] = cur.v[k][u];
-    bf16x8 g[3][2];
-    split_tile(e, g);
-    fill(b == 0 ? 2 : b - 1, t + 2);  // into stage t-1's slot; P(t+2) into the set stage t-1 split
-    pload(nxt2, t + 2);
-    split_acc_chain<H>(lds + b * ST::STAGE_B, lo, g, acc);
+      for (int u = 0; u < 4; ++u) e[4 * k + u] = pf[0].v[k][u];
+    split_tile(e, g[0]);
+  }
+  SplitOp ring[kSd];
+#pragma unroll
+  for (int i = 0; i < kSd; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) split_acc_piece<H>(ring[i], i, j, slot_tile(0), lo);
+
+  int sl = 0;  // ring slot of tile t
+  // unit t: Acc chain of tile t from gc; P(t+1) (pn) split into gn; P(t+3) issued into pi
+  auto unit = [&](int64_t t, const bf16x8 (&gc)[3][2], bf16x8 (&gn)[3][2], SplitPSet& pn, SplitPSet& pi) {
+    const int s1 = sl == 2 ? 0 : sl + 1, sf = s1 == 2 ? 0 : s1 + 1;
+    const lds_char_t* tile = slot_tile(sl);
+    const lds_char_t* ntile = slot_tile(s1);
+    TT_TRACE_B(0);
+#ifdef TT_SCORER_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t < 64) g_tt_trace_b[t * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+#endif
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NF + 4) : "memory");  // P(t+1) landed
+    TT_TRACE_B(1);
+    split_p_tie(pn);
+    pload(pi, t + 3);
+    float r1[EPS], r2[EPS];
+#pragma unroll
+    for (int i = 0; i < NSA; ++i) {
+      if (i == NSA - kSd) {  // the barrier point: fill(t+1) landed (younger: P(t+3))
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        TT_TRACE_B(2);
+        asm volatile("s_barrier" ::: "memory");
+        TT_TRACE_B(3);
+      }
+      SplitOp nx;
+      const int s2 = i / NHT, ht = i % NHT;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        acc[ht] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ring[i % kSd].a(kPa[j]), gc[kPb[j]][s2], acc[ht], 0, 0, 0);
+        const int f = (i - (NSA - kSd)) * 6 + j;  // fill(t+2) into tile t-1's slot, after the barrier
+        if (f >= 0 && f < NF) fill_piece(sf, t + 2, f);
+        if (i + kSd < NSA) split_acc_piece<H>(nx, i + kSd, j, tile, lo);
+        else split_acc_piece<H>(nx, i + kSd - NSA, j, ntile, lo);
+#pragma unroll
+        for (int q = 0; q < EPS; ++q) {  // G values v = EPS i + q of tile t+1 (e index 4k + u)
+          const int v = EPS * i + q;
+          const float x = pn.v[v >> 2][v & 3];
+          if (j == 2) {
+            const __bf16 h0 = (__bf16)x;
+            gn[0][v >> 3][v & 7] = h0;
+            r1[q] = x - (float)h0;
+            asm volatile("" : "+v"(r1[q]));
+          } else if (j == 3) {
+            const __bf16 h1 = (__bf16)r1[q];
+            gn[1][v >> 3][v & 7] = h1;
+            r2[q] = r1[q] - (float)h1;
+            asm volatile("" : "+v"(r2[q]));
+          } else if (j == 4) {
+            gn[2][v >> 3][v & 7] = (__bf16)r2[q];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      ring[i % kSd] = nx;
+    }
+    sl = s1;
   };
-  // unrolled by the ring's three slots: every register set is named, no copies across iterations
+  TT_KTRACE_K(0, 1);
   int64_t t = 0;
-  for (; t + 3 <= ntiles; t += 3) {
-    stage(t, 0, pf[0], pf[2]);
-    stage(t + 1, 1, pf[1], pf[0]);
-    stage(t + 2, 2, pf[2], pf[1]);
+  for (; t + 4 <= ntiles; t += 4) {
+    unit(t, g[0], g[1], pf[1], pf[3]);
+    unit(t + 1, g[1], g[0], pf[2], pf[0]);
+    unit(t + 2, g[0], g[1], pf[3], pf[1]);
+    unit(t + 3, g[1], g[0], pf[0], pf[2]);
   }
-  if (t < ntiles) {
-    stage(t, 0, pf[0], pf[2]);
-    if (t + 1 < ntiles) stage(t + 1, 1, pf[1], pf[0]);
-  }
+  if (t < ntiles) unit(t, g[0], g[1], pf[1], pf[3]);
+  if (t + 1 < ntiles) unit(t + 1, g[1], g[0], pf[2], pf[0]);
+  if (t + 2 < ntiles) unit(t + 2, g[0], g[1], pf[3], pf[1]);
+  TT_KTRACE_K(0, 2);
   drain_dma();  // no load may outlive the workgroup
 #pragma unroll
-  for (int k = 0; k < 3; ++k) split_p_tie(pf[k]);
+  for (int k = 0; k < 4; ++k) split_p_tie(pf[k]);
   write_partials<DD, H>(acc, 0.f, split, nC, ct * 32 + r32, hh, acc_part, nullptr);
+  TT_KTRACE_K(0, 3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2444,7 +2702,7 @@ int launch_engine(int dtype, const void* R, int64_t nR, const void* C, int64_t n
                   const float* lse2, const Ws& w, int n_dmax, hipStream_t s, const Skip& sk = Skip{}) {
   if constexpr (H >= 64) {
     if (dtype == TT_F32 && MODE == FWD && w.P && w.Dp) {  // split-bf16 forward storing fp32 G
-      score_split_fwd_kernel<H><<<dim3(p.grid), dim3(NT), SplitTile<H>::LDS_BYTES, s>>>(
+      score_split_fwd_kernel<H><<<dim3(p.grid), dim3(NT), SplitFwdRing<H>::LDS_BYTES, s>>>(
           w.Dp, (nR + kTailRows) * H, nR, static_cast<const float*>(C), nC, p.S, p.rows_per_split, c2, w.qnorm,
           w.dmax_part, n_dmax, w.acc_part, w.l_part, reinterpret_cast<float*>(w.P), w.p_nqt, w.dmax_fold);
       TT_LAUNCH_CHECK("score_split_fwd");
