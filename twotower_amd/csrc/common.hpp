@@ -166,18 +166,24 @@ __device__ __forceinline__ f32x4 sum_slabs(const f32x4* __restrict__ p, size_t s
 // same order, so the same bits.  `part` is 1024 floats of LDS.  Every thread returns the mean.
 __device__ inline float block256_mean_as_1024(const float* __restrict__ x, int64_t n, float* part) {
   const int t = threadIdx.x;
+  // thread t's four partials (t + 256 k, k < 4) in element order, eight elements per round with
+  // the eight loads in flight (unconditional clamped loads; the adds skip what lies past n).  Kept
+  // to eight registers of loads: the block shares its kernel's register budget with latency-bound
+  // rows (32 in flight doubled bwd_combine's VGPRs and halved its occupancy).
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float s = 0.f;
-    int64_t i = t + 256 * k;
-    for (; i + 7 * 1024 < n; i += 8 * 1024) {
+    for (int64_t i0 = t + 256 * k; i0 < n; i0 += 8 * 1024) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = x[i + u * 1024];
+      for (int u = 0; u < 8; ++u) {
+        const int64_t i = i0 + 1024 * u;
+        v[u] = x[i < n ? i : n - 1];
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 8; ++u)
+        if (i0 + 1024 * u < n) s += v[u];
     }
-    for (; i < n; i += 1024) s += x[i];
     part[t + 256 * k] = s;
   }
   __syncthreads();

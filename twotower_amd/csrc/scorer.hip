@@ -236,6 +236,43 @@ __device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], floa
   }
 }
 
+// write_partials through the wave's LDS image (32 columns x H fp32 = 128 H bytes at img; the
+// caller has passed a barrier after its last read of the ring): every lane writes its 16-B pieces
+// to [column][16-B chunk ^ (column & 15)], then each 1 KiB store instruction takes whole rows of
+// acc_part (1024 / 4H rows) instead of 32 rows x 32 B (a store-issue-bound epilogue,
+// MI355X_MICROARCH.md 'epilogue store tail').  Same values, same places as write_partials.
+template <int MODE, int H>
+__device__ __forceinline__ void write_partials_t(const f32x16 (&acc)[H / 32], float l_run, int split, int64_t nC,
+                                                 int64_t col0, int r32, int hh, float* acc_part, float* l_part,
+                                                 lds_char_t* img) {
+  if constexpr (H < 64) {  // (a 128-B row: the direct stores are already whole 128-B pieces)
+    write_partials<MODE, H>(acc, l_run, split, nC, col0 + r32, hh, acc_part, l_part);
+    return;
+  }
+  constexpr int NCH = H / 4, RPI = kWave / NCH;  // 16-B chunks per row, rows per store instruction
+  static_assert(H < 64 || (NCH >= 16 && NCH <= kWave), "H = 32 .. 256");
+#pragma unroll
+  for (int ht = 0; ht < H / 32; ++ht)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int ch = 8 * ht + 2 * g4 + hh;
+      *(lds_f32x4_t*)(img + r32 * (H * 4) + ((ch ^ (r32 & 15)) << 4)) =
+          f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
+    }
+  const int lane = lane_id(), rl = lane / NCH, ch = lane % NCH;
+#pragma unroll
+  for (int k = 0; k < 32 / RPI; ++k) {
+    const int row = k * RPI + rl;
+    const f32x4 v = *(const lds_f32x4_t*)(img + row * (H * 4) + ((ch ^ (row & 15)) << 4));
+    const int64_t col = col0 + row;
+    if (col < nC) *reinterpret_cast<f32x4*>(acc_part + ((int64_t)split * nC + col) * H + 4 * ch) = v;
+  }
+  if constexpr (MODE == FWD) {
+    l_run += __shfl_xor(l_run, 32);
+    if (col0 + r32 < nC && hh == 0) l_part[(int64_t)split * nC + col0 + r32] = l_run;
+  }
+}
+
 // G for one 32x32 X tile: forward 2^(x c2 - shift) (accumulating l), backward 2^(x c2 - lse2_row).
 template <int MODE>
 __device__ __forceinline__ void map_tile(const f32x16& x, float (&e)[16], float c2, float shift,
@@ -630,6 +667,24 @@ __device__ __forceinline__ f32x4 load4(const __bf16* p, int lane) {
   const bf16x4 v = reinterpret_cast<const bf16x4*>(p)[lane];
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+// V consecutive elements per lane (rows of H = 64 V): the combines' row bodies
+template <int V>
+struct RowVec {
+  typedef float f __attribute__((ext_vector_type(V)));
+  typedef __bf16 b __attribute__((ext_vector_type(V)));
+};
+template <int V>
+__device__ __forceinline__ typename RowVec<V>::f loadv(const float* p, int lane) {
+  return reinterpret_cast<const typename RowVec<V>::f*>(p)[lane];
+}
+template <int V>
+__device__ __forceinline__ typename RowVec<V>::f loadv(const __bf16* p, int lane) {
+  const typename RowVec<V>::b v = reinterpret_cast<const typename RowVec<V>::b*>(p)[lane];
+  typename RowVec<V>::f o;
+#pragma unroll
+  for (int u = 0; u < V; ++u) o[u] = (float)v[u];
+  return o;
+}
 // sum over s < S of p[s * stride4], in split order (the same order as the generic path), with up
 // to eight splits' loads in flight (round 3: four; C2's forward has S = 8)
 // sum over s < S of w_s p[s * stride] (w_s = f_loc for s < S_loc, else 1: the product is skipped,
@@ -658,12 +713,13 @@ __device__ __forceinline__ float sum_parts1(const float* __restrict__ p, int64_t
   return o;
 }
 
-__device__ __forceinline__ f32x4 sum_parts4(const f32x4* __restrict__ p, int64_t stride4, int S) {
-  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+template <typename VT>
+__device__ __forceinline__ VT sum_parts4(const VT* __restrict__ p, int64_t stride4, int S) {
+  VT o = VT{};
   for (int s0 = 0; s0 < S; s0 += 8) {  // up to 8 splits' loads in one round
-    f32x4 v[8];
+    VT v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 8; ++u) v[u] = s0 + u < S ? p[(int64_t)(s0 + u) * stride4] : VT{};
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       if (s0 + u < S) o += v[u];
@@ -703,24 +759,30 @@ __device__ void exact_row(const DT* __restrict__ qr, const DT* __restrict__ Dm, 
   }
 }
 
-// fwd_combine's row body at H = 256 (one float4 per lane), shared by fwd_combine_kernel and the
-// engine's folded combine so both produce the same bits: l = the split-summed row sum of query
-// row i (before the pad correction), get_o() = this lane's float4 of O_i = sum_s Acc_s,i.  Writes
-// lse, lse2, dqu and qs (and xrows for a row redone exactly); returns loss_i on every lane.  The
-// fma chains are spelled out so no kernel's contraction choice changes a bit.
-__device__ __forceinline__ float dot4(const f32x4& a, const f32x4& b) {
-  return __builtin_fmaf(a[3], b[3], __builtin_fmaf(a[2], b[2], __builtin_fmaf(a[1], b[1], a[0] * b[0])));
+// fwd_combine's row body at H = 64 V (V consecutive floats per lane: every load of the row in
+// one round): l = the split-summed row sum of query row i (before the pad correction), get_o() =
+// this lane's V floats of O_i = sum_s Acc_s,i.  Writes lse, lse2, dqu and qs / qsp (and xrows for
+// a row redone exactly); returns loss_i on every lane.  The fma chains are spelled out so no
+// contraction choice changes a bit.
+template <int V>
+__device__ __forceinline__ float dotv(const typename RowVec<V>::f& a, const typename RowVec<V>::f& b) {
+  float d = a[0] * b[0];
+#pragma unroll
+  for (int u = 1; u < V; ++u) d = __builtin_fmaf(a[u], b[u], d);
+  return d;
 }
 
-template <typename DT, class GetO>
-__device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, float sh, int n_pad, int64_t M,
+template <typename DT, int V, class GetO>
+__device__ __forceinline__ float combine_rowv(int64_t i, float l, GetO get_o, float sh, int n_pad, int64_t M,
                                                 float c2, float inv_tau, int64_t label_off,
                                                 const DT* __restrict__ Qmat, const DT* __restrict__ Dmat,
                                                 float* __restrict__ lse, float* __restrict__ lse2,
                                                 float* __restrict__ dqu, DT* __restrict__ qs,
                                                 int* __restrict__ xrows, int lane, __bf16* __restrict__ qsp = nullptr,
                                                 int64_t qsp_plane = 0) {
-  constexpr int H = 4 * kWave;
+  constexpr int H = V * kWave;
+  using FV = typename RowVec<V>::f;
+  using BV = typename RowVec<V>::b;
   l = __builtin_fmaf(-(float)n_pad, __builtin_amdgcn_exp2f(-sh), l);  // pad rows: X = 0 exactly
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
@@ -735,7 +797,7 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
     }
     const float inv_l = 1.f / lx;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < V; ++u) {  // (exact_row's layout: element lane + 64 u)
       const int h = lane + kWave * u;
       if (dqu) dqu[i * H + h] = o[u] * inv_l - (float)dl[h];
       if (qs) qs[i * H + h] = (DT)0.f;  // its stored P underflowed: the backward combine adds the row
@@ -750,23 +812,26 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
   }
   const float lse2_i = sh + log2f(l);  // log2 units, for the backward engine
   const float lse_i = lse2_i * kLn2;
-  const f32x4 qv = load4(qr, lane), dv = load4(dl, lane);
-  const float dot = wave_sum(dot4(qv, dv));
+  const FV qv = loadv<V>(qr, lane), dv = loadv<V>(dl, lane);
+  const float dot = wave_sum(dotv<V>(qv, dv));
   if (qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
     const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
-    if constexpr (std::is_same_v<DT, float>)
-      reinterpret_cast<f32x4*>(qs + i * H)[lane] = f32x4{qv[0] * f, qv[1] * f, qv[2] * f, qv[3] * f};
-    else
-      reinterpret_cast<bf16x4*>(qs + i * H)[lane] =
-          bf16x4{(__bf16)(qv[0] * f), (__bf16)(qv[1] * f), (__bf16)(qv[2] * f), (__bf16)(qv[3] * f)};
+    if constexpr (std::is_same_v<DT, float>) {
+      reinterpret_cast<FV*>(qs + i * H)[lane] = qv * f;
+    } else {
+      BV o;
+#pragma unroll
+      for (int u = 0; u < V; ++u) o[u] = (__bf16)(qv[u] * f);
+      reinterpret_cast<BV*>(qs + i * H)[lane] = o;
+    }
   }
   if (qsp) {  // the split-bf16 backward's planes of the same fp32 products
     const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
-    bf16x4 pl[3];
+    BV pl[3];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) { __bf16 a0, a1, a2; split3(qv[u] * f, a0, a1, a2); pl[0][u] = a0; pl[1][u] = a1; pl[2][u] = a2; }
+    for (int u = 0; u < V; ++u) { __bf16 a0, a1, a2; split3(qv[u] * f, a0, a1, a2); pl[0][u] = a0; pl[1][u] = a1; pl[2][u] = a2; }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) reinterpret_cast<bf16x4*>(qsp + k * qsp_plane + i * H)[lane] = pl[k];
+    for (int k = 0; k < 3; ++k) reinterpret_cast<BV*>(qsp + k * qsp_plane + i * H)[lane] = pl[k];
   }
   if (lane == 0) {
     lse[i] = lse_i;
@@ -774,10 +839,11 @@ __device__ __forceinline__ float combine_row256(int64_t i, float l, GetO get_o, 
   }
   if (dqu) {
     const float inv_l = 1.f / l;
-    const f32x4 o = get_o();
-    reinterpret_cast<f32x4*>(dqu + i * H)[lane] =
-        f32x4{__builtin_fmaf(o[0], inv_l, -dv[0]), __builtin_fmaf(o[1], inv_l, -dv[1]),
-              __builtin_fmaf(o[2], inv_l, -dv[2]), __builtin_fmaf(o[3], inv_l, -dv[3])};
+    const FV o = get_o();
+    FV r;
+#pragma unroll
+    for (int u = 0; u < V; ++u) r[u] = __builtin_fmaf(o[u], inv_l, -dv[u]);
+    reinterpret_cast<FV*>(dqu + i * H)[lane] = r;
   }
   return __builtin_fmaf(-dot, inv_tau, lse_i);
 }
@@ -968,7 +1034,9 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
 #endif
   if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
-  write_partials<MODE, H>(acc, l_run, split + split_base, nC, my_col, hh, acc_part, l_part);
+  __syncthreads();  // every wave is past its last ring read: the ring takes the partial images
+  write_partials_t<MODE, H>(acc, l_run, split + split_base, nC, my_col - r32, r32, hh, acc_part, l_part,
+                            (lds_char_t*)smem + wid * 32 * H * 4);
 #ifdef TT_SCORER_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -1187,9 +1255,11 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   drain_dma();  // no load may outlive the workgroup
 #pragma unroll
   for (int k = 0; k < 5; ++k) tie(pf[k]);
+  __syncthreads();  // every wave is past its last ring read: the ring takes the partial images
 #pragma unroll
   for (int c = 0; c < CW; ++c)
-    write_partials<DD, H>(acc[c], 0.f, split, nC, (ct0 + c) * 32 + r32, hh, acc_part, nullptr);
+    write_partials_t<DD, H>(acc[c], 0.f, split, nC, (ct0 + c) * 32, r32, hh, acc_part, nullptr,
+                            (lds_char_t*)smem + wid * 32 * H * 4);
 #ifdef TT_SCORER_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -1416,9 +1486,10 @@ __device__ __forceinline__ void split_fill_offs(unsigned (&fo)[SplitTile<H>::NPP
   }
 }
 
-#ifndef TT_SPLIT_ABLATE
-#define TT_SPLIT_ABLATE 0  // timing ablations of score_split_fwd_kernel (bits: 1 P stores, 2 map, 4 operand reads, 8 fills)
+#ifndef TT_SPLIT_STORE_ACC
+#define TT_SPLIT_STORE_ACC 0
 #endif
+// The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
 // The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
 template <int H>
 struct SplitFwdRing {
@@ -1507,6 +1578,9 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   constexpr int NSLOT = SplitFwdRing<H>::NSLOT;
   constexpr int kSd = 2, SPS = 16 / NK;
   static_assert(NSTEP % kSd == 0 && kSd <= 2 * NHT, "the barrier point follows the map's stores");
+  // TT_SPLIT_STORE_ACC: P stores in the Acc steps before the barrier point (three a step), where the
+  // gaps carry only operand reads, instead of beside the map's VALU in the S steps
+  constexpr bool kStoreInAcc = TT_SPLIT_STORE_ACC && (NSTEP - kSd - NK) * 3 >= 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const lds_char_t* lds = (const lds_char_t*)smem;
   const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1644,9 +1718,13 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
     float ls = 0.f;
     bf16x8 g[3][2];
     float r1[SPS], r2[SPS];
+    auto pstore = [&](int v) {
+      asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(pvo), "v"(e[v]), "s"(pblk), "n"(acc_row(v, 0) * 128)
+                   : "memory");  // (+ 4 hh rows in pvo: hh is per lane)
+    };
 #pragma unroll
     for (int i = 0; i < NSTEP; ++i) {
-      if (i == NSTEP - kSd && !(TT_SPLIT_ABLATE & 8)) {  // the barrier point: fill(t+2) landed (younger: this unit's 16 P stores)
+      if (i == NSTEP - kSd) {  // the barrier point: fill(t+2) landed (younger: this unit's 16 P stores)
         asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 #pragma unroll
         for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(e_prev[v]));  // unit t-1's stores have read them
@@ -1666,33 +1744,19 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
         }
         if constexpr (NSLOT == 4) {  // fill(t+3) into tile t-1's slot, one piece per MFMA gap after the barrier
           const int f = (i - (NSTEP - kSd)) * 6 + j;
-          if (f >= 0 && f < NF && !(TT_SPLIT_ABLATE & 8)) fill_piece(sl == 0 ? 3 : sl - 1, t + 3, f);
+          if (f >= 0 && f < NF) fill_piece(sl == 0 ? 3 : sl - 1, t + 3, f);
         }
-#if TT_SPLIT_ABLATE & 4  // timing ablation (never in a real build): no operand reads
-        nx.h[j % 3][j / 3] = bf16x4{(__bf16)(float)i, (__bf16)(float)j, 0, 0};
-#else
         split_fwd_piece<H>(nx, i + kSd, j, s_tile, a_tile, n_tile, lo);
-#endif
         if (i < NK) {  // the map of tile t, slots [SPS i, SPS (i + 1))
 #pragma unroll
           for (int q = 0; q < SPS; ++q) {
             const int v = SPS * i + q;
             if (j == 0) {
-#if TT_SPLIT_ABLATE & 2  // timing ablation: no exp, no split (below)
-              e[v] = xa[v];
-#else
               e[v] = __builtin_amdgcn_exp2f(xa[v] * c2 - shift);
-#endif
               asm volatile("" : "+v"(e[v]));
             } else if (j == 1) {
               ls += e[v];
-#if !(TT_SPLIT_ABLATE & 1)  // (timing ablation: no P stores)
-              asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(pvo), "v"(e[v]), "s"(pblk),
-                           "n"(acc_row(v, 0) * 128)
-                           : "memory");  // (+ 4 hh rows in pvo: hh is per lane)
-#endif
-            } else if (TT_SPLIT_ABLATE & 2) {
-              if (j == 2) g[0][v >> 3][v & 7] = g[1][v >> 3][v & 7] = g[2][v >> 3][v & 7] = (__bf16)e[v];
+              if (!kStoreInAcc) pstore(v);
             } else if (j == 2) {
               const __bf16 h0 = (__bf16)e[v];
               g[0][v >> 3][v & 7] = h0;
@@ -1708,6 +1772,10 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
             }
           }
           if (j == 1) asm volatile("" : "+v"(ls));
+        }
+        if (kStoreInAcc && i >= NK && (j & 1)) {  // three P stores per Acc step before the barrier point
+          const int v = (i - NK) * 3 + (j >> 1);
+          if (v < 16) pstore(v);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1729,12 +1797,15 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   for (int k = 0; k < 2; ++k)
 #pragma unroll
     for (int v = 0; v < 16; ++v) asm volatile("" : "+v"(ev[k][v]));
-  write_partials<FWD, H>(acc, l_run, split, nC, my_col, hh, acc_part, l_part);
+  __syncthreads();  // every wave is past its last ring read: the ring takes the partial images
+  write_partials_t<FWD, H>(acc, l_run, split, nC, my_col - r32, r32, hh, acc_part, l_part,
+                           (lds_char_t*)smem + wid * 32 * H * 4);
   TT_KTRACE_K(1, 3);
 }
 
 // P fragment of one 32-query tile for lane (candidate r32, hh): queries 8k + 4 hh + u (k, u < 4)
-// of its candidate row, four 16-B asm loads (no compiler vmcnt waits: the stage barrier counts them).
+// of its candidate row, four 16-B asm loads (no compiler vmcnt waits: the unit's own waits count
+// them).
 struct SplitPSet {
   f32x4 v[4];
 };
@@ -1900,14 +1971,19 @@ __global__ __launch_bounds__(NT, 1) void score_split_ddp_kernel(const __bf16* __
     unit(t + 2, g[0], g[1], pf[3], pf[1]);
     unit(t + 3, g[1], g[0], pf[0], pf[2]);
   }
-  if (t < ntiles) unit(t, g[0], g[1], pf[1], pf[3]);
-  if (t + 1 < ntiles) unit(t + 1, g[1], g[0], pf[2], pf[0]);
-  if (t + 2 < ntiles) unit(t + 2, g[0], g[1], pf[3], pf[1]);
+  if (t < ntiles) {  // (nested: no path runs a later unit without the earlier, whose loads it counts on)
+    unit(t, g[0], g[1], pf[1], pf[3]);
+    if (t + 1 < ntiles) {
+      unit(t + 1, g[1], g[0], pf[2], pf[0]);
+      if (t + 2 < ntiles) unit(t + 2, g[0], g[1], pf[3], pf[1]);
+    }
+  }
   TT_KTRACE_K(0, 2);
   drain_dma();  // no load may outlive the workgroup
 #pragma unroll
   for (int k = 0; k < 4; ++k) split_p_tie(pf[k]);
-  write_partials<DD, H>(acc, 0.f, split, nC, ct * 32 + r32, hh, acc_part, nullptr);
+  __syncthreads();  // every wave is past its last ring read: the ring takes the partial images
+  write_partials_t<DD, H>(acc, 0.f, split, nC, ct * 32, r32, hh, acc_part, nullptr, (lds_char_t*)smem + wid * 32 * H * 4);
   TT_KTRACE_K(0, 3);
 }
 
@@ -2009,7 +2085,7 @@ __global__ __launch_bounds__(256) void prep_qd_kernel(const float* __restrict__ 
   }
   float mx = 0.f;
   if ((int)blockIdx.x < gq) {
-    if (xrows)  // no query row redone exactly yet (see combine_row256)
+    if (xrows)  // no query row redone exactly yet (see combine_rowv)
       for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gq * blockDim.x)
         xrows[1 + i] = 0;
     prep_rows(q, B, H, qb, qnorm, blockIdx.x, gq, mx);
@@ -2110,7 +2186,7 @@ __global__ __launch_bounds__(64 * kL2PrepWaves) void l2_prep_kernel(float* __res
   }
   float mx = 0.f;
   if ((int)blockIdx.x < gq) {
-    if (xrows)  // no query row redone exactly yet (see combine_row256)
+    if (xrows)  // no query row redone exactly yet (see combine_rowv)
       for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gq * blockDim.x)
         xrows[1 + i] = 0;
     l2_prep_rows(y, B, qb, norms, qnorm, blockIdx.x, gq, mx);
@@ -2157,33 +2233,52 @@ __global__ __launch_bounds__(256) void l2_prep128_kernel(float* __restrict__ y, 
   const bool isq = (int)blockIdx.x < gq;
   const int64_t b0 = isq ? blockIdx.x : blockIdx.x - gq, nb = isq ? gq : gridDim.x - gq;
   const int64_t rows = isq ? B : M, base = isq ? 0 : B;
-  if (isq && xrows)  // no query row redone exactly yet (see combine_row256)
+  if (isq && xrows)  // no query row redone exactly yet (see combine_rowv)
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gq * blockDim.x)
       xrows[1 + i] = 0;
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   float mx = 0.f;
-  for (int64_t r = b0 * 4 + wid; r < rows; r += nb * 4) {
-    f32x2* p = reinterpret_cast<f32x2*>(y + (base + r) * H) + lane;
-    f32x2 v = *p;
-    const float ss = wave_sum(__builtin_fmaf(v[1], v[1], v[0] * v[0]));  // head_normalize_kernel<128>
-    const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
-    v[0] *= inv;
-    v[1] *= inv;
-    *p = v;
-    if (lane == 0) norms[base + r] = nrm;
-    if (dp && !isq) {
-      bf16x2 pl[3];
+  // a wave's rows r0 + k stride (k < NR) at once: their loads in flight together and their shuffle
+  // reductions interleaved (one row at a time waited a load and 12 shuffles per row); NR = 2 keeps
+  // the kernel near 50 VGPRs (every wave of the grid resident)
+  constexpr int NR = 2;
+  const int64_t stride = nb * 4;
+  for (int64_t r0 = b0 * 4 + wid; r0 < rows; r0 += NR * stride) {
+    f32x2 v[NR];
+    float nrm[NR], n[NR];
 #pragma unroll
-      for (int e = 0; e < 2; ++e) { __bf16 a0, a1, a2; split3(v[e], a0, a1, a2); pl[0][e] = a0; pl[1][e] = a1; pl[2][e] = a2; }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) reinterpret_cast<bf16x2*>(dp + k * dp_plane + r * H)[lane] = pl[k];
+    for (int k = 0; k < NR; ++k) {
+      const int64_t r = r0 + k * stride;
+      v[k] = reinterpret_cast<const f32x2*>(y + (base + (r < rows ? r : r0)) * H)[lane];
     }
-    // prep_rows (H = 128): lane L < 32 holds elements 4L .. 4L + 3, i.e. lanes 2L and 2L + 1 here
-    const int src = (2 * lane) & (kWave - 1);
-    const f32x4 v4 = {__shfl(v[0], src), __shfl(v[1], src), __shfl(v[0], src + 1), __shfl(v[1], src + 1)};
-    const float n = sqrtf(wave_sum(lane < 32 ? sumsq4(v4) : 0.f));
-    if (isq && lane == 0) qnorm[r] = n;
-    mx = fmaxf(mx, n);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {  // (rows past the end repeat row r0: computed, never stored)
+      const float ss = wave_sum(__builtin_fmaf(v[k][1], v[k][1], v[k][0] * v[k][0]));  // head_normalize_kernel<128>
+      nrm[k] = sqrtf(ss);
+      const float inv = 1.f / fmaxf(nrm[k], 1e-12f);
+      v[k][0] *= inv;
+      v[k][1] *= inv;
+      // prep_rows (H = 128): lane L < 32 holds elements 4L .. 4L + 3, i.e. lanes 2L and 2L + 1 here
+      const int src = (2 * lane) & (kWave - 1);
+      const f32x4 v4 = {__shfl(v[k][0], src), __shfl(v[k][1], src), __shfl(v[k][0], src + 1), __shfl(v[k][1], src + 1)};
+      n[k] = sqrtf(wave_sum(lane < 32 ? sumsq4(v4) : 0.f));
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t r = r0 + k * stride;
+      if (r >= rows) break;  // (wave-uniform)
+      reinterpret_cast<f32x2*>(y + (base + r) * H)[lane] = v[k];
+      if (lane == 0) norms[base + r] = nrm[k];
+      if (dp && !isq) {
+        bf16x2 pl[3];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) { __bf16 a0, a1, a2; split3(v[k][e], a0, a1, a2); pl[0][e] = a0; pl[1][e] = a1; pl[2][e] = a2; }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) reinterpret_cast<bf16x2*>(dp + q * dp_plane + r * H)[lane] = pl[q];
+      }
+      if (isq && lane == 0) qnorm[r] = n[k];
+      mx = fmaxf(mx, n[k]);
+    }
   }
   if (isq) return;
   if (lane == 0) wmax[wid] = mx;
@@ -2248,19 +2343,22 @@ __global__ __launch_bounds__(256) void fwd_combine_kernel(
   const float f_loc = S_loc > 0 ? __builtin_amdgcn_exp2f(col_shift(c2, qnorm[i], fold_dmax(dmax_loc, n_dmax_loc)) - sh)
                                 : 1.f;
   float l = sum_parts1(l_part + i, B, S, S_loc, f_loc);
-  if (H == 4 * kWave) {  // one float4 per lane: every split's loads in flight together
-    const float loss_i = combine_row256<DT>(
+  auto row_v = [&](auto vtag) {  // V = H / 64 floats per lane: every split's loads in flight together
+    constexpr int V = decltype(vtag)::value;
+    using FV = typename RowVec<V>::f;
+    const float loss_i = combine_rowv<DT, V>(
         i, l,
         [&] {
-          const f32x4* p = reinterpret_cast<const f32x4*>(acc_part) + i * (H / 4) + lane;
-          if (S_loc == 0) return sum_parts4(p, B * (H / 4), S);
-          return sum_parts4(p + (int64_t)S_loc * B * (H / 4), B * (H / 4), S - S_loc) +
-                 f_loc * sum_parts4(p, B * (H / 4), S_loc);
+          const FV* p = reinterpret_cast<const FV*>(acc_part) + i * (H / V) + lane;
+          if (S_loc == 0) return sum_parts4(p, B * (H / V), S);
+          return sum_parts4(p + (int64_t)S_loc * B * (H / V), B * (H / V), S - S_loc) +
+                 f_loc * sum_parts4(p, B * (H / V), S_loc);
         },
         sh, n_pad, M, c2, inv_tau, label_off, Qmat, Dmat, lse, lse2, dqu, qs, xrows, lane, qsp, qsp_plane);
     if (lane == 0) loss_rows[i] = loss_i;
-    return;
-  }
+  };
+  if (H == 4 * kWave) return row_v(std::integral_constant<int, 4>{});
+  if (H == 2 * kWave) return row_v(std::integral_constant<int, 2>{});
   l -= (float)n_pad * __builtin_amdgcn_exp2f(-sh);
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
