@@ -1486,9 +1486,6 @@ __device__ __forceinline__ void split_fill_offs(unsigned (&fo)[SplitTile<H>::NPP
   }
 }
 
-#ifndef TT_SPLIT_STORE_ACC
-#define TT_SPLIT_STORE_ACC 0
-#endif
 // The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
 // The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
 template <int H>
@@ -1578,9 +1575,6 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
   constexpr int NSLOT = SplitFwdRing<H>::NSLOT;
   constexpr int kSd = 2, SPS = 16 / NK;
   static_assert(NSTEP % kSd == 0 && kSd <= 2 * NHT, "the barrier point follows the map's stores");
-  // TT_SPLIT_STORE_ACC: P stores in the Acc steps before the barrier point (three a step), where the
-  // gaps carry only operand reads, instead of beside the map's VALU in the S steps
-  constexpr bool kStoreInAcc = TT_SPLIT_STORE_ACC && (NSTEP - kSd - NK) * 3 >= 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const lds_char_t* lds = (const lds_char_t*)smem;
   const int lane = lane_id(), wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1756,7 +1750,7 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
               asm volatile("" : "+v"(e[v]));
             } else if (j == 1) {
               ls += e[v];
-              if (!kStoreInAcc) pstore(v);
+              pstore(v);
             } else if (j == 2) {
               const __bf16 h0 = (__bf16)e[v];
               g[0][v >> 3][v & 7] = h0;
@@ -1772,10 +1766,6 @@ __global__ __launch_bounds__(NT, 1) void score_split_fwd_kernel(
             }
           }
           if (j == 1) asm volatile("" : "+v"(ls));
-        }
-        if (kStoreInAcc && i >= NK && (j & 1)) {  // three P stores per Acc step before the barrier point
-          const int v = (i - NK) * 3 + (j >> 1);
-          if (v < 16) pstore(v);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
