@@ -1487,7 +1487,6 @@ __device__ __forceinline__ void split_fill_offs(unsigned (&fo)[SplitTile<H>::NPP
 }
 
 // The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
-// The forward's LDS ring: four stages where they fit beside nothing else (H <= 128), else three.
 template <int H>
 struct SplitFwdRing {
   static constexpr int NSLOT = 4 * SplitTile<H>::STAGE_B <= 128 * 1024 ? 4 : 3;
