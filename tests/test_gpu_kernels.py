@@ -348,7 +348,7 @@ def test_in_batch_stored_backward_vs_oracle_and_recompute(H, B, M, off):
 
 @pytest.mark.parametrize("H", [32, 64, 128, 256])
 @pytest.mark.parametrize("B,M,off", [(300, 700, 0), (129, 129, 0), (64, 256, 128), (1, 64, 0), (320, 330, 10),
-                                     (2500, 2600, 100)])
+                                     (2500, 2600, 100), (768, 800, 16)])
 def test_in_batch_fp32_stored_backward_vs_oracle_and_recompute(H, B, M, off):
     """The fp32 stored-probability passes against the float64 oracle at the fp32 bar (1e-5) and
     against the fp32 recompute form (score_f32_kernel, exact f32 MFMA).  H = 64, 128, 256: the
@@ -356,7 +356,8 @@ def test_in_batch_fp32_stored_backward_vs_oracle_and_recompute(H, B, M, off):
     per fp32 product, G^T from the forward's fp32 P, the per-query factor folded into three bf16
     planes of the scaled q); H = 32: score_f32_kernel's stored form, whose dq is the recompute
     form's bit for bit (same forward).  B, M off the 32- and 128-row tiles exercise the partial
-    blocks."""
+    blocks; the query tiles per split run 1-3 past the pipelined backward's four-unit loop (B 1 ..
+    2500; 768 x 800: three tiles in every split) and 1 past the forward's two-unit loop."""
     rng = np.random.default_rng(11 * H + B + M)
     q, d = _unit(rng, B, H), _unit(rng, M, H)
     g = 0.7
