@@ -207,7 +207,7 @@ __device__ __forceinline__ int piece_len(int len) {
 // step (j / 64) % 4, lane j % 64; a wave forms each step's same-digit lane set with D ballots,
 // and keeps its running per-digit counts in its own LDS row; the wave offsets per digit are an
 // exclusive scan over the waves' rows.  Bytes per pass: keys (+ values) read twice, written once.
-constexpr int kSortThreads = 512;
+constexpr int kSortThreads = 512;  // (256: the C3 step 0.870-0.874 vs 0.861-0.863 ms, round 4)
 constexpr int kSortWaves = kSortThreads / kWave;
 constexpr int kSortIPT = 4;  // entries per thread per tile
 constexpr int kSortTile = kSortThreads * kSortIPT;
@@ -289,9 +289,11 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
 // One WAVE per digit: cnt[d][0..ntiles) -> its exclusive scan, total[d] = the row sum.  Every
 // chunk of 64 tiles is loaded before the first scan step (up to kScanChunks loads in flight per
 // lane), then scanned with a carry.  Round 3 ran one 512-thread workgroup per digit (512 of them
-// at D = 9): 4.8 us alone but 42 us beside the gather, whose CUs those workgroups had to share;
-// 8-wave workgroups of 8 digits leave 1/8 of the workgroups to dispatch.
-constexpr int kScanWaves = 8;
+// at D = 9): 4.8 us alone but 42 us beside the gather, whose CUs those workgroups had to share.
+// Round 4: 2-wave workgroups of 2 digits, which find room beside the gather's workgroups more
+// readily than 8-wave ones (C3 step 0.8566 / 0.8566 vs 0.8611 / 0.8631 ms with 8 waves, 0.8592 /
+// 0.8543 with 1; profiles/r04z_plan_shapes_ab.txt).
+constexpr int kScanWaves = 2;
 constexpr int kScanChunks = 16;  // chunks of 64 tiles held per lane: 1,024 tiles per round
 __global__ __launch_bounds__(kScanWaves * kWave) void plan_sort_scan_kernel(int32_t* __restrict__ cnt, int64_t ntiles,
                                                                             int nd, int32_t* __restrict__ total) {
