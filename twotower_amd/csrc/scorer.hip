@@ -1211,7 +1211,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
       constexpr int F0 = NS / 2;
 #pragma unroll
       for (int c = 0; c < NPC2; ++c)
-        if (c * F0 / NPC2 == i) fill(NPC1 + c, hbuf, hrow);
+        if (c * F0 / (NPC2 > 0 ? NPC2 : 1) == i) fill(NPC1 + c, hbuf, hrow);
 #pragma unroll
       for (int k = 0; k < NPL; ++k)
         if (F0 + k * (NS - F0) / NPL == i) pload(ahead, t + 3, k);
@@ -1522,7 +1522,6 @@ __device__ __forceinline__ void split_fwd_piece(SplitOp& o, int i, int j, const 
                                                 const lds_char_t* a_tile, const lds_char_t* n_tile,
                                                 const LdsOffs<H>& lo) {
   using ST = SplitTile<H>;
-  using T = typename ST::T;
   constexpr int NK = H / 16, NHT = H / 32, NSTEP = NK + 2 * NHT;
   if (i >= NSTEP) {
     i -= NSTEP;
