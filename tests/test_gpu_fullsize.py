@@ -119,24 +119,28 @@ def test_c3_scorer_full_size_vs_fp64(form, tol):
     assert _rel_t(Q.grad, rdq) < tol and _rel_t(D.grad, rdd) < tol
 
 
-def test_c4_rank_scorer_at_eight_gpu_shape_vs_fp64():
+@pytest.mark.parametrize("per_rank", [2, 1])
+def test_c4_rank_scorer_at_eight_gpu_shape_vs_fp64(per_rank):
     """One rank of the 8-GPU cross-device step (BASELINE.json configs[3], C4): its B 8192 queries
-    against all 8 x 2B = 131072 gathered candidates, labels offset to rank 5's block, H 256, on
-    the bf16 scorer (stored probabilities: 2 GiB of P), against float64 on the same bf16-rounded
-    operands: loss to 1e-6, gradients to 1e-5 (measured 5.5e-6 / 2.0e-6)."""
+    against all gathered candidates, labels offset to rank 5's block, H 256, on the bf16 scorer
+    (stored probabilities), against float64 on the same bf16-rounded operands: loss to 1e-6,
+    gradients to 1e-5 (measured 5.5e-6 / 2.0e-6 in the triplet form).  per_rank 2: the triplet
+    form, 8 x 2B = 131072 candidates (2 GiB of P); per_rank 1: the pairs form as configs[3]
+    states it, 8 x B = 65536 global negatives (bench.py's c4_pairs entry)."""
     world, rank = 8, 5
-    M = world * 2 * B
+    M = world * per_rank * B
     g = torch.Generator(device=DEV).manual_seed(9)
     q = torch.nn.functional.normalize(torch.randn(B, E, device=DEV, generator=g), dim=-1)
     d = torch.nn.functional.normalize(torch.randn(M, E, device=DEV, generator=g), dim=-1)
     Q, D = q.clone().requires_grad_(True), d.clone().requires_grad_(True)
-    loss = ops.in_batch_softmax_loss(Q, D, 0.1, label_off=rank * 2 * B, compute_dtype="bf16")
+    off = rank * per_rank * B
+    loss = ops.in_batch_softmax_loss(Q, D, 0.1, label_off=off, compute_dtype="bf16")
     loss.backward()
-    rl, rdq, rdd = _ref64_in_batch(q.bfloat16().float(), d.bfloat16().float(), 0.1, rank * 2 * B)
+    rl, rdq, rdd = _ref64_in_batch(q.bfloat16().float(), d.bfloat16().float(), 0.1, off)
     assert abs(loss.item() - rl) < 1e-6 * abs(rl)
     assert _rel_t(Q.grad, rdq) < 1e-5 and _rel_t(D.grad, rdd) < 1e-5
     # candidates of other ranks' blocks receive only softmax mass: no label term there
-    assert float(D.grad[:rank * 2 * B].abs().max()) < float(D.grad[rank * 2 * B:(rank * 2 + 1) * B].abs().max())
+    assert float(D.grad[:off].abs().max()) < float(D.grad[off:off + B].abs().max())
 
 
 def test_c3_step_graph_equals_eager_full_size():
