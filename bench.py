@@ -354,11 +354,15 @@ class PlainLoop:
     own ``torch.optim.AdamW(model.parameters(), lr)`` (:358-359: a dense V x E table gradient and
     torch's foreach AdamW over it), and the per-batch monitors: two cosine-similarity means and the
     loss, three ``.item()`` host syncs (:144-154).  What a user gets by swapping the registries
-    and nothing else."""
+    and nothing else.  table_update "backward": the same loop with the config opt-in
+    ``hip: {table_update: backward}`` (optim.fuse_table_update: the table's fused scatter + AdamW at
+    the end of each backward, torch's AdamW for the towers)."""
 
-    def __init__(self, model, loss_fn, lr: float = 1e-3):
+    def __init__(self, model, loss_fn, lr: float = 1e-3, table_update: str = "optimizer"):
         self.model, self.loss_fn = model, loss_fn
         self.optimizer = torch.optim.AdamW(model.parameters(), lr=lr)
+        if table_update == "backward":
+            tt.optim.fuse_table_update(self.optimizer, model)
 
     def __call__(self, q, p, n=None):
         ins = (q, p) if n is None else (q, p, n)
@@ -460,16 +464,25 @@ def c4_pairs_entry(cfg, scorer_dtype: str, dev, world: int, rank: int, steps: in
 
 
 def plain_loop_entry(cfg, loss_fn, batches, dev, steps: int, trainstep_ms: float) -> dict:
-    """PlainLoop timed on the bench's batches (fresh model, torch.optim.AdamW)."""
-    _, model = build_model(cfg, dev)
-    loop = PlainLoop(model, loss_fn)
-    ms = time_steps(loop, batches, steps, 3)
-    del loop, model
-    return {"ms_per_step": round(ms, 4), "pairs_per_s": round(cfg["B"] / (ms * 1e-3), 1), "steps": steps,
-            "trainstep_ms_per_step": round(trainstep_ms, 4), "slowdown_vs_trainstep": round(ms / trainstep_ms, 3),
-            "loop": "twotower/train.py:103-154 body unchanged: eager model(q,p,n), loss_fn, zero_grad/backward/"
-                    "step with torch.optim.AdamW(model.parameters(), lr=1e-3) (dense V x E table gradient), "
-                    "cosine monitors + 3 .item() syncs per step"}
+    """PlainLoop timed on the bench's batches (fresh model, torch.optim.AdamW), as is and with the
+    config opt-in hip: {table_update: backward}."""
+    out = {}
+    for mode in ("optimizer", "backward"):
+        _, model = build_model(cfg, dev)
+        loop = PlainLoop(model, loss_fn, table_update=mode)
+        ms = time_steps(loop, batches, steps, 3)
+        del loop, model
+        out[mode] = {"ms_per_step": round(ms, 4), "pairs_per_s": round(cfg["B"] / (ms * 1e-3), 1),
+                     "slowdown_vs_trainstep": round(ms / trainstep_ms, 3)}
+    e = dict(out["optimizer"])
+    e.update({"steps": steps, "trainstep_ms_per_step": round(trainstep_ms, 4),
+              "loop": "twotower/train.py:103-154 body unchanged: eager model(q,p,n), loss_fn, zero_grad/backward/"
+                      "step with torch.optim.AdamW(model.parameters(), lr=1e-3) (dense V x E table gradient), "
+                      "cosine monitors + 3 .item() syncs per step",
+              "table_update_backward": dict(out["backward"], config="hip: {table_update: backward} (the same loop; the "
+                                            "table's fused scatter + AdamW at the end of loss.backward(), torch's "
+                                            "AdamW for the towers)")})
+    return e
 
 
 def parse():
@@ -487,7 +500,7 @@ def parse():
                          "size 1, TT_DIST_FORCE=1), e.g. to check the N-rank step under HIP-graph capture on one GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard", "owner"],
+    ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard", "owner", "column"],
                     help="N ranks: table update from gathered ids + row grads on every rank (gather), row-sharded "
                          "AdamW after a gradient reduce-scatter (shard), or each rank's own rows from the gathered "
                          "factored gradient (owner); auto picks gather up to 4 ranks")
@@ -501,6 +514,8 @@ def parse():
                          "tools/profile_round.sh sets it so every kernel in the trace belongs to a step")
     ap.add_argument("--zipf", type=float, default=None,
                     help="token ids ~ Zipf(s) over the vocabulary (text-like hot rows); default uniform")
+    ap.add_argument("--table-update", default="optimizer", choices=["optimizer", "backward"],
+                    help="--loop plain: the config opt-in hip: {table_update: backward} (fused table update in backward)")
     ap.add_argument("--loop", default="trainstep", choices=["trainstep", "plain"],
                     help="plain: time the reference's loop body unchanged (bench.PlainLoop: eager, torch.optim.AdamW, "
                          "three .item() syncs) instead of TrainStep")
@@ -602,7 +617,7 @@ def main():
     if plain:
         if dp:
             raise SystemExit("--loop plain runs one GPU (the reference loop has no data parallelism)")
-        opt, step = None, PlainLoop(model, loss_fn)
+        opt, step = None, PlainLoop(model, loss_fn, table_update=args.table_update)
     else:
         # one rank: scatter fused with the table AdamW; N ranks: table rows sharded over the ranks
         # (reduce-scatter, AdamW on own rows, all-gather), tower grads all-reduced
@@ -756,7 +771,8 @@ def main():
                    "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
                    "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if dp else "local"),
                    "hip_graph": use_graph, "graph_canary": canary,
-                   "loop": "reference loop body unchanged (bench.PlainLoop)" if plain else "TrainStep"},
+                   "loop": (f"reference loop body unchanged (bench.PlainLoop, table_update {args.table_update})" if plain
+                            else "TrainStep")},
         "gather_hbm_gbs": gather["achieved"] if gather else None,
         "gather_hbm": gather_hbm_evidence(args.config, gather, V, d),
         "roofline": roofline,

@@ -141,6 +141,28 @@ int tt_bag_mean_bwd_adamw_planned_rows(const float* d_pooled, const float* denom
                                        float* exp_avg_rows, float* exp_avg_sq_rows, const void* adam_args,
                                        tt_stream_t stream);
 
+/* ---- column-sharded table (data parallel, optim.AdamW(table_sync="column")) -------------------
+ * Replaces, per rank, the embedding's dense backward + AdamW (twotower/embeddings.py:30 via
+ * train.py:138-139) for the columns [c0, c0 + El) this rank owns of every table row (its slab,
+ * V x El, and the slab's moments).  The forward is tt_bag_mean_fwd over the slab with every rank's
+ * ids (E = El); these two entry points are the backward:
+ *   tt_bag_scale_rows  gs = d_pooled / denom per row (the division autograd applies at
+ *                      encoders.py:72), nseq x E, before gs is exchanged all-to-all by columns;
+ *   tt_bag_col_reduce  row r's gradient = the sum of gs over every rank's tokens of row r, from the
+ *                      all-gathered per-rank plans (tt_bag_plan): seg_all (nsrc x (V + 1)) row
+ *                      starts and vals_all (nsrc x nL) sorted sequence indices of source src's
+ *                      nseq sequences, gs_all (nsrc * nseq x El) row src * nseq + s.  The sources
+ *                      are merged in rank order inside the reduce (the global batch's stable order),
+ *                      with tt_bag_mean_bwd_planned's interleaved partial sums.  grad != NULL: the
+ *                      gradient rows (V x El) are written; grad == NULL: AdamW on slab / exp_avg /
+ *                      exp_avg_sq with the device scalars adam_args (tt_adam_prepare).
+ *                      El in {32, 64, 128, 256}. */
+int tt_bag_scale_rows(const float* d_pooled, const float* denom, int64_t nseq, int E, float* gs,
+                      tt_stream_t stream);
+int tt_bag_col_reduce(const int32_t* seg_all, const int32_t* vals_all, int64_t nL, int nsrc, int64_t nseq,
+                      const float* gs_all, int64_t V, int El, float* grad, float* slab, float* exp_avg,
+                      float* exp_avg_sq, const void* adam_args, tt_stream_t stream);
+
 /* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
  * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;
  * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps).   step is 1-based.

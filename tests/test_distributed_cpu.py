@@ -236,20 +236,48 @@ def test_capture_blocker_rules(monkeypatch):
     monkeypatch.setattr(D.dist, "is_initialized", lambda: True)
     monkeypatch.setattr(D.dist, "get_backend", lambda group=None: "nccl")
     monkeypatch.setitem(D._AT_IMPORT, "group_existed", False)
-    monkeypatch.setitem(D._AT_IMPORT, "event_cache", "0")
+    monkeypatch.setitem(D._AT_IMPORT, "event_cache", None)
     monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-    assert D.capture_blocker() is None  # group created after the import, the default left alone
+    assert D.capture_blocker() is None  # group created after the import, the default applied
     monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")  # the caller turned the cache back on
     assert "TORCH_NCCL_CUDA_EVENT_CACHE" in D.capture_blocker()
     monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
-    monkeypatch.setitem(D._AT_IMPORT, "event_cache", "1")  # set before the import: setdefault kept it
-    assert D.capture_blocker() is not None
     monkeypatch.setitem(D._AT_IMPORT, "group_existed", True)  # a group created before the import ...
+    assert "before twotower_amd.distributed was imported" in D.capture_blocker()  # ... variable unset
+    monkeypatch.setitem(D._AT_IMPORT, "event_cache", "1")  # ... with the cache on
     assert "before twotower_amd.distributed was imported" in D.capture_blocker()
     monkeypatch.setitem(D._AT_IMPORT, "event_cache", "0")  # ... with the cache off
     assert D.capture_blocker() is None
+    monkeypatch.setattr(D.dist, "get_backend", lambda group=None: "cuda:nccl,cpu:gloo")  # mixed: nccl rules
+    monkeypatch.setitem(D._AT_IMPORT, "event_cache", None)
+    assert "before twotower_amd.distributed was imported" in D.capture_blocker()
     monkeypatch.setattr(D.dist, "get_backend", lambda group=None: "gloo")
     assert "gloo" in D.capture_blocker()
+
+
+def test_capture_blocker_group_before_import_unset_variable():
+    """a process group created before the module's import with the variable unset:
+    the import-time record must keep 'unset' (not the default the import then applies), so the
+    capture is refused."""
+    import subprocess
+    import sys
+
+    code = """
+import os, sys, torch.distributed as dist
+sys.path.insert(0, %r)
+os.environ.pop("TORCH_NCCL_CUDA_EVENT_CACHE", None)
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(%d))
+dist.init_process_group("gloo", rank=0, world_size=1)
+import twotower_amd.distributed as D
+assert D._AT_IMPORT == {"event_cache": None, "group_existed": True}, D._AT_IMPORT
+assert os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] == "0"
+dist.get_backend = lambda group=None: "nccl"
+why = D.capture_blocker()
+assert why is not None and "before" in why, why
+print("ok")
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), _free_port())
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
 
 
 def test_capture_error_classification():
@@ -258,6 +286,9 @@ def test_capture_error_classification():
     assert _is_capture_error(RuntimeError("operation not permitted when stream is capturing"))
     assert _is_capture_error(RuntimeError("hipErrorStreamCaptureUnsupported"))
     assert not _is_capture_error(RuntimeError("mat1 and mat2 shapes cannot be multiplied"))
+    # unrelated errors that merely contain the words a substring match used to take
+    assert not _is_capture_error(RuntimeError("value not permitted for this argument"))
+    assert not _is_capture_error(RuntimeError("the captured tensor was freed"))
 
 
 def test_deferred_loss_mean_only_for_the_bare_in_batch_loss():
@@ -274,3 +305,66 @@ def test_deferred_loss_mean_only_for_the_bare_in_batch_loss():
     assert not tt.TrainStep(model, lambda q, p, n: 0.5 * bare(q, p, n), opt)._defer_mean
     assert not tt.TrainStep(model, tt.losses.build("in_batch", cross_device_negatives=True), opt)._defer_mean
     assert not tt.TrainStep(model, tt.losses.build("triplet"), opt)._defer_mean
+
+
+# ---------------------------------------------------------------------------------------------
+# Column-sharded table (table_sync "column"): the exchanges of BagMeanPoolColumn around the HIP
+# kernels, with torch CPU pooling / scatter standing in for tt_bag_mean_fwd / tt_bag_col_reduce.
+def _column_flow(rank):
+    from twotower_amd import ops
+
+    V, E, nseq, L = 37, 64, 5, 7
+    g = torch.Generator().manual_seed(3)
+    table = torch.randn(V, E, generator=g)
+    ids_all = torch.randint(0, V, (WORLD * nseq, L), generator=g)  # the global batch, rank-major
+    dpool_all = torch.randn(WORLD * nseq, E, generator=g)
+    w = torch.nn.Parameter(table.clone())
+    col = D.ColumnTable(w, None)
+    assert col.El == E // WORLD and torch.equal(col.slab, table[:, rank * col.El:(rank + 1) * col.El])
+
+    def pool(t, ids):  # encoders.py:62-72 on CPU
+        m = (ids > 0).float()
+        return (t[ids] * m[..., None]).sum(1) / (m.sum(1, keepdim=True) + 1e-9)
+
+    # all-to-all semantics
+    x = torch.arange(WORLD * 3 * 2, dtype=torch.float32).view(WORLD * 3, 2) + 100 * rank
+    y = torch.empty_like(x)
+    D.all_to_all_rows(y, x)
+    for s in range(WORLD):
+        assert torch.equal(y[s * 3:(s + 1) * 3], torch.arange(rank * 3 * 2, (rank + 1) * 3 * 2,
+                                                             dtype=torch.float32).view(3, 2) + 100 * s)
+    # forward: this rank's columns for every rank's sequences -> this rank's whole pooled rows
+    part = pool(col.slab, ids_all)
+    pooled = ops.column_pooled_exchange(part, col, nseq)
+    want = pool(table, ids_all[rank * nseq:(rank + 1) * nseq])
+    assert torch.allclose(pooled, want, rtol=1e-6, atol=1e-6)
+    # backward: this rank's gs -> every rank's gs at this rank's columns
+    gs_all = ops.column_grad_exchange(dpool_all[rank * nseq:(rank + 1) * nseq].contiguous(), col)
+    assert torch.equal(gs_all, dpool_all[:, col.c0:col.c0 + col.El])
+    # slabs back into the parameter, moments to full width and back
+    col.slab.mul_(2.0)
+    col.stale = True
+    col.materialize()
+    assert torch.equal(w.data, table * 2.0) and not col.stale
+    m = col.slab * 3.0
+    full = col.gather_cols(m)
+    assert torch.equal(full, table * 6.0) and torch.equal(col.own_cols(full), m)
+    w.data.copy_(table)
+    col.load_from_weight()
+    assert torch.equal(col.slab, table[:, col.c0:col.c0 + col.El])
+
+
+def test_column_table_exchanges_gloo():
+    _run(_column_flow)
+
+
+def test_column_mode_selection(monkeypatch):
+    monkeypatch.setattr(D, "is_active", lambda group=None: True)
+    monkeypatch.setattr(D.dist, "get_world_size", lambda group=None: 8)
+    assert D.table_sync_mode("auto", None, E=256) == "column"   # C3 / C4 / C5 at N = 8: 32 columns each
+    assert D.table_sync_mode("auto", None, E=48) == "shard"     # 6 columns: no column kernel
+    assert D.table_sync_mode("column", None, E=256) == "column"
+    monkeypatch.setattr(D.dist, "get_world_size", lambda group=None: 2)
+    assert D.table_sync_mode("auto", None, E=256) == "column"   # 128 columns each
+    assert D.table_sync_mode("auto", None, E=1024) == "gather"  # 512 columns: past the kernels' slabs
+    assert not D.column_ok(256, 3) and D.column_ok(128, 4)

@@ -136,3 +136,48 @@ def test_unknown_names_raise_the_reference_errors(ref_pkg):
         ref_pkg["encoders"].build_two_tower("nope", None, hidden_dim=4)
     with pytest.raises(ValueError, match="Unknown loss"):
         ref_pkg["losses"].build("nope")
+
+
+@pytest.mark.parametrize("install_before_train_import", [True, False])
+def test_config_opts_in_to_backward_table_update(ref_pkg, tmp_path, install_before_train_import):
+    """`hip: {table_update: backward}` in an otherwise reference config (a namespace the reference
+    never reads) makes the wrapped build_pipeline attach the fused table update to the loop's own
+    torch.optim.AdamW; without it nothing changes; an unknown mode raises."""
+    import twotower_amd as tt
+
+    if install_before_train_import:
+        tt.install("twotower")  # build_pipeline is wrapped when train.py is imported
+        train = importlib.import_module("twotower.train")
+    else:
+        train = importlib.import_module("twotower.train")
+        tt.install("twotower")
+    assert getattr(train.build_pipeline, "_tt_wrapped", False)
+    data = tmp_path / "triplets.parquet"
+    _triplet_parquet(data)
+    model, _, optimizer, _ = train.build_pipeline(_config(ref_pkg, data), device="cpu")
+    assert not hasattr(model.query_tower.embedding.embedding.weight, "_tt_deferred")
+    cfg = _config(ref_pkg, data)
+    cfg["hip"] = {"table_update": "backward"}
+    model, _, optimizer, _ = train.build_pipeline(cfg, device="cpu")
+    assert type(optimizer) is torch.optim.AdamW
+    w = model.query_tower.embedding.embedding.weight
+    upd = w._tt_deferred.on_backward
+    assert isinstance(upd, tt.optim.BackwardTableUpdate) and upd.optimizer is optimizer and upd.weight is w
+    cfg["hip"] = {"table_update": "sideways"}
+    with pytest.raises(ValueError, match="table_update"):
+        train.build_pipeline(cfg, device="cpu")
+
+
+def test_backward_table_update_refuses_what_it_does_not_implement():
+    import twotower_amd as tt
+
+    emb = tt.embeddings.build("lookup", vocab_size=20, embedding_dim=8)
+    model = tt.build_two_tower("mean", emb, hidden_dim=8, tied_weights=True)
+    with pytest.raises(TypeError):
+        tt.optim.fuse_table_update(torch.optim.SGD(model.parameters(), lr=0.1), model)
+    with pytest.raises(ValueError, match="amsgrad"):
+        tt.optim.fuse_table_update(torch.optim.AdamW(model.parameters(), amsgrad=True), model)
+    ups = tt.optim.fuse_table_update(torch.optim.AdamW(model.parameters()), [model, emb])
+    assert len(ups) == 1  # one shared table, attached once
+    with pytest.raises(ValueError, match="already owned"):
+        tt.optim.fuse_table_update(torch.optim.AdamW(model.parameters()), model)

@@ -23,7 +23,12 @@ pytestmark = pytest.mark.gpu
 
 WORLD = 2
 LR = 1e6  # the parameter change dominates the O(1) parameters, so it is read back at fp32 precision
-V, E, B, L = 3001, 64, 64, 24
+V, B, L = 3001, 64, 24
+# tower widths E = H: 64 runs the library head (ops.TowerFF, outside ops.HEAD_WIDTHS); 128 and 256
+# run the shipping hand-written head (tt_head_gemm, tt_head_wgrad2 on the "wgrad" side stream and
+# the SideGrads join that the tower-gradient all-reduce waits on), with the in-batch operand prep
+# in the head's normalise pass and the fused F.normalize backward where those shapes take them
+WIDTHS = (64, 128, 256)
 
 
 def _free_port() -> int:
@@ -32,7 +37,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _build(loss_name, world, table_sync="auto", groups=False):
+def _build(loss_name, world, table_sync="auto", groups=False, E=64):
     import twotower_amd as tt
 
     torch.manual_seed(7)
@@ -60,7 +65,7 @@ def _batch():
     return tt.data.synthetic_triplets(WORLD * B, L, V, seed=3, device="cuda:0")
 
 
-def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1", groups=False):
+def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1", groups=False, E=64):
     # every process recomputes G in the backward (the default; the candidate-owner passes always
     # do), so single process and ranks form the same bf16 products
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TT_INBATCH_DP=inbatch_dp,
@@ -69,22 +74,25 @@ def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1
         torch.cuda.set_device(0)
         if rank >= 0:
             dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-        model, step = _build(loss_name, WORLD if rank >= 0 else 1, table_sync, groups)
+        from twotower_amd import _lib
+
+        model, step = _build(loss_name, WORLD if rank >= 0 else 1, table_sync, groups, E)
         init = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
         full = _batch()
         b = full if rank < 0 else tuple(t[rank * B:(rank + 1) * B] for t in full)
-        loss = step(*b).clone()
+        with _lib.record_calls() as calls:
+            loss = step(*b).clone()
         torch.cuda.synchronize()
         if rank >= 0:
             dist.all_reduce(loss)
             loss /= WORLD
         # numpy arrays travel by value (torch CPU tensors would travel as fds of a dying process)
         delta = {n: p.detach().cpu().numpy() - init[n] for n, p in model.named_parameters()}
-        q.put((rank, float(loss), init, delta, [t.cpu().numpy() for t in full]))
+        q.put((rank, float(loss), init, delta, [t.cpu().numpy() for t in full], sorted(calls)))
     except Exception as e:
         import traceback
 
-        q.put((rank, f"{e!r}\n{traceback.format_exc()}", None, None, None))
+        q.put((rank, f"{e!r}\n{traceback.format_exc()}", None, None, None, None))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -95,70 +103,81 @@ KEYS = {"table": "query_tower.embedding.embedding.weight", "W1": "query_tower.fe
         "b2": "query_tower.feed_forward.2.bias"}
 
 
-@pytest.mark.parametrize("loss_name,table_sync,groups", [("in_batch", "gather", False), ("in_batch", "shard", False),
-                                                         ("triplet", "gather", False), ("triplet", "shard", False),
-                                                         ("triplet", "gather", True), ("in_batch", "shard", True),
-                                                         ("in_batch", "owner", False), ("triplet", "owner", True)])
-def test_dp_step_equals_global_batch(loss_name, table_sync, groups):
-    """One step, eps 1, no decay: delta = -lr g / (|g| + 1), so g is recovered from the parameter
-    change and compared with the float64 oracle on the global batch.  groups: the parameters in
-    two param groups (weights with the table, biases apart), where a per-group all-reduce would
-    sum the gradients twice."""
-    from oracle import reference_math as O
+def _check_head(E, calls, who):
+    """The hand-written head ran at the widths it ships for (and its weight gradients as the
+    one-launch pair on the side stream), the library head below them."""
+    hand = {"tt_head_gemm", "tt_head_wgrad2"}
+    if E in (128, 256):
+        assert hand <= set(calls), (who, E, calls)
+    else:
+        assert not hand & set(calls), (who, E, calls)
 
+
+def _run(loss_name, table_sync, inbatch_dp="owner", overlap="1", groups=False, E=64):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, table_sync, q, "owner", "1", groups))
+    ref = ctx.Process(target=_worker, args=(-1, 0, loss_name, table_sync, q, "owner", "1", groups, E))
     ref.start()
-    _, r_loss, init, r_delta, ids = q.get(timeout=300)
+    single = q.get(timeout=300)
     ref.join(timeout=60)
-    assert init is not None, r_loss
+    assert single[2] is not None, single[1]
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, table_sync, q, "owner", "1", groups))
+    procs = [ctx.Process(target=_worker, args=(r, port, loss_name, table_sync, q, inbatch_dp, overlap, groups, E))
              for r in range(WORLD)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
+    for r, loss, _, delta, _, _ in out:
+        assert delta is not None, loss
+    for who, calls in [("single", single[5])] + [(f"rank{o[0]}", o[5]) for o in out]:
+        _check_head(E, calls, who)
+    return single, out
+
+
+_DP_CASES = [("in_batch", "gather", False), ("in_batch", "shard", False), ("triplet", "gather", False),
+             ("triplet", "shard", False), ("triplet", "gather", True), ("in_batch", "shard", True),
+             ("in_batch", "owner", False), ("triplet", "owner", True), ("in_batch", "column", False),
+             ("triplet", "column", True)]
+
+
+@pytest.mark.parametrize("E", WIDTHS)
+@pytest.mark.parametrize("loss_name,table_sync,groups", _DP_CASES)
+def test_dp_step_equals_global_batch(loss_name, table_sync, groups, E):
+    """One step, eps 1, no decay: delta = -lr g / (|g| + 1), so g is recovered from the parameter
+    change and compared with the float64 oracle on the global batch.  groups: the parameters in
+    two param groups (weights with the table, biases apart), where a per-group all-reduce would
+    sum the gradients twice.  E = H in WIDTHS: 128 and 256 are the shipping
+    hand-written head (checked by the C-ABI calls each process made)."""
+    from oracle import reference_math as O
+
+    (_, r_loss, init, r_delta, ids, _), out = _run(loss_name, table_sync, groups=groups, E=E)
     params = {k: init[v] for k, v in KEYS.items()}
     kw = {"temperature": 0.1} if loss_name == "in_batch" else {"margin": 0.2}
     o_loss, _, o_grads = O.tied_step_grads(params, *ids, loss=loss_name, **kw)
     assert abs(r_loss - o_loss) < 1e-5
-    runs = [("single", r_loss, r_delta)] + [(f"rank{r}", l_, d_) for r, l_, _, d_, _ in out]
+    runs = [("single", r_loss, r_delta)] + [(f"rank{r}", l_, d_) for r, l_, _, d_, _, _ in out]
     for name, loss, delta in runs:
-        assert delta is not None, loss
         assert abs(loss - o_loss) < 1e-5, (name, loss, o_loss)
         for k, key in KEYS.items():
             d = delta[key].astype("float64")
             u = -d / LR
             g = u / (1.0 - abs(u))
             err = abs(g - o_grads[k]).max() / abs(o_grads[k]).max()
-            assert err < 1e-5, (name, k, float(err))
+            assert err < 1e-5, (name, E, k, float(err))
 
 
-@pytest.mark.parametrize("inbatch_dp,overlap", [("owner", "1"), ("owner", "0"), ("allgather", "1")])
-def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp, overlap):
+@pytest.mark.parametrize("E", WIDTHS)
+@pytest.mark.parametrize("inbatch_dp,overlap,table_sync", [("owner", "1", "gather"), ("owner", "0", "gather"),
+                                                           ("allgather", "1", "gather"), ("owner", "1", "column")])
+def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp, overlap, table_sync, E):
     """bf16 scorer with cross-device negatives: candidate-owner gradients (bf16 copies gathered,
     no gradient reduce-scatter; the forward in two launches, own candidates scored while the
     others arrive, or in one launch after the gather) and the fp32-row all-gather + reduce-scatter
     form all give the single process's bf16 gradients on the global batch (same bf16 products,
     other fp32 sum orders), recovered from the parameter change as above."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ref = ctx.Process(target=_worker, args=(-1, 0, "in_batch_bf16", "gather", q))
-    ref.start()
-    _, r_loss, init, r_delta, _ = q.get(timeout=300)
-    ref.join(timeout=60)
-    assert init is not None, r_loss
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, "in_batch_bf16", "gather", q, inbatch_dp, overlap))
-             for r in range(WORLD)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    (_, r_loss, _, r_delta, _, _), out = _run("in_batch_bf16", table_sync, inbatch_dp, overlap, E=E)
 
     def grads(delta):
         out = {}
@@ -168,13 +187,12 @@ def test_dp_step_bf16_in_batch_equals_global_batch(inbatch_dp, overlap):
         return out
 
     want = grads(r_delta)
-    for r, loss, _, delta, _ in out:
-        assert delta is not None, loss
+    for r, loss, _, delta, _, _ in out:
         assert abs(loss - r_loss) < 1e-5, (r, loss, r_loss)
         got = grads(delta)
         for k in KEYS:
             err = abs(got[k] - want[k]).max() / abs(want[k]).max()
-            assert err < 1e-5, (inbatch_dp, r, k, float(err))
+            assert err < 1e-5, (inbatch_dp, E, r, k, float(err))
 
 
 def _seed_worker(rank, port, q, seeds, Bq, M, H):
@@ -205,15 +223,16 @@ def _seed_worker(rank, port, q, seeds, Bq, M, H):
             dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("H", WIDTHS)
 @pytest.mark.parametrize("seeds", [(0.5, 0.5), (0.3, 1.7), (0.0, 1.0)])
-def test_owner_backward_takes_each_ranks_seed(seeds):
+def test_owner_backward_takes_each_ranks_seed(seeds, H):
     """Candidate-owner gradients when the ranks seed their loss backward differently (ADVICE
     round 1): the objective is sum_r seed_r * loss_r, and the gradient of each rank's candidates
     must weigh every remote query's terms by that query's own rank seed.  Checked against float64
     autograd on the bf16-rounded operands at the bf16 scorer's bar."""
     import numpy as np
 
-    Bq, M, H = 96, 192, 64
+    Bq, M = 96, 192
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -241,7 +260,8 @@ def test_owner_backward_takes_each_ranks_seed(seeds):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("table_sync,loss_name", [("gather", "in_batch"), ("shard", "in_batch"),
-                                                  ("shard", "multiple_negatives"), ("owner", "multiple_negatives")])
+                                                  ("shard", "multiple_negatives"), ("owner", "multiple_negatives"),
+                                                  ("column", "in_batch"), ("column", "multiple_negatives")])
 def test_dp_graph_replay_equals_eager_one_rank_rccl(table_sync, loss_name):
     """The N-rank step captured in one HIP graph (its RCCL collectives included: candidate
     all-gathers, the table exchange, the gradient all-reduce on the communication stream) replays
@@ -260,3 +280,66 @@ def test_dp_graph_replay_equals_eager_one_rank_rccl(table_sync, loss_name):
     assert res["graph_kept"], res
     assert res["eager"] == res["graph"], res
     assert res["max_param_diff"] == 0.0, res
+
+
+def _owner_vs_gather_worker(rank, port, q, Vt, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        import twotower_amd as tt
+
+        res = {}
+        for mode in ("gather", "owner"):
+            torch.manual_seed(5)
+            emb = tt.embeddings.build("lookup", vocab_size=Vt, embedding_dim=128)
+            model = tt.build_two_tower("mean", emb, hidden_dim=128, tied_weights=True).to("cuda:0")
+            opt = tt.optim.AdamW(model.parameters(), lr=1e-2, fused_tables=True, tables=[emb], capturable=True,
+                                 table_sync=mode)
+            step = tt.TrainStep(model, tt.losses.build("triplet", margin=0.2), opt)
+            for s in range(steps):
+                full = tt.data.synthetic_triplets(WORLD * B, L, Vt, seed=20 + s, device="cuda:0")
+                step(*(t[rank * B:(rank + 1) * B] for t in full))
+            torch.cuda.synchronize()
+            w = emb.embedding.weight
+            sh = opt._shards.get(id(w))
+            pad = None
+            if sh is not None:  # the storage rows past V (the last chunks' padding) must stay zero
+                pad = float(sh.storage()[sh.V:].abs().max()) if sh.Vp > sh.V else 0.0
+                res["layout"] = (sh.NC, sh.R, sh.Vp)
+            res[mode] = (w.detach().cpu().numpy().copy(), pad)
+        q.put((rank, res))
+    except Exception as e:
+        import traceback
+
+        q.put((rank, f"{e!r}\n{traceback.format_exc()}"))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("Vt", [17, 3001])
+def test_owner_equals_gather_when_rows_do_not_divide(Vt):
+    """the "owner" exchange at a vocabulary that is not a multiple of chunks x ranks.
+    V = 3001 (NC 8, R 188): the last owned slab of rank 1 is clipped; V = 17 (NC 8, R 2): whole
+    chunks are padding and some ranks own no row of a chunk at all, while the chunk is still
+    all-gathered.  After two steps the table equals the replicated "gather" update bit for bit on
+    every rank, and the padding rows of the storage stay zero."""
+    import numpy as np
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_vs_gather_worker, args=(r, port, q, Vt, 2)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for r, res in out:
+        assert isinstance(res, dict), res
+        g, _ = res["gather"]
+        o, pad = res["owner"]
+        assert pad == 0.0, (r, pad, res["layout"])
+        assert np.array_equal(g, o), (r, float(np.abs(g - o).max()), res["layout"])
+    assert np.array_equal(out[0][1]["owner"][0], out[1][1]["owner"][0])

@@ -10,7 +10,7 @@
   unjoined    a side stream forked from the capture and never joined (no collective)
   step_gather the bench's DP TrainStep (--dp gather) captured through TrainStep(graph=True)
 
-Usage: python tools/dbg/capture_probe.py MODE   (prints one JSON line; segfaults are the finding)"""
+Usage: python tools/repro/capture_probe.py MODE   (prints one JSON line; segfaults are the finding)"""
 import faulthandler
 import json
 import os

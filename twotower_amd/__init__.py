@@ -34,6 +34,10 @@ def install(package: str = "twotower") -> None:
 
     Call before ``import twotower.train`` (its ``from .encoders import build_two_tower`` binds
     the name at import); names already bound in an imported ``twotower.train`` are patched too.
+    ``train.build_pipeline`` (train.py:298-371) is wrapped, now or when train is imported, so a
+    config may opt in to the fused table update for the loop's own torch.optim.AdamW under a
+    namespace the reference ignores: ``hip: {table_update: backward}`` (optim.fuse_table_update;
+    default / ``optimizer``: the dense table gradient stepped by the optimizer, as before).
     """
     emb = importlib.import_module(f"{package}.embeddings")
     enc = importlib.import_module(f"{package}.encoders")
@@ -47,4 +51,61 @@ def install(package: str = "twotower") -> None:
         los.LOSS_REGISTRY[name] = fn
     train_mod = sys.modules.get(f"{package}.train")
     if train_mod is not None:
-        train_mod.build_two_tower = build_two_tower
+        _patch_train(train_mod)
+    elif not any(isinstance(f, _TrainImportHook) and f.name == f"{package}.train" for f in sys.meta_path):
+        sys.meta_path.insert(0, _TrainImportHook(f"{package}.train"))
+
+
+TABLE_UPDATES = ("optimizer", "backward")
+
+
+def _patch_train(train_mod) -> None:
+    train_mod.build_two_tower = build_two_tower
+    orig = getattr(train_mod, "build_pipeline", None)
+    if orig is None or getattr(orig, "_tt_wrapped", False):
+        return
+
+    def build_pipeline(config, device):
+        hip = config.get("hip", {}) or {}
+        mode = hip.get("table_update", "optimizer")
+        if mode not in TABLE_UPDATES:
+            raise ValueError(f"hip.table_update must be one of {TABLE_UPDATES}, got {mode!r}")
+        model, dataset, optimizer, loss_fn = orig(config, device)
+        if mode == "backward":
+            optim.fuse_table_update(optimizer, model)
+        return model, dataset, optimizer, loss_fn
+
+    build_pipeline._tt_wrapped = True
+    build_pipeline.__wrapped__ = orig
+    build_pipeline.__doc__ = orig.__doc__
+    train_mod.build_pipeline = build_pipeline
+
+
+class _TrainImportHook:
+    """Patches ``<package>.train`` right after it is first imported (install() ran before it)."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def find_spec(self, fullname, path=None, target=None):
+        if fullname != self.name:
+            return None
+        import importlib.machinery
+        import importlib.util
+
+        sys.meta_path.remove(self)
+        try:
+            spec = importlib.util.find_spec(fullname)
+        finally:
+            sys.meta_path.insert(0, self)
+        if spec is None or spec.loader is None:
+            return spec
+        loader = spec.loader
+        exec_module = loader.exec_module
+
+        def exec_and_patch(module):
+            exec_module(module)
+            _patch_train(module)
+
+        loader.exec_module = exec_and_patch
+        return spec

@@ -71,6 +71,9 @@ _SIGNATURES = {
                                                _vp, _vp]),
     "tt_bag_mean_bwd_adamw_planned_rows": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _c_i64,
                                                     _c_i64, _vp, _vp, _vp, _vp, _vp]),
+    "tt_bag_scale_rows": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp]),
+    "tt_bag_col_reduce": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp,
+                                   _vp]),
     "tt_adam_prepare": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _vp]),
     "tt_adam_prepare_ex": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64,
                                     _c_int, _c_int, _vp]),
@@ -360,9 +363,25 @@ class OpTimer:
 
 TIMER = OpTimer()
 
+# names of the C-ABI entry points called while a record_calls() block is open (tests and smoke()
+# use it to show which kernels a path actually ran, e.g. the hand-written head vs the library one)
+_CALLS: list[set] = []
+
+
+@contextlib.contextmanager
+def record_calls():
+    seen: set = set()
+    _CALLS.append(seen)
+    try:
+        yield seen
+    finally:
+        _CALLS.remove(seen)
+
 
 def call(name: str, *args) -> None:
     fn = getattr(lib(), name)
+    for seen in _CALLS:
+        seen.add(name)
     check(TIMER.run(name, lambda: fn(*args)), name)
 
 

@@ -763,6 +763,98 @@ __global__ __launch_bounds__(kBlock) void bag_bwd_reduce_generic_kernel(
   }
 }
 
+// Column-sharded table (data parallel, table_sync "column"): this rank owns columns [c0, c0 + El)
+// of every row as its slab (V x El, with its moments), and their gradient sums every rank's tokens.
+// Each rank sorted only its own tokens (tt_bag_plan); the plans are all-gathered -- vals (nsrc, nL)
+// sorted sequence indices, seg (nsrc, V + 1) row starts -- and gs (nsrc * nseq, El) holds every
+// rank's d_pooled / denom at these columns (all-to-all).  Row r's tokens in the global stable order
+// (ascending global sequence src * nseq + s, the order of the reference's dense backward over the
+// global batch) are source 0's segment of row r, then source 1's, ...: the per-source plans merged
+// inside the reduce, no global sort.  Merged entry k goes to partial k % U, as entry (e - st) does in
+// bag_bwd_reduce(_sliced)_kernel, and the partials fold in the same order, so a row's sum equals the
+// single-plan reduce of the concatenated batch bit for bit (rows without pieces).  The invariant
+// "the next entry goes to part[0]" is kept by rotating the partials at each source boundary.
+// One wave holds RPI = 64 / LPR rows (El = 4 * LPR floats each: 128 B at El = 32), then AdamW on
+// (slab, m, v) row r (FUSED) or the gradient row is written.
+template <int U>
+__device__ __forceinline__ void rotate_parts(f32x4 (&part)[U], int r) {
+  // part[j] <- part[(j + r) % U]
+  static_assert(U == 4, "rotation written for U = 4");
+  if (r & 1) {
+    const f32x4 t = part[0];
+    part[0] = part[1]; part[1] = part[2]; part[2] = part[3]; part[3] = t;
+  }
+  if (r & 2) {
+    f32x4 t = part[0]; part[0] = part[2]; part[2] = t;
+    t = part[1]; part[1] = part[3]; part[3] = t;
+  }
+}
+
+template <int LPR, int U, bool FUSED, bool NT>
+__global__ __launch_bounds__(kBlock) void bag_col_reduce_kernel(
+    const int32_t* __restrict__ seg, const int32_t* __restrict__ vals, int64_t nL, int nsrc, int64_t nseq,
+    const float* __restrict__ gs, int64_t V, float* __restrict__ grad, float* __restrict__ param,
+    float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq, const AdamArgs* __restrict__ aa_dev) {
+  constexpr int RPI = kWave / LPR;
+  constexpr int El = 4 * LPR;
+  const int lane = lane_id();
+  const int sub = lane / LPR, c = lane % LPR;
+  const int64_t row = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  if (row >= V) return;
+  f32x4 pv, mv, vv;
+  AdamArgs aa{};
+  if constexpr (FUSED) {
+    aa = *aa_dev;
+    pv = ld4<NT>(param + row * El, c);
+    mv = ld4<NT>(exp_avg + row * El, c);
+    vv = ld4<NT>(exp_avg_sq + row * El, c);
+  }
+  f32x4 part[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int64_t total = 0;
+  for (int src = 0; src < nsrc; ++src) {
+    const int32_t* sg = seg + (int64_t)src * (V + 1);
+    const int st = sg[row], en = sg[row + 1];
+    const int32_t* vl = vals + (int64_t)src * nL;
+    const float* g = gs + (int64_t)src * nseq * El;
+    for (int e = st; e < en; e += U) {
+      int sq[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sq[u] = (e + u < en) ? vl[e + u] : -1;
+      f32x4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[u] = (sq[u] >= 0) ? reinterpret_cast<const f32x4*>(g + (int64_t)sq[u] * El)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) part[u] += x[u];
+    }
+    const int cnt = en - st;
+    total += cnt;
+    rotate_parts(part, cnt % U);  // the next source's first entry goes to part[0]
+  }
+  // part[j] holds the entries k == total + j (mod U): back to part[j] = entries k == j (mod U)
+  rotate_parts(part, (int)((U - total % U) % U));
+  f32x4 acc = part[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) acc += part[u];
+  if constexpr (!FUSED) {
+    st4<NT>(grad + row * El, c, acc);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float pj = pv[j], mj = mv[j], vj = vv[j];
+      adam_update(pj, acc[j], mj, vj, aa);
+      pv[j] = pj;
+      mv[j] = mj;
+      vv[j] = vj;
+    }
+    st4<NT>(param + row * El, c, pv);
+    st4<NT>(exp_avg + row * El, c, mv);
+    st4<NT>(exp_avg_sq + row * El, c, vv);
+  }
+}
+
 // Atomic path: one wave per sequence; lane owns columns lane, lane+64, ... so each
 // global_atomic_add_f32 wave-instruction covers 256 contiguous bytes of the row.
 template <typename IdT>
@@ -895,6 +987,7 @@ int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nse
 #define TT_FWD(LPR, NV, U) \
   bag_fwd_kernel<IdT, LPR, NV, U><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom, sj, planes, nsplit)
   switch (E) {
+    case 32: TT_FWD(8, 1, 4); break;  // a column slab of E = 256 over 8 ranks (table_sync "column")
     case 64: TT_FWD(16, 1, 4); break;
     case 128: TT_FWD(32, 1, 4); break;
     case 256: TT_FWD(64, 1, 8); break;
@@ -1277,4 +1370,52 @@ extern "C" int tt_bag_mean_bwd_adamw(const float* d_pooled, const float* denom, 
   if (rc) return rc;
   return apply_impl<true>(d_pooled, denom, nseq, L, V, E, ws, ws_bytes, nullptr, table, exp_avg, exp_avg_sq, aa,
                           nullptr, s);
+}
+
+// ---- column-sharded table (table_sync "column") ------------------------------------------------
+extern "C" int tt_bag_scale_rows(const float* d_pooled, const float* denom, int64_t nseq, int E, float* gs,
+                                 tt_stream_t stream) {
+  TT_REQUIRE(nseq >= 0 && E > 0 && E % 4 == 0, "tt_bag_scale_rows: nseq=%lld E=%d (E a multiple of 4)",
+             (long long)nseq, E);
+  TT_REQUIRE(nseq == 0 || (d_pooled && denom && gs), "null pointer");
+  if (nseq == 0) return TT_OK;
+  bag_scale_rows_kernel<<<dim3((unsigned)((nseq + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0,
+                          reinterpret_cast<hipStream_t>(stream)>>>(d_pooled, denom, nseq, E, gs);
+  TT_LAUNCH_CHECK("tt_bag_scale_rows");
+  return TT_OK;
+}
+
+extern "C" int tt_bag_col_reduce(const int32_t* seg_all, const int32_t* vals_all, int64_t nL, int nsrc,
+                                 int64_t nseq, const float* gs_all, int64_t V, int El, float* grad, float* slab,
+                                 float* exp_avg, float* exp_avg_sq, const void* adam_args, tt_stream_t stream) {
+  TT_REQUIRE(V > 0 && V < (int64_t(1) << 31) - 1 && nsrc > 0 && nseq >= 0 && nL >= 0 && nL < (int64_t(1) << 31),
+             "tt_bag_col_reduce: bad shape (V=%lld nsrc=%d nseq=%lld nL=%lld)", (long long)V, nsrc, (long long)nseq,
+             (long long)nL);
+  TT_REQUIRE(El == 32 || El == 64 || El == 128 || El == 256, "tt_bag_col_reduce: El %d not in {32, 64, 128, 256}", El);
+  TT_REQUIRE(seg_all && (nL == 0 || (vals_all && gs_all)), "null pointer");
+  const bool fused = grad == nullptr;
+  TT_REQUIRE(fused ? (slab && exp_avg && exp_avg_sq && adam_args) : true, "null pointer (fused update)");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const AdamArgs* aa = static_cast<const AdamArgs*>(adam_args);
+  const int LPR = El / 4, rpi = kWave / LPR;
+  const int64_t waves = (V + rpi - 1) / rpi;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+#define TT_COL(L)                                                                                             \
+  do {                                                                                                        \
+    if (fused)                                                                                                \
+      bag_col_reduce_kernel<L, 4, true, false><<<grid, block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
+                                                                     nullptr, slab, exp_avg, exp_avg_sq, aa);  \
+    else                                                                                                      \
+      bag_col_reduce_kernel<L, 4, false, false><<<grid, block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
+                                                                      grad, nullptr, nullptr, nullptr, nullptr); \
+  } while (0)
+  switch (El) {
+    case 32: TT_COL(8); break;
+    case 64: TT_COL(16); break;
+    case 128: TT_COL(32); break;
+    default: TT_COL(64); break;
+  }
+#undef TT_COL
+  TT_LAUNCH_CHECK("tt_bag_col_reduce");
+  return TT_OK;
 }

@@ -31,11 +31,22 @@ import torch.distributed as dist
 # groups created after this import with the variable left alone: capture_blocker() tells the
 # others apart, and TrainStep then stays eager instead of capturing.
 _EVENT_CACHE_VAR = "TORCH_NCCL_CUDA_EVENT_CACHE"
-os.environ.setdefault(_EVENT_CACHE_VAR, "0")
-# what held when this module was imported: the value, and whether a process group already existed
-# (its ProcessGroupNCCL then read the variable before the default above could apply)
+# what held when this module was imported, read BEFORE the default below is applied: the caller's
+# own value (None: unset), and whether a process group already existed (its ProcessGroupNCCL then
+# read the variable at its creation, before the default could apply: an unset variable meant the
+# cache was on)
 _AT_IMPORT = {"event_cache": os.environ.get(_EVENT_CACHE_VAR),
               "group_existed": dist.is_available() and dist.is_initialized()}
+os.environ.setdefault(_EVENT_CACHE_VAR, "0")
+
+
+def _backend_kind(group=None) -> str:
+    """"nccl", "gloo" or "other" for `group`'s backend; a mixed device:backend string
+    ('cuda:nccl,cpu:gloo') counts as nccl, since its GPU collectives are ProcessGroupNCCL's."""
+    b = str(dist.get_backend(group)).lower()
+    if "nccl" in b:
+        return "nccl"
+    return "gloo" if "gloo" in b else "other"
 
 
 def capture_blocker(group=None) -> str | None:
@@ -45,22 +56,23 @@ def capture_blocker(group=None) -> str | None:
     collectives recorded during a capture, and its watchdog thread then queries an event last
     recorded in a capturing stream: an uncatchable abort (std::terminate in the watchdog).  The
     cache is off only for a group created while TORCH_NCCL_CUDA_EVENT_CACHE=0; this module sets
-    that default at import, so a group created before the import, or with the variable set to
-    anything else, is refused here.  gloo groups are not captured at all (their collectives
-    stage through host memory)."""
+    that default at import, so a group created before the import without the caller having set
+    the variable to '0', or any group while the variable is anything else, is refused here.  gloo
+    groups are not captured at all (their collectives stage through host memory)."""
     if not (dist.is_available() and dist.is_initialized()):
         return None
-    backend = dist.get_backend(group)
-    if backend == "gloo":
+    kind = _backend_kind(group)
+    if kind == "gloo":
         return "gloo collectives cannot be captured in a HIP graph"
-    if backend != "nccl":
+    if kind != "nccl":
         return None
     if _AT_IMPORT["group_existed"]:
         if _AT_IMPORT["event_cache"] != "0":
-            return (f"the process group was created before twotower_amd.distributed was imported, without "
-                    f"{_EVENT_CACHE_VAR}=0 (ProcessGroupNCCL's event cache aborts the watchdog under graph capture)")
+            return (f"the process group was created before twotower_amd.distributed was imported, with "
+                    f"{_EVENT_CACHE_VAR}={_AT_IMPORT['event_cache']!r} (not '0': ProcessGroupNCCL's event cache "
+                    f"aborts the watchdog under graph capture)")
         return None
-    if os.environ.get(_EVENT_CACHE_VAR) != "0" or _AT_IMPORT["event_cache"] != "0":
+    if os.environ.get(_EVENT_CACHE_VAR) != "0":
         return (f"{_EVENT_CACHE_VAR} is {os.environ.get(_EVENT_CACHE_VAR)!r}, not '0' (ProcessGroupNCCL's event "
                 f"cache aborts the watchdog under graph capture)")
     return None
@@ -75,7 +87,7 @@ def is_active(group=None) -> bool:
     return dist.get_world_size(group) > 1 or os.environ.get("TT_DIST_FORCE") == "1"
 
 
-def table_sync_mode(requested: str, group=None) -> str:
+def table_sync_mode(requested: str, group=None, E: int | None = None) -> str:
     """How an embedding table's gradient crosses ranks:
       "local"  -- one rank (no exchange);
       "gather" -- all-gather the factored gradient (ids in the forward, d_pooled/denom after the
@@ -86,20 +98,27 @@ def table_sync_mode(requested: str, group=None) -> str:
       "owner"  -- all-gather the factored gradient as "gather" does, but each rank scatters and
                   updates only the rows it owns (shard's row partition and moment shards), then
                   the rows are all-gathered: (N-1) x 31 MB + 205 MB x (N-1)/N per rank at C3,
-                  1/N of the update's HBM traffic, no dense gradient.
-    "auto": gather up to 4 ranks (its bytes grow with N; at N <= 4 a rank pair shares few xGMI
-    links, where the dense exchange is link-bound), shard beyond."""
+                  1/N of the update's HBM traffic, no dense gradient;
+      "column" -- each rank owns E / N columns of every row (ColumnTable): the ids are all-gathered,
+                  pooled and d_pooled column blocks exchanged all-to-all, no table row ever crosses
+                  the links, 1/N of the update per rank (C5 at N = 8: ~0.26 GB per rank and step,
+                  against 1.3-1.8 GB for owner / shard).
+    "auto": "column" when the width splits into the column kernels' slabs (E / N in 32..256: C3/C4/C5
+    at N = 2, 4, 8), else gather up to 4 ranks, shard beyond."""
     if not is_active(group):
         return "local"
     if requested == "auto":
-        return "gather" if dist.get_world_size(group) <= 4 else "shard"
-    if requested not in ("gather", "shard", "owner"):
-        raise ValueError(f"table_sync must be 'auto', 'gather', 'shard' or 'owner', got {requested!r}")
+        world = dist.get_world_size(group)
+        if E is not None and column_ok(E, world):
+            return "column"
+        return "gather" if world <= 4 else "shard"
+    if requested not in ("gather", "shard", "owner", "column"):
+        raise ValueError(f"table_sync must be 'auto', 'gather', 'shard', 'owner' or 'column', got {requested!r}")
     return requested
 
 
 def _is_gloo(group=None) -> bool:
-    return dist.get_backend(group) == "gloo"
+    return _backend_kind(group) == "gloo"
 
 
 def reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
@@ -235,6 +254,84 @@ class ShardedRows:
         for c in range(self.NC):
             lo, hi = self.chunk(c)
             all_gather_rows(st[lo:hi], self.own(st, c), self.group)
+
+
+def all_to_all_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """Equal-split all-to-all over rows: block s of `out` (rows [s n, (s + 1) n), n = rows / world)
+    = block r of rank s's `inp`, r = this rank."""
+    world = dist.get_world_size(group)
+    if _is_gloo(group):  # no gloo all-to-all on GPU tensors: all-gather the send buffers, keep our blocks
+        full = inp.new_empty((world,) + tuple(inp.shape))
+        all_gather_rows(full.view((world * inp.shape[0],) + tuple(inp.shape[1:])), inp.contiguous(), group)
+        n = inp.shape[0] // world
+        r = dist.get_rank(group)
+        out.copy_(full[:, r * n:(r + 1) * n].reshape(out.shape))
+        return
+    dist.all_to_all_single(out, inp.contiguous(), group=group)
+
+
+COLUMN_WIDTHS = (32, 64, 128, 256)  # slab widths El the column kernels take (tt_bag_col_reduce)
+
+
+def column_ok(E: int, world: int) -> bool:
+    """A (V, E) table can be column-sharded over `world` ranks."""
+    return world >= 1 and E % world == 0 and E // world in COLUMN_WIDTHS
+
+
+class ColumnTable:
+    """Column partition of a (V, E) embedding table over the ranks of `group` (table_sync
+    "column"): rank r owns columns [r El, (r + 1) El) of EVERY row, El = E / world, as a compact
+    (V, El) fp32 slab with its AdamW moments.  Nothing of the table crosses the links:
+      * forward: every rank's ids are all-gathered, each rank pools ITS columns for every rank's
+        sequences (tt_bag_mean_fwd over the slab, El wide) and the pooled column blocks are
+        exchanged all-to-all, so each rank gets its own sequences' whole pooled rows;
+      * backward: d_pooled / denom is cut into column blocks and exchanged all-to-all, and each rank
+        forms the gradient of its slab from every rank's tokens (the per-rank sort plans,
+        all-gathered during the forward, merged in rank order: tt_bag_col_reduce) fused with AdamW
+        on its slab -- the dense AdamW of train.py:139 over every element, exactly once, 1/world of
+        the table's optimizer traffic per rank.
+    The parameter tensor (V, E) is kept for the model's API (state_dict keys, shapes) but goes
+    stale after the first update: materialize() all-gathers the slabs into it (a collective: every
+    rank calls it), and the owning nn.Embedding does so before state_dict() (a pre-hook); a
+    load_state_dict() into the module reloads the slab from the loaded weight."""
+
+    def __init__(self, weight: torch.Tensor, group=None, module: torch.nn.Module | None = None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.V, self.E = weight.shape
+        if not column_ok(self.E, self.world):
+            raise ValueError(f"table_sync 'column' needs E / world in {COLUMN_WIDTHS} (E {self.E}, world {self.world})")
+        self.El = self.E // self.world
+        self.c0 = self.rank * self.El
+        self.weight = weight
+        self.slab = weight.detach()[:, self.c0:self.c0 + self.El].contiguous().clone()
+        self.stale = False
+        if module is not None:
+            module.register_state_dict_pre_hook(lambda *_a, **_k: self.materialize())
+            module.register_load_state_dict_post_hook(lambda *_a, **_k: self.load_from_weight())
+
+    def gather_cols(self, t: torch.Tensor) -> torch.Tensor:
+        """(V, E) tensor whose column block r is rank r's (V, El) `t` (an all-gather)."""
+        buf = t.new_empty(self.world * self.V, self.El)
+        all_gather_rows(buf, t.contiguous(), self.group)
+        return buf.view(self.world, self.V, self.El).permute(1, 0, 2).reshape(self.V, self.E)
+
+    def own_cols(self, full: torch.Tensor) -> torch.Tensor:
+        """This rank's (V, El) columns of a (V, E) tensor (a copy)."""
+        return full[:, self.c0:self.c0 + self.El].contiguous()
+
+    @torch.no_grad()
+    def materialize(self) -> None:
+        """Write every rank's slab into the (V, E) parameter (collective)."""
+        if self.stale:
+            self.weight.data.copy_(self.gather_cols(self.slab))
+            self.stale = False
+
+    @torch.no_grad()
+    def load_from_weight(self) -> None:
+        self.slab.copy_(self.weight.data[:, self.c0:self.c0 + self.El])
+        self.stale = False
 
 
 class AllGatherRows(torch.autograd.Function):

@@ -226,14 +226,30 @@ def bag_mean_backward_planned_rows(d_pooled: torch.Tensor, denom: torch.Tensor |
 class DeferredTableGrad:
     """Table gradient kept in its factored form (ids, d_pooled, denom, plan) so a fused optimizer
     can apply scatter + AdamW in one pass (tt_bag_mean_bwd_adamw) without the dense V x E buffer.
-    gather_group: data parallel, replicated table update (the plan covers every rank's ids)."""
+    gather_group: data parallel, replicated table update (the plan covers every rank's ids).
+    on_backward: a callable queued to run once at the end of each backward pass that produced
+    parts (optim.BackwardTableUpdate: the fused update inside loss.backward(), for a loop that
+    keeps torch.optim.AdamW)."""
 
-    __slots__ = ("parts", "padding_idx", "gather_group")
+    __slots__ = ("parts", "padding_idx", "gather_group", "on_backward", "queued")
 
-    def __init__(self, padding_idx: int | None = 0, gather_group=None):
+    def __init__(self, padding_idx: int | None = 0, gather_group=None, on_backward=None):
         self.parts: list[tuple] = []
         self.padding_idx = padding_idx
         self.gather_group = gather_group
+        self.on_backward = on_backward
+        self.queued = False
+
+    def added(self) -> None:
+        """A backward node appended its part: queue on_backward for the end of this backward pass
+        (once, however many bag calls on the table the pass differentiates)."""
+        if self.on_backward is not None and not self.queued:
+            self.queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._fire)
+
+    def _fire(self) -> None:
+        self.queued = False
+        self.on_backward()
 
 
 class BagMeanPool(torch.autograd.Function):
@@ -295,6 +311,7 @@ class BagMeanPool(torch.autograd.Function):
         if deferred is not None:
             # A fused optimizer owns this table: hand it the factored gradient.
             deferred.parts.append((ids, d_pooled.contiguous(), denom, plan))
+            deferred.added()
             return None, None, None, None, None
         if plan is not None:
             return bag_mean_backward_planned(d_pooled, denom, plan), None, None, None, None
@@ -304,8 +321,166 @@ class BagMeanPool(torch.autograd.Function):
         return grad, None, None, None, None
 
 
+class ColumnPlan:
+    """The sort plan of this rank's tokens (a BagPlan over the local ids, El wide) and, once
+    ``exchange()`` ran, every rank's plan all-gathered on the plan's side stream: seg_all
+    (world, V + 1) row starts and vals_all (world, nseq * L) sorted sequence indices, the inputs of
+    tt_bag_col_reduce.  ``ready`` marks the exchange's end on the side stream."""
+
+    __slots__ = ("plan", "seg_all", "vals_all", "nL", "ready")
+
+    def __init__(self, ids: torch.Tensor, V: int, El: int, padding_idx):
+        self.plan = BagPlan(ids, V, El, padding_idx)
+        self.nL = self.plan.nseq * self.plan.L
+        self.seg_all = self.vals_all = self.ready = None
+
+    def exchange(self, col) -> None:
+        """All-gather the plan's row starts and sorted indices (issued after the forward's pooled
+        all-to-all, so the communicator does not hold that exchange behind the sort)."""
+        from .distributed import all_gather_rows
+
+        p = self.plan
+        dev = p.buf.device
+        offs = (ctypes.c_int64 * 3)()
+        call("tt_bag_plan_layout", p.nseq, p.L, p.V, p.E, offs)
+        base = (-p.buf.data_ptr()) % 256
+        side = _lib.side_stream(dev)
+        with torch.cuda.stream(side):  # behind the sort on its own stream
+            vals = p.buf[base + offs[1]: base + offs[1] + 4 * self.nL].view(torch.int32)
+            seg = p.buf[base + offs[2]: base + offs[2] + 4 * (p.V + 1)].view(torch.int32)
+            self.vals_all = torch.empty(col.world * self.nL, dtype=torch.int32, device=dev)
+            self.seg_all = torch.empty(col.world * (p.V + 1), dtype=torch.int32, device=dev)
+            if self.nL:
+                all_gather_rows(self.vals_all, vals, col.group)
+            all_gather_rows(self.seg_all, seg, col.group)
+            self.ready = torch.cuda.Event()
+            self.ready.record(side)
+
+    def wait(self) -> None:
+        cur = torch.cuda.current_stream(self.plan.buf.device)
+        cur.wait_event(self.ready)
+        for t in (self.plan.buf, self.seg_all, self.vals_all):
+            t.record_stream(cur)
+
+
+def column_pooled_exchange(part: torch.Tensor, col, nseq: int) -> torch.Tensor:
+    """part (world * nseq, El): this rank's columns of every rank's sequences (rank-major).  Returns
+    this rank's (nseq, E) pooled rows: block s of the all-to-all is rank s's columns of them."""
+    from .distributed import all_to_all_rows
+
+    recv = torch.empty_like(part)
+    all_to_all_rows(recv, part, col.group)
+    return recv.view(col.world, nseq, col.El).permute(1, 0, 2).reshape(nseq, col.world * col.El)
+
+
+def column_grad_exchange(gs: torch.Tensor, col) -> torch.Tensor:
+    """gs (nseq, E): this rank's d_pooled / denom.  Returns (world * nseq, El): every rank's gs at this
+    rank's columns, rank-major (block s of the all-to-all = rank s's sequences)."""
+    from .distributed import all_to_all_rows
+
+    nseq, W, El = gs.shape[0], col.world, col.El
+    send = gs.view(nseq, W, El).permute(1, 0, 2).reshape(W * nseq, El)
+    gs_all = torch.empty(W * nseq, El, dtype=gs.dtype, device=gs.device)
+    all_to_all_rows(gs_all, send, col.group)
+    return gs_all
+
+
+class BagMeanPoolColumn(torch.autograd.Function):
+    """BagMeanPool for a column-sharded table (distributed.ColumnTable, table_sync "column"):
+    every rank's ids all-gathered, this rank's columns pooled for all of them from its slab
+    (tt_bag_mean_fwd, El wide), the column blocks exchanged all-to-all, so each rank returns the
+    whole pooled rows of its own sequences (encoders.py:62-72).  Backward: d_pooled / denom cut
+    into column blocks and exchanged all-to-all; the factored gradient (every rank's gs at this
+    rank's columns + the all-gathered plans) goes to the optimizer (tt_bag_col_reduce fused with
+    AdamW on the slab)."""
+
+    @staticmethod
+    def forward(ctx, weight, ids, padding_idx, col, want_grad):
+        from .distributed import all_gather_rows
+
+        require_gpu(weight, ids)
+        if ids.dim() != 2:
+            raise ValueError(f"ids must be (batch, seq_len), got shape {tuple(ids.shape)}")
+        ids = ids.contiguous()
+        nseq, L = ids.shape
+        W, El, V = col.world, col.El, col.V
+        dev = weight.device
+        cplan = ColumnPlan(ids, V, El, padding_idx) if want_grad else None  # local sort, side stream
+        ids_all = ids.new_empty((W * nseq, L))
+        all_gather_rows(ids_all, ids, col.group)
+        part = torch.empty(W * nseq, El, dtype=_FLOAT, device=dev)
+        den_all = torch.empty(W * nseq, dtype=_FLOAT, device=dev)
+        if W * nseq:
+            call("tt_bag_mean_fwd", ptr(col.slab), V, El, ptr(ids_all), _lib.ids_dtype_code(ids_all), W * nseq, L, L,
+                 ptr(part), ptr(den_all), stream_of(weight))
+        pooled = column_pooled_exchange(part, col, nseq)
+        denom = den_all[col.rank * nseq:(col.rank + 1) * nseq]
+        if cplan is not None:
+            cplan.exchange(col)
+        ctx.cplan, ctx.col = cplan, col
+        ctx.save_for_backward(denom)
+        ctx.token = None
+        if want_grad:
+            ctx.token = pooled._tt_bag_token = _BagGradToken(denom)
+        ctx.weight_ref = weight
+        return pooled
+
+    @staticmethod
+    def backward(ctx, d_pooled):
+        (denom,) = ctx.saved_tensors
+        col, cplan = ctx.col, ctx.cplan
+        ctx.cplan = None
+        tok, ctx.token = ctx.token, None
+        if not ctx.needs_input_grad[0] or cplan is None:
+            return None, None, None, None, None
+        if tok is not None and tok.grad is not None:
+            if tok.grad.data_ptr() != d_pooled.data_ptr() or tok.grad.shape != d_pooled.shape:
+                raise RuntimeError("bag output pre-scaled by its head was combined with another gradient")
+            tok.grad = None
+            gs = d_pooled.contiguous()  # the sole consuming head already divided by the denominators
+        else:
+            d_pooled = _contig_f32(d_pooled, "d_pooled")
+            gs = torch.empty_like(d_pooled)
+            call("tt_bag_scale_rows", ptr(d_pooled), ptr(denom), d_pooled.shape[0], d_pooled.shape[1], ptr(gs),
+                 stream_of(d_pooled))
+        nseq = gs.shape[0]
+        gs_all = column_grad_exchange(gs, col)
+        deferred = getattr(ctx.weight_ref, "_tt_deferred", None)
+        if deferred is None:
+            raise RuntimeError("a column-sharded table needs its optimizer (optim.AdamW(table_sync='column'))")
+        deferred.parts.append(("column", gs_all, nseq, cplan))
+        deferred.added()
+        return None, None, None, None, None
+
+
+def bag_col_update(col, parts, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, adam_args: torch.Tensor) -> None:
+    """The column-sharded table's AdamW step on its slab from the factored gradients of this step's
+    bag calls (BagMeanPoolColumn): one fused launch for one call (tt_bag_col_reduce, grad NULL); for
+    several calls on the table, their gradient rows are summed first, then one dense AdamW."""
+    slab = col.slab
+    if len(parts) == 1:
+        _, gs_all, nseq, cp = parts[0]
+        cp.wait()
+        call("tt_bag_col_reduce", ptr(cp.seg_all), ptr(cp.vals_all), cp.nL, col.world, nseq, ptr(gs_all), col.V,
+             col.El, None, ptr(slab), ptr(exp_avg), ptr(exp_avg_sq), ptr(adam_args), stream_of(slab))
+    else:
+        g = torch.zeros_like(slab)
+        for _, gs_all, nseq, cp in parts:
+            cp.wait()
+            gi = torch.empty_like(slab)
+            call("tt_bag_col_reduce", ptr(cp.seg_all), ptr(cp.vals_all), cp.nL, col.world, nseq, ptr(gs_all), col.V,
+                 col.El, ptr(gi), None, None, None, None, stream_of(slab))
+            g += gi
+        adamw_multi([(slab, g, exp_avg, exp_avg_sq, adam_args)])
+    col.stale = True
+
+
 def bag_mean_pool(weight: torch.Tensor, ids: torch.Tensor, padding_idx: int | None = 0,
                   scatter_mode: int = _lib.TT_SCATTER_SORTED) -> torch.Tensor:
+    col = getattr(weight, "_tt_column", None)
+    if col is not None:  # data parallel, column-sharded table (distributed.ColumnTable)
+        want = torch.is_grad_enabled() and weight.requires_grad
+        return BagMeanPoolColumn.apply(weight, ids, padding_idx, col, want)
     want_plan = torch.is_grad_enabled() and weight.requires_grad
     return BagMeanPool.apply(weight, ids, padding_idx, scatter_mode, want_plan)
 

@@ -41,6 +41,7 @@ class AdamW(torch.optim.Optimizer):
         self._backward_done = None
         self._args: dict[int, torch.Tensor] = {}  # id(param) -> device per-step scalars (capturable)
         self._shards: dict[int, distributed.ShardedRows] = {}  # data parallel: row-sharded tables
+        self._columns: dict[int, distributed.ColumnTable] = {}  # data parallel: column-sharded tables
         # moment tensors already in the sharded layout (by identity; weak, so loaded state replaces them)
         self._sharded_moments: dict[int, weakref.ref] = {}
         # capturable: id(step tensor) -> (hyper-parameters, that tensor) of the args formed one step
@@ -55,7 +56,7 @@ class AdamW(torch.optim.Optimizer):
                 pad = getattr(inner, "padding_idx", 0) if inner is not None else 0
                 if id(w) not in ids:
                     raise ValueError("fused table is not among the optimizer's parameters")
-                mode = distributed.table_sync_mode(table_sync, group)
+                mode = distributed.table_sync_mode(table_sync, group, E=w.shape[1])
                 # (None is the "no exchange" sentinel there: name the default group explicitly)
                 gg = ((group if group is not None else torch.distributed.group.WORLD) if mode in ("gather", "owner")
                       else None)
@@ -63,6 +64,9 @@ class AdamW(torch.optim.Optimizer):
                 self._tables.append(w)
                 if mode in ("shard", "owner"):  # owner: shard's row partition, gather's inputs
                     self._shards[id(w)] = distributed.ShardedRows(w, group)
+                elif mode == "column":  # each rank owns E / world columns of every row (its slab)
+                    col = distributed.ColumnTable(w, group, module=inner if inner is not None else None)
+                    self._columns[id(w)] = w._tt_column = col
             # the dense parameters' gradients may then be computed on a side stream beside the
             # fused table update (ops.TowerHead); step() joins them after launching that update
             tabs = {id(w) for w in self._tables}
@@ -72,10 +76,15 @@ class AdamW(torch.optim.Optimizer):
                         p._tt_side_grads = self._side_grads
 
     def release_tables(self) -> None:
-        """Return the tables to ordinary dense gradients (and every gradient to the current stream)."""
+        """Return the tables to ordinary dense gradients (and every gradient to the current stream);
+        a column-sharded table is materialized first (collective)."""
         for w in self._tables:
             if hasattr(w, "_tt_deferred"):
                 del w._tt_deferred
+            col = self._columns.pop(id(w), None)
+            if col is not None:
+                col.materialize()
+                del w._tt_column
         self._tables = []
         for g in self.param_groups:
             for p in g["params"]:
@@ -88,14 +97,23 @@ class AdamW(torch.optim.Optimizer):
         if not st:
             st["step"] = torch.tensor(0.0, dtype=torch.float32, device=p.device if capturable else "cpu")
             sh = self._shards.get(id(p))
-            like = p if sh is None else p.new_empty(sh.Vs, sh.E)  # sharded table: this rank's rows only
+            col = self._columns.get(id(p))
+            like = (p if sh is None else p.new_empty(sh.Vs, sh.E)) if col is None else col.slab  # own rows / columns
             st["exp_avg"] = torch.zeros_like(like, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(like, memory_format=torch.preserve_format)
-            if sh is not None:
+            if sh is not None or col is not None:
                 self._mark_sharded(st["exp_avg"])
         else:
             if capturable and st["step"].device != p.device:
                 st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+            col = self._columns.get(id(p))
+            if col is not None and not self._is_sharded(st["exp_avg"]):  # full-table moments loaded: own columns
+                for k in ("exp_avg", "exp_avg_sq"):
+                    if tuple(st[k].shape) != (col.V, col.E):
+                        raise ValueError(f"column table state: {k} has shape {tuple(st[k].shape)}, expected "
+                                         f"{(col.V, col.E)}")
+                    st[k] = col.own_cols(st[k].to(col.slab.device))
+                self._mark_sharded(st["exp_avg"])
             sh = self._shards.get(id(p))
             # full-table moments loaded (load_state_dict): keep this rank's rows.  Told apart from
             # the moments this optimizer sharded itself by identity, not by shape: at one rank the
@@ -123,17 +141,18 @@ class AdamW(torch.optim.Optimizer):
         moments (all-gathered over the ranks), so the state loads into torch.optim.AdamW and
         into a differently sharded run."""
         sd = super().state_dict()
-        if not self._shards:
+        if not self._shards and not self._columns:
             return sd
         index = {id(p): i for i, p in enumerate(p for g in self.param_groups for p in g["params"])}
         for p in (p for g in self.param_groups for p in g["params"]):
             sh = self._shards.get(id(p))
+            col = self._columns.get(id(p))
             st = sd["state"].get(index[id(p)])
-            if sh is None or st is None:
+            if (sh is None and col is None) or st is None:
                 continue
             st = sd["state"][index[id(p)]] = dict(st)  # the packed dict aliases the live state
             for k in ("exp_avg", "exp_avg_sq"):
-                st[k] = sh.gather_full(st[k])[:sh.V].clone()
+                st[k] = sh.gather_full(st[k])[:sh.V].clone() if sh is not None else col.gather_cols(st[k])
         return sd
 
     def load_state_dict(self, state_dict) -> None:
@@ -193,6 +212,12 @@ class AdamW(torch.optim.Optimizer):
             if deferred is not None and deferred.parts:
                 st = self._state(p, False)
                 st["step"] += 1
+                col = self._columns.get(id(p))
+                if col is not None:  # "column": this rank's slab from every rank's factored gradient
+                    args = _host_adam_args(lr, b1, b2, eps, wd, int(st["step"]), p.device)
+                    ops.bag_col_update(col, list(deferred.parts), st["exp_avg"], st["exp_avg_sq"], args)
+                    deferred.parts.clear()
+                    continue
                 ids, dp, den, plan = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
                 if deferred.gather_group is not None:
@@ -219,13 +244,18 @@ class AdamW(torch.optim.Optimizer):
     def _step_device(self, group: dict) -> None:
         """Capturable form: one tt_adam_prepare launch, one multi-tensor launch per 16 dense
         parameters, one fused scatter + AdamW launch per table."""
-        slots, dense, fused, shards, dense_ids = [], [], [], [], []
+        slots, dense, fused, shards, dense_ids, columns = [], [], [], [], [], []
         for p in group["params"]:
             deferred = getattr(p, "_tt_deferred", None)
             if deferred is not None and deferred.parts:
                 st = self._state(p, True)
                 a = self._adam_args(p)
                 slots.append((st["step"], a))
+                col = self._columns.get(id(p))
+                if col is not None:  # "column": every rank's factored gradient at this rank's columns
+                    columns.append((col, list(deferred.parts), st, a))
+                    deferred.parts.clear()
+                    continue
                 parts = _merge_parts(deferred.parts, p, deferred.padding_idx)
                 deferred.parts.clear()
                 sh = self._shards.get(id(p))
@@ -278,6 +308,8 @@ class AdamW(torch.optim.Optimizer):
         for p, st, (ids, dp, den, plan) in fused:
             ops.bag_mean_backward_adamw_planned(dp, den, plan, p.data, st["exp_avg"], st["exp_avg_sq"],
                                                 self._adam_args(p))
+        for col, parts, st, a in columns:  # column-sharded tables: this rank's slab, no exchange left
+            ops.bag_col_update(col, parts, st["exp_avg"], st["exp_avg_sq"], a)
         # data parallel, row-sharded tables: the chunk-pipelined exchange (its collectives are
         # issued before the tower all-reduce, so they lead on the communicator)
         for sh, parts, st, a, update in shards:
@@ -378,6 +410,93 @@ class AdamW(torch.optim.Optimizer):
             with torch.cuda.stream(comm):
                 clo, chi = sh.chunk(c)
                 distributed.all_gather_rows(stor[clo:chi], sh.own(stor, c), sh.group)
+
+
+class BackwardTableUpdate:
+    """The fused table update for a loop that keeps ``torch.optim.AdamW`` (the reference's
+    ``train.py:359``, stepped at ``:139``): at the end of every ``loss.backward()`` the table's
+    factored gradient goes through the sorted scatter fused with AdamW
+    (tt_bag_mean_bwd_adamw_planned) with the hyper-parameters of the table's param group in that
+    optimizer, and the table never gets a ``.grad``, so ``optimizer.step()`` skips it (torch's
+    AdamW steps only parameters with a gradient) and updates the tower parameters as before.
+
+    The moments and step counter live in ``optimizer.state[table]`` under torch's own keys
+    ('step' a CPU float32 tensor, 'exp_avg', 'exp_avg_sq'), so ``optimizer.state_dict()``,
+    ``save_checkpoint`` / ``load_checkpoint`` (utils.py:231-330) and a later switch back to the
+    plain path all see the same state.  The arithmetic is the fused update's, checked against
+    torch.optim.AdamW elementwise (tests).  What differs from torch's order of events: the table is
+    updated inside backward (once per backward pass), so a loop that accumulates several
+    backwards per optimizer step, or skips a step, must not use it; train.py does neither."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer, weight: torch.Tensor, padding_idx: int | None = 0):
+        if not isinstance(optimizer, torch.optim.AdamW) or isinstance(optimizer, AdamW):
+            raise TypeError("table_update 'backward' drives a torch.optim.AdamW the loop keeps "
+                            f"(twotower_amd.optim.AdamW(fused_tables=True) fuses it itself); got {type(optimizer).__name__}")
+        self.optimizer = optimizer
+        self.weight = weight
+        self.group = next((g for g in optimizer.param_groups if any(p is weight for p in g["params"])), None)
+        if self.group is None:
+            raise ValueError("the table is not among the optimizer's parameters")
+        self._check(self.group)
+        if getattr(weight, "_tt_deferred", None) is not None:
+            raise ValueError("the table's gradient is already owned by a fused optimizer")
+        weight._tt_deferred = ops.DeferredTableGrad(padding_idx, on_backward=self)
+
+    @staticmethod
+    def _check(group: dict) -> None:
+        for k in ("amsgrad", "maximize", "differentiable"):
+            if group.get(k, False):
+                raise ValueError(f"table_update 'backward' implements AdamW without {k}")
+        if group.get("capturable", False) or group.get("fused", False):
+            raise ValueError("table_update 'backward' keeps torch's host step counter (capturable=False, fused=False)")
+
+    def release(self) -> None:
+        """Back to the dense table gradient stepped by the optimizer (the state stays valid)."""
+        if getattr(self.weight, "_tt_deferred", None) is not None and self.weight._tt_deferred.on_backward is self:
+            del self.weight._tt_deferred
+
+    @torch.no_grad()
+    def __call__(self) -> None:
+        w = self.weight
+        deferred = w._tt_deferred
+        if not deferred.parts:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("table_update 'backward' runs eagerly (host step counter); use TrainStep with "
+                               "twotower_amd.optim.AdamW(capturable=True) for a captured step")
+        g = self.group
+        self._check(g)  # (a param group's options can be changed between steps)
+        ids, dp, den, plan = _merge_parts(deferred.parts, w, deferred.padding_idx)
+        deferred.parts.clear()
+        st = self.optimizer.state[w]
+        if not st:  # torch.optim.AdamW's _init_group layout (non-capturable: step a CPU float32 tensor)
+            st["step"] = torch.tensor(0.0, dtype=torch.float32)
+            st["exp_avg"] = torch.zeros_like(w, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(w, memory_format=torch.preserve_format)
+        st["step"] += 1
+        b1, b2 = g["betas"]
+        lr = float(g["lr"])
+        args = _host_adam_args(lr, b1, b2, g["eps"], g["weight_decay"], int(st["step"]), w.device)
+        ops.bag_mean_backward_adamw_planned(dp, den, plan, w.data, st["exp_avg"], st["exp_avg_sq"], args)
+
+
+def fuse_table_update(optimizer: torch.optim.Optimizer, model_or_tables) -> list[BackwardTableUpdate]:
+    """Attach a BackwardTableUpdate to every lookup table of ``model_or_tables`` (a model, an
+    embedding, or a list of them; shared tables once) for the loop's own torch.optim.AdamW.
+    The opt-in behind the reference config's ``hip: {table_update: backward}`` (twotower_amd.install)."""
+    items = model_or_tables if isinstance(model_or_tables, (list, tuple)) else [model_or_tables]
+    seen, out = set(), []
+    for item in items:
+        mods = item.modules() if isinstance(item, torch.nn.Module) else [item]
+        for m in mods:
+            inner = getattr(m, "embedding", None)
+            if not isinstance(inner, torch.nn.Embedding) or id(inner.weight) in seen:
+                continue
+            seen.add(id(inner.weight))
+            out.append(BackwardTableUpdate(optimizer, inner.weight, inner.padding_idx))
+    if not out:
+        raise ValueError("no lookup table (an nn.Embedding at .embedding) found")
+    return out
 
 
 def _gather_parts(parts, group):

@@ -115,20 +115,28 @@ class TrainStep:
                 self._eager_left -= 1
                 return self.eager(*inputs)
             why = capture_blocker(self.group) if is_active(self.group) else None
-            err = None
+            err = fatal = None
             if why is None:
                 try:
                     hit = self._capture(inputs)
                 except RuntimeError as e:  # e.g. a collective this backend cannot capture
-                    if not _is_capture_error(e):
-                        raise  # a real error of the step itself: not hidden behind a fallback
-                    err = e
+                    if _is_capture_error(e):
+                        err = e
+                    else:
+                        fatal = e  # a real error of the step itself: not hidden behind a fallback
             # every rank replays, or none does: a rank whose capture failed steps eagerly, and its
-            # collectives must not meet graph-replayed ones on the other ranks
-            ok = why is None and err is None
+            # collectives must not meet graph-replayed ones on the other ranks.  A rank whose step
+            # raised joins the agreement too (code -1) before it re-raises, so its peers fail at
+            # once instead of waiting in their next collective until the backend's timeout.
+            code = -1 if fatal is not None else (1 if why is None and err is None else 0)
             if is_active(self.group):
-                ok = _all_ranks(ok, self.group, inputs[0].device)
-            if not ok:
+                code = _all_ranks_min(code, self.group, inputs[0].device)
+            if code < 0:
+                self._discard_partial_step()
+                if fatal is not None:
+                    raise fatal
+                raise RuntimeError("TrainStep: another rank's step raised while its HIP graph was captured")
+            if code == 0:
                 import warnings
 
                 self._discard_partial_step()
@@ -177,21 +185,36 @@ class TrainStep:
         return graph, static_all, static_loss
 
 
+# messages of errors raised because a call is refused inside stream capture (HIP's and CUDA's
+# error names and texts, torch's own capture guards), matched as whole phrases: a broad substring
+# ("captur", "not permitted") would also hide unrelated errors behind the eager fallback
+_CAPTURE_ERRORS = (
+    "hiperrorstreamcapture",  # hipErrorStreamCaptureUnsupported / Invalidated / Unjoined / Isolation ...
+    "cudaerrorstreamcapture",
+    "operation not permitted when stream is capturing",
+    "operation not permitted on an event last recorded in a capturing stream",
+    "operation would make the legacy stream depend on a capturing blocking stream",
+    "during cuda graph capture",
+    "during hip graph capture",
+    "while a stream is capturing",
+)
+
+
 def _is_capture_error(e: BaseException) -> bool:
     """An error raised because the step was being captured (a call HIP or a backend refuses inside
     stream capture), as opposed to an error of the step itself."""
     msg = str(e).lower()
-    return any(k in msg for k in ("captur", "hipgraph", "cudagraph", "not permitted"))
+    return any(k in msg for k in _CAPTURE_ERRORS)
 
 
-def _all_ranks(flag: bool, group, device) -> bool:
-    """True iff `flag` holds on every rank of `group` (MIN all-reduce, outside any capture)."""
+def _all_ranks_min(code: int, group, device) -> int:
+    """MIN of `code` over the ranks of `group` (an all-reduce outside any capture)."""
     import torch.distributed as dist
 
-    t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+    t = torch.tensor([int(code)], dtype=torch.int32,
                      device=device if dist.get_backend(group) != "gloo" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
-    return bool(t.item())
+    return int(t.item())
 
 
 def _packed_like(inputs):
