@@ -86,8 +86,10 @@ def _worker(rank, port, loss_name, table_sync, q, inbatch_dp="owner", overlap="1
         if rank >= 0:
             dist.all_reduce(loss)
             loss /= WORLD
-        # numpy arrays travel by value (torch CPU tensors would travel as fds of a dying process)
-        delta = {n: p.detach().cpu().numpy() - init[n] for n, p in model.named_parameters()}
+        # numpy arrays travel by value (torch CPU tensors would travel as fds of a dying process);
+        # the parameters through state_dict(), which materialises a column-sharded table (every rank)
+        sd = model.state_dict()
+        delta = {n: sd[n].detach().cpu().numpy() - init[n] for n, _ in model.named_parameters()}
         q.put((rank, float(loss), init, delta, [t.cpu().numpy() for t in full], sorted(calls)))
     except Exception as e:
         import traceback
@@ -274,7 +276,7 @@ def test_dp_graph_replay_equals_eager_one_rank_rccl(table_sync, loss_name):
     env = dict(os.environ, MASTER_PORT=str(_free_port()))
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, os.path.join(here, "_dp_graph_check.py"), table_sync, loss_name], env=env,
-                       capture_output=True, text=True, timeout=240)
+                       capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert res["graph_kept"], res

@@ -14,7 +14,13 @@ all-gather / reduce-scatter rate (xGMI: 7 links x 153.6 GB/s bidirectional = 537
 per GPU; RCCL reaches 60-80 % of that on large messages, so 320-430 GB/s, given as --bw).  Exposed
 link time is what cannot overlap: the table exchange sits between the backward and the next forward
 (twotower/train.py:138-139), minus the chunk pipeline's overlap with the update work itself.
-Usage: python tools/dp_forecast.py --table-sync c3.jsonl c5.jsonl --scorer-dp dp.jsonl [--bw 320 430]"""
+Column exchange (--column, tools/mb.py column_sync): per rank the one-GPU step minus its own gather and
+table update, plus the column gather of every rank's sequences from the (V, E/N) slab, the two layout
+copies, the merged-plan slab update, and the exposed links: the ids all-gather before the gather, the
+pooled all-to-all after it and the gs all-to-all after the backward (the plan all-gather runs on the
+plan's stream beside the towers and the loss, and is not charged).
+Usage: python tools/dp_forecast.py --table-sync c3.jsonl c5.jsonl --scorer-dp dp.jsonl [--column col.jsonl]
+       [--bw 320 430]"""
 import argparse
 import json
 
@@ -54,6 +60,7 @@ def main():
     ap.add_argument("--step-ms", nargs=3, type=float, default=[0.857, 0.672, 1.90], metavar=("C3", "C4P", "C5"))
     ap.add_argument("--update-ms", nargs=3, type=float, default=[0.276, 0.276, 1.211], metavar=("C3", "C4P", "C5"))
     ap.add_argument("--bw", nargs="+", type=float, default=[320.0, 430.0])
+    ap.add_argument("--column", nargs="*", default=[])
     a = ap.parse_args()
     ts = load(a.table_sync)
     sdp = {r["world"]: r for r in load([a.scorer_dp])} if a.scorer_dp else {}
@@ -79,6 +86,20 @@ def main():
                     work, link = exch(mode, r, bw)
                     t = base + extra_scorer + (work + link) / 1e3
                     rows.append((cfg, N, mode, bw, round(t, 3), round(N * step / t, 2)))
+    for r in load(a.column) if a.column else []:
+        N = r["ranks"]
+        if N < 2:
+            continue
+        cfg = r["config"]
+        step, upd = (a.step_ms[2], a.update_ms[2]) if cfg == "c5" else (a.step_ms[0], a.update_ms[0])
+        work = (r["col_gather_us"] - r["gather_own_us"] + r["permute_pooled_us"] + r["permute_grad_us"]
+                + r["col_update_us"])
+        mb = r["link_MB_per_rank"]
+        exposed_mb = mb["ids_allgather"] + mb["pooled_alltoall"] + mb["grad_alltoall"]
+        for bw in a.bw:
+            t = step - upd + (work + exposed_mb * 1e6 / (bw * 1e9) * 1e6) / 1e3
+            rows.append((cfg + ("" if cfg == "c5" else " (per-sample losses)"), N, "column", bw, round(t, 3),
+                         round(N * step / t, 2)))
     print("| workload | N | table exchange | RCCL GB/s per rank | forecast ms/step | speedup vs 1 GPU |")
     print("|---|---|---|---|---|---|")
     for cfg, N, mode, bw, t, s in rows:

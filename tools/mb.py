@@ -12,6 +12,8 @@
   python tools/mb.py split_fwd                   two-launch vs one-launch data-parallel forward
   python tools/mb.py table_sync [c3|c5]          per-rank GPU cost of the table exchanges at N ranks
                                                  (gather / shard / owner) and their link bytes
+  python tools/mb.py column_sync [c5|c3]         per-rank GPU cost and link bytes of the column-sharded table
+                                                 (table_sync "column") at N = 1, 2, 4, 8
   python tools/mb.py l2prep                      the head's normalise fused with the scorer's operand prep,
                                                  alone (C3 and B x B rows)
   python tools/mb.py scorer_once B M H [dtype] [lib]   three scorer fwd + bwd calls, nothing else (for
@@ -135,6 +137,31 @@ def head(a):
     print(f"split planes: {graph_us(lambda: ops._planes(W, True), 20):.1f} us")
     print(f"torch addmm (hipBLASLt): {graph_us(lambda: torch.addmm(b, x, W.t()), 20):.1f} us")
     print(f"head_wgrad (dW + db): {graph_us(lambda: ops.head_wgrad(g2, x), 20):.1f} us")
+    # the fused chains (head_chain.hip) against the launches they replace, same rows (C3: 3 B rows)
+    W2 = torch.randn(256, 256, device=DEV) / 16
+    P2, P1t, P2t = ops._planes(W2, False), ops._planes(W, True), ops._planes(W2, True)
+    h, y, dh, dx = (torch.empty(N, 256, device=DEV) for _ in range(4))
+    bits = torch.empty(_lib.lib().tt_head_chain_bits_bytes(N, 256) // 4, dtype=torch.int32, device=DEV)
+    den = torch.full((N,), 40.0, device=DEV)
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+
+    def fwd(norm):
+        return lambda: call("tt_head_fwd_chain", ptr(x), N, 256, 256, 256, ptr(P), ptr(P2), ptr(b), ptr(b), ptr(bits),
+                            ptr(h), ptr(y), ptr(norms), norm, st())
+
+    bwd = lambda: call("tt_head_bwd_chain", ptr(g2), N, 256, 256, 256, ptr(P2t), ptr(P1t), ptr(bits), ptr(den),  # noqa: E731
+                       ptr(dh), ptr(dx), st())
+    unf_f = graph_us(lambda: (ops._head_gemm(x, P, 0, bias=b, mask=mask), ops._head_gemm(h, P2, 4, bias=b)), 20)
+    unf_f1 = graph_us(lambda: (ops._head_gemm(x, P, 0, bias=b, mask=mask), ops._head_gemm(h, P2, 1, bias=b,
+                                                                                         norms=norms)), 20)
+    unf_b = graph_us(lambda: (ops._head_gemm(g2, P2t, 2, mask=mask), ops._head_gemm(dh, P1t, 5, bias=den)), 20)
+    print(json.dumps({"rows": N, "fwd_chain_bias_us": round(graph_us(fwd(0), 20), 1),
+                      "fwd_chain_l2_us": round(graph_us(fwd(1), 20), 1), "bwd_chain_rowdiv_us": round(graph_us(bwd, 20), 1),
+                      "unfused_fwd_bias_us": round(unf_f, 1), "unfused_fwd_l2_us": round(unf_f1, 1),
+                      "unfused_bwd_rowdiv_us": round(unf_b, 1),
+                      # two GEMMs per pass, six 32x32x16 MFMAs of 32 cycles per 32 x 32 x 16 block, 1024 SIMDs
+                      "mfma_floor_us_at_2GHz_per_pass": round(2 * (N / 32) * 8 * 16 * 6 / 1024 * 32 / 2e9 * 1e6, 1)}),
+          flush=True)
 
 
 def scorer(a):
@@ -295,6 +322,78 @@ def table_sync(a):
         torch.cuda.empty_cache()
 
 
+def column_sync(a):
+    """table_sync "column" at N ranks, per rank (the N ranks' sequences simulated by N independent
+    batches on one GPU): the forward gather of this rank's E/N columns for every rank's sequences
+    from its (V, E/N) slab, the two layout copies around the all-to-alls, the fused slab update from
+    the N per-rank plans merged in the reduce (tt_bag_col_reduce), against the one-GPU gather and
+    fused update of the rank's own batch (full width); plus the link bytes per rank: ids all-gather,
+    pooled and gs all-to-alls (exposed) and the plan all-gather (issued on the plan's stream during
+    the forward)."""
+    B, L, E = 8192, 64, 256
+    shape = a.shape or "c5"
+    V, K = (200_000, 1) if shape == "c3" else (1_000_000, 4)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    table = torch.randn(V, E, device=DEV, generator=g) * 0.02
+    m, v = torch.zeros_like(table), torch.zeros_like(table)
+    _, args = adam_args()
+    own = ids_for(B, L, V, K)
+    nown = own.shape[0]
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    base = {}
+    pooled = torch.empty(nown, E, device=DEV)
+    den = torch.empty(nown, device=DEV)
+    base["gather_own_us"] = graph_us(lambda: call("tt_bag_mean_fwd", ptr(table), V, E, ptr(own), _lib.TT_IDS_I32, nown,
+                                                  L, L, ptr(pooled), ptr(den), st()))
+    d_pooled = torch.randn(nown, E, device=DEV, generator=g)
+    p1 = ops.BagPlan(own, V, E, 0)
+    p1.wait()
+    base["update_own_us"] = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, None, p1, table, m, v, args))
+    del p1
+    for R in (1, 2, 4, 8):
+        El = E // R
+        ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r) for r in range(1, R)]).contiguous()
+        N = ids.shape[0]
+        slab = table[:, :El].contiguous()
+        ms, vs = torch.zeros_like(slab), torch.zeros_like(slab)
+        part = torch.empty(N, El, device=DEV)
+        den_all = torch.empty(N, device=DEV)
+        res = {"config": shape, "ranks": R, "El": El, "tokens_per_rank": int((own > 0).sum())}
+        res.update(base)
+        res["col_gather_us"] = graph_us(lambda: call("tt_bag_mean_fwd", ptr(slab), V, El, ptr(ids), _lib.TT_IDS_I32, N,
+                                                     L, L, ptr(part), ptr(den_all), st()))
+        recv = torch.randn(N, El, device=DEV)
+        out = torch.empty(nown, E, device=DEV)
+        res["permute_pooled_us"] = graph_us(lambda: out.copy_(recv.view(R, nown, El).permute(1, 0, 2).reshape(nown, E)))
+        gs = torch.randn(nown, E, device=DEV)
+        send = torch.empty(N, El, device=DEV)
+        res["permute_grad_us"] = graph_us(lambda: send.view(R, nown, El).copy_(gs.view(nown, R, El).permute(1, 0, 2)))
+        segs, valss = [], []
+        for r in range(R):
+            pl = ops.BagPlan(ids[r * nown:(r + 1) * nown], V, El, 0)
+            pl.wait()
+            offs = (ctypes.c_int64 * 3)()
+            call("tt_bag_plan_layout", pl.nseq, pl.L, V, El, offs)
+            b0 = (-pl.buf.data_ptr()) % 256
+            valss.append(pl.buf[b0 + offs[1]: b0 + offs[1] + 4 * nown * L].view(torch.int32).clone())
+            segs.append(pl.buf[b0 + offs[2]: b0 + offs[2] + 4 * (V + 1)].view(torch.int32).clone())
+            del pl
+        seg_all, vals_all = torch.cat(segs), torch.cat(valss)
+        gs_all = torch.randn(N, El, device=DEV, generator=g) * 1e-3
+        res["col_update_us"] = graph_us(lambda: call("tt_bag_col_reduce", ptr(seg_all), ptr(vals_all), nown * L, R, nown,
+                                                     ptr(gs_all), V, El, None, ptr(slab), ptr(ms), ptr(vs), ptr(args),
+                                                     st()))
+        res = {k: (round(x, 1) if isinstance(x, float) else x) for k, x in res.items()}
+        res["link_MB_per_rank"] = {
+            "ids_allgather": round((R - 1) * nown * L * 4 / 1e6, 1),
+            "pooled_alltoall": round((R - 1) / R * nown * E * 4 / 1e6, 1),
+            "grad_alltoall": round((R - 1) / R * nown * E * 4 / 1e6, 1),
+            "plan_allgather_hidden": round((R - 1) * (nown * L + V + 1) * 4 / 1e6, 1)}
+        print(json.dumps(res), flush=True)
+        del ids, slab, ms, vs, part, recv, out, gs, send, seg_all, vals_all, gs_all, segs, valss
+        torch.cuda.empty_cache()
+
+
 def l2prep(a):
     """tt_inbatch_l2_prep alone (the head's normalise fused with the scorer's operand prep) at C3's
     rows (B = 8192 queries + 16384 candidates, H = 256, bf16), the B x B pairs form (8192 + 8192) and
@@ -335,8 +434,8 @@ def scorer_once(a):
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync", "l2prep",
-                                     "scorer_once"])
+    ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
+                                     "column_sync", "l2prep", "scorer_once"])
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")
     ap.add_argument("--zipf", type=float, default=None)

@@ -695,21 +695,28 @@ class TowerHead(torch.autograd.Function):
             call("tt_head_split_ff2", ptr(_contig_f32(W1, "W1")), ptr(_contig_f32(W2, "W2")), E, H, ptr(planes),
                  stream_of(x))
         p_w1, p_w2 = planes[:n1], planes[n1:n1 + n2]
-        mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
-        h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
         req = _SCORER_PREP[-1] if _SCORER_PREP and _prep_fusable(width, _SCORER_PREP[-1][1]) else None
-        if req is not None and 0 < req[0] < rows:
+        prep = req is not None and 0 < req[0] < rows
+        ctx.chain = head_chain()
+        if ctx.chain:  # both Linears (and F.normalize) in one launch, h never re-read (head_chain.hip)
+            mask = torch.empty(_lib.lib().tt_head_chain_bits_bytes(rows, H) // 4, dtype=torch.int32, device=x.device)
+            h = torch.empty(rows, H, dtype=_FLOAT, device=x.device)
+            out = torch.empty(rows, H, dtype=_FLOAT, device=x.device)
+            call("tt_head_fwd_chain", ptr(x), rows, x.stride(0), E, H, ptr(p_w1), ptr(p_w2), ptr(_contig_f32(b1, "b1")),
+                 ptr(_contig_f32(b2, "b2")), ptr(mask), ptr(h), ptr(out), ptr(norm), int(not prep), stream_of(x))
+        else:
+            mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
+            h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
+            out = _head_gemm(h, p_w2, 4, bias=b2) if prep else _head_gemm(h, p_w2, 1, bias=b2, norms=norm)
+        if prep:
             nq, dt = req  # normalise pass fused with the in-batch scorer's operand prep
-            out = _head_gemm(h, p_w2, 4, bias=b2)
             ws = torch.empty(_lib.lib().tt_inbatch_ws_size(nq, rows - nq, width, dt), dtype=torch.uint8,
                              device=x.device)
             call("tt_inbatch_l2_prep", ptr(out), nq, rows - nq, width, dt, ptr(norm), ptr(ws), ws.numel(),
                  stream_of(x))
             ctx.l2_token = _L2Token(norm)
             out._tt_inbatch_prep = (nq, rows - nq, dt, ws, ctx.l2_token)
-        else:
-            out = _head_gemm(h, p_w2, 1, bias=b2, norms=norm)
         if req is None or not 0 < req[0] < rows:
             ctx.l2_token = None
         ctx.save_for_backward(x, h, mask, out, norm, planes)
@@ -760,14 +767,25 @@ class TowerHead(torch.autograd.Function):
             with torch.cuda.stream(aux):
                 head_wgrad(G, X, dW, db)
 
-        dh = _head_gemm(dy, p_w2t, 2, mask=mask, N=H)
         tok, ctx.bag_token = ctx.bag_token, None
         dx = None
-        if ctx.needs_input_grad[0] and tok is not None:  # dx / denom for the bag backward (epi 5)
-            dx = _head_gemm(dh, p_w1t, 5, bias=tok.denom, N=E)
-            tok.grad = dx
-        elif ctx.needs_input_grad[0]:
-            dx = _head_gemm(dh, p_w1t, 3, N=E)
+        if ctx.chain:  # dh and dx (/ denom for the bag backward) in one launch (head_chain.hip)
+            dh = torch.empty(dy.shape[0], H, dtype=_FLOAT, device=dy.device)
+            dxc = torch.empty(dy.shape[0], E, dtype=_FLOAT, device=dy.device)
+            div = tok.denom if (ctx.needs_input_grad[0] and tok is not None) else None
+            call("tt_head_bwd_chain", ptr(dy), dy.shape[0], dy.stride(0), E, H, ptr(p_w2t), ptr(p_w1t), ptr(mask),
+                 ptr(div), ptr(dh), ptr(dxc), stream_of(dy))
+            if ctx.needs_input_grad[0]:
+                dx = dxc
+                if tok is not None:
+                    tok.grad = dx
+        else:
+            dh = _head_gemm(dy, p_w2t, 2, mask=mask, N=H)
+            if ctx.needs_input_grad[0] and tok is not None:  # dx / denom for the bag backward (epi 5)
+                dx = _head_gemm(dh, p_w1t, 5, bias=tok.denom, N=E)
+                tok.grad = dx
+            elif ctx.needs_input_grad[0]:
+                dx = _head_gemm(dh, p_w1t, 3, N=E)
         two = E == H  # square heads: both weight gradients in one launch (tt_head_wgrad2)
         if not on_side:
             if two:
@@ -799,6 +817,12 @@ class TowerHead(torch.autograd.Function):
         done.record(aux)
         side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)))
         return dx, dW1, db1, dW2, db2
+
+
+def head_chain() -> bool:
+    """The tower head runs as two fused chains (tt_head_fwd_chain / tt_head_bwd_chain: one launch per
+    pass); TT_HEAD_CHAIN=0 runs the four tt_head_gemm launches (and the normalise pass) instead."""
+    return os.environ.get("TT_HEAD_CHAIN", "1") != "0"
 
 
 def head_wgrad(G: torch.Tensor, X: torch.Tensor, dW: torch.Tensor | None = None,
