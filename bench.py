@@ -253,6 +253,15 @@ def scorer_entry(ops_t: dict, timing_steps: int, B: int, M: int, d: int, world: 
     algo = 6.0 * B * M * d
     executed = ((2.0 + 2.0 * mult) + (2.0 if stored_p else 2.0 + 2.0 * mult)) * B * M * d
     achieved = algo / (ms * 1e-3) / 1e12
+    # fp32 stored-P passes at H 64 / 128 / 256 run the split-bf16 engines: six bf16 MFMA products per
+    # fp32 product, so the peak their instruction mix can reach is the bf16 peak / 6 (a
+    # fraction against the 157 TF fp32 MFMA rate above 1 said nothing about the engines)
+    split_engines = scorer_dtype == "fp32" and stored_p and d in (64, 128, 256)
+    extra = {}
+    if split_engines:
+        extra = {"peak_basis": "split-bf16 engines: 2.5 PF bf16 / 6 products per fp32 product",
+                 "frac_vs_fp32_mfma_157tf": round(achieved / MFMA_PEAK_TFLOPS["fp32"], 4)}
+        pk = MFMA_PEAK_TFLOPS["bf16"] / 6.0
     form = (f"{scorer_dtype}, backward from stored {scorer_dtype} probabilities" if stored_p else
             {"bf16": "bf16, recompute backward", "bf16_split": "bf16 with hi/lo-split probabilities",
              "fp32": "fp32 MFMA, recompute backward"}[scorer_dtype])
@@ -271,6 +280,7 @@ def scorer_entry(ops_t: dict, timing_steps: int, B: int, M: int, d: int, world: 
         # profiles/r02_scorer_error_table.jsonl): against float64 on the same bf16-rounded
         # operands, and against float64 on the fp32 operands (what the reference computes)
         "grad_error": SCORER_GRAD_ERROR.get((scorer_dtype, stored_p)),
+        **extra,
     }
 
 
@@ -455,6 +465,7 @@ def c4_pairs_entry(cfg, scorer_dtype: str, dev, world: int, rank: int, steps: in
     t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms = float(t.item()) / steps * 1e3
+    step.release()  # a captured all-to-all holds RCCL resources until its graph goes
     del step, opt, model, emb
     return {"value": round(B * world / (ms * 1e-3), 1), "unit": "pairs/s", "ms_per_step": round(ms, 4),
             "steps": steps, "warmup": warmup, "M": B * world,
@@ -688,6 +699,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = B * world * args.steps / elapsed
 
+    if hasattr(step, "release"):  # the captured graphs go before the process group (RCCL resources)
+        step.release()
     if rank != 0:
         if dist.is_initialized():
             dist.destroy_process_group()

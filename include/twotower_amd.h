@@ -417,7 +417,8 @@ int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int count, voi
  *                                     epi 0 for the same rows)
  *   epi 3: .                         (dx = dh W1)
  *   epi 4: . + bias                  (epi 1 before its normalise pass, which the caller runs:
- *                                     tt_inbatch_l2_prep)
+ *                                     tt_inbatch_l2_prep; also a plain Linear + bias, K = 64 included:
+ *                                     AveragePoolingTower's projection, encoders.py:84-155)
  *   epi 5: . / bias[r]               (dx = dh W1 divided by per-row divisors, IEEE division: the
  *                                     bag backward's d_pooled / denom (encoders.py:72) formed in
  *                                     the head's epilogue; bias = denom, length rows). */

@@ -45,6 +45,7 @@ for graph in modes:
     losses = [float(step(*batches[s % 4])) for s in range(5)]
     torch.cuda.synchronize()
     out.append((losses, {k: v.detach().clone() for k, v in model.state_dict().items()}, step.graph))
+    step.release()  # before the process group goes: a captured all-to-all holds RCCL resources
 diff = max(float((out[1][1][k] - out[0][1][k]).abs().max()) for k in out[1][1])
 print(json.dumps({"eager": out[0][0], "graph": out[1][0], "max_param_diff": diff, "modes": sys.argv[3:],
                   "graph_kept": out[1][2] == modes[1]}), flush=True)

@@ -1,8 +1,8 @@
 """The tower head's fused chains (head_chain.hip: tt_head_fwd_chain, tt_head_bwd_chain) against the
 four-launch head (tt_head_gemm epi 0 / 4 / 1 / 2 / 3 / 5) on the same planes, and against float64
 (encoders.py:38-42,77): the chains form the same split-bf16 products operand for operand, so h, dh,
-dx and the unnormalised y must equal the unfused kernels' bit for bit; the in-register F.normalize
-sums its squares in another order (1e-6), and everything is held to float64 at 1e-5.  Row counts
+dx, y and the normalised rows (staged through LDS into head_normalize_kernel's layout and arithmetic) must
+equal the unfused kernels' bit for bit, and everything is held to float64 at 1e-5.  Row counts
 cover partial tiles, partial 128-row blocks and more row blocks than workgroups (the ring carried
 across blocks)."""
 import numpy as np
@@ -49,7 +49,8 @@ def test_head_chains_equal_unfused_kernels_and_float64(E, H, rows):
     o_u = ops._head_gemm(h_u, p2, 1, bias=b2, norms=n_u)
     # forward chain, both epilogues
     bits = torch.empty(_lib.lib().tt_head_chain_bits_bytes(rows, H) // 4, dtype=torch.int32, device=DEV)
-    h, y, o, nrm = (torch.empty(rows, H, device=DEV) for _ in range(3)) + (torch.empty(rows, device=DEV),)
+    h, y, o = (torch.empty(rows, H, device=DEV) for _ in range(3))
+    nrm = torch.empty(rows, device=DEV)
     ops.call("tt_head_fwd_chain", x.data_ptr(), rows, E, E, H, p1.data_ptr(), p2.data_ptr(), b1.data_ptr(),
              b2.data_ptr(), bits.data_ptr(), h.data_ptr(), y.data_ptr(), None, 0, st)
     h2 = torch.empty_like(h)
@@ -58,7 +59,7 @@ def test_head_chains_equal_unfused_kernels_and_float64(E, H, rows):
     torch.cuda.synchronize()
     assert torch.equal(h, h_u) and torch.equal(h2, h_u)
     assert torch.equal(y, y_u)
-    assert _rel(o, o_u) < 1e-6 and _rel(nrm, n_u) < 1e-6
+    assert torch.equal(o, o_u) and torch.equal(nrm, n_u)  # head_normalize_kernel's arithmetic
     h64, y64, o64 = _ref64(x, W1, b1, W2, b2)
     assert _rel(o, o64) < 1e-5 and _rel(nrm, y64.norm(dim=1)) < 1e-5 and _rel(h, h64) < 1e-5
     # backward chain: dh = (dy W2) relu'(h), dx = dh W1 (and / denominators)
@@ -102,4 +103,36 @@ def test_tower_head_chain_equals_four_launch_head(E, H, monkeypatch):
         torch.cuda.synchronize()
         res[mode] = [out.detach()] + [t.grad for t in [x] + ps]
     for a, b in zip(res["1"], res["0"]):
-        assert _rel(a, b) < 1e-6
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("E,H", [(64, 128), (256, 128), (128, 256), (64, 256)])
+def test_avg_pool_projection_linear_head(E, H):
+    """AveragePoolingTower's projection Linear(E, H) on the split-bf16 kernels (ops.LinearHead,
+    encoders.py:84-155): output and the x / W / b gradients against float64, and the tower in eval
+    mode against the same tower whose projection runs F.linear."""
+    import twotower_amd as tt
+
+    g = torch.Generator(device=DEV).manual_seed(E + H)
+    rows = 2000
+    x = torch.randn(rows, E, device=DEV, generator=g).requires_grad_(True)
+    W = (torch.randn(H, E, device=DEV, generator=g) / E ** 0.5).requires_grad_(True)
+    b = (torch.randn(H, device=DEV, generator=g) * 0.1).requires_grad_(True)
+    dy = torch.randn(rows, H, device=DEV, generator=g)
+    y = ops.linear(x, W, b)
+    y.backward(dy)
+    x64, W64, b64 = (t.detach().double().requires_grad_(True) for t in (x, W, b))
+    y64 = x64 @ W64.T + b64
+    y64.backward(dy.double())
+    assert _rel(y, y64) < 1e-5
+    for got, want in ((x.grad, x64.grad), (W.grad, W64.grad), (b.grad, b64.grad)):
+        assert _rel(got, want) < 1e-5
+    emb = tt.embeddings.build("lookup", vocab_size=500, embedding_dim=E)
+    tower = tt.build_tower("avg_pool", emb, hidden_dim=H).to(DEV).eval()
+    ids = torch.randint(0, 500, (300, 20), device=DEV, generator=g)
+    with ops._lib.record_calls() as calls:
+        out = tower(ids)
+    assert "tt_head_gemm" in calls
+    lin, _, ln = tower.projection
+    ref = torch.nn.functional.normalize(ln(lin(emb.pool_mean(ids))), dim=-1)
+    assert _rel(out, ref) < 1e-5

@@ -49,9 +49,11 @@ def main() -> int:
                                        negatives=max(K, 1))[:(2 if K == 0 else 3)]
     losses = [float(step(*batch)) for _ in range(3)]
     torch.cuda.synchronize()
+    graphed = step.graph
+    step.release()  # before the process group goes: a captured all-to-all holds RCCL resources
     dist.barrier()
     dist.destroy_process_group()
-    if step.graph and all(math.isfinite(x) for x in losses):
+    if graphed and all(math.isfinite(x) for x in losses):
         print(f"canary ok: losses {losses}", flush=True)
         return 0
     print(f"canary failed: graph {step.graph}, losses {losses}", flush=True)

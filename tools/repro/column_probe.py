@@ -49,5 +49,10 @@ for s in range(4):
     say(f"step {s} done loss {float(loss):.6f} graph {step.graph}")
 sd = model.state_dict()
 say(f"state_dict ok, table sum {float(sd['query_tower.embedding.embedding.weight'].sum()):.6f}")
+if len(sys.argv) > 3 and sys.argv[3] == "release":
+    step.release()
+    say("graphs released")
+dist.barrier()
+say("barrier ok")
 dist.destroy_process_group()
 say("done")

@@ -714,7 +714,8 @@ extern "C" int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, co
   float* part = static_cast<float*>(ws);
   int rc;
   TT_REQUIRE(N > 64 || (epi != EPI_BIAS_L2 && epi != EPI_BIAS_RELU), "tt_head_gemm: N = 64 only for the dx GEMMs (epi 3, 5)");
-  TT_REQUIRE(K > 64 || epi == EPI_BIAS_RELU, "tt_head_gemm: K = 64 only for the first Linear (epi 0)");
+  TT_REQUIRE(K > 64 || epi == EPI_BIAS_RELU || (epi == EPI_BIAS_L2 && defer_l2),
+             "tt_head_gemm: K = 64 only for a first Linear (epi 0, or epi 4: AveragePoolingTower's projection)");
 #define TT_HG(KK, NN) \
   if (K == KK && N == NN) rc = launch_head_gemm<KK, NN>(A, rows, lda, P, epi, bias, relu_mask, out, part, s)
   TT_HG(256, 256);

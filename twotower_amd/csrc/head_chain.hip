@@ -31,6 +31,9 @@ namespace {
 constexpr int kCW = 4;       // waves per workgroup
 constexpr int kCRows = 32;   // rows per wave
 constexpr int kCSlots = 3;   // LDS ring slots
+#ifndef TT_CHAIN_PERMLANE
+#define TT_CHAIN_PERMLANE 0      // 1: the half exchange by v_permlane32_swap instead of ds_bpermute
+#endif
 
 // MODE1: 0 forward first Linear (bias + ReLU, ReLU bits written, h stored)
 //        1 backward dh GEMM (ReLU bits read, dh stored)
@@ -54,6 +57,7 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
   constexpr int XP = XB / 1024;                            // its LDS-DMA pieces
   constexpr int F = (3 * RMAX / 32 + XP + kCW - 1) / kCW;  // LDS-DMA pieces per wave and chunk
   constexpr int NW1 = (NT1 + 1) / 2;                       // ReLU words per lane and row tile
+  constexpr int STG_ROW = R2 * 4 + 16;                     // MODE2 1 staging row (padded: no bank conflicts)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8_t;
   typedef __attribute__((address_space(3))) f32x4 lds_f32x4_t;
@@ -105,10 +109,13 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
   // chunk g's pieces landed for every wave (this wave's: all but the F pieces of chunk g + 1 may be
   // outstanding; the last chunk has none after it), and every wave is done with chunk g - 1
   auto arrive = [&](int64_t g) {
+    // lgkmcnt(0): this wave's ring reads of chunk g - 1 have returned (the compiler may sink the
+    // MFMAs that consume them, and their waits, below an asm barrier), so the fill of chunk g + 2
+    // that some wave issues after the barrier cannot overwrite a slot still being read
     if (g + 1 < total) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(F) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(F) : "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     asm volatile("s_barrier" ::: "memory");  // (not __syncthreads: its fence would drain the fills ahead)
   };
@@ -201,18 +208,29 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
           *reinterpret_cast<f32x4*>(hrow + 32 * t + 8 * gq) =
               f32x4{acc1[t][4 * gq], acc1[t][4 * gq + 1], acc1[t][4 * gq + 2], acc1[t][4 * gq + 3]};
     }
-    // to the A operand layout: registers (8 s + i, 8 s + 4 + i) hold units 16 s + 8 hh + [0, 8)
+    // to the A operand layout: registers (8 s + i, 8 s + 4 + i) hold units 16 s + 8 hh + [0, 8): the
+    // upper half's group 2 s goes to the lower half's group 2 s + 1 register and the lower half's
+    // group 2 s + 1 to the upper half's group 2 s register (T21's half exchange)
 #pragma unroll
     for (int t = 0; t < NT1; ++t)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+#if TT_CHAIN_PERMLANE
           const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, acc1[t][8 * s + i]),
                                                           __builtin_bit_cast(unsigned, acc1[t][8 * s + 4 + i]), false,
                                                           false);
           acc1[t][8 * s + i] = __builtin_bit_cast(float, (unsigned)r[0]);
           acc1[t][8 * s + 4 + i] = __builtin_bit_cast(float, (unsigned)r[1]);
+#else
+          const float send = hh ? acc1[t][8 * s + i] : acc1[t][8 * s + 4 + i];
+          const float got = __shfl_xor(send, 32);
+          if (hh)
+            acc1[t][8 * s + i] = got;
+          else
+            acc1[t][8 * s + 4 + i] = got;
+#endif
         }
     // ---- second product: acc2[t2] = (this wave's rows, as A) x (P2 rows 32 t2 .. +31)^T
     f32x16 acc2[NT2];
@@ -257,27 +275,53 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
         for (int v = 0; v < 16; ++v) acc2[t][v] += bv;  // head.hip EPI_BIAS_L2's y += bias
       }
     }
-    if constexpr (MODE2 == 1) {  // F.normalize: x / max(|x|, 1e-12) over the row's R2 columns
-      float ss[16];
+    if constexpr (MODE2 == 1) {
+      // F.normalize (x / max(|x|, 1e-12)) with head_normalize_kernel's arithmetic bit for bit (so the
+      // head's output is the same whether or not tt_inbatch_l2_prep normalises it): 8 rows at a time
+      // through this wave's LDS staging area into that kernel's layout (lane L: columns G L .. G L + G - 1,
+      // G = R2 / 64), its sum-of-squares chain and butterfly, and whole 1-KiB rows stored.
+      static_assert(R2 == 128 || R2 == 256, "F.normalize epilogue widths");
+      constexpr int G = R2 / 64;
+      lds_char_t* stg = lds + kCSlots * SLOT + wid * (8 * STG_ROW);
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        float a = acc2[0][v] * acc2[0][v];
+      for (int k = 0; k < 4; ++k) {  // rows 8 k .. 8 k + 7 of the tile: v = 4 k .. 4 k + 3, both halves
 #pragma unroll
-        for (int t = 1; t < NT2; ++t) a = __builtin_fmaf(acc2[t][v], acc2[t][v], a);
-        ss[v] = a;
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < NT2; ++t)
+            *reinterpret_cast<__attribute__((address_space(3))) float*>(stg + (4 * hh + i) * STG_ROW +
+                                                                        (32 * t + r32) * 4) = acc2[t][4 * k + i];
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const int64_t row = r0 + 8 * k + rr;
+          if constexpr (G == 4) {
+            f32x4 v = *reinterpret_cast<const lds_f32x4_t*>(stg + rr * STG_ROW + 16 * lane);
+            const float ss = wave_sum(sumsq4(v));
+            const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
+            v[0] *= inv;
+            v[1] *= inv;
+            v[2] *= inv;
+            v[3] *= inv;
+            if (row < rows) {
+              reinterpret_cast<f32x4*>(Y + row * R2)[lane] = v;
+              if (lane == 0) norms[row] = nrm;
+            }
+          } else {
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            typedef __attribute__((address_space(3))) f32x2 lds_f32x2_t;
+            f32x2 v = *reinterpret_cast<const lds_f32x2_t*>(stg + rr * STG_ROW + 8 * lane);
+            const float ss = wave_sum(__builtin_fmaf(v[1], v[1], v[0] * v[0]));
+            const float nrm = sqrtf(ss), inv = 1.f / fmaxf(nrm, 1e-12f);
+            v[0] *= inv;
+            v[1] *= inv;
+            if (row < rows) {
+              reinterpret_cast<f32x2*>(Y + row * R2)[lane] = v;
+              if (lane == 0) norms[row] = nrm;
+            }
+          }
+        }
       }
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1)  // the 32 columns of a half (its lanes hold one row set)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) ss[v] += __shfl_xor(ss[v], o);
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const float nrm = sqrtf(ss[v]), inv = 1.f / fmaxf(nrm, 1e-12f);
-#pragma unroll
-        for (int t = 0; t < NT2; ++t) acc2[t][v] *= inv;
-        const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
-        if (r32 == v && rr < rows) norms[rr] = nrm;
-      }
+      continue;  // the rows are stored
     }
     if constexpr (MODE2 == 2) {
 #pragma unroll
@@ -313,7 +357,8 @@ int launch_chain(const float* X, int64_t rows, int64_t ldx, const __bf16* P1, co
   constexpr int RMAX = R1 > R2 ? R1 : R2;
   const int64_t nblk = (rows + kCW * kCRows - 1) / (kCW * kCRows);
   const dim3 grid((unsigned)std::min<int64_t>(nblk, 256)), block(kCW * 64);
-  head_chain_kernel<K1, R1, R2, MODE1, MODE2><<<grid, block, kCSlots * (3 * RMAX * 32 + kCW * kCRows * 64), s>>>(
+  const int lds_bytes = kCSlots * (3 * RMAX * 32 + kCW * kCRows * 64) + (MODE2 == 1 ? kCW * 8 * (R2 * 4 + 16) : 0);
+  head_chain_kernel<K1, R1, R2, MODE1, MODE2><<<grid, block, lds_bytes, s>>>(
       X, rows, ldx, P1, P2, b1, b2, bits, Hout, Y, norms, nblk);
   TT_LAUNCH_CHECK("tt_head_chain");
   return TT_OK;

@@ -137,7 +137,12 @@ class AveragePoolingTower(BaseTower):
         lin, drop, ln = self.projection
         if (isinstance(lin, nn.Linear) and isinstance(drop, nn.Dropout) and isinstance(ln, nn.LayerNorm)
                 and ln.elementwise_affine and ln.weight.shape[0] % 4 == 0):
-            h = F.dropout(F.linear(pooled, lin.weight, lin.bias), drop.p, self.training)
+            if (pooled.is_cuda and lin.bias is not None
+                    and ops.linear_widths_ok(lin.in_features, lin.out_features)):
+                h = ops.linear(pooled.contiguous(), lin.weight, lin.bias)  # split-bf16 MFMA Linear
+            else:  # widths outside the hand-written kernels: the library GEMM
+                h = F.linear(pooled, lin.weight, lin.bias)
+            h = F.dropout(h, drop.p, self.training)
             return ops.layernorm_l2_normalize(h, ln.weight, ln.bias, ln.eps)  # one fused row pass
         return ops.l2_normalize(self.projection(pooled).contiguous())
 

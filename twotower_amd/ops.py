@@ -604,7 +604,9 @@ EMB_WIDTHS = (64, 128, 256)  # its first Linear's input widths E (C1's char towe
 
 
 def _planes(W: torch.Tensor, transpose: bool) -> torch.Tensor:
-    N, K = W.shape
+    """The three bf16 planes of W (N x K), or of W^T (K x N) when transpose (tt_head_split's N, K are
+    the planes' own rows and columns)."""
+    N, K = W.shape if not transpose else (W.shape[1], W.shape[0])
     buf = torch.empty(_lib.lib().tt_head_planes_bytes(N, K), dtype=torch.uint8, device=W.device)
     call("tt_head_split", ptr(W.contiguous()), N, K, int(transpose), ptr(buf), stream_of(W))
     return buf
@@ -885,6 +887,39 @@ def head_wgrad2_reduce(ws: torch.Tensor, dW1, db1, dW2, db2) -> None:
 
 def tower_head(x, W1, b1, W2, b2):
     return TowerHead.apply(x, W1, b1, W2, b2)
+
+
+def linear_widths_ok(E: int, H: int) -> bool:
+    """(in E, out H) shapes of the hand-written Linear (LinearHead): tt_head_gemm epi 4 forward
+    (K = E, N = H), epi 3 dx (K = H, N = E), tt_head_wgrad_ex (NG = H, NX = E)."""
+    return E in EMB_WIDTHS and H in HEAD_WIDTHS
+
+
+class LinearHead(torch.autograd.Function):
+    """y = x W^T + b on the split-bf16 MFMA head kernels (fp32 accuracy): AveragePoolingTower's
+    projection Linear(E, H) (encoders.py:84-155), forward tt_head_gemm epi 4 (bias), backward dx by
+    epi 3 on the planes of W^T, dW and db by tt_head_wgrad_ex."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        require_gpu(x, W, b)
+        x = _contig_f32(x, "x")
+        H, E = W.shape
+        y = _head_gemm(x, _planes(_contig_f32(W, "W"), False), 4, bias=_contig_f32(b, "b"), N=H)
+        ctx.save_for_backward(x, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dy = _contig_f32(dy, "dy")
+        dx = _head_gemm(dy, _planes(W, True), 3, N=W.shape[1]) if ctx.needs_input_grad[0] else None
+        dW, db = head_wgrad(dy, x)
+        return dx, dW, db
+
+
+def linear(x, W, b):
+    return LinearHead.apply(x, W, b)
 
 
 # --------------------------------------------------------------------------------------------

@@ -158,6 +158,18 @@ class TrainStep:
         graph.replay()
         return static_loss
 
+    def release(self) -> None:
+        """Drop the captured graphs (and the static buffers they own).  Call before tearing down the
+        process group: a replayable graph keeps the RCCL resources of the collectives it captured
+        (the point-to-point sends and receives of an all-to-all among them) registered with the
+        communicator, whose destruction would otherwise wait for them."""
+        torch.cuda.synchronize()
+        self._graphs.clear()
+        import gc
+
+        gc.collect()
+        torch.cuda.synchronize()
+
     def _discard_partial_step(self) -> None:
         """Forget what a failed capture queued for the optimizer: the factored table gradients the
         bag backward handed over and the side-stream gradient events (none of that ran)."""
