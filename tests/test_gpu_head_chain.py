@@ -83,7 +83,7 @@ def test_head_chains_equal_unfused_kernels_and_float64(E, H, rows):
 
 @pytest.mark.parametrize("E,H", [(256, 256), (64, 128), (128, 128)])
 def test_tower_head_chain_equals_four_launch_head(E, H, monkeypatch):
-    """ops.TowerHead through autograd, chain (default) against TT_HEAD_CHAIN=0: the output, every
+    """ops.TowerHead through autograd, TT_HEAD_CHAIN=1 against the four launches (the default): the output, every
     gradient (weights on the side-stream-free path) and the input gradient."""
     g = torch.Generator(device=DEV).manual_seed(5)
     rows = 3000

@@ -7,6 +7,7 @@ Checked: the golden trajectory captured from the reference (3 steps incl. the de
 rows), torch.optim.AdamW's own dense-gradient update on the same weights and batches (tower and
 table, at the reference's defaults), and a save_checkpoint / load_checkpoint round trip in the
 middle of training that must continue the same trajectory."""
+import copy
 import os
 
 import numpy as np
@@ -87,6 +88,10 @@ def test_backward_table_update_equals_torch_adamw(E):
     optim.fuse_table_update(fopt, fused)
     loss_fn = tt.losses.build("triplet", margin=0.2)
     for s in range(3):
+        if s:  # each step from the same state (the weights and moments the reference reached): an
+            # eps-flipped table element would otherwise move every later gradient by rounding
+            fused.load_state_dict(ref.state_dict())
+            fopt.load_state_dict(copy.deepcopy(ropt.state_dict()))  # (torch's load keeps the tensors)
         batch = tt.data.synthetic_triplets(B, L, V, seed=40 + s, device=DEV)
         lr_ = _loop_step(ref, loss_fn, ropt, *batch)
         g_tab = ref.query_tower.embedding.embedding.weight.grad.detach().clone()
@@ -94,13 +99,14 @@ def test_backward_table_update_equals_torch_adamw(E):
         assert abs(lf - lr_) < 1e-6 * max(1.0, abs(lr_)), (s, lf, lr_)
         for (k, a), (_, b) in zip(ref.named_parameters(), fused.named_parameters()):
             want, got = a.detach().double(), b.detach().double()
-            tol = 1e-5 * 1e-3 * (s + 1) + 4 * 2.0 ** -24 * want.abs()
+            tol = 1e-5 * 1e-3 + 4 * 2.0 ** -24 * want.abs()
             bad = (got - want).abs() > tol
-            if bad.any():  # AdamW at eps 1e-8 amplifies gradients of order eps (ulp-level changes of the
-                # table after step 0 move them); only such elements, and few of them, may differ
+            if bad.any():  # AdamW at eps 1e-8 amplifies gradients of order eps: only such table
+                # elements, and few of them, may differ
                 nb = int(bad.sum())
-                assert ("embedding" in k and float(g_tab[bad].abs().max()) < 1e-6
-                        and nb <= max(4, a.numel() // 10_000)), (s, k, nb, float(g_tab[bad].abs().max()))
+                assert "embedding" in k, (s, k, nb, float((got - want).abs().max()))
+                assert float(g_tab[bad].abs().max()) < 1e-6 and nb <= max(4, a.numel() // 10_000), (
+                    s, k, nb, float(g_tab[bad].abs().max()))
     wr, wf = ref.query_tower.embedding.embedding.weight, fused.query_tower.embedding.embedding.weight
     for key in ("exp_avg", "exp_avg_sq"):
         assert _rel(fopt.state[wf][key], ropt.state[wr][key]) < 1e-5, key

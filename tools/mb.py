@@ -432,10 +432,32 @@ def scorer_once(a):
     torch.cuda.synchronize()
 
 
+def head_once(a):
+    """One round of the head's fused chains and the unfused launches at C3's rows (counter passes)."""
+    N, E = 24576, 256
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x, g2 = torch.randn(N, E, device=DEV, generator=g), torch.randn(N, E, device=DEV, generator=g)
+    W, W2 = (torch.randn(E, E, device=DEV, generator=g) / 16 for _ in range(2))
+    b = torch.randn(E, device=DEV, generator=g)
+    P, P2, P1t, P2t = ops._planes(W, False), ops._planes(W2, False), ops._planes(W, True), ops._planes(W2, True)
+    h, y, dh, dx = (torch.empty(N, E, device=DEV) for _ in range(4))
+    norms, den = torch.empty(N, device=DEV), torch.full((N,), 40.0, device=DEV)
+    mask = torch.empty(N, 8, dtype=torch.int32, device=DEV)
+    bits = torch.empty(_lib.lib().tt_head_chain_bits_bytes(N, E) // 4, dtype=torch.int32, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        call("tt_head_fwd_chain", ptr(x), N, E, E, E, ptr(P), ptr(P2), ptr(b), ptr(b), ptr(bits), ptr(h), ptr(y),
+             ptr(norms), 0, st)
+        call("tt_head_bwd_chain", ptr(g2), N, E, E, E, ptr(P2t), ptr(P1t), ptr(bits), ptr(den), ptr(dh), ptr(dx), st)
+        ops._head_gemm(x, P, 0, bias=b, mask=mask)
+        ops._head_gemm(h, P2, 4, bias=b)
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
-                                     "column_sync", "l2prep", "scorer_once"])
+                                     "column_sync", "l2prep", "scorer_once", "head_once"])
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")
     ap.add_argument("--zipf", type=float, default=None)

@@ -1,11 +1,18 @@
 """Summarise tools/pmc_scorer.sh output: per scorer kernel, average duration and counter values.
 Usage: pmc_report.py OUTDIR [JSON]: with JSON, also write the per-pass MFMA utilisation and the
-engines' average durations there (bench.py reports them beside the scorer's algorithmic rate)."""
+engines' average durations there (bench.py reports them beside the scorer's algorithmic rate).
+pmc_report.py OUTDIR --match SUBSTR: group the counters per kernel name containing SUBSTR instead
+(tools/pmc_kernels.sh output)."""
 import csv, glob, json, sys, collections, re
 out = sys.argv[1]
+MATCH = sys.argv[3] if len(sys.argv) > 3 and sys.argv[2] == "--match" else None
+if MATCH:
+    sys.argv = sys.argv[:2]
 
 
 def _pass(name: str) -> str:
+    if MATCH:
+        return re.sub(r"\(.*", "", name.replace("tt::(anonymous namespace)::", "").replace("void ", ""))[:70]
     """forward engines: score_bf16_kernel<0, ...> (Li0E), score_ws_kernel, score_split_fwd_kernel"""
     return "fwd" if ("<0," in name or "Li0E" in name or "score_ws" in name or "split_fwd" in name) else "bwd"
 
@@ -20,7 +27,7 @@ for r in ks:
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{out}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "score_" in r["Kernel_Name"]:
+        if (MATCH or "score_") in r["Kernel_Name"]:
             k = _pass(r["Kernel_Name"])
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in vals.items():

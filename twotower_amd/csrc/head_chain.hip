@@ -25,6 +25,19 @@
 // block's first chunks arrive while the current block's second product runs.
 #include "common.hpp"
 
+// Timing ablations (tools/build_variants.sh; never in the shipped build): TT_CHAB_NOMFMA keeps the
+// operand reads and drops the products, TT_CHAB_NOFILL drops the LDS-DMA pieces, TT_CHAB_NOBAR the
+// chunk barriers, TT_CHAB_NOSTORE the h and y stores.  Their results are wrong by construction.
+#ifdef TT_CHAB_NOMFMA
+__device__ __forceinline__ tt::f32x16 tt_ch_nomfma(tt::bf16x8 a, tt::bf16x8 b, tt::f32x16 c) {
+  asm volatile("" ::"v"(a), "v"(b));
+  return c;
+}
+#define TT_CH_MFMA(a, b, c) tt_ch_nomfma((a), (b), (c))
+#else
+#define TT_CH_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+#endif
+
 namespace tt {
 namespace {
 
@@ -32,7 +45,7 @@ constexpr int kCW = 4;       // waves per workgroup
 constexpr int kCRows = 32;   // rows per wave
 constexpr int kCSlots = 3;   // LDS ring slots
 #ifndef TT_CHAIN_PERMLANE
-#define TT_CHAIN_PERMLANE 0      // 1: the half exchange by v_permlane32_swap instead of ds_bpermute
+#define TT_CHAIN_PERMLANE 0      // 1, 2: the half exchange by v_permlane32_swap (operand orders) instead of ds_bpermute
 #endif
 
 // MODE1: 0 forward first Linear (bias + ReLU, ReLU bits written, h stored)
@@ -55,7 +68,10 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
   constexpr int XB = kCW * kCRows * 64;                    // B-operand rows of a first-product chunk (8 KiB)
   constexpr int SLOT = WB + XB;
   constexpr int XP = XB / 1024;                            // its LDS-DMA pieces
-  constexpr int F = (3 * RMAX / 32 + XP + kCW - 1) / kCW;  // LDS-DMA pieces per wave and chunk
+  constexpr int WP1 = 3 * R1 / 32, WP2 = 3 * R2 / 32;       // plane pieces of a first / second chunk
+  constexpr int WU1 = WP1 / kCW, XU = XP / kCW;             // ... per wave (first: plane, then row pieces)
+  constexpr int F1 = WU1 + XU, F2 = (WP2 + kCW - 1) / kCW;  // LDS-DMA pieces per wave: first / second chunk
+  static_assert(WP1 % kCW == 0 && XP % kCW == 0, "first-chunk pieces split evenly over the waves");
   constexpr int NW1 = (NT1 + 1) / 2;                       // ReLU words per lane and row tile
   constexpr int STG_ROW = R2 * 4 + 16;                     // MODE2 1 staging row (padded: no bank conflicts)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -64,81 +80,116 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
   typedef __attribute__((address_space(3))) char lds_char_t;
   lds_char_t* lds = (lds_char_t*)smem;
   const int lane = lane_id(), r32 = lane & 31, hh = lane >> 5;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar fill addressing)
-  const int64_t nmine = (nblk - (int64_t)blockIdx.x + gridDim.x - 1) / gridDim.x;
+  const int wid0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar fill addressing)
+  const int wid = wid0;
+  const int nmine = (int)((nblk - (int64_t)blockIdx.x + gridDim.x - 1) / gridDim.x);
   if (nmine <= 0) return;  // workgroup-uniform
-  const int64_t total = nmine * CT;
   const unsigned lds_base = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds);
 
-  // Chunk g of this workgroup's sequence: row block blockIdx.x + (g / CT) grid, chunk g % CT.  Chunks
-  // [0, C1): the P1 planes' 16-k slice j = chunk, plus the block's 128 B-operand rows at k 16 j ..
-  // 16 j + 15 (64 B per row; 16-B slot s of row r at slot s ^ ((r >> 2) & 3): the lanes of a
-  // ds_read_b128 quarter hit 16 different bank groups); [C1, CT): the P2 planes' slice chunk - C1.
-  auto fill = [&](int64_t g) {
-    if (g >= total) return;  // workgroup-uniform
-    const int cl = (int)(g % CT);
-    const bool first = cl < C1;
-    const int j = first ? cl : cl - C1;
-    const int nrows = first ? R1 : R2, kc = first ? K1 : R1;
-    const int wpieces = 3 * nrows / 32, ppl = nrows / 32;
-    const int npieces = wpieces + (first ? XP : 0);
-    const char* wsrc = reinterpret_cast<const char*>(first ? P1 : P2);
-    const unsigned slot = lds_base + (unsigned)((g % kCSlots) * SLOT);
-    const int64_t rb = blockIdx.x + (g / CT) * gridDim.x;
+  // Chunk cl of row block rb goes to ring slot `slot` (chunks are numbered continuously over this
+  // workgroup's blocks, slot = number % 3).  Chunks [0, C1): the P1 planes' 16-k slice j = cl (32 B
+  // per plane row) and the block's 128 B-operand rows at k 16 j .. 16 j + 15 (64 B per row); [C1, CT):
+  // the P2 planes' slice cl - C1.  Swizzles (so the lanes of every ds_read_b128 quarter hit distinct
+  // bank groups): the 16-B half s of plane row r sits at half s ^ ((r >> 3) & 1); the 16-B slot s of
+  // B-operand row r at slot s ^ ((r >> 2) & 3).  LDS-DMA writes linearly (lane l: byte 16 l of the
+  // piece), so the swizzle goes on the source.  Source offsets: a per-lane part (below) plus a
+  // wave-uniform part per piece; the chunk's k offset goes on the scalar base.
+  const int lw = lane >> 1;                                        // plane piece: row within 32
+  const unsigned wsw = (unsigned)(((lane & 1) ^ ((lw >> 3) & 1)) * 16);
+  const unsigned lw1 = (unsigned)(lw * K1 * 2) + wsw, lw2 = (unsigned)(lw * R1 * 2) + wsw;
+  const int lx = lane >> 2;                                        // row piece: row within 16
+  const unsigned lxs = (unsigned)(((lane & 3) ^ ((lx >> 2) & 3)) * 16);
+  const unsigned ldx4 = (unsigned)(ldx * 4);
+  auto issue = [&](unsigned off, const void* base, unsigned m0) {
+#ifndef TT_CHAB_NOFILL
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "s"(m0)
+                 : "memory");
+#endif
+  };
+  auto fill = [&](const int cl, const int64_t rb, const int slot) {
+    const unsigned sbase = lds_base + (unsigned)(slot * SLOT);
+    int wid = wid0;  // laundered: the pieces' wave-uniform offsets are recomputed per fill (a few
+    asm volatile("" : "+s"(wid));  // SALU) rather than hoisted out of the block loop and spilled
+    if (cl < C1) {
+      const char* wb = reinterpret_cast<const char*>(P1) + cl * 32;
 #pragma unroll
-    for (int u = 0; u < F; ++u) {
-      const int q = min(u * kCW + wid, npieces - 1);  // surplus issues repeat the last piece (same bytes)
-      if (q < wpieces) {
-        const int p = q / ppl, row = (q % ppl) * 32 + (lane >> 1);
-        const unsigned off = (unsigned)(((size_t)p * nrows * kc + (size_t)row * kc) * 2 + j * 32 + (lane & 1) * 16);
-        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(wsrc),
-                     "s"(__builtin_amdgcn_readfirstlane(slot + q * 1024))
-                     : "memory");
-      } else {  // B-operand rows: piece xq holds rows 16 xq .. 16 xq + 15 of the block
-        const int xq = q - wpieces, rl = xq * 16 + (lane >> 2);
-        int64_t r = rb * (kCW * kCRows) + rl;
-        r = r < rows ? r : rows - 1;
-        const int sq = (lane & 3) ^ ((rl >> 2) & 3);
-        const float* src = X + r * ldx + j * 16 + sq * 4;
-        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
-                     "s"(__builtin_amdgcn_readfirstlane(slot + WB + xq * 1024))
-                     : "memory");
+      for (int u = 0; u < WU1; ++u) {
+        const int q = u * kCW + wid, pl = q / (R1 / 32), g = q % (R1 / 32);
+        issue(lw1 + (unsigned)((pl * R1 + g * 32) * K1 * 2), wb, sbase + q * 1024);
+      }
+      const float* xb = X + rb * (kCW * kCRows) * ldx + cl * 16;
+      const int64_t left = rows - 1 - rb * (kCW * kCRows);  // rows past the end read the last row
+      const int lim = (int)(left < kCW * kCRows - 1 ? left : kCW * kCRows - 1);
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        const int xq = u * kCW + wid, rl = min(xq * 16 + lx, lim);
+        issue((unsigned)rl * ldx4 + lxs, xb, sbase + WB + xq * 1024);
+      }
+    } else {
+      const char* wb = reinterpret_cast<const char*>(P2) + (cl - C1) * 32;
+#pragma unroll
+      for (int u = 0; u < F2; ++u) {
+        const int q = min(u * kCW + wid, WP2 - 1), pl = q / (R2 / 32), g = q % (R2 / 32);
+        issue(lw2 + (unsigned)((pl * R2 + g * 32) * R1 * 2), wb, sbase + q * 1024);
       }
     }
   };
-  // chunk g's pieces landed for every wave (this wave's: all but the F pieces of chunk g + 1 may be
-  // outstanding; the last chunk has none after it), and every wave is done with chunk g - 1
-  auto arrive = [&](int64_t g) {
-    // lgkmcnt(0): this wave's ring reads of chunk g - 1 have returned (the compiler may sink the
-    // MFMAs that consume them, and their waits, below an asm barrier), so the fill of chunk g + 2
-    // that some wave issues after the barrier cannot overwrite a slot still being read
-    if (g + 1 < total) {
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(F) : "memory");
+  // the chunk two ahead of chunk cl of block rb (the next block's when it wraps; none past the last)
+  // (the chunk number is laundered through an SGPR in the unrolled second product: with it a
+  // compile-time constant the compiler hoists every chunk's addresses out of the block loop)
+  auto fill_ahead = [&](int cl, const int bi, const int64_t rb, const int slot) {
+    int nc = cl + 2;
+    asm volatile("" : "+s"(nc));
+    const int ns = slot + 2 >= kCSlots ? slot + 2 - kCSlots : slot + 2;
+    if (nc < CT) {
+      fill(nc, rb, ns);
+    } else if (bi + 1 < nmine) {
+      fill(nc - CT, rb + gridDim.x, ns);
+    }
+  };
+  // chunk cl's pieces landed for every wave (this wave's: all but the pieces of chunk cl + 1 may be
+  // outstanding, F1 or F2 of them, none after the last chunk), and every wave is done with the
+  // previous chunk.  lgkmcnt(0): this wave's ring reads of that chunk have returned (the compiler
+  // may sink the MFMAs that consume them, and their waits, below an asm barrier), so the fill two
+  // ahead that some wave issues after the barrier cannot overwrite a slot still being read.
+  auto arrive = [&](const int cl, const int bi) {
+    const int nc = cl + 1;
+    if (nc < C1 || (nc == CT && bi + 1 < nmine)) {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(F1) : "memory");
+    } else if (nc < CT) {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(F2) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
+#ifndef TT_CHAB_NOBAR
     asm volatile("s_barrier" ::: "memory");  // (not __syncthreads: its fence would drain the fills ahead)
+#endif
   };
 
-  fill(0);
-  fill(1);
+  fill(0, blockIdx.x, 0);
+  if (CT > 1) fill(1, blockIdx.x, 1);
 
-  int64_t g = 0;
-  for (int64_t bi = 0; bi < nmine; ++bi) {
-    const int64_t rb = blockIdx.x + bi * gridDim.x;
+  int slot = 0;  // ring slot of the current chunk
+  for (int bi = 0; bi < nmine; ++bi) {
+    const int64_t rb = blockIdx.x + (int64_t)bi * gridDim.x;
     const int64_t r0 = rb * (kCW * kCRows) + wid * kCRows;  // this wave's first row
     f32x16 acc1[NT1];
 #pragma unroll
     for (int t = 0; t < NT1; ++t) acc1[t] = f32x16{};
     // ---- first product, transposed: acc1[t] = (P1 rows 32 t .. 32 t + 31) x (this wave's rows)^T
     const int xr = wid * kCRows + r32;  // this lane's row in the block
-#pragma unroll
-    for (int j = 0; j < C1; ++j, ++g) {
-      arrive(g);
-      fill(g + 2);
-      const lds_char_t* sl = lds + (g % kCSlots) * SLOT;
-      const lds_char_t* ch = sl + r32 * 32 + hh * 16;
+#pragma unroll 1
+    for (int j = 0; j < C1; ++j) {
+      arrive(j, bi);
+      fill_ahead(j, bi, rb, slot);
+      const lds_char_t* sl = lds + slot * SLOT;
+      const lds_char_t* ch = sl + r32 * 32 + (hh ^ ((r32 >> 3) & 1)) * 16;
       const lds_char_t* xrow = sl + WB + xr * 64;
+      // the tile-0 weight operands and the rows first, then the split while they arrive; each tile's
+      // operands are read one tile ahead into the other register set (no LDS round trip between tiles)
+      bf16x8 w[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[0][p] = *reinterpret_cast<const lds_bf16x8_t*>(ch + p * R1 * 32);
       const f32x4 xa = *reinterpret_cast<const lds_f32x4_t*>(xrow + (((2 * hh) ^ ((xr >> 2) & 3)) << 4));
       const f32x4 xb = *reinterpret_cast<const lds_f32x4_t*>(xrow + (((2 * hh + 1) ^ ((xr >> 2) & 3)) << 4));
       __bf16 x0[8], x1[8], x2[8];
@@ -153,18 +204,24 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
       }
 #pragma unroll
       for (int t = 0; t < NT1; ++t) {
-        const bf16x8 w0 = *reinterpret_cast<const lds_bf16x8_t*>(ch + 0 * R1 * 32 + t * 1024);
-        const bf16x8 w1 = *reinterpret_cast<const lds_bf16x8_t*>(ch + 1 * R1 * 32 + t * 1024);
-        const bf16x8 w2 = *reinterpret_cast<const lds_bf16x8_t*>(ch + 2 * R1 * 32 + t * 1024);
+        if (t + 1 < NT1) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            w[(t + 1) & 1][p] = *reinterpret_cast<const lds_bf16x8_t*>(ch + p * R1 * 32 + (t + 1) * 1024);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8(&wt)[3] = w[t & 1];
         // head.hip's products with the operands in the other roles (x terms b, W terms w):
         // x2 W0, x1 W1, x0 W2, x1 W0, x0 W1, x0 W0
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b2, acc1[t], 0, 0, 0);
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b1, acc1[t], 0, 0, 0);
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc1[t], 0, 0, 0);
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b1, acc1[t], 0, 0, 0);
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc1[t], 0, 0, 0);
-        acc1[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b0, acc1[t], 0, 0, 0);
+        acc1[t] = TT_CH_MFMA(wt[0], b2, acc1[t]);
+        acc1[t] = TT_CH_MFMA(wt[1], b1, acc1[t]);
+        acc1[t] = TT_CH_MFMA(wt[2], b0, acc1[t]);
+        acc1[t] = TT_CH_MFMA(wt[0], b1, acc1[t]);
+        acc1[t] = TT_CH_MFMA(wt[1], b0, acc1[t]);
+        acc1[t] = TT_CH_MFMA(wt[0], b0, acc1[t]);
+        __builtin_amdgcn_sched_barrier(0);
       }
+      slot = slot + 1 == kCSlots ? 0 : slot + 1;
     }
     // ---- first epilogue: lane = row r0 + r32, acc1[t][v] = unit 32 t + (v & 3) + 8 (v >> 2) + 4 hh
     const int64_t row = r0 + r32;
@@ -199,7 +256,11 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc1[t][v] = (word[t >> 1] >> (16 * (t & 1) + v)) & 1u ? acc1[t][v] : 0.f;
     }
+#ifdef TT_CHAB_NOSTORE
+    if (row_ok && rows < 0) {
+#else
     if (row_ok) {
+#endif
       float* hrow = Hout + row * R1 + 4 * hh;
 #pragma unroll
       for (int t = 0; t < NT1; ++t)
@@ -217,19 +278,26 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-#if TT_CHAIN_PERMLANE
+#if TT_CHAIN_PERMLANE == 1
           const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, acc1[t][8 * s + i]),
                                                           __builtin_bit_cast(unsigned, acc1[t][8 * s + 4 + i]), false,
                                                           false);
           acc1[t][8 * s + i] = __builtin_bit_cast(float, (unsigned)r[0]);
           acc1[t][8 * s + 4 + i] = __builtin_bit_cast(float, (unsigned)r[1]);
+#elif TT_CHAIN_PERMLANE == 2
+          const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, acc1[t][8 * s + 4 + i]),
+                                                          __builtin_bit_cast(unsigned, acc1[t][8 * s + i]), false,
+                                                          false);
+          acc1[t][8 * s + 4 + i] = __builtin_bit_cast(float, (unsigned)r[0]);
+          acc1[t][8 * s + i] = __builtin_bit_cast(float, (unsigned)r[1]);
 #else
-          const float send = hh ? acc1[t][8 * s + i] : acc1[t][8 * s + 4 + i];
-          const float got = __shfl_xor(send, 32);
-          if (hh)
-            acc1[t][8 * s + i] = got;
-          else
-            acc1[t][8 * s + 4 + i] = got;
+          // (the pair made opaque first: a select between two elements of one vector otherwise becomes
+          // a lane-varying element index, extracted and inserted by 16-way v_cndmask chains)
+          float a = acc1[t][8 * s + i], b = acc1[t][8 * s + 4 + i];
+          asm volatile("" : "+v"(a), "+v"(b));
+          const float got = __shfl_xor(hh ? a : b, 32);
+          acc1[t][8 * s + i] = hh ? got : a;
+          acc1[t][8 * s + 4 + i] = hh ? b : got;
 #endif
         }
     // ---- second product: acc2[t2] = (this wave's rows, as A) x (P2 rows 32 t2 .. +31)^T
@@ -237,10 +305,13 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
 #pragma unroll
     for (int t = 0; t < NT2; ++t) acc2[t] = f32x16{};
 #pragma unroll
-    for (int j = 0; j < C2; ++j, ++g) {
-      arrive(g);
-      fill(g + 2);
-      const lds_char_t* ch = lds + (g % kCSlots) * SLOT + r32 * 32 + hh * 16;
+    for (int j = 0; j < C2; ++j) {
+      arrive(C1 + j, bi);
+      fill_ahead(C1 + j, bi, rb, slot);
+      const lds_char_t* ch = lds + slot * SLOT + r32 * 32 + (hh ^ ((r32 >> 3) & 1)) * 16;
+      bf16x8 w[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[0][p] = *reinterpret_cast<const lds_bf16x8_t*>(ch + p * R2 * 32);
       const f32x16& hv = acc1[j >> 1];
       const int o = 8 * (j & 1);
       __bf16 h0[8], h1[8], h2[8];
@@ -255,16 +326,22 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
       }
 #pragma unroll
       for (int t = 0; t < NT2; ++t) {
-        const bf16x8 w0 = *reinterpret_cast<const lds_bf16x8_t*>(ch + 0 * R2 * 32 + t * 1024);
-        const bf16x8 w1 = *reinterpret_cast<const lds_bf16x8_t*>(ch + 1 * R2 * 32 + t * 1024);
-        const bf16x8 w2 = *reinterpret_cast<const lds_bf16x8_t*>(ch + 2 * R2 * 32 + t * 1024);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, w0, acc2[t], 0, 0, 0);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w1, acc2[t], 0, 0, 0);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w2, acc2[t], 0, 0, 0);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w0, acc2[t], 0, 0, 0);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w1, acc2[t], 0, 0, 0);
-        acc2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w0, acc2[t], 0, 0, 0);
+        if (t + 1 < NT2) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            w[(t + 1) & 1][p] = *reinterpret_cast<const lds_bf16x8_t*>(ch + p * R2 * 32 + (t + 1) * 1024);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8(&wt)[3] = w[t & 1];
+        acc2[t] = TT_CH_MFMA(a2, wt[0], acc2[t]);
+        acc2[t] = TT_CH_MFMA(a1, wt[1], acc2[t]);
+        acc2[t] = TT_CH_MFMA(a0, wt[2], acc2[t]);
+        acc2[t] = TT_CH_MFMA(a1, wt[0], acc2[t]);
+        acc2[t] = TT_CH_MFMA(a0, wt[1], acc2[t]);
+        acc2[t] = TT_CH_MFMA(a0, wt[0], acc2[t]);
+        __builtin_amdgcn_sched_barrier(0);
       }
+      slot = slot + 1 == kCSlots ? 0 : slot + 1;
     }
     // ---- second epilogue: acc2[t][v] = row r0 + (v & 3) + 8 (v >> 2) + 4 hh, column 32 t + r32
     if constexpr (MODE2 == 0 || MODE2 == 1) {
@@ -333,7 +410,11 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
       }
     }
     float* orow = Y + r0 * R2 + r32;
+#ifdef TT_CHAB_NOSTORE
+    if (rows < 0) {
+#else
     if (__builtin_amdgcn_readfirstlane((int)(r0 + kCRows <= rows))) {
+#endif
 #pragma unroll
       for (int t = 0; t < NT2; ++t)
 #pragma unroll

@@ -822,9 +822,11 @@ class TowerHead(torch.autograd.Function):
 
 
 def head_chain() -> bool:
-    """The tower head runs as two fused chains (tt_head_fwd_chain / tt_head_bwd_chain: one launch per
-    pass); TT_HEAD_CHAIN=0 runs the four tt_head_gemm launches (and the normalise pass) instead."""
-    return os.environ.get("TT_HEAD_CHAIN", "1") != "0"
+    """TT_HEAD_CHAIN=1: the tower head runs as two fused chains (tt_head_fwd_chain /
+    tt_head_bwd_chain: one launch per pass).  Off by default: at C3's 24,576 rows the chains take
+    54.6 / 56.2 us per pass against 46.7 / 46.8 us for the two tt_head_gemm launches they replace
+    (profiles/r05h_head_chain_ablations.txt); the outputs are bit-identical either way."""
+    return os.environ.get("TT_HEAD_CHAIN", "0") == "1"
 
 
 def head_wgrad(G: torch.Tensor, X: torch.Tensor, dW: torch.Tensor | None = None,
