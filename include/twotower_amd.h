@@ -53,6 +53,14 @@ const char* tt_last_error(void);
 int tt_bag_mean_fwd(const float* table, int64_t V, int E,
                     const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
                     float* pooled, float* denom, tt_stream_t stream);
+/* tt_bag_mean_fwd over a column slab (table_sync "column": this rank's El columns of every row,
+ * slab V x El): pooled (nseq x El) summed in the order tt_bag_mean_fwd sums those columns at the
+ * full width E, so the assembled rows equal the one-GPU forward's bit for bit.  El in
+ * {32, 64, 128, 256} dividing E.  Replaces the reference's per-rank embedding lookup + masked mean
+ * (twotower/embeddings.py:30, encoders.py:67-72) for a column-sharded table. */
+int tt_bag_mean_fwd_cols(const float* slab, int64_t V, int El, int E,
+                         const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                         float* pooled, float* denom, tt_stream_t stream);
 /* tt_bag_mean_fwd whose launch also forms the four weight plane sets of the tower head that
  * consumes the pooled rows (W1 H x E, W2 H x H: tt_head_split_ff2's output in `planes`, bit for
  * bit) in extra workgroups, so the split leaves the path between the gather and the first head

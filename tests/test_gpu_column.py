@@ -106,3 +106,32 @@ def test_bag_forward_slab_32_columns():
     one[:, 0] = rng.integers(1, V, size=64)
     p1, _ = ops.bag_mean_forward(torch.as_tensor(tbl, device=DEV), torch.as_tensor(one, device=DEV))
     assert np.array_equal(p1.cpu().numpy(), (tbl[one[:, 0]] / np.float32(1.0 + 1e-9)).astype(np.float32))
+
+
+@pytest.mark.parametrize("E,El", [(256, 32), (256, 64), (256, 128), (256, 256), (128, 32), (128, 64), (64, 32),
+                                  (512, 64)])
+@pytest.mark.parametrize("L", [64, 100, 7])
+def test_column_slab_forward_equals_full_width_bits(E, El, L):
+    """tt_bag_mean_fwd_cols over each column slab of a table equals tt_bag_mean_fwd at the full width
+    on those columns bit for bit (the pooled rows a column-sharded step assembles are the one-GPU
+    forward's), with ragged / padded / out-of-range ids and L past one 64-token chunk; int32 and
+    int64 ids."""
+    rng = np.random.default_rng(E + El + L)
+    V, N = 3000, 777
+    ids = rng.integers(0, V + 3, size=(N, L))  # a few ids >= V: masked, as the full-width gather does
+    ids[np.arange(L)[None, :] >= rng.integers(0, L + 1, size=N)[:, None]] = 0
+    ids[0, :] = 0
+    ids[1, :] = V - 1
+    tbl = torch.as_tensor(rng.standard_normal((V, E)).astype(np.float32), device=DEV)
+    for dt in (torch.int64, torch.int32):
+        idt = torch.as_tensor(ids, device=DEV).to(dt)
+        full, fden = ops.bag_mean_forward(tbl, idt)
+        for c0 in range(0, E, El):
+            slab = tbl[:, c0:c0 + El].contiguous()
+            part = torch.empty(N, El, device=DEV)
+            den = torch.empty(N, device=DEV)
+            ops.call("tt_bag_mean_fwd_cols", slab.data_ptr(), V, El, E, idt.data_ptr(), _lib.ids_dtype_code(idt), N, L,
+                     L, part.data_ptr(), den.data_ptr(), _lib.stream_of(slab))
+            torch.cuda.synchronize()
+            assert torch.equal(part, full[:, c0:c0 + El]), (dt, c0)
+            assert torch.equal(den, fden)

@@ -360,8 +360,10 @@ def column_sync(a):
         den_all = torch.empty(N, device=DEV)
         res = {"config": shape, "ranks": R, "El": El, "tokens_per_rank": int((own > 0).sum())}
         res.update(base)
-        res["col_gather_us"] = graph_us(lambda: call("tt_bag_mean_fwd", ptr(slab), V, El, ptr(ids), _lib.TT_IDS_I32, N,
-                                                     L, L, ptr(part), ptr(den_all), st()))
+        res["col_gather_us"] = graph_us(lambda: call("tt_bag_mean_fwd_cols", ptr(slab), V, El, E, ptr(ids),
+                                                     _lib.TT_IDS_I32, N, L, L, ptr(part), ptr(den_all), st()))
+        res["col_gather_free_order_us"] = graph_us(lambda: call("tt_bag_mean_fwd", ptr(slab), V, El, ptr(ids),
+                                                                _lib.TT_IDS_I32, N, L, L, ptr(part), ptr(den_all), st()))
         recv = torch.randn(N, El, device=DEV)
         out = torch.empty(nown, E, device=DEV)
         res["permute_pooled_us"] = graph_us(lambda: out.copy_(recv.view(R, nown, El).permute(1, 0, 2).reshape(nown, E)))

@@ -53,6 +53,7 @@ _SIGNATURES = {
     "tt_version": (_c_int, []),
     "tt_last_error": (ctypes.c_char_p, []),
     "tt_bag_mean_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _c_int, _c_i64, _c_int, _c_i64, _vp, _vp, _vp]),
+    "tt_bag_mean_fwd_cols": (_c_int, [_vp, _c_i64, _c_int, _c_int, _vp, _c_int, _c_i64, _c_int, _c_i64, _vp, _vp, _vp]),
     "tt_bag_mean_fwd_split": (_c_int, [_vp, _c_i64, _c_int, _vp, _c_int, _c_i64, _c_int, _c_i64, _vp, _vp, _vp, _vp,
                                        _c_int, _vp, _vp]),
     "tt_bag_mean_bwd_ws_size": (_c_sz, [_c_i64, _c_int, _c_i64, _c_int]),

@@ -118,6 +118,91 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_kernel(
   if (lane == 0) denom[seq] = den;
 }
 
+// Column slab forward (table_sync "column"): pooled columns of a (V, El) slab summed in the
+// order bag_fwd_kernel sums them at the full width E, so the pooled rows every rank assembles
+// equal the one-GPU forward's bit for bit.  That order: valid token j of each 64-token chunk goes
+// to sub-row j % RPIF (RPIF = 64 / LPR of the full-width launch: 4 at E = 64, 2 at E = 128, 1 from
+// E = 256 on, where the sum is plain token order), each sub-row summed in token order, the
+// sub-rows folded pairwise ((s0 + s1) + (s2 + s3): the butterfly's result in sub-row 0).  Here a
+// wave holds 64 / LPRC sequences (LPRC = El / 4 lanes each), a lane keeps the RPIF sub-row sums of
+// its float4 column, and U tokens' rows are in flight per step.
+template <typename IdT, int LPRC, int RPIF, int U>
+__global__ __launch_bounds__(kBlock) void bag_fwd_cols_kernel(
+    const float* __restrict__ slab, int64_t V, int El, const IdT* __restrict__ ids, int64_t nseq, int L,
+    int64_t ld, float* __restrict__ pooled, float* __restrict__ denom) {
+  constexpr int SPW = kWave / LPRC;
+  const int lane = lane_id(), g = lane / LPRC, c = lane % LPRC;
+  const int64_t seq = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * SPW + g;
+  const bool live = seq < nseq;
+  const IdT* rid = ids + (live ? seq : 0) * ld;
+  f32x4 acc[RPIF];
+#pragma unroll
+  for (int r = 0; r < RPIF; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int cnt = 0;
+  for (int base = 0; base < L; base += kWave) {
+    const int lim = L - base < kWave ? L - base : kWave;
+    int j = 0;  // valid tokens of this chunk so far
+    for (int t0 = 0; t0 < lim; t0 += U) {
+      int id[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = t0 + u;
+        const int64_t v = (live && t < lim) ? (int64_t)rid[base + t] : 0;
+        id[u] = (v > 0 && v < V) ? (int)v : -1;
+      }
+      f32x4 x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        x[u] = id[u] >= 0 ? reinterpret_cast<const f32x4*>(slab + (int64_t)id[u] * El)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (id[u] >= 0) {
+          if constexpr (RPIF == 1) {
+            acc[0] += x[u];
+          } else {
+            const int r = j % RPIF;
+#pragma unroll
+            for (int k = 0; k < RPIF; ++k)
+              if (k == r) acc[k] += x[u];
+          }
+          ++j;
+        }
+      }
+    }
+    cnt += j;
+  }
+  f32x4 sum = acc[0];
+  if constexpr (RPIF == 2) sum = acc[0] + acc[1];
+  if constexpr (RPIF == 4) sum = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  if (!live) return;
+  const float den = (float)cnt + 1e-9f;  // mask.sum(1) + 1e-9, encoders.py:72
+  reinterpret_cast<f32x4*>(pooled + seq * El)[c] = sum / den;
+  if (c == 0) denom[seq] = den;
+}
+
+template <typename IdT>
+int launch_fwd_cols(const float* slab, int64_t V, int El, int E, const IdT* ids, int64_t nseq, int L, int64_t ld,
+                    float* pooled, float* denom, hipStream_t s) {
+  const int rpif = E == 64 ? 4 : E == 128 ? 2 : 1;
+  const int spw = kWave / (El / 4);
+  const int64_t waves = (nseq + spw - 1) / spw;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+#define TT_FC(LPRC, R) \
+  bag_fwd_cols_kernel<IdT, LPRC, R, 8><<<grid, block, 0, s>>>(slab, V, El, ids, nseq, L, ld, pooled, denom)
+#define TT_FCR(LPRC) \
+  if (rpif == 4) TT_FC(LPRC, 4); else if (rpif == 2) TT_FC(LPRC, 2); else TT_FC(LPRC, 1)
+  switch (El) {
+    case 32: TT_FCR(8); break;
+    case 64: TT_FCR(16); break;
+    case 128: TT_FCR(32); break;
+    default: TT_FCR(64); break;  // 256
+  }
+#undef TT_FCR
+#undef TT_FC
+  TT_LAUNCH_CHECK("tt_bag_mean_fwd_cols");
+  return TT_OK;
+}
+
 // Any E: lanes stride the columns, tokens are walked one at a time (wave-uniform row).
 template <typename IdT>
 __global__ __launch_bounds__(kBlock) void bag_fwd_generic_kernel(
@@ -1178,6 +1263,21 @@ extern "C" int tt_bag_mean_fwd(const float* table, int64_t V, int E, const void*
   if (ids_dtype == TT_IDS_I32)
     return launch_fwd(table, V, E, static_cast<const int32_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
   return launch_fwd(table, V, E, static_cast<const int64_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
+}
+
+extern "C" int tt_bag_mean_fwd_cols(const float* slab, int64_t V, int El, int E, const void* ids, int ids_dtype,
+                                    int64_t nseq, int L, int64_t ld_ids, float* pooled, float* denom,
+                                    tt_stream_t stream) {
+  int rc = check_common(V, El, ids, ids_dtype, nseq, L, ld_ids);
+  if (rc) return rc;
+  TT_REQUIRE(slab && pooled && denom, "null pointer");
+  TT_REQUIRE((El == 32 || El == 64 || El == 128 || El == 256) && E >= El && E % El == 0,
+             "tt_bag_mean_fwd_cols: El in {32, 64, 128, 256} dividing E (got El=%d E=%d)", El, E);
+  if (nseq == 0) return TT_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ids_dtype == TT_IDS_I32)
+    return launch_fwd_cols(slab, V, El, E, static_cast<const int32_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
+  return launch_fwd_cols(slab, V, El, E, static_cast<const int64_t*>(ids), nseq, L, ld_ids, pooled, denom, s);
 }
 
 extern "C" int tt_bag_mean_fwd_split(const float* table, int64_t V, int E, const void* ids, int ids_dtype,

@@ -283,7 +283,7 @@ class ColumnTable:
     "column"): rank r owns columns [r El, (r + 1) El) of EVERY row, El = E / world, as a compact
     (V, El) fp32 slab with its AdamW moments.  Nothing of the table crosses the links:
       * forward: every rank's ids are all-gathered, each rank pools ITS columns for every rank's
-        sequences (tt_bag_mean_fwd over the slab, El wide) and the pooled column blocks are
+        sequences (tt_bag_mean_fwd_cols over the slab, El wide, the full-width sum order) and the pooled column blocks are
         exchanged all-to-all, so each rank gets its own sequences' whole pooled rows;
       * backward: d_pooled / denom is cut into column blocks and exchanged all-to-all, and each rank
         forms the gradient of its slab from every rank's tokens (the per-rank sort plans,

@@ -388,7 +388,7 @@ def column_grad_exchange(gs: torch.Tensor, col) -> torch.Tensor:
 class BagMeanPoolColumn(torch.autograd.Function):
     """BagMeanPool for a column-sharded table (distributed.ColumnTable, table_sync "column"):
     every rank's ids all-gathered, this rank's columns pooled for all of them from its slab
-    (tt_bag_mean_fwd, El wide), the column blocks exchanged all-to-all, so each rank returns the
+    (tt_bag_mean_fwd_cols, El wide, in the full-width sum order), the column blocks exchanged all-to-all, so each rank returns the
     whole pooled rows of its own sequences (encoders.py:62-72).  Backward: d_pooled / denom cut
     into column blocks and exchanged all-to-all; the factored gradient (every rank's gs at this
     rank's columns + the all-gathered plans) goes to the optimizer (tt_bag_col_reduce fused with
@@ -411,8 +411,8 @@ class BagMeanPoolColumn(torch.autograd.Function):
         part = torch.empty(W * nseq, El, dtype=_FLOAT, device=dev)
         den_all = torch.empty(W * nseq, dtype=_FLOAT, device=dev)
         if W * nseq:
-            call("tt_bag_mean_fwd", ptr(col.slab), V, El, ptr(ids_all), _lib.ids_dtype_code(ids_all), W * nseq, L, L,
-                 ptr(part), ptr(den_all), stream_of(weight))
+            call("tt_bag_mean_fwd_cols", ptr(col.slab), V, El, weight.shape[1], ptr(ids_all),
+                 _lib.ids_dtype_code(ids_all), W * nseq, L, L, ptr(part), ptr(den_all), stream_of(weight))
         pooled = column_pooled_exchange(part, col, nseq)
         denom = den_all[col.rank * nseq:(col.rank + 1) * nseq]
         if cplan is not None:

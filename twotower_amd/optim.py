@@ -516,11 +516,44 @@ def _gather_parts(parts, group):
     return plan.ids, dp_all, den_all, plan
 
 
+class _ArgsRing:
+    """Host-to-device staging of the per-step AdamW scalars without a host sync: a pageable
+    ``torch.tensor(...).to(device)`` is a blocking copy ordered behind everything queued on the
+    stream, i.e. a full drain in the middle of the step (the unchanged train.py loop issues its
+    next kernels only after it).  The scalars go into one of a ring of pinned buffers and are
+    copied on the current stream (non_blocking); a buffer is rewritten only once its last copy
+    has executed (its event, long complete by then in practice)."""
+
+    def __init__(self, n: int = 16):
+        self.n, self.k = n, 0
+        self.host = None
+        self.events: list = [None] * n
+
+    def __call__(self, vals, device) -> torch.Tensor:
+        if self.host is None:
+            self.host = torch.empty((self.n, len(vals)), dtype=torch.float32).pin_memory()
+        k, self.k = self.k, (self.k + 1) % self.n
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        self.host[k].copy_(torch.tensor(vals, dtype=torch.float32))
+        out = torch.empty(len(vals), dtype=torch.float32, device=device)
+        out.copy_(self.host[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self.events[k] = ev
+        return out
+
+
+_ARGS_RING = _ArgsRing()
+
+
 def _host_adam_args(lr, b1, b2, eps, wd, step, device) -> torch.Tensor:
     """The per-step scalars of make_adam (csrc/common.hpp) formed in Python doubles, rounded to
-    fp32 once, as a TT_ADAM_ARGS_BYTES device buffer."""
+    fp32 once, as a TT_ADAM_ARGS_BYTES device buffer (staged through _ArgsRing: no host sync)."""
     vals = [1.0 - lr * wd, 1.0 - b1, b2, 1.0 - b2, lr / (1.0 - b1 ** step), math.sqrt(1.0 - b2 ** step), eps, 0.0]
-    return torch.tensor(vals, dtype=torch.float32).to(device)
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("host AdamW scalars cannot be staged inside a graph capture")
+    return _ARGS_RING(vals, torch.device(device))
 
 
 def _merge_parts(parts, table: torch.Tensor, padding_idx):
