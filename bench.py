@@ -371,8 +371,10 @@ class PlainLoop:
     def __init__(self, model, loss_fn, lr: float = 1e-3, table_update: str = "optimizer"):
         self.model, self.loss_fn = model, loss_fn
         self.optimizer = torch.optim.AdamW(model.parameters(), lr=lr)
-        if table_update == "backward":
+        if table_update in ("backward", "backward_all"):
             tt.optim.fuse_table_update(self.optimizer, model)
+        if table_update == "backward_all":  # hip: {table_update: backward, dense_update: backward}
+            tt.optim.fuse_dense_update(self.optimizer, model)
 
     def __call__(self, q, p, n=None):
         ins = (q, p) if n is None else (q, p, n)
@@ -478,7 +480,7 @@ def plain_loop_entry(cfg, loss_fn, batches, dev, steps: int, trainstep_ms: float
     """PlainLoop timed on the bench's batches (fresh model, torch.optim.AdamW), as is and with the
     config opt-in hip: {table_update: backward}."""
     out = {}
-    for mode in ("optimizer", "backward"):
+    for mode in ("optimizer", "backward", "backward_all"):
         _, model = build_model(cfg, dev)
         loop = PlainLoop(model, loss_fn, table_update=mode)
         ms = time_steps(loop, batches, steps, 3)
@@ -492,7 +494,11 @@ def plain_loop_entry(cfg, loss_fn, batches, dev, steps: int, trainstep_ms: float
                       "cosine monitors + 3 .item() syncs per step",
               "table_update_backward": dict(out["backward"], config="hip: {table_update: backward} (the same loop; the "
                                             "table's fused scatter + AdamW at the end of loss.backward(), torch's "
-                                            "AdamW for the towers)")})
+                                            "AdamW for the towers)"),
+              "table_and_dense_update_backward": dict(
+                  out["backward_all"], config="hip: {table_update: backward, dense_update: backward} (the same loop; "
+                  "the towers' AdamW too as one multi-tensor launch at the end of loss.backward(), optimizer.step() "
+                  "then has nothing left)")})
     return e
 
 
@@ -525,8 +531,9 @@ def parse():
                          "tools/profile_round.sh sets it so every kernel in the trace belongs to a step")
     ap.add_argument("--zipf", type=float, default=None,
                     help="token ids ~ Zipf(s) over the vocabulary (text-like hot rows); default uniform")
-    ap.add_argument("--table-update", default="optimizer", choices=["optimizer", "backward"],
-                    help="--loop plain: the config opt-in hip: {table_update: backward} (fused table update in backward)")
+    ap.add_argument("--table-update", default="optimizer", choices=["optimizer", "backward", "backward_all"],
+                    help="--loop plain: the config opt-in hip: {table_update: backward} (fused table update in "
+                         "backward); backward_all adds hip: {dense_update: backward} (the towers' AdamW too)")
     ap.add_argument("--loop", default="trainstep", choices=["trainstep", "plain"],
                     help="plain: time the reference's loop body unchanged (bench.PlainLoop: eager, torch.optim.AdamW, "
                          "three .item() syncs) instead of TrainStep")

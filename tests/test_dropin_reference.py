@@ -163,8 +163,18 @@ def test_config_opts_in_to_backward_table_update(ref_pkg, tmp_path, install_befo
     w = model.query_tower.embedding.embedding.weight
     upd = w._tt_deferred.on_backward
     assert isinstance(upd, tt.optim.BackwardTableUpdate) and upd.optimizer is optimizer and upd.weight is w
+    assert getattr(optimizer, "_tt_dense_update", None) is None
+    cfg["hip"] = {"table_update": "backward", "dense_update": "backward"}
+    model, _, optimizer, _ = train.build_pipeline(cfg, device="cpu")
+    dense = optimizer._tt_dense_update
+    assert isinstance(dense, tt.optim.BackwardDenseUpdate) and dense.optimizer is optimizer
+    assert {id(p) for p in dense.params} == {id(p) for p in model.parameters()} - {
+        id(model.query_tower.embedding.embedding.weight)}
     cfg["hip"] = {"table_update": "sideways"}
     with pytest.raises(ValueError, match="table_update"):
+        train.build_pipeline(cfg, device="cpu")
+    cfg["hip"] = {"dense_update": "sideways"}
+    with pytest.raises(ValueError, match="dense_update"):
         train.build_pipeline(cfg, device="cpu")
 
 

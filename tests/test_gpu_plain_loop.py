@@ -41,7 +41,10 @@ def _loop_step(model, loss_fn, opt, q, p, n):
     return float(loss.item())
 
 
-def test_backward_table_update_trajectory_matches_reference(golden):
+@pytest.mark.parametrize("dense", [False, True])
+def test_backward_table_update_trajectory_matches_reference(golden, dense):
+    """dense: hip: {dense_update: backward} too (the towers' AdamW in one launch at the end of
+    backward; optimizer.step() then has nothing left)."""
     g = golden("trajectory")
     V, E = g["table"].shape
     H = g["W1"].shape[0]
@@ -55,6 +58,8 @@ def test_backward_table_update_trajectory_matches_reference(golden):
         t.feed_forward[2].bias.copy_(_cuda(g["b2"]))
     opt = torch.optim.AdamW(model.parameters(), lr=float(g["lr"]))  # train.py:359
     (upd,) = optim.fuse_table_update(opt, model)
+    if dense:
+        optim.fuse_dense_update(opt, model)
     loss_fn = tt.losses.build("triplet", margin=0.2)
     w = t.embedding.embedding.weight
     for s in range(3):
@@ -65,6 +70,11 @@ def test_backward_table_update_trajectory_matches_reference(golden):
         assert _rel(t.feed_forward[0].weight, g[f"step{s}_W1"]) < 1e-5
         assert _rel(t.feed_forward[2].bias, g[f"step{s}_b2"]) < 1e-5
     assert int(opt.state[w]["step"]) == 3 and opt.state[w]["step"].device.type == "cpu"
+    W1 = t.feed_forward[0].weight
+    assert int(opt.state[W1]["step"]) == 3 and opt.state[W1]["step"].device.type == "cpu"
+    if dense:
+        assert W1.grad is None  # stepped inside backward
+        opt._tt_dense_update.release()
     upd.release()
     assert not hasattr(w, "_tt_deferred")
 
@@ -75,8 +85,9 @@ def _model(V, E, seed):
     return tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV)
 
 
+@pytest.mark.parametrize("dense", [False, True])
 @pytest.mark.parametrize("E", [128, 256])
-def test_backward_table_update_equals_torch_adamw(E):
+def test_backward_table_update_equals_torch_adamw(E, dense):
     """Three loop steps at torch.optim.AdamW's defaults (lr 1e-3, wd 0.01, eps 1e-8): the fused
     table update against torch's AdamW stepping the dense table gradient of the same model (the
     planned scatter), every parameter elementwise to a few ulp + 1e-5 of lr per step; only elements
@@ -86,6 +97,8 @@ def test_backward_table_update_equals_torch_adamw(E):
     ropt = torch.optim.AdamW(ref.parameters())
     fopt = torch.optim.AdamW(fused.parameters())
     optim.fuse_table_update(fopt, fused)
+    if dense:
+        optim.fuse_dense_update(fopt, fused)
     loss_fn = tt.losses.build("triplet", margin=0.2)
     for s in range(3):
         if s:  # each step from the same state (the weights and moments the reference reached): an
@@ -113,7 +126,8 @@ def test_backward_table_update_equals_torch_adamw(E):
     assert int(fopt.state[wf]["step"]) == int(ropt.state[wr]["step"]) == 3
 
 
-def test_backward_table_update_checkpoint_round_trip(tmp_path):
+@pytest.mark.parametrize("dense", [False, True])
+def test_backward_table_update_checkpoint_round_trip(tmp_path, dense):
     """save_checkpoint after two steps, load into a fresh model + torch.optim.AdamW with the fused
     table update, and the third step equals the uninterrupted run's bit for bit (the table moments
     and step counter travel in the optimizer's state_dict under torch's keys)."""
@@ -123,6 +137,8 @@ def test_backward_table_update_checkpoint_round_trip(tmp_path):
     a = _model(V, E, 4)
     aopt = torch.optim.AdamW(a.parameters())
     optim.fuse_table_update(aopt, a)
+    if dense:
+        optim.fuse_dense_update(aopt, a)
     for s in range(2):
         _loop_step(a, loss_fn, aopt, *batches[s])
     path = checkpoint.save_checkpoint(a, {"<pad>": 0}, aopt, epoch=1, loss=0.5, checkpoint_dir=str(tmp_path),
@@ -133,6 +149,8 @@ def test_backward_table_update_checkpoint_round_trip(tmp_path):
     b = _model(V, E, 99)  # other weights: everything must come from the checkpoint
     bopt = torch.optim.AdamW(b.parameters())
     optim.fuse_table_update(bopt, b)
+    if dense:
+        optim.fuse_dense_update(bopt, b)
     ck = checkpoint.load_checkpoint(path, b, bopt, device=DEV)
     assert ck["epoch"] == 1
     wb = b.query_tower.embedding.embedding.weight

@@ -2,7 +2,7 @@
 
 Times the loop as is and with parts removed (monitors, optimizer step), and prints torch.profiler's
 per-op CPU / GPU totals over a few steps plus the GPU-busy fraction of the step (sum of kernel
-times / wall).  Usage: python tools/repro/plain_profile.py [steps]"""
+times / wall).  Usage: python tools/repro/plain_profile.py [steps] [optimizer|backward|backward_all]"""
 import os
 import sys
 import time
@@ -20,7 +20,8 @@ B, L, V, K = cfg["B"], cfg["L"], cfg["V"], cfg.get("K", 1)
 batches = [tt.data.synthetic_triplets(B, L, V, seed=100 + k, device=dev) for k in range(4)]
 loss_fn = tt.losses.build("in_batch", temperature=0.1, compute_dtype="bf16")
 _, model = bench.build_model(cfg, dev)
-loop = bench.PlainLoop(model, loss_fn, table_update="backward")
+mode = sys.argv[2] if len(sys.argv) > 2 else "backward"
+loop = bench.PlainLoop(model, loss_fn, table_update=mode)
 
 
 def no_monitor(q, p, n):
@@ -71,3 +72,18 @@ print(ka.table(sort_by="cpu_time_total", row_limit=30), flush=True)
 print(ka.table(sort_by="device_time_total", row_limit=25), flush=True)
 gpu_us = sum(e.self_device_time_total for e in ka if e.device_type is not None and str(e.device_type).endswith("CUDA"))
 print({"gpu_kernel_us_per_step": round(gpu_us / 3, 1)}, flush=True)
+
+# Python-side cost of issuing a step (no monitors: no host syncs), by function
+import cProfile  # noqa: E402
+import pstats  # noqa: E402
+
+torch.cuda.synchronize()
+pr = cProfile.Profile()
+pr.enable()
+for k in range(steps):
+    no_monitor(*batches[k % 4])
+pr.disable()
+torch.cuda.synchronize()
+st = pstats.Stats(pr)
+st.sort_stats("tottime").print_stats(45)
+st.sort_stats("cumulative").print_stats(45)

@@ -37,7 +37,9 @@ def install(package: str = "twotower") -> None:
     ``train.build_pipeline`` (train.py:298-371) is wrapped, now or when train is imported, so a
     config may opt in to the fused table update for the loop's own torch.optim.AdamW under a
     namespace the reference ignores: ``hip: {table_update: backward}`` (optim.fuse_table_update;
-    default / ``optimizer``: the dense table gradient stepped by the optimizer, as before).
+    default / ``optimizer``: the dense table gradient stepped by the optimizer, as before), and
+    ``hip: {dense_update: backward}`` for the tower parameters (optim.fuse_dense_update: one
+    multi-tensor AdamW launch at the end of backward instead of torch's foreach step).
     """
     emb = importlib.import_module(f"{package}.embeddings")
     enc = importlib.import_module(f"{package}.encoders")
@@ -68,11 +70,15 @@ def _patch_train(train_mod) -> None:
     def build_pipeline(config, device):
         hip = config.get("hip", {}) or {}
         mode = hip.get("table_update", "optimizer")
-        if mode not in TABLE_UPDATES:
-            raise ValueError(f"hip.table_update must be one of {TABLE_UPDATES}, got {mode!r}")
+        dense = hip.get("dense_update", "optimizer")
+        for key, val in (("table_update", mode), ("dense_update", dense)):
+            if val not in TABLE_UPDATES:
+                raise ValueError(f"hip.{key} must be one of {TABLE_UPDATES}, got {val!r}")
         model, dataset, optimizer, loss_fn = orig(config, device)
         if mode == "backward":
             optim.fuse_table_update(optimizer, model)
+        if dense == "backward":
+            optim.fuse_dense_update(optimizer, model)
         return model, dataset, optimizer, loss_fn
 
     build_pipeline._tt_wrapped = True

@@ -434,13 +434,15 @@ class BackwardTableUpdate:
                             f"(twotower_amd.optim.AdamW(fused_tables=True) fuses it itself); got {type(optimizer).__name__}")
         self.optimizer = optimizer
         self.weight = weight
-        self.group = next((g for g in optimizer.param_groups if any(p is weight for p in g["params"])), None)
-        if self.group is None:
-            raise ValueError("the table is not among the optimizer's parameters")
         self._check(self.group)
         if getattr(weight, "_tt_deferred", None) is not None:
             raise ValueError("the table's gradient is already owned by a fused optimizer")
         weight._tt_deferred = ops.DeferredTableGrad(padding_idx, on_backward=self)
+
+    @property
+    def group(self) -> dict:
+        """The table's param group, looked up each time (load_state_dict replaces the group dicts)."""
+        return _group_of(self.optimizer, self.weight)
 
     @staticmethod
     def _check(group: dict) -> None:
@@ -468,16 +470,101 @@ class BackwardTableUpdate:
         self._check(g)  # (a param group's options can be changed between steps)
         ids, dp, den, plan = _merge_parts(deferred.parts, w, deferred.padding_idx)
         deferred.parts.clear()
-        st = self.optimizer.state[w]
-        if not st:  # torch.optim.AdamW's _init_group layout (non-capturable: step a CPU float32 tensor)
-            st["step"] = torch.tensor(0.0, dtype=torch.float32)
-            st["exp_avg"] = torch.zeros_like(w, memory_format=torch.preserve_format)
-            st["exp_avg_sq"] = torch.zeros_like(w, memory_format=torch.preserve_format)
+        st = _torch_adamw_state(self.optimizer, w)  # torch.optim.AdamW's _init_group layout
         st["step"] += 1
         b1, b2 = g["betas"]
         lr = float(g["lr"])
         args = _host_adam_args(lr, b1, b2, g["eps"], g["weight_decay"], int(st["step"]), w.device)
         ops.bag_mean_backward_adamw_planned(dp, den, plan, w.data, st["exp_avg"], st["exp_avg_sq"], args)
+
+
+def _group_of(optimizer: torch.optim.Optimizer, p: torch.Tensor) -> dict:
+    g = next((g for g in optimizer.param_groups if any(q is p for q in g["params"])), None)
+    if g is None:
+        raise ValueError("the parameter is not among the optimizer's parameters")
+    return g
+
+
+def _torch_adamw_state(optimizer: torch.optim.Optimizer, p: torch.Tensor) -> dict:
+    """optimizer.state[p] in torch.optim.AdamW's non-capturable layout (step a CPU float32 tensor)."""
+    st = optimizer.state[p]
+    if not st:
+        st["step"] = torch.tensor(0.0, dtype=torch.float32)
+        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    return st
+
+
+class BackwardDenseUpdate:
+    """The companion of BackwardTableUpdate for the dense (tower) parameters of the same
+    ``torch.optim.AdamW`` (config ``hip: {dense_update: backward}``): once every parameter's
+    gradient of a ``loss.backward()`` has been accumulated, one multi-tensor AdamW launch
+    (tt_adamw_multi, 16 tensors per launch) steps them all with their groups' hyper-parameters and
+    the moments in ``optimizer.state[p]`` (torch's keys and layout), then drops their ``.grad``,
+    so ``optimizer.step()`` finds nothing left to do.  torch's foreach AdamW is ~10 launches over
+    the same bytes (108 us per C3 step on the GPU, profiles/r05i_plain_profile.txt, against a few
+    us here).  Same caveat as the table: one backward per optimizer step, and nothing may read the
+    parameters' ``.grad`` between ``backward()`` and ``step()`` (train.py:137-139 does neither)."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer, params):
+        if not isinstance(optimizer, torch.optim.AdamW) or isinstance(optimizer, AdamW):
+            raise TypeError(f"dense_update 'backward' drives a torch.optim.AdamW; got {type(optimizer).__name__}")
+        self.optimizer = optimizer
+        self.params = []
+        for p in params:
+            if not p.requires_grad or getattr(p, "_tt_deferred", None) is not None:
+                continue
+            BackwardTableUpdate._check(_group_of(optimizer, p))
+            self.params.append(p)
+        self._ids = {id(p) for p in self.params}
+        self._queued = False
+        self._handles = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def _on_grad(self, _p) -> None:
+        if not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._run)
+
+    @torch.no_grad()
+    def _run(self) -> None:
+        self._queued = False
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dense_update 'backward' runs eagerly (host step counter)")
+        items, done, args_for = [], [], {}
+        for g in self.optimizer.param_groups:
+            BackwardTableUpdate._check(g)
+            b1, b2 = g["betas"]
+            for p in g["params"]:
+                if id(p) not in self._ids or p.grad is None:
+                    continue
+                if p.grad.is_sparse or p.dtype != torch.float32:
+                    raise RuntimeError("dense_update 'backward' steps dense float32 parameters")
+                st = _torch_adamw_state(self.optimizer, p)
+                st["step"] += 1
+                key = (id(g), int(st["step"]))
+                if key not in args_for:
+                    args_for[key] = _host_adam_args(float(g["lr"]), b1, b2, g["eps"], g["weight_decay"], key[1],
+                                                    p.device)
+                items.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], args_for[key]))
+                done.append(p)
+        ops.adamw_multi(items)
+        for p in done:
+            p.grad = None
+
+    def release(self) -> None:
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+
+def fuse_dense_update(optimizer: torch.optim.Optimizer, model: torch.nn.Module) -> BackwardDenseUpdate:
+    """Attach a BackwardDenseUpdate to every dense parameter of ``model`` the loop's own
+    torch.optim.AdamW steps (the tables are fuse_table_update's).  The opt-in behind
+    ``hip: {dense_update: backward}`` (twotower_amd.install)."""
+    if getattr(optimizer, "_tt_dense_update", None) is not None:
+        raise ValueError("the optimizer's dense parameters already have a backward update")
+    upd = optimizer._tt_dense_update = BackwardDenseUpdate(optimizer, [p for p in model.parameters()])
+    return upd
 
 
 def fuse_table_update(optimizer: torch.optim.Optimizer, model_or_tables) -> list[BackwardTableUpdate]:
