@@ -46,9 +46,11 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_kernel(
   }
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
-  const int64_t seq = (int64_t)(blockIdx.x - split_blocks) * kWavesPerBlock + (threadIdx.x >> 6);
-  if (seq >= nseq) return;  // wave-uniform
   const int sub = lane / LPR, c = lane % LPR;
+  // a capped grid (TT_GATHER_GRID) walks the sequences; the default grid has one wave per sequence
+  const int64_t nwaves = (int64_t)(gridDim.x - split_blocks) * kWavesPerBlock;
+  for (int64_t seq = (int64_t)(blockIdx.x - split_blocks) * kWavesPerBlock + (threadIdx.x >> 6); seq < nseq;
+       seq += nwaves) {
   const IdT* rid = ids + seq * ld;
 
   f32x4 acc[NV];
@@ -116,6 +118,7 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_kernel(
     for (int k = 0; k < NV; ++k) out[k * LPR + c] = acc[k] / den;
   }
   if (lane == 0) denom[seq] = den;
+  }
 }
 
 // Column slab forward (table_sync "column"): pooled columns of a (V, El) slab summed in the
@@ -354,21 +357,24 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
                                                                        int32_t* __restrict__ cnt) {
   __shared__ int32_t h[1 << kSortMaxD];
   const int nd = 1 << D;
-  for (int d = threadIdx.x; d < nd; d += kSortThreads) h[d] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // (a capped grid walks tiles)
+    for (int d = threadIdx.x; d < nd; d += kSortThreads) h[d] = 0;
+    __syncthreads();
+    const int64_t base = tile * kSortTile;
 #pragma unroll
-  for (int k = 0; k < kSortIPT; ++k) {
-    const int64_t i = base + k * kSortThreads + threadIdx.x;
-    if (i < n) {
-      uint32_t key;
-      int32_t val;
-      src.load(i, key, val);
-      atomicAdd(&h[(key >> shift) & (nd - 1)], 1);
+    for (int k = 0; k < kSortIPT; ++k) {
+      const int64_t i = base + k * kSortThreads + threadIdx.x;
+      if (i < n) {
+        uint32_t key;
+        int32_t val;
+        src.load(i, key, val);
+        atomicAdd(&h[(key >> shift) & (nd - 1)], 1);
+      }
     }
+    __syncthreads();
+    for (int d = threadIdx.x; d < nd; d += kSortThreads) cnt[(int64_t)d * ntiles + tile] = h[d];
+    __syncthreads();
   }
-  __syncthreads();
-  for (int d = threadIdx.x; d < nd; d += kSortThreads) cnt[(int64_t)d * ntiles + blockIdx.x] = h[d];
 }
 
 // One WAVE per digit: cnt[d][0..ntiles) -> its exclusive scan, total[d] = the row sum.  Every
@@ -426,92 +432,95 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
   __shared__ int32_t sv[kSortTile];       // writes of a digit's run are consecutive lanes)
   __shared__ int32_t wsum[kSortWaves];
   const int w = threadIdx.x >> 6, lane = lane_id();
-  for (int d = threadIdx.x; d < kSortWaves * ND; d += kSortThreads) (&hw[0][0])[d] = 0;
-  __syncthreads();
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // (a capped grid walks tiles)
+    for (int d = threadIdx.x; d < kSortWaves * ND; d += kSortThreads) (&hw[0][0])[d] = 0;
+    __syncthreads();
 
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-  const int64_t wbase = base + (int64_t)w * (kWave * kSortIPT);
-  const int tile_n = (int)(n - base < kSortTile ? n - base : kSortTile);
-  const uint64_t lt = (uint64_t(1) << lane) - 1;
-  uint32_t key[kSortIPT];
-  int32_t val[kSortIPT], rk[kSortIPT];
-#pragma unroll
-  for (int k = 0; k < kSortIPT; ++k) {
-    const int64_t i = wbase + k * kWave + lane;
-    key[k] = 0;
-    val[k] = 0;
-    if (i < n) src.load(i, key[k], val[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < kSortIPT; ++k) {
-    const bool ok = wbase + k * kWave + lane < n;
-    const int d = (int)((key[k] >> shift) & (ND - 1));
-    uint64_t peers = __ballot(ok);
-#pragma unroll
-    for (int b = 0; b < D; ++b) {
-      const bool bit = (d >> b) & 1;
-      const uint64_t bal = __ballot(bit);
-      peers &= bit ? bal : ~bal;
+    const int64_t base = (int64_t)tile * kSortTile;
+    const int64_t wbase = base + (int64_t)w * (kWave * kSortIPT);
+    const int tile_n = (int)(n - base < kSortTile ? n - base : kSortTile);
+    const uint64_t lt = (uint64_t(1) << lane) - 1;
+    uint32_t key[kSortIPT];
+    int32_t val[kSortIPT], rk[kSortIPT];
+  #pragma unroll
+    for (int k = 0; k < kSortIPT; ++k) {
+      const int64_t i = wbase + k * kWave + lane;
+      key[k] = 0;
+      val[k] = 0;
+      if (i < n) src.load(i, key[k], val[k]);
     }
-    const int below = __popcll(peers & lt);
-    const int32_t prior = ok ? hw[w][d] : 0;
-    rk[k] = prior + below;
-    if (ok && below == 0) hw[w][d] = prior + __popcll(peers);  // the lowest peer lane writes
-  }
-  __syncthreads();
-  // per digit: the waves' offsets inside the tile's run, the run's length, its global start
-  // (exclusive scan of the digit totals + this tile's row offset) and its tile-sorted start
-  int32_t tv[DPT], tl[DPT], part = 0, tpart = 0;
-#pragma unroll
-  for (int j = 0; j < DPT; ++j) {
-    const int d = threadIdx.x * DPT + j;
-    tv[j] = d < ND ? total[d] : 0;
-    tl[j] = 0;
-    if (d < ND) {
-#pragma unroll
-      for (int v = 0; v < kSortWaves; ++v) {
-        const int32_t c = hw[v][d];
-        hw[v][d] = tl[j];
-        tl[j] += c;
+  #pragma unroll
+    for (int k = 0; k < kSortIPT; ++k) {
+      const bool ok = wbase + k * kWave + lane < n;
+      const int d = (int)((key[k] >> shift) & (ND - 1));
+      uint64_t peers = __ballot(ok);
+  #pragma unroll
+      for (int b = 0; b < D; ++b) {
+        const bool bit = (d >> b) & 1;
+        const uint64_t bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+      }
+      const int below = __popcll(peers & lt);
+      const int32_t prior = ok ? hw[w][d] : 0;
+      rk[k] = prior + below;
+      if (ok && below == 0) hw[w][d] = prior + __popcll(peers);  // the lowest peer lane writes
+    }
+    __syncthreads();
+    // per digit: the waves' offsets inside the tile's run, the run's length, its global start
+    // (exclusive scan of the digit totals + this tile's row offset) and its tile-sorted start
+    int32_t tv[DPT], tl[DPT], part = 0, tpart = 0;
+  #pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const int d = threadIdx.x * DPT + j;
+      tv[j] = d < ND ? total[d] : 0;
+      tl[j] = 0;
+      if (d < ND) {
+  #pragma unroll
+        for (int v = 0; v < kSortWaves; ++v) {
+          const int32_t c = hw[v][d];
+          hw[v][d] = tl[j];
+          tl[j] += c;
+        }
+      }
+      part += tv[j];
+      tpart += tl[j];
+    }
+    int32_t run = sort_block_excl_scan(part, wsum, nullptr);
+    int32_t trun = sort_block_excl_scan(tpart, wsum, nullptr);
+  #pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const int d = threadIdx.x * DPT + j;
+      if (d < ND) {
+        gdst[d] = run + cnt[(int64_t)d * ntiles + tile];
+        tst[d] = trun;
+      }
+      run += tv[j];
+      trun += tl[j];
+    }
+    __syncthreads();
+  #pragma unroll
+    for (int k = 0; k < kSortIPT; ++k) {
+      if (wbase + k * kWave + lane < n) {
+        const int d = (int)((key[k] >> shift) & (ND - 1));
+        const int lp = tst[d] + hw[w][d] + rk[k];
+        sk[lp] = key[k];
+        sv[lp] = val[k];
       }
     }
-    part += tv[j];
-    tpart += tl[j];
-  }
-  int32_t run = sort_block_excl_scan(part, wsum, nullptr);
-  int32_t trun = sort_block_excl_scan(tpart, wsum, nullptr);
-#pragma unroll
-  for (int j = 0; j < DPT; ++j) {
-    const int d = threadIdx.x * DPT + j;
-    if (d < ND) {
-      gdst[d] = run + cnt[(int64_t)d * ntiles + blockIdx.x];
-      tst[d] = trun;
+    __syncthreads();
+    // the tile in sorted order: consecutive lanes write consecutive positions of each digit's run
+  #pragma unroll
+    for (int k = 0; k < kSortIPT; ++k) {
+      const int s = k * kSortThreads + threadIdx.x;
+      if (s < tile_n) {
+        const uint32_t kk = sk[s];
+        const int d = (int)((kk >> shift) & (ND - 1));
+        const int64_t pos = (int64_t)gdst[d] + (s - tst[d]);
+        keys_out[pos] = kk;
+        vals_out[pos] = sv[s];
+      }
     }
-    run += tv[j];
-    trun += tl[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kSortIPT; ++k) {
-    if (wbase + k * kWave + lane < n) {
-      const int d = (int)((key[k] >> shift) & (ND - 1));
-      const int lp = tst[d] + hw[w][d] + rk[k];
-      sk[lp] = key[k];
-      sv[lp] = val[k];
-    }
-  }
-  __syncthreads();
-  // the tile in sorted order: consecutive lanes write consecutive positions of each digit's run
-#pragma unroll
-  for (int k = 0; k < kSortIPT; ++k) {
-    const int s = k * kSortThreads + threadIdx.x;
-    if (s < tile_n) {
-      const uint32_t kk = sk[s];
-      const int d = (int)((kk >> shift) & (ND - 1));
-      const int64_t pos = (int64_t)gdst[d] + (s - tst[d]);
-      keys_out[pos] = kk;
-      vals_out[pos] = sv[s];
-    }
+    __syncthreads();  // the tile's LDS reads done before the next tile's writes
   }
 }
 
@@ -1068,7 +1077,13 @@ int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nse
     for (int j = 0; j < 4; ++j) big = std::max<int64_t>(big, (int64_t)sj.n[j] * sj.k[j]);
     nsplit = (int)((big + kBlock - 1) / kBlock);
   }
-  const dim3 grid((unsigned)(nsplit + (nseq + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+  static const int64_t gather_grid = [] {
+    const char* e = getenv("TT_GATHER_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  int64_t gblocks = (nseq + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (gather_grid > 0 && gather_grid < gblocks) gblocks = gather_grid;
+  const dim3 grid((unsigned)(nsplit + gblocks)), block(kBlock);
 #define TT_FWD(LPR, NV, U) \
   bag_fwd_kernel<IdT, LPR, NV, U><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom, sj, planes, nsplit)
   switch (E) {
@@ -1167,6 +1182,13 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   // (keys_in, vals_in) otherwise, so the last pass lands in the _out arrays
   const SortShape sh = sort_shape(n, V);
   const int nd = 1 << sh.D;
+  // TT_PLAN_GRID > 0: count / scatter launch at most that many workgroups, each walking tiles
+  // (fewer slots held beside the gather and the first head GEMM); 0: one workgroup per tile
+  static const int64_t plan_grid = [] {
+    const char* e = getenv("TT_PLAN_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  const unsigned sgrid = (unsigned)(plan_grid > 0 && plan_grid < sh.ntiles ? plan_grid : sh.ntiles);
   int32_t* cnt = static_cast<int32_t*>(w.sort_tmp);
   int32_t* total = cnt + (size_t)nd * sh.ntiles;
   SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr, L > 0 ? 1.0 / (double)L : 0.0};
@@ -1175,7 +1197,7 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     uint32_t* ko = to_out ? w.keys_out : w.keys_in;
     int32_t* vo = to_out ? w.vals_out : w.vals_in;
     const int shift = p * sh.D;
-    plan_sort_count_kernel<IdT><<<dim3((unsigned)sh.ntiles), dim3(kSortThreads), 0, s>>>(src, n, shift, sh.D,
+    plan_sort_count_kernel<IdT><<<dim3(sgrid), dim3(kSortThreads), 0, s>>>(src, n, shift, sh.D,
                                                                                        sh.ntiles, cnt);
     TT_LAUNCH_CHECK("plan_sort_count");
     plan_sort_scan_kernel<<<dim3((unsigned)((nd + kScanWaves - 1) / kScanWaves)), dim3(kScanWaves * kWave), 0, s>>>(
@@ -1184,7 +1206,7 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     switch (sh.D) {
 #define TT_SC(DD)                                                                                         \
   case DD:                                                                                                \
-    plan_sort_scatter_kernel<IdT, DD><<<dim3((unsigned)sh.ntiles), dim3(kSortThreads), 0, s>>>(src, n, shift, \
+    plan_sort_scatter_kernel<IdT, DD><<<dim3(sgrid), dim3(kSortThreads), 0, s>>>(src, n, shift,            \
                                                                                              sh.ntiles, cnt, \
                                                                                              total, ko, vo);  \
     break;
