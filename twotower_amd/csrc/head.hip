@@ -117,11 +117,18 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
 #else
   constexpr int kAStep = 4, kAHalf = 1;
 #endif
-  f32x4 areg[kSteps][2];
+  // A chunks in flight: the whole next tile (kAR = kSteps: 128 VGPRs at K = 256, one wave per SIMD
+  // with the rest), or TT_HEAD_AHALF: half a tile ahead (kAR = kSteps / 2, ~64 VGPRs less, so the
+  // kernel fits 256 registers and other kernels' waves can share its SIMDs)
+#ifndef TT_HEAD_AHALF
+#define TT_HEAD_AHALF 1
+#endif
+  constexpr int kAR = TT_HEAD_AHALF && kSteps >= 4 ? kSteps / 2 : kSteps;
+  f32x4 areg[kAR][2];
   {
     const f32x4* src = a_src(0);
 #pragma unroll
-    for (int j = 0; j < kSteps; ++j) {
+    for (int j = 0; j < kAR; ++j) {
       areg[j][0] = *(src + j * kAStep);
       areg[j][1] = *(src + j * kAStep + kAHalf);
     }
@@ -204,7 +211,8 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     if (__builtin_amdgcn_readfirstlane((int)(trow0 >= rows))) break;
     const bool more = t + 1 < tiles && trow0 + kWaves * kTileRows < rows;
     // unconditional refills keep each step one basic block; the last tile re-reads itself (L2)
-    const f32x4* nsrc = more ? a_src(t + 1) : a_src(t);
+    const f32x4* csrc = a_src(t);
+    const f32x4* nsrc = more ? a_src(t + 1) : csrc;
     f32x16 acc[2] = {f32x16{}, f32x16{}};
     const int64_t mask_idx = ((trow0 / kTileRows) * kSlices + c) * 64 + lane;
     unsigned mword = 0;
@@ -228,15 +236,20 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int p = 0; p < 3; ++p) nb[ct][p] = rdb(ct, p, jn);
-      // areg[j] was split during the previous step: refill it with the next tile
+      // chunk j (slot j % kAR) was split during the previous step: refill the slot with chunk j + kAR
+      // of the stream (this tile's, or the next tile's once past the end)
+      {
+        const int c = j + kAR;  // (j is a compile-time constant after unrolling: so is the branch)
+        const f32x4* rs = c < kSteps ? csrc + c * kAStep : nsrc + (c - kSteps) * kAStep;
 #ifndef TT_HABL_NOALOAD
-      areg[j][0] = *(nsrc + j * kAStep);
-      areg[j][1] = *(nsrc + j * kAStep + kAHalf);
+        areg[j % kAR][0] = *rs;
+        areg[j % kAR][1] = *(rs + kAHalf);
 #else
-      asm volatile("" : "+v"(areg[j][0]), "+v"(areg[j][1]));
+        asm volatile("" : "+v"(areg[j % kAR][0]), "+v"(areg[j % kAR][1]));
 #endif
+      }
 #ifdef TT_HABL_NOSPLIT
-      split_all(areg[jn], na);
+      split_all(areg[jn % kAR], na);
 #endif
       __builtin_amdgcn_sched_barrier(0);
       const bf16x8 a0 = __builtin_bit_cast(bf16x8, ca[0]), a1 = __builtin_bit_cast(bf16x8, ca[1]),
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         }
 #endif
 #ifndef TT_HABL_NOSPLIT
-        split_piece(areg[jn], m, st, na);
+        split_piece(areg[jn % kAR], m, st, na);
 #endif
         __builtin_amdgcn_sched_barrier(0);
       }
