@@ -123,7 +123,10 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
 #ifndef TT_HEAD_AHALF
 #define TT_HEAD_AHALF 1
 #endif
-  constexpr int kAR = TT_HEAD_AHALF && kSteps >= 4 ? kSteps / 2 : kSteps;
+#ifndef TT_HEAD_ADIV
+#define TT_HEAD_ADIV 4  // with TT_HEAD_AHALF: 1 / TT_HEAD_ADIV of a tile ahead
+#endif
+  constexpr int kAR = TT_HEAD_AHALF && kSteps >= 2 * TT_HEAD_ADIV ? kSteps / TT_HEAD_ADIV : kSteps;
   f32x4 areg[kAR][2];
   {
     const f32x4* src = a_src(0);
