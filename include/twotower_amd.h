@@ -115,6 +115,12 @@ int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom, int64_t n
  * seg_start[r + 1]), r = V the masked tail).  The sort is the stable sort of the (row, seq) pairs
  * by row, so these are fixed by the ids: what the parity tests compare with a CPU stable sort. */
 int tt_bag_plan_layout(int64_t nseq, int L, int64_t V, int E, int64_t* offs);
+/* tt_bag_plan in two halves on one stream (same plan, same bytes): part 0 runs every sort pass
+ * but the last, part 1 the last pass, the segment starts and the pieces, so a caller can place the
+ * second half later in its step (the same ids and plan buffer in both calls). */
+int tt_bag_plan_part(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids,
+                     int64_t V, int E, int64_t padding_idx, void* plan, size_t plan_bytes, int part,
+                     tt_stream_t stream);
 int tt_bag_mean_bwd_adamw_planned(const float* d_pooled, const float* denom, int64_t nseq, int L,
                                   int64_t V, int E, const void* plan, size_t plan_bytes,
                                   float* table, float* exp_avg, float* exp_avg_sq,

@@ -717,14 +717,17 @@ def test_plan_sort_equals_stable_sort(case):
         V, pad = 3001, 7
         ids = edge_ids(300, 40, 3001, rng, torch.int32)
         ids[5:50, 3] = 7
-    plan = ops.BagPlan(ids, V, 64, pad)
-    plan.wait()
-    n = ids.numel()
-    keys, seqs, starts = _plan_out(plan, n)
     wk, ws, wst = O.bag_plan(ids.cpu().numpy(), V, pad)
-    assert np.array_equal(keys, wk)
-    assert np.array_equal(seqs, ws)
-    assert np.array_equal(starts, wst)
+    n = ids.numel()
+    for split in (False, True):  # split: tt_bag_plan_part 0, then 1 (queued by flush_plans / wait)
+        plan = ops.BagPlan(ids, V, 64, pad, split=split)
+        if split:
+            ops.flush_plans()
+        plan.wait()
+        keys, seqs, starts = _plan_out(plan, n)
+        assert np.array_equal(keys, wk), split
+        assert np.array_equal(seqs, ws), split
+        assert np.array_equal(starts, wst), split
 
 
 @pytest.mark.parametrize("E,denom", [(256, True), (64, True), (48, False), (256, False)])

@@ -63,6 +63,8 @@ _SIGNATURES = {
                                        _vp, _vp, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _c_i64, _vp, _c_sz, _vp]),
     "tt_bag_plan_ws_size": (_c_sz, [_c_i64, _c_int, _c_i64, _c_int]),
     "tt_bag_plan": (_c_int, [_vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp, _c_sz, _vp]),
+    "tt_bag_plan_part": (_c_int, [_vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _c_i64, _vp, _c_sz, _c_int,
+                                  _vp]),
     "tt_bag_plan_layout": (_c_int, [_c_i64, _c_int, _c_i64, _c_int, _vp]),
     "tt_bag_mean_bwd_planned": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _vp, _vp]),
     "tt_bag_mean_bwd_planned_prepare": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _c_int, _vp, _c_sz, _vp]),

@@ -1169,9 +1169,12 @@ int launch_piece_sum(const BwdWs& w, int64_t V, int E, hipStream_t s) {
 // pieces of long rows (bag_plan_starts_kernel, bag_plan_pieces_kernel).
 template <typename IdT>
 int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64_t padding_idx, const BwdWs& w,
-               hipStream_t s) {
+               hipStream_t s, int part = -1) {
+  // part -1: the whole plan; 0: every sort pass but the last; 1: the last pass, the segment starts
+  // and the pieces (tt_bag_plan_part: the two halves on one stream compute what one call does)
   const int64_t n = nseq * L;
   const dim3 block(kBlock);
+  if (part == 0 && n == 0) return TT_OK;
   if (n == 0) {  // no tokens: every segment empty, no pieces
     TT_HIP(hipMemsetAsync(w.seg_start, 0, (size_t)(V + 1) * 4, s), "memset seg_start");
     TT_HIP(hipMemsetAsync(w.nch, 0, (size_t)(V + 1) * 4, s), "memset nch");
@@ -1192,7 +1195,13 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   int32_t* cnt = static_cast<int32_t*>(w.sort_tmp);
   int32_t* total = cnt + (size_t)nd * sh.ntiles;
   SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr, L > 0 ? 1.0 / (double)L : 0.0};
-  for (int p = 0; p < sh.P; ++p) {
+  const int p_begin = part == 1 ? sh.P - 1 : 0, p_end = part == 0 ? sh.P - 1 : sh.P;
+  if (p_begin > 0) {  // the previous pass's output (pass p writes _out when P - 1 - p is even)
+    const bool prev_out = ((sh.P - 1 - (p_begin - 1)) & 1) == 0;
+    src.keys = prev_out ? w.keys_out : w.keys_in;
+    src.vals = prev_out ? w.vals_out : w.vals_in;
+  }
+  for (int p = p_begin; p < p_end; ++p) {
     const bool to_out = ((sh.P - 1 - p) & 1) == 0;
     uint32_t* ko = to_out ? w.keys_out : w.keys_in;
     int32_t* vo = to_out ? w.vals_out : w.vals_in;
@@ -1218,6 +1227,7 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
     src.keys = ko;
     src.vals = vo;
   }
+  if (part == 0) return TT_OK;
   const int64_t nst = (n + 1 + kStartsPT - 1) / kStartsPT;
   bag_plan_starts_kernel<<<dim3((unsigned)((nst + kBlock - 1) / kBlock)), block, 0, s>>>(w.keys_out, n, V, w.seg_start,
                                                                                        w.piece_off + V);
@@ -1331,14 +1341,14 @@ static BwdWs plan_layout(void* ws, int64_t nseq, int L, int64_t V, int E) {
 }
 
 static int plan_impl(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld, int64_t V, int E,
-                     int64_t padding_idx, void* ws, size_t ws_bytes, hipStream_t s) {
+                     int64_t padding_idx, void* ws, size_t ws_bytes, hipStream_t s, int part = -1) {
   const BwdWs w = plan_layout(ws, nseq, L, V, E);
   TT_REQUIRE(ws != nullptr && w.total + 256 <= ws_bytes, "workspace too small: need %zu have %zu",
              w.total + 256, ws_bytes);
-  if (nseq == 0 || L == 0) return plan_front<int32_t>(nullptr, 0, 0, 0, V, padding_idx, w, s);
+  if (nseq == 0 || L == 0) return plan_front<int32_t>(nullptr, 0, 0, 0, V, padding_idx, w, s, part);
   return ids_dtype == TT_IDS_I32
-             ? plan_front(static_cast<const int32_t*>(ids), nseq, L, ld, V, padding_idx, w, s)
-             : plan_front(static_cast<const int64_t*>(ids), nseq, L, ld, V, padding_idx, w, s);
+             ? plan_front(static_cast<const int32_t*>(ids), nseq, L, ld, V, padding_idx, w, s, part)
+             : plan_front(static_cast<const int64_t*>(ids), nseq, L, ld, V, padding_idx, w, s, part);
 }
 
 template <bool FUSED>
@@ -1362,6 +1372,16 @@ extern "C" int tt_bag_plan(const void* ids, int ids_dtype, int64_t nseq, int L, 
   if (rc) return rc;
   return plan_impl(ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, plan, plan_bytes,
                    reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int tt_bag_plan_part(const void* ids, int ids_dtype, int64_t nseq, int L, int64_t ld_ids, int64_t V,
+                                int E, int64_t padding_idx, void* plan, size_t plan_bytes, int part,
+                                tt_stream_t stream) {
+  int rc = check_common(V, E, ids, ids_dtype, nseq, L, ld_ids);
+  if (rc) return rc;
+  TT_REQUIRE(part == 0 || part == 1, "tt_bag_plan_part: part 0 or 1 (got %d)", part);
+  return plan_impl(ids, ids_dtype, nseq, L, ld_ids, V, E, padding_idx, plan, plan_bytes,
+                   reinterpret_cast<hipStream_t>(stream), part);
 }
 
 extern "C" int tt_bag_plan_layout(int64_t nseq, int L, int64_t V, int E, int64_t* offs) {

@@ -126,18 +126,22 @@ class BagPlan:
     as the forward has its ids, so its radix sort runs beside the towers and the scorer.  The
     backward (or the fused optimizer) waits on ``ready`` before using it."""
 
-    __slots__ = ("ids", "buf", "ready", "nseq", "L", "V", "E")
+    __slots__ = ("ids", "buf", "ready", "nseq", "L", "V", "E", "pad")
 
-    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None, gather_group=None):
+    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None, gather_group=None,
+                 split: bool = False):
         """gather_group: data parallel with a replicated table update -- the plan covers the ids
-        of every rank (all-gathered here, on the side stream, rank-major)."""
+        of every rank (all-gathered here, on the side stream, rank-major).  split: only the first
+        half of the sort here (tt_bag_plan_part 0); the second half is queued by finish() (the next
+        loss forward calls flush_plans(), or wait() does), so it runs beside the loss instead of
+        beside the head and the scorer's operand prep."""
         dev = ids.device
         self.V, self.E = V, E
         main = torch.cuda.current_stream(dev)
         side = _lib.side_stream(dev)
         side.wait_stream(main)
         ids.record_stream(side)  # allocated on the current stream, read on the side stream
-        pad = -1 if padding_idx is None else int(padding_idx)
+        self.pad = -1 if padding_idx is None else int(padding_idx)
         with torch.cuda.stream(side):
             if gather_group is not None:
                 from .distributed import all_gather_rows
@@ -150,15 +154,55 @@ class BagPlan:
             self.nseq, self.L = ids.shape
             nbytes = _lib.lib().tt_bag_plan_ws_size(self.nseq, self.L, V, E)
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, pad,
-                 ptr(self.buf), self.buf.numel(), side.cuda_stream)
+            if split:
+                call("tt_bag_plan_part", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E,
+                     self.pad, ptr(self.buf), self.buf.numel(), 0, side.cuda_stream)
+            else:
+                call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, self.pad,
+                     ptr(self.buf), self.buf.numel(), side.cuda_stream)
+        self.ready = None
+        if split:
+            flush_plans()  # (at most one plan waits for its second half)
+            _PENDING_PLANS.append(self)
+        else:
+            self.ready = torch.cuda.Event()
+            self.ready.record(side)
+
+    def finish(self) -> None:
+        """Queue the second half of a split plan on the side stream, behind the current stream's
+        work so far (idempotent)."""
+        if self.ready is not None:
+            return
+        dev = self.buf.device
+        side = _lib.side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        call("tt_bag_plan_part", ptr(self.ids), _lib.ids_dtype_code(self.ids), self.nseq, self.L, self.L, self.V,
+             self.E, self.pad, ptr(self.buf), self.buf.numel(), 1, side.cuda_stream)
         self.ready = torch.cuda.Event()
         self.ready.record(side)
+        if self in _PENDING_PLANS:
+            _PENDING_PLANS.remove(self)
 
     def wait(self) -> None:
+        self.finish()
         cur = torch.cuda.current_stream(self.buf.device)
         cur.wait_event(self.ready)
         self.buf.record_stream(cur)  # allocated on the side stream, read here
+
+
+_PENDING_PLANS: list = []  # split plans whose second half is not queued yet
+
+
+def flush_plans() -> None:
+    """Queue the second half of every split plan (called by the loss forwards: the sort's last
+    pass then runs beside the loss, not beside the head and the scorer's operand prep)."""
+    while _PENDING_PLANS:
+        _PENDING_PLANS[0].finish()
+
+
+def plan_split() -> bool:
+    """TT_PLAN_SPLIT=1: split plans (BagPlan split=True) for the tower bag's sort."""
+    return os.environ.get("TT_PLAN_SPLIT", "0") == "1"
 
 
 class _BagGradToken:
@@ -273,7 +317,8 @@ class BagMeanPool(torch.autograd.Function):
         if early:
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
-            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
+            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group,
+                               split=plan_split())
         pooled, denom = bag_mean_forward(weight, ids)
         if plan_now and not early:
             # forked after the gather: the sort runs beside the towers and the scorer (forked
@@ -943,6 +988,7 @@ def _triplet_bwd(q, p, n, margin, g, dq, dp, dn):
 class TripletLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, p, n, margin):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(q, p, n)
         q, p, n = (_contig_f32(t, nm) for t, nm in ((q, "q"), (p, "p"), (n, "n")))
         ctx.save_for_backward(q, p, n)
@@ -963,6 +1009,7 @@ class TripletLossPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qpn, margin):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(qpn)
         qpn = _contig_f32(qpn, "qpn")
         q, p, n = torch.chunk(qpn, 3)
@@ -983,6 +1030,7 @@ class TripletLossPacked(torch.autograd.Function):
 class MultiNegLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, p, negs, inv_tau):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(q, p, negs)
         q, p, negs = _contig_f32(q, "q"), _contig_f32(p, "p"), _contig_f32(negs, "negs")
         B, H = q.shape
@@ -1014,6 +1062,7 @@ class MultiNegLossPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qpn, B, K, inv_tau):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(qpn)
         qpn = _contig_f32(qpn, "qpn")
         H = qpn.shape[1]
@@ -1095,6 +1144,7 @@ def _inbatch_bwd(meta, q, d, lse, dqu, ws, g, dq, dd, mean=None):
 class InBatchSoftmaxLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(q, d)
         q, d = _contig_f32(q, "q"), _contig_f32(d, "d")
         want_grad = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
@@ -1117,6 +1167,7 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qd, nq, inv_tau, compute_dtype, grad_scale):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(qd)
         prep = qd.__dict__.pop("_tt_inbatch_prep", None)  # taken once (TowerHead under scorer_prep)
         qd = _contig_f32(qd, "qd")
@@ -1223,6 +1274,7 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q, d, inv_tau, compute_dtype, grad_scale, group):
+        flush_plans()  # a split sort plan's second half runs beside the loss
         from .distributed import all_gather_rows
 
         require_gpu(q, d)
