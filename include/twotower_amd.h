@@ -277,6 +277,12 @@ int tt_multi_neg_fwd(const float* q, const float* p, const float* negs, int64_t 
 int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t B, int N, int H,
                      float inv_tau, const float* grad_loss, float* dq, float* dp, float* dnegs,
                      tt_stream_t stream);
+/* tt_multi_neg_bwd fused with the tower head's F.normalize backward (encoders.py:77), H = 256,
+ * N <= 15: qpn is the head's output [q; p; negs] ((2 + N) B x 256, the normalised rows), norms its
+ * row norms in the same order; dx (same shape) receives the gradient before F.normalize, equal bit
+ * for bit to tt_multi_neg_bwd followed by tt_l2norm_bwd on those rows. */
+int tt_multi_neg_bwd_l2(const float* qpn, int64_t B, int N, const float* norms, float inv_tau,
+                        const float* grad_loss, float* dx, tt_stream_t stream);
 
 /* ---- in-batch sampled softmax (in_batch_sampled_softmax_loss, twotower/losses.py:88-118)
  * S = q d^T (B x M, never materialised), logits = S * inv_tau, label of row i is column

@@ -236,6 +236,52 @@ def test_inbatch_combine_fused_with_head_l2_backward_is_bit_identical(graph, dty
         assert torch.equal(got[k], want[k]), k
 
 
+@pytest.mark.parametrize("graph", [False, True])
+@pytest.mark.parametrize("K", [1, 4, 7])
+def test_multi_neg_fused_with_head_l2_backward_is_bit_identical(graph, K, monkeypatch):
+    """TrainStep runs the multiple-negatives loss backward fused with the tower head's F.normalize
+    backward (tt_multi_neg_bwd_l2, H = 256: the loss writes the gradient before F.normalize, the
+    head skips tt_l2norm_bwd); parameters and losses after four steps equal the two launches
+    (TT_FUSED_L2_BWD=0) bit for bit, for 1, 4 and 7 negatives per query (C5: 4)."""
+    V, B, L, d = 4000, 160, 20, 256
+    rng = np.random.default_rng(11 + K)
+    batches = [[_ids(B, L, V, rng), _ids(B, L, V, rng), _ids(B * K, L, V, rng)] for _ in range(4)]
+
+    def run():
+        torch.manual_seed(5)
+        emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=d)
+        model = tt.build_two_tower("mean", emb, hidden_dim=d, tied_weights=True).to(DEV)
+        opt = tt.optim.AdamW(model.parameters(), lr=1e-3, fused_tables=True, tables=[emb], capturable=True)
+        mn = tt.losses.build("multiple_negatives", temperature=0.1)
+
+        def loss_fn(q, p, n):  # negatives viewed (B, K, H), as bench.py's C5 line feeds them
+            return mn(q, p, n.view(q.shape[0], K, q.shape[1]))
+
+        step = tt.TrainStep(model, loss_fn, opt, graph=graph, eager_steps=1)
+        losses = [step(*b).clone() for b in batches]
+        torch.cuda.synchronize()
+        return losses, {k: v.detach().clone() for k, v in model.named_parameters()}
+
+    seen = []
+    real_call = ops.call
+
+    def spy(name, *args):
+        seen.append(name)
+        return real_call(name, *args)
+
+    monkeypatch.setattr(ops, "call", spy)
+    got_l, got = run()
+    assert "tt_multi_neg_bwd_l2" in seen and "tt_l2norm_bwd" not in seen
+    monkeypatch.setenv("TT_FUSED_L2_BWD", "0")
+    seen.clear()
+    want_l, want = run()
+    assert "tt_multi_neg_bwd_l2" not in seen and "tt_l2norm_bwd" in seen
+    for a, b in zip(got_l, want_l):
+        assert torch.equal(a, b)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+
+
 @pytest.mark.parametrize("E,H", [(256, 256), (128, 128), (64, 128), (128, 256)])
 def test_bag_forward_split_workgroups_equal_head_split(E, H):
     """tt_bag_mean_fwd_split: the pooled rows and denominators equal tt_bag_mean_fwd's and the

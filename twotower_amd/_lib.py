@@ -123,6 +123,7 @@ _SIGNATURES = {
     "tt_triplet_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
     "tt_multi_neg_fwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp]),
     "tt_multi_neg_bwd": (_c_int, [_vp, _vp, _vp, _c_i64, _c_int, _c_int, _c_f32, _vp, _vp, _vp, _vp, _vp]),
+    "tt_multi_neg_bwd_l2": (_c_int, [_vp, _c_i64, _c_int, _vp, _c_f32, _vp, _vp, _vp]),
     "tt_inbatch_set_backward": (_c_int, [_c_int]),
     "tt_inbatch_ws_size": (_c_sz, [_c_i64, _c_i64, _c_int, _c_int]),
     "tt_inbatch_fwd": (_c_int, [_vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_i64, _c_int, _vp, _vp, _vp, _vp,

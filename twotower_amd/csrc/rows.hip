@@ -314,13 +314,18 @@ __global__ __launch_bounds__(kBlock) void multi_neg_fwd_h256_kernel(const float*
   if (lane_id() == 0) loss_rows[r] = mx + logf(se) - z[0];
 }
 
+// l2n non-null (tt_multi_neg_bwd_l2: q, p, negs are the consecutive row blocks of the tower head's
+// output [q; p; negs] and l2n its row norms in that order): each gradient row goes through the head's
+// F.normalize backward (l2_bwd_row4, l2norm_bwd_kernel's arithmetic) before it is stored, so the
+// head needs no L2 backward pass of its own (bit for bit the two launches).
 template <int NMAX>
 __global__ __launch_bounds__(kBlock) void multi_neg_bwd_h256_kernel(const float* __restrict__ q,
                                                                     const float* __restrict__ p,
                                                                     const float* __restrict__ negs, int64_t B, int N,
                                                                     float inv_tau, const float* __restrict__ grad_loss,
                                                                     float* __restrict__ dq, float* __restrict__ dp,
-                                                                    float* __restrict__ dnegs) {
+                                                                    float* __restrict__ dnegs,
+                                                                    const float* __restrict__ l2n = nullptr) {
   const int64_t r = wave_row();
   if (r >= B) return;
   const int lane = lane_id();
@@ -353,8 +358,10 @@ __global__ __launch_bounds__(kBlock) void multi_neg_bwd_h256_kernel(const float*
         gd[j] = gcos * (m.q[j] * a_other - a_d * m.d[k][j]);
       }
       float* ddr = (k == 0) ? dp + r * 256 : dnegs + (r * N + (k - 1)) * (int64_t)256;
+      if (l2n) gd = l2_bwd_row4(gd, m.d[k], l2n[k == 0 ? B + r : 2 * B + r * N + (k - 1)]);
       reinterpret_cast<f32x4*>(ddr)[lane] = gd;
     }
+  if (l2n) gq = l2_bwd_row4(gq, m.q, l2n[r]);
   reinterpret_cast<f32x4*>(dq + r * 256)[lane] = gq;
 }
 
@@ -597,6 +604,26 @@ extern "C" int tt_multi_neg_fwd(const float* q, const float* p, const float* neg
     TT_LAUNCH_CHECK("tt_multi_neg_fwd");
   }
   return launch_mean(loss_rows, B, loss, s);
+}
+
+extern "C" int tt_multi_neg_bwd_l2(const float* qpn, int64_t B, int N, const float* norms, float inv_tau,
+                                   const float* grad_loss, float* dx, tt_stream_t stream) {
+  TT_REQUIRE(B >= 0 && N >= 0 && N <= 15, "tt_multi_neg_bwd_l2: bad shape B=%lld N=%d (N <= 15)", (long long)B, N);
+  if (B == 0) return TT_OK;
+  TT_REQUIRE(qpn && norms && grad_loss && dx, "null pointer");
+  constexpr int H = 256;
+  const float *q = qpn, *p = qpn + B * H, *negs = qpn + 2 * B * H;
+  float *dq = dx, *dp = dx + B * H, *dn = dx + 2 * B * H;
+  TT_REQUIRE(aligned16(q, p, negs) && aligned16(dq, dp, dn), "qpn / dx must be 16-byte aligned");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (N <= 4)
+    multi_neg_bwd_h256_kernel<4><<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, inv_tau, grad_loss, dq, dp, dn,
+                                                                       norms);
+  else
+    multi_neg_bwd_h256_kernel<15><<<rows_grid(B), dim3(kBlock), 0, s>>>(q, p, negs, B, N, inv_tau, grad_loss, dq, dp,
+                                                                        dn, norms);
+  TT_LAUNCH_CHECK("tt_multi_neg_bwd_l2");
+  return TT_OK;
 }
 
 extern "C" int tt_multi_neg_bwd(const float* q, const float* p, const float* negs, int64_t B, int N, int H,

@@ -765,7 +765,10 @@ class TowerHead(torch.autograd.Function):
             ctx.l2_token = _L2Token(norm)
             out._tt_inbatch_prep = (nq, rows - nq, dt, ws, ctx.l2_token)
         if req is None or not 0 < req[0] < rows:
-            ctx.l2_token = None
+            # a loss that takes the whole output as one tensor (MultiNegLossPacked) may apply
+            # F.normalize's backward itself under fused_head_backward and leave dy here
+            ctx.l2_token = _L2Token(norm)
+            out._tt_l2_token = ctx.l2_token
         ctx.save_for_backward(x, h, mask, out, norm, planes)
         sides = {id(getattr(w, "_tt_side_grads", None)) for w in (W1, b1, W2, b2)}
         ctx.side_grads = W1._tt_side_grads if len(sides) == 1 and hasattr(W1, "_tt_side_grads") else None
@@ -1074,6 +1077,8 @@ class MultiNegLossPacked(torch.autograd.Function):
         call("tt_multi_neg_fwd", ptr(q), ptr(p), ptr(n), B, K, H, float(inv_tau), ptr(rows), ptr(loss), stream_of(qpn))
         ctx.save_for_backward(qpn)
         ctx.meta = (B, K, float(inv_tau))
+        tok = getattr(qpn, "_tt_l2_token", None)  # the tower head's output itself, whole
+        ctx.l2_token = tok if tok is not None and tok.norms.shape[0] == qpn.shape[0] and H == 256 and K <= 15 else None
         return loss
 
     @staticmethod
@@ -1083,6 +1088,11 @@ class MultiNegLossPacked(torch.autograd.Function):
         H = qpn.shape[1]
         g = g.to(_FLOAT).contiguous().reshape(1)
         grad = torch.empty_like(qpn)
+        tok, ctx.l2_token = ctx.l2_token, None
+        if tok is not None and _FUSED_HEAD_BWD[0] > 0:  # the head's F.normalize backward in the same pass
+            call("tt_multi_neg_bwd_l2", ptr(qpn), B, K, ptr(tok.norms), inv_tau, ptr(g), ptr(grad), stream_of(qpn))
+            tok.dy = grad
+            return grad, None, None, None
         q, p, n = qpn[:B], qpn[B:2 * B], qpn[2 * B:]
         call("tt_multi_neg_bwd", ptr(q), ptr(p), ptr(n), B, K, H, inv_tau, ptr(g), ptr(grad[:B]), ptr(grad[B:2 * B]),
              ptr(grad[2 * B:]), stream_of(qpn))
