@@ -390,6 +390,9 @@ def call(name: str, *args) -> None:
     fn = getattr(lib(), name)
     for seen in _CALLS:
         seen.add(name)
+    if not (TIMER.enabled or TIMER.stamping):  # the common case: no per-op timing, no capture query
+        check(fn(*args), name)
+        return
     check(TIMER.run(name, lambda: fn(*args)), name)
 
 
@@ -397,7 +400,14 @@ def ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(t: torch.Tensor) -> int:
+    """The raw handle of the current stream on t's device (without building a Stream object: this
+    runs once per kernel launch on the eager paths)."""
+    if _RAW_STREAM is not None and t.device.index is not None:
+        return _RAW_STREAM(t.device.index)
     return torch.cuda.current_stream(t.device).cuda_stream
 
 

@@ -613,21 +613,23 @@ class _ArgsRing:
 
     def __init__(self, n: int = 16):
         self.n, self.k = n, 0
-        self.host = None
+        self.host = self.host_np = None
         self.events: list = [None] * n
+        self.used = [False] * n
 
     def __call__(self, vals, device) -> torch.Tensor:
         if self.host is None:
             self.host = torch.empty((self.n, len(vals)), dtype=torch.float32).pin_memory()
+            self.host_np = self.host.numpy()
+            self.events = [torch.cuda.Event() for _ in range(self.n)]
         k, self.k = self.k, (self.k + 1) % self.n
-        if self.events[k] is not None:
+        if self.used[k]:
             self.events[k].synchronize()
-        self.host[k].copy_(torch.tensor(vals, dtype=torch.float32))
+        self.host_np[k, :] = vals  # (float64 -> float32 rounding, as torch.tensor(vals, float32))
         out = torch.empty(len(vals), dtype=torch.float32, device=device)
         out.copy_(self.host[k], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
-        self.events[k] = ev
+        self.events[k].record(torch.cuda.current_stream(device))
+        self.used[k] = True
         return out
 
 
