@@ -789,7 +789,7 @@ def main():
                        f" = {M})" if world > 1 and cfg["loss"] == "in_batch" else ""),
                    "vocab": V, "d": d, "seq_len": L, "global_batch": B * world, "candidates_per_query": M,
                    "tokens_per_step_per_gpu": nnz, "parallelism": f"dp{world}", "scorer_dtype": scorer_dtype,
-                   "table_sync": (tt.distributed.table_sync_mode(args.table_sync) if dp else "local"),
+                   "table_sync": (tt.distributed.table_sync_mode(args.table_sync, E=d) if dp else "local"),
                    "hip_graph": use_graph, "graph_canary": canary,
                    "loop": (f"reference loop body unchanged (bench.PlainLoop, table_update {args.table_update})" if plain
                             else "TrainStep")},
