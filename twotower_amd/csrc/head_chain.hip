@@ -11,20 +11,24 @@
 // Layout of the work.  The first product is computed TRANSPOSED, h^T = W1 x^T: the W1 planes are the
 // A operand (rows = hidden units) and the x rows the B operand (lane = row, 8 consecutive k), so in
 // the 32 x 32 accumulator a lane holds one ROW and 16 hidden units (4 consecutive per group g = 0..3,
-// 8 apart).  One v_permlane32_swap per register pair (groups 2s, 2s + 1) turns that into the A
-// operand layout of the second product (lane = row, 8 consecutive hidden units per k-half): the
+// 8 apart).  One half-wave exchange per register pair (groups 2s, 2s + 1; a ds_bpermute) turns that
+// into the A operand layout of the second product (lane = row, 8 consecutive hidden units per k-half): the
 // second product y = h W2^T is then an ordinary A x B^T with the W2 planes as B, whose accumulator
 // (lane = output column, 16 rows) stores whole 128-B row segments.  The products are the ones
 // head.hip's kernels form, operand for operand, so h, dh and the unnormalised y equal theirs.
 //
 // Weights: the planes stream through a 3-slot LDS ring in 16-k chunks ([plane][row][32 B], lane
-// (row r, half hh) reads 16 B at 32 r + 16 hh: one contiguous 1 KiB per wave-instruction), filled by
+// (row r, half hh) reads 16 B at 32 r + 16 (hh ^ bit 3 of r): one 1 KiB per wave-instruction), filled by
 // LDS-DMA two chunks ahead, one barrier per chunk; the four waves (128 rows) share each chunk.  A
 // workgroup walks row blocks b, b + grid, ... and the ring continues across them; the next block's
 // B-operand rows (x or dy) ride in the same chunks (their 16 k of the block's 128 rows), so the next
 // block's first chunks arrive while the current block's second product runs.
 #include "common.hpp"
 
+// Measured slower than head.hip's four launches (54.6 / 56.2 against 46.7 / 46.8 us per
+// pass at 24,576 rows; one wave per SIMD serialises the split, the plane reads and the fills with the
+// products), so ops.TowerHead runs it only under TT_HEAD_CHAIN=1.
+//
 // Timing ablations (tools/build_variants.sh; never in the shipped build): TT_CHAB_NOMFMA keeps the
 // operand reads and drops the products, TT_CHAB_NOFILL drops the LDS-DMA pieces, TT_CHAB_NOBAR the
 // chunk barriers, TT_CHAB_NOSTORE the h and y stores.  Their results are wrong by construction.
@@ -44,9 +48,6 @@ namespace {
 constexpr int kCW = 4;       // waves per workgroup
 constexpr int kCRows = 32;   // rows per wave
 constexpr int kCSlots = 3;   // LDS ring slots
-#ifndef TT_CHAIN_PERMLANE
-#define TT_CHAIN_PERMLANE 0      // 1, 2: the half exchange by v_permlane32_swap (operand orders) instead of ds_bpermute
-#endif
 
 // MODE1: 0 forward first Linear (bias + ReLU, ReLU bits written, h stored)
 //        1 backward dh GEMM (ReLU bits read, dh stored)
@@ -278,19 +279,6 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-#if TT_CHAIN_PERMLANE == 1
-          const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, acc1[t][8 * s + i]),
-                                                          __builtin_bit_cast(unsigned, acc1[t][8 * s + 4 + i]), false,
-                                                          false);
-          acc1[t][8 * s + i] = __builtin_bit_cast(float, (unsigned)r[0]);
-          acc1[t][8 * s + 4 + i] = __builtin_bit_cast(float, (unsigned)r[1]);
-#elif TT_CHAIN_PERMLANE == 2
-          const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, acc1[t][8 * s + 4 + i]),
-                                                          __builtin_bit_cast(unsigned, acc1[t][8 * s + i]), false,
-                                                          false);
-          acc1[t][8 * s + 4 + i] = __builtin_bit_cast(float, (unsigned)r[0]);
-          acc1[t][8 * s + i] = __builtin_bit_cast(float, (unsigned)r[1]);
-#else
           // (the pair made opaque first: a select between two elements of one vector otherwise becomes
           // a lane-varying element index, extracted and inserted by 16-way v_cndmask chains)
           float a = acc1[t][8 * s + i], b = acc1[t][8 * s + 4 + i];
@@ -298,7 +286,6 @@ __global__ __launch_bounds__(256, 1) void head_chain_kernel(
           const float got = __shfl_xor(hh ? a : b, 32);
           acc1[t][8 * s + i] = hh ? got : a;
           acc1[t][8 * s + 4 + i] = hh ? b : got;
-#endif
         }
     // ---- second product: acc2[t2] = (this wave's rows, as A) x (P2 rows 32 t2 .. +31)^T
     f32x16 acc2[NT2];
