@@ -205,6 +205,22 @@ def plan_split() -> bool:
     return os.environ.get("TT_PLAN_SPLIT", "0") == "1"
 
 
+def plan_fork_early(table_bytes: int) -> bool:
+    """Whether the tower bag's sort forks before its gather (see BagMeanPool.forward).
+    TT_PLAN_FORK: "auto" (default) forks before the gather inside a graph capture when the table
+    fits the 256 MiB Infinity Cache, and after it otherwise and in every eager step: an eager step
+    that starts on an idle GPU (the reference loop's .item() syncs) then does not queue its gather
+    behind the sort's host launches (C3 reference loop with both opt-ins, same box, 5 runs each:
+    1.107-1.149 against 1.136-1.204 ms/step, profiles/r05zl_plain_fork_ab.txt).  "size" applies the
+    table-size rule in eager steps too; "early" and "late" force one side."""
+    mode = os.environ.get("TT_PLAN_FORK", "auto")
+    if mode in ("early", "late"):
+        return mode == "early"
+    if mode == "auto" and not torch.cuda.is_current_stream_capturing():
+        return False
+    return table_bytes <= 256 * 2 ** 20
+
+
 class _BagGradToken:
     """Shared by a BagMeanPool node and the TowerHead that is the sole consumer of its output:
     the head's dx GEMM divides each row by its bag denominator in its epilogue (tt_head_gemm epi
@@ -307,13 +323,14 @@ class BagMeanPool(torch.autograd.Function):
         ids = ids.contiguous()
         ctx.plan = None
         plan_now = want_plan and scatter_mode == _lib.TT_SCATTER_SORTED
-        # Where the sort forks onto its side stream: before the gather, beside it, when the table
-        # fits the 256 MiB Infinity Cache (the gather then reads the cache, and the latency-bound
-        # sort beside it costs it little: C3 0.8381 vs 0.8419 ms/step), after it otherwise (an
-        # HBM-bound gather of a larger table: C5 1.8235 early vs 1.8178 after;
-        # profiles/r03p_c3_plan_fork_ab.txt, r03w_plan_fork_auto_ab.txt)
-        # (round 4, same box: early 0.8256 vs late 0.8343 ms/step at C3, profiles/r04f_plan_fork_ab.txt)
-        early = plan_now and weight.numel() * weight.element_size() <= 256 * 2 ** 20
+        # Where the sort forks onto its side stream (plan_fork_early): in a captured step, before
+        # the gather, beside it, when the table fits the 256 MiB Infinity Cache (the gather then
+        # reads the cache, and the latency-bound sort beside it costs it little: C3 0.8381 vs
+        # 0.8419 ms/step), after it otherwise (an HBM-bound gather of a larger table: C5 1.8235
+        # early vs 1.8178 after; profiles/r03p_c3_plan_fork_ab.txt, r03w_plan_fork_auto_ab.txt)
+        # (round 4, same box: early 0.8256 vs late 0.8343 ms/step at C3, profiles/r04f_plan_fork_ab.txt);
+        # in an eager step, after the gather (round 5, profiles/r05zl_plain_fork_ab.txt)
+        early = plan_now and plan_fork_early(weight.numel() * weight.element_size())
         if early:
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
