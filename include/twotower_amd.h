@@ -405,12 +405,25 @@ int tt_cosine_scores(const float* q, int64_t nq, const float* docs, int64_t nd, 
                      tt_stream_t stream);
 int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float* out_vals, int64_t* out_idx,
                  tt_stream_t stream);
+/* tt_topk_rows_ex: the same result; with a workspace of tt_topk_rows_ws_size bytes (0 when the rows
+ * are short) long rows run in two stages (chunks in parallel, then a merge), so a row is not left
+ * to one workgroup; ws = NULL takes tt_topk_rows's one-workgroup-per-row form. */
+size_t tt_topk_rows_ws_size(int64_t nrows, int64_t ncols, int k);
+int tt_topk_rows_ex(const float* scores, int64_t nrows, int64_t ncols, int k, void* ws, size_t ws_bytes,
+                    float* out_vals, int64_t* out_idx, tt_stream_t stream);
 
 /* ---- device-resident batch feeder (TripletDataset.__getitem__ + DataLoader collate,
  * twotower/dataset.py:262-285, twotower/train.py:411-417): dst[r, :L] = src[idx[r], :L] for int32
  * id rows; an index outside [0, n_src) yields an all-padding row and sets *bad to 1 (caller zeroes). */
 int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n, int L,
                        int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream);
+/* tt_gather_rows_i32_ex: nfield such gathers in one launch (field f reads src + f * src_field and
+ * writes dst + f * dst_field: the (q, d+, d-) rows of a batch); a bad index sets *bad to
+ * max(*bad, gen), gen >= 1, so a caller passing a new gen per call tests *bad == gen instead of
+ * zeroing the flag before each call. */
+int tt_gather_rows_i32_ex(const int32_t* src, int64_t ld_src, int64_t n_src, int64_t src_field, int nfield,
+                          const int64_t* idx, int64_t n, int L, int32_t* dst, int64_t ld_dst, int64_t dst_field,
+                          int* bad, int gen, tt_stream_t stream);
 
 /* ---- measurement (bench.py's per-op times from a replayed graph) ----
  * tt_stamp: writes the device's constant-rate wall clock (tt_wall_clock_khz ticks per ms) to

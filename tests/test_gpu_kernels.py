@@ -1015,6 +1015,34 @@ def test_cosine_topk_vs_reference_math(nq, nd, H, k):
     assert np.array_equal(vals.cpu().numpy(), np.take_along_axis(sc, order, 1))
 
 
+@pytest.mark.parametrize("nq,ncols,k,levels", [(3, 300_000, 100, 50), (2, 1_000_000, 1000, 7), (5, 200_000, 10, 1000000),
+                                                (1, 65_536 * 4, 1, 3)])
+def test_topk_two_stage_ties_across_chunks(nq, ncols, k, levels):
+    """Long rows take the two-stage top-k (tt_topk_rows_ws_size > 0); quantised scores put thousands
+    of exact ties on the k-th value across chunk boundaries: the lower columns must win."""
+    assert _lib.lib().tt_topk_rows_ws_size(nq, ncols, k) > 0
+    g = torch.Generator(device=DEV).manual_seed(ncols + k)
+    x = torch.randint(0, levels, (nq, ncols), device=DEV, generator=g).float() / levels
+    vals, idx = ops.topk_rows(x, k)
+    xs = x.cpu().numpy()
+    order = np.lexsort((np.arange(ncols)[None].repeat(nq, 0), -xs), axis=1)[:, :k]
+    assert np.array_equal(idx.cpu().numpy(), order)
+    assert np.array_equal(vals.cpu().numpy(), np.take_along_axis(xs, order, 1))
+
+
+@pytest.mark.parametrize("nq,nd,H", [(40, 2049, 256), (70, 999, 64), (9, 300, 36), (33, 4097, 512), (5, 129, 1024)])
+def test_cosine_scores_many_queries_and_widths(nq, nd, H):
+    """Query passes (up to 32 per pass, fewer at wide H), partial document tiles, H not a multiple
+    of the staged chunk."""
+    rng = np.random.default_rng(nq * nd + H)
+    q = rng.standard_normal((nq, H)).astype(np.float32)
+    d = rng.standard_normal((nd, H)).astype(np.float32)
+    s = ops.cosine_scores(cuda(q), cuda(d))
+    ref = torch.nn.functional.cosine_similarity(torch.as_tensor(q).double()[:, None], torch.as_tensor(d).double()[None],
+                                                dim=2).numpy()
+    assert np.abs(s.cpu().numpy() - ref).max() < 1e-6
+
+
 def test_topk_ties_and_extremes():
     x = torch.tensor([[1.0, 3.0, 3.0, -2.0, 3.0, float("-inf"), 0.0, -0.0]], device=DEV)
     vals, idx = ops.topk_rows(x, 4)
@@ -1071,10 +1099,23 @@ def test_device_feeder_matches_dataloader_collate():
     for (q, p, n), (rq, rp, rn) in zip(got, loader):
         assert torch.equal(q.cpu().long(), rq) and torch.equal(p.cpu().long(), rp) and torch.equal(n.cpu().long(), rn)
         assert q.dtype == torch.int32 and q._base is p._base  # packed [q; p; n]
-    assert int(store._bad.item()) == 0
-    # out-of-range index: padding row + flag
+    assert not store.bad_index()
+    # out-of-range index: padding row + flag, and the next good gather reads clear
     q, p, n = store.gather(torch.tensor([0, 1000], device=DEV))
-    assert torch.equal(q[1], torch.zeros_like(q[1])) and int(store._bad.item()) == 1
+    assert torch.equal(q[1], torch.zeros_like(q[1])) and store.bad_index()
+    store.gather(torch.tensor([0, 1], device=DEV))
+    assert not store.bad_index()
+
+
+@pytest.mark.parametrize("N,L,B", [(1000, 64, 777), (50, 7, 33), (300, 130, 256), (10, 256, 5)])
+def test_device_feeder_gather_equals_index_select(N, L, B):
+    rows = torch.randint(0, 10_000, (3, N, L), dtype=torch.int32, device=DEV)
+    store = tt.data.DeviceTripletStore(rows)
+    idx = torch.randint(0, N, (B,), device=DEV)
+    q, p, n = store.gather(idx)
+    for k, t in enumerate((q, p, n)):
+        assert torch.equal(t, rows[k].index_select(0, idx))
+    assert not store.bad_index()
 
 
 @pytest.mark.parametrize("rows,H", [(37, 24), (1000, 256), (5, 1024)])

@@ -18,6 +18,10 @@
                                                  alone (C3 and B x B rows)
   python tools/mb.py scorer_once B M H [dtype] [lib]   three scorer fwd + bwd calls, nothing else (for
                                                  counter collection: tools/pmc_scorer.sh)
+  python tools/mb.py next_rows                   SURVEY section 8(f) rows: the device feeder's batch gather,
+                                                 forward-only encode, cosine scores + top-k over a 1M-document
+                                                 index, and the AveragePoolingTower head (LinearHead +
+                                                 LayerNorm/L2), each against its HBM roofline and a torch form
 """
 import argparse
 import ctypes
@@ -456,10 +460,87 @@ def head_once(a):
     torch.cuda.synchronize()
 
 
+def next_rows(a):
+    """each op's device time (graph replay), algorithmic bytes and the fraction of 8 TB/s,
+    with the torch expression of the same result beside it."""
+    out = {}
+    peak = 8000.0
+
+    def rec(name, us, nbytes, torch_us=None, **kw):
+        e = {"us": round(us, 2), "algorithmic_MB": round(nbytes / 1e6, 2), "gbs": round(nbytes / us / 1e3, 1),
+             "frac_of_8TBs": round(nbytes / us / 1e3 / peak, 3)}
+        if torch_us is not None:
+            e["torch_us"] = round(torch_us, 2)
+        e.update(kw)
+        out[name] = e
+        print(name, json.dumps(e), flush=True)
+
+    g = torch.Generator(device=DEV).manual_seed(0)
+    # f1 device feeder: 500k resident int32 triplets of 64 tokens (384 MB), one C3 batch of 8192 by index
+    N, L, B = 500_000, 64, 8192
+    rows = torch.randint(1, 200_000, (3, N, L), device=DEV, dtype=torch.int32, generator=g)
+    store = tt.data.DeviceTripletStore(rows)
+    idx = torch.randperm(N, device=DEV, generator=g)[:B]
+    buf = torch.empty(3 * B, L, dtype=torch.int32, device=DEV)
+    rec("f1_feeder_gather", graph_us(lambda: store.gather(idx, out=buf), 20), 2 * 3 * B * L * 4 + B * 8,
+        graph_us(lambda: rows.index_select(1, idx), 20), shape=f"(3, {N}, {L}) int32 store, batch {B}")
+    del rows, store
+    # f2 forward-only encode (C3 tower, no grad): bag gather + head + F.normalize over 8192 documents
+    V, E = 200_000, 256
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=E, tied_weights=True).to(DEV).eval()
+    ids = tt.data.synthetic_triplets(B, L, V, seed=3, device=DEV)[1]
+    nnz = int((ids > 0).sum())
+    with torch.no_grad():
+        us = graph_us(lambda: model.encode_document(ids), 10)
+    rec("f2_encode_documents", us, ids.numel() * ids.element_size() + nnz * E * 4 + B * E * 4 * 3,
+        docs_per_s=round(B / us * 1e6), note="bytes: ids + gathered rows + pooled, h, y rows (head MFMA-bound)")
+    # f2 cosine scores over a 1M x 256 index, top-k of each query's row
+    ND = 1_000_000
+    docs = torch.nn.functional.normalize(torch.randn(ND, E, device=DEV, generator=g), dim=-1)
+    for nq in (1, 16, 64):
+        q = torch.randn(nq, E, device=DEV, generator=g)
+        dn = docs.norm(dim=1)
+        t_us = graph_us(lambda: (q @ docs.t()) / (q.norm(dim=1, keepdim=True) * dn).clamp_min(1e-8), 10)
+        rec(f"f2_cosine_scores_nq{nq}", graph_us(lambda: ops.cosine_scores(q, docs), 10),
+            ND * E * 4 + nq * ND * 4 + nq * E * 4, t_us, note="torch: mm / norms (not the ATen eps form)")
+        sc = ops.cosine_scores(q, docs)
+        for k in (10, 100):
+            rec(f"f2_topk_nq{nq}_k{k}", graph_us(lambda: ops.topk_rows(sc, k), 10), nq * ND * 4 + nq * k * 12,
+                graph_us(lambda: torch.topk(sc, k, dim=1), 10))
+    del docs
+    # f4 AveragePoolingTower head at C3 rows (3 x 8192): projection 256 -> 128, LayerNorm + L2, fwd + bwd
+    R, H = 3 * B, 128
+    x = torch.randn(R, E, device=DEV, generator=g)
+    W = torch.randn(H, E, device=DEV, generator=g) / 16
+    b, gam, bet = (torch.randn(H, device=DEV, generator=g) for _ in range(3))
+    hproj = ops.linear(x, W, b)
+    dy = torch.randn(R, H, device=DEV, generator=g)
+    rec("f4_linear_fwd", graph_us(lambda: ops.linear(x, W, b), 20), R * E * 4 + R * H * 4,
+        graph_us(lambda: torch.addmm(b, x, W.t()), 20), note="split-bf16 MFMA, fp32 accuracy; torch: hipBLASLt fp32")
+    rec("f4_ln_l2_fwd", graph_us(lambda: ops.layernorm_l2_normalize(hproj, gam, bet, 1e-5), 20),
+        R * H * 4 * 2 + R * 12, graph_us(lambda: torch.nn.functional.normalize(
+            torch.nn.functional.layer_norm(hproj, (H,), gam, bet, 1e-5), dim=-1), 20))
+    hp = hproj.detach().requires_grad_(True)
+    gp, bp = gam.detach().requires_grad_(True), bet.detach().requires_grad_(True)
+    yv = ops.layernorm_l2_normalize(hp, gp, bp, 1e-5)
+    # backward passes timed eagerly (HIP events around back-to-back autograd calls)
+    rec("f4_ln_l2_bwd", event_us(lambda: torch.autograd.grad(yv, (hp, gp, bp), dy, retain_graph=True), 20),
+        R * H * 4 * 3 + R * 12 + 2 * H * 4)
+    xp, Wp, bb = x.detach().requires_grad_(True), W.detach().requires_grad_(True), b.detach().requires_grad_(True)
+    yl = ops.linear(xp, Wp, bb)
+    rec("f4_linear_bwd", event_us(lambda: torch.autograd.grad(yl, (xp, Wp, bb), dy, retain_graph=True), 20),
+        R * H * 4 * 2 + R * E * 4 * 2 + H * E * 4, note="dx (MFMA) + dW, db")
+    path = a.shape
+    if path:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
-                                     "column_sync", "l2prep", "scorer_once", "head_once"])
+                                     "column_sync", "l2prep", "scorer_once", "head_once", "next_rows"])
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")
     ap.add_argument("--zipf", type=float, default=None)

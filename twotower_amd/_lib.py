@@ -86,8 +86,12 @@ _SIGNATURES = {
                                    _vp]),
     "tt_cosine_scores": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_topk_rows": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
+    "tt_topk_rows_ws_size": (_c_sz, [_c_i64, _c_i64, _c_int]),
+    "tt_topk_rows_ex": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _c_sz, _vp, _vp, _vp]),
     "tt_pack_blocks": (_c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_c_i64), _c_int, _vp, _vp]),
     "tt_gather_rows_i32": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
+    "tt_gather_rows_i32_ex": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _c_i64, _c_int, _vp, _c_i64, _c_i64,
+                                       _vp, _c_int, _vp]),
     "tt_ln_l2_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_f32, _vp, _vp, _vp]),
     "tt_ln_l2_bwd": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tt_head_planes_bytes": (_c_sz, [_c_int, _c_int]),

@@ -3,8 +3,8 @@
 // buffer the fused TwoTower forward reads (replaces TripletDataset.__getitem__ + DataLoader
 // collate + .to(device), twotower/dataset.py:262-285, twotower/train.py:411-417).
 //
-// One wave per destination row: L int32 ids (L*4 bytes) copied with 16-byte loads when the
-// rows are 16-byte aligned, HBM-bound (a batch of 3 x 8192 x 64 ids is 6.3 MB).
+// A group of lanes per destination row (16 at L = 64: one 16-byte unit each), the three fields
+// in one launch, HBM-bound (a batch of 3 x 8192 x 64 ids is 6.3 MB).
 #include "common.hpp"
 
 namespace tt {
@@ -12,28 +12,31 @@ namespace {
 
 constexpr int kBlock = 256;
 
-template <bool VEC>
+// G lanes per destination row (G = 64 / rows per wave), 16-byte units when the rows are 16-byte
+// aligned; blockIdx.y = the field (q, d+, d-: src / dst advanced by their field strides).  An
+// index out of range writes a zero (all padding) row and raises the flag: atomicMax(bad, gen), so
+// a caller that passes a new gen per call reads "bad == gen" without clearing the flag first.
+template <typename U, int G>
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(const int32_t* __restrict__ src, int64_t ld_src,
-                                                             int64_t n_src, const int64_t* __restrict__ idx,
-                                                             int64_t n, int L, int32_t* __restrict__ dst,
-                                                             int64_t ld_dst, int* __restrict__ bad) {
-  const int64_t r = (int64_t)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+                                                             int64_t n_src, int64_t src_field,
+                                                             const int64_t* __restrict__ idx, int64_t n, int L,
+                                                             int32_t* __restrict__ dst, int64_t ld_dst,
+                                                             int64_t dst_field, int* __restrict__ bad, int gen) {
+  constexpr int kRows = kBlock / G;
+  const int64_t r = (int64_t)blockIdx.x * kRows + threadIdx.x / G;
   if (r >= n) return;
-  const int lane = lane_id();
+  const int g = threadIdx.x % G;
   const int64_t s = idx[r];
-  int32_t* out = dst + r * ld_dst;
-  if (s < 0 || s >= n_src) {  // out of range: a zero (all padding) row, and the flag is raised
-    for (int c = lane; c < L; c += kWave) out[c] = 0;
-    if (lane == 0) atomicOr(bad, 1);
+  constexpr int kPer = sizeof(U) / 4;  // int32 per unit
+  U* out = reinterpret_cast<U*>(dst + blockIdx.y * dst_field + r * ld_dst);
+  const int units = L / kPer;
+  if (s < 0 || s >= n_src) {
+    for (int c = g; c < units; c += G) out[c] = U{};
+    if (g == 0) atomicMax(bad, gen);
     return;
   }
-  const int32_t* in = src + s * ld_src;
-  if constexpr (VEC) {
-    for (int c = lane; c < L / 4; c += kWave)
-      reinterpret_cast<int4*>(out)[c] = reinterpret_cast<const int4*>(in)[c];
-  } else {
-    for (int c = lane; c < L; c += kWave) out[c] = in[c];
-  }
+  const U* in = reinterpret_cast<const U*>(src + blockIdx.y * src_field + s * ld_src);
+  for (int c = g; c < units; c += G) out[c] = in[c];
 }
 
 // tt_pack_blocks: up to kPackMax contiguous byte blocks copied into consecutive ranges of one
@@ -101,21 +104,51 @@ extern "C" int tt_pack_blocks(const void* const* srcs, const int64_t* bytes, int
   return TT_OK;
 }
 
-extern "C" int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n,
-                                  int L, int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream) {
-  TT_REQUIRE(n >= 0 && L >= 0 && n_src >= 0 && ld_src >= L && ld_dst >= L, "bad shape");
+extern "C" int tt_gather_rows_i32_ex(const int32_t* src, int64_t ld_src, int64_t n_src, int64_t src_field,
+                                     int nfield, const int64_t* idx, int64_t n, int L, int32_t* dst, int64_t ld_dst,
+                                     int64_t dst_field, int* bad, int gen, tt_stream_t stream) {
+  TT_REQUIRE(n >= 0 && L >= 0 && n_src >= 0 && ld_src >= L && ld_dst >= L && nfield >= 1 && nfield <= 65535,
+             "bad shape");
+  TT_REQUIRE(gen >= 1, "gen=%d must be >= 1", gen);
   if (n == 0 || L == 0) return TT_OK;
   TT_REQUIRE(src && idx && dst && bad, "null pointer");
-  const bool vec = (L % 4 == 0) && (ld_src % 4 == 0) && (ld_dst % 4 == 0) &&
+  const bool vec = (L % 4 == 0) && (ld_src % 4 == 0) && (ld_dst % 4 == 0) && (src_field % 4 == 0) &&
+                   (dst_field % 4 == 0) &&
                    ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
-  const dim3 grid((unsigned)((n + kBlock / kWave - 1) / (kBlock / kWave))), block(kBlock);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (vec)
-    gather_rows_kernel<true><<<grid, block, 0, s>>>(src, ld_src, n_src, idx, n, L, dst, ld_dst, bad);
-  else
-    gather_rows_kernel<false><<<grid, block, 0, s>>>(src, ld_src, n_src, idx, n, L, dst, ld_dst, bad);
+  const int units = vec ? L / 4 : L;
+  // lanes per row: the units of a row rounded up to a power of two, 4..64
+  int G = 4;
+  while (G < 64 && G < units) G <<= 1;
+  const dim3 grid((unsigned)((n + kBlock / G - 1) / (kBlock / G)), (unsigned)nfield), block(kBlock);
+#define TT_GATHER(U, GG)                                                                                     \
+  gather_rows_kernel<U, GG><<<grid, block, 0, s>>>(src, ld_src, n_src, src_field, idx, n, L, dst, ld_dst,   \
+                                                   dst_field, bad, gen)
+  if (vec) {
+    switch (G) {
+      case 4: TT_GATHER(int4, 4); break;
+      case 8: TT_GATHER(int4, 8); break;
+      case 16: TT_GATHER(int4, 16); break;
+      case 32: TT_GATHER(int4, 32); break;
+      default: TT_GATHER(int4, 64); break;
+    }
+  } else {
+    switch (G) {
+      case 4: TT_GATHER(int, 4); break;
+      case 8: TT_GATHER(int, 8); break;
+      case 16: TT_GATHER(int, 16); break;
+      case 32: TT_GATHER(int, 32); break;
+      default: TT_GATHER(int, 64); break;
+    }
+  }
+#undef TT_GATHER
   TT_LAUNCH_CHECK("tt_gather_rows_i32");
   return TT_OK;
+}
+
+extern "C" int tt_gather_rows_i32(const int32_t* src, int64_t ld_src, int64_t n_src, const int64_t* idx, int64_t n,
+                                  int L, int32_t* dst, int64_t ld_dst, int* bad, tt_stream_t stream) {
+  return tt_gather_rows_i32_ex(src, ld_src, n_src, 0, 1, idx, n, L, dst, ld_dst, 0, bad, 1, stream);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -4,12 +4,13 @@
 //   top-k of each score row, descending, ties broken by the lower document index.
 //
 // cosine kernel: HBM-bound on the document matrix (nd x H fp32, read once per pass of up to
-// kQ queries).  One wave per document row; the queries' normalised rows sit in LDS; each lane
-// holds 4 consecutive features (16 B loads, a 1 KiB row per wave-instruction at H = 256).
-// top-k kernel: exact radix select per row (one 256-thread workgroup per row): four 8-bit digit
-// passes over the order-preserving uint32 image of the scores find the k-th largest value, a
-// collect pass gathers everything above it plus the lowest-index ties, and a bitonic sort in
-// LDS orders the k survivors.
+// kQMax queries) for a few queries, FMA-bound for many; a lane owns documents (below).
+// top-k: exact radix select by one 256-thread workgroup (topk_block): four 8-bit digit passes
+// over the order-preserving uint32 image of the scores find the k-th largest value (the digit
+// chosen by a one-wave scan of the histogram), a collect pass gathers everything above it plus
+// the lowest-index ties, and a bitonic sort in LDS orders the k survivors.  Long rows run it in
+// two stages (chunks of the row in parallel, then a merge of the chunks' candidates), so a row
+// is not left to one CU.
 #include <cstring>
 
 #include "common.hpp"
@@ -17,48 +18,107 @@
 namespace tt {
 namespace {
 
-constexpr int kQ = 8;            // queries per cosine pass
 constexpr int kBlock = 256;
 constexpr int kTopkMax = 1024;   // k limit (LDS sort of kTopkMax keys + indices)
 constexpr float kCosEps = 1e-8f;
 
+// ---- cosine scores.  A lane owns documents, not features: a wave takes a tile of kDocsW = 128
+// documents (lane l: documents l and l + 64) and streams them in kFC-feature chunks through a
+// wave-private LDS image (rows padded to kFC + 4 floats, so each lane's 16-B reads of its own row
+// hit distinct banks), while the pass's normalised queries sit in LDS and are read as broadcasts.
+// Each product is an in-lane FMA: no cross-lane reduction per document (the previous one-wave-
+// per-document form spent its time in 9 wave reductions per row).  The next chunk's global loads
+// are issued before the current chunk's FMAs.  A pass covers up to kQMax queries; more take more
+// passes over the documents.
+constexpr int kFC = 32;                    // features per staged chunk
+constexpr int kRowF = kFC + 4;             // padded LDS row (floats)
+constexpr int kDocsW = 128;                // documents per wave tile (2 per lane)
+constexpr int kQMax = 32;                  // queries per pass
+constexpr int kLoadsW = kDocsW * kFC / 4 / kWave;  // f32x4 loads per lane per chunk (16)
+
+template <int QP>
 __global__ __launch_bounds__(kBlock) void cosine_scores_kernel(const float* __restrict__ q, int nq,
                                                                const float* __restrict__ docs, int64_t nd, int H,
                                                                float* __restrict__ scores, int64_t ld_scores) {
-  extern __shared__ float qs[];  // nq x H normalised query rows
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Hp = (H + kFC - 1) / kFC * kFC;
+  float* qs = smem;                                              // QP x Hp normalised queries (zero padded)
   const int lane = lane_id(), wid = threadIdx.x >> 6;
-  // normalise the queries (each wave takes some rows), ATen: x / max(|x|, eps)
-  for (int i = wid; i < nq; i += kBlock / kWave) {
+  float* dl = smem + QP * Hp + wid * (kDocsW * kRowF);           // this wave's document image
+  // normalise the queries (ATen: x / max(|x|, eps)); rows past nq and features past H are zero
+  for (int i = wid; i < QP; i += kBlock / kWave) {
     float ss = 0.f;
-    for (int h = lane; h < H; h += kWave) ss += q[(int64_t)i * H + h] * q[(int64_t)i * H + h];
+    if (i < nq)
+      for (int h = lane; h < H; h += kWave) ss += q[(int64_t)i * H + h] * q[(int64_t)i * H + h];
     const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), kCosEps);
-    for (int h = lane; h < H; h += kWave) qs[i * H + h] = q[(int64_t)i * H + h] * inv;
+    for (int h = lane; h < Hp; h += kWave) qs[i * Hp + h] = (i < nq && h < H) ? q[(int64_t)i * H + h] * inv : 0.f;
   }
   __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * (kBlock / kWave);
-  for (int64_t j = (int64_t)blockIdx.x * (kBlock / kWave) + wid; j < nd; j += stride) {
-    const float* row = docs + j * H;
-    float dot[kQ];
+  const int nchunks = Hp / kFC;
+  const int64_t ntiles = (nd + kDocsW - 1) / kDocsW;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / kWave);
+  // staging: load u of a chunk = row 8 u + lane / 8 of the tile, features 4 (lane % 8) .. + 3
+  const int srow = lane >> 3, scol = (lane & 7) * 4;
+  for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + wid; t < ntiles; t += wstride) {
+    const int64_t j0 = t * kDocsW;
+    auto load_chunk = [&](int c, f32x4 (&r)[kLoadsW]) {
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) dot[i] = 0.f;
-    float ss = 0.f;
-    for (int c = lane; c < H / 4; c += kWave) {
-      const f32x4 v = reinterpret_cast<const f32x4*>(row)[c];
-      ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      for (int u = 0; u < kLoadsW; ++u) {
+        int64_t j = j0 + 8 * u + srow;
+        j = j < nd ? j : nd - 1;  // rows past the end: a clamped row, never stored
+        const int f = c * kFC + scol;
+        r[u] = f < H ? *reinterpret_cast<const f32x4*>(docs + j * H + f) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    f32x4 cur[kLoadsW];
+    load_chunk(0, cur);
+    float acc[QP][2], ss[2] = {0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < kQ; ++i) {
-        if (i < nq) {
-          const f32x4 w = *reinterpret_cast<const f32x4*>(qs + i * H + 4 * c);
-          dot[i] += v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+    for (int i = 0; i < QP; ++i) acc[i][0] = acc[i][1] = 0.f;
+    for (int c = 0; c < nchunks; ++c) {
+#pragma unroll
+      for (int u = 0; u < kLoadsW; ++u) *reinterpret_cast<f32x4*>(dl + (8 * u + srow) * kRowF + scol) = cur[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (c + 1 < nchunks) load_chunk(c + 1, cur);
+      float part[QP][2];  // this chunk's sums (two-level: chunk sums of kFC products, then the row)
+#pragma unroll
+      for (int i = 0; i < QP; ++i) part[i][0] = part[i][1] = 0.f;
+      const float* qc = qs + c * kFC;
+#pragma unroll
+      for (int f = 0; f < kFC; f += 4) {
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(dl + lane * kRowF + f);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(dl + (lane + kWave) * kRowF + f);
+        ss[0] += d0[0] * d0[0] + d0[1] * d0[1] + d0[2] * d0[2] + d0[3] * d0[3];
+        ss[1] += d1[0] * d1[0] + d1[1] * d1[1] + d1[2] * d1[2] + d1[3] * d1[3];
+#pragma unroll
+        for (int i = 0; i < QP; ++i) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(qc + i * Hp + f);  // same address: broadcast
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            part[i][0] = __builtin_fmaf(d0[e], w[e], part[i][0]);
+            part[i][1] = __builtin_fmaf(d1[e], w[e], part[i][1]);
+          }
         }
       }
-    }
-    const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), kCosEps);
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) {
-      if (i < nq) {
-        const float s = wave_sum(dot[i]) * inv;
-        if (lane == 0) scores[(int64_t)i * ld_scores + j] = s;
+      for (int i = 0; i < QP; ++i) {
+        acc[i][0] += part[i][0];
+        acc[i][1] += part[i][1];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads of this image before the next writes
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t j = j0 + lane + h * kWave;
+      const float inv = 1.f / fmaxf(sqrtf(ss[h]), kCosEps);
+      if (j < nd) {
+#pragma unroll
+        for (int i = 0; i < QP; ++i)
+          if (i < nq) scores[(int64_t)i * ld_scores + j] = acc[i][h] * inv;
       }
     }
   }
@@ -73,15 +133,15 @@ __device__ __forceinline__ float key2f(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-__global__ __launch_bounds__(kBlock) void topk_rows_kernel(const float* __restrict__ scores, int64_t ncols, int k,
-                                                           float* __restrict__ out_vals, int64_t* __restrict__ out_idx) {
+// Exact top-k of one row by one 256-thread workgroup; emit(i, value, position) receives the k
+// survivors in order (value descending, position ascending among equal values).
+template <class Emit>
+__device__ __forceinline__ void topk_block(const float* __restrict__ row, int64_t ncols, int k, Emit emit) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t sel_prefix, sel_mask, sel_need;  // digits fixed so far, how many still to take
   __shared__ uint32_t n_above, n_tie;
   __shared__ uint32_t skey[kTopkMax];
   __shared__ int32_t sidx[kTopkMax];
-  const int64_t r = blockIdx.x;
-  const float* row = scores + r * ncols;
   const int tid = threadIdx.x;
   if (tid == 0) {
     sel_prefix = 0;
@@ -98,15 +158,31 @@ __global__ __launch_bounds__(kBlock) void topk_rows_kernel(const float* __restri
       if ((key & msk) == pre) atomicAdd(&hist[(key >> shift) & 255u], 1u);
     }
     __syncthreads();
-    if (tid == 0) {
-      uint32_t need = sel_need, d = 255;
-      for (;; --d) {  // from the largest digit down
-        if (hist[d] >= need || d == 0) break;
-        need -= hist[d];
+    if (tid < kWave) {  // the digit: from the largest down, the first whose running count reaches need
+      // lane l holds digits 255 - 4l .. 252 - 4l (descending); an inclusive scan over the lanes
+      const int lane = tid;
+      uint32_t c[4], tot = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) tot += (c[t] = hist[255 - 4 * lane - t]);
+      uint32_t inc = tot;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t v = __shfl_up(inc, o);
+        if (lane >= o) inc += v;
       }
-      sel_prefix = pre | (d << shift);
-      sel_mask = msk | (255u << shift);
-      sel_need = need;  // how many keys equal to the final threshold are taken
+      const uint32_t need0 = sel_need;
+      const uint64_t hit = __ballot(inc >= need0);
+      const int L = hit ? __builtin_ctzll(hit) : kWave - 1;  // none: the last digit (0) takes the rest
+      if (lane == L) {
+        uint32_t need = need0 - (inc - tot), d = 255 - 4 * lane;
+        for (int t = 0; t < 4; ++t, --d) {
+          if (c[t] >= need || t == 3) break;
+          need -= c[t];
+        }
+        sel_prefix = pre | (d << shift);
+        sel_mask = msk | (255u << shift);
+        sel_need = need;  // how many keys equal to the final threshold are taken
+      }
     }
     __syncthreads();
   }
@@ -180,10 +256,57 @@ __global__ __launch_bounds__(kBlock) void topk_rows_kernel(const float* __restri
       __syncthreads();
     }
   }
-  for (int i = tid; i < k; i += kBlock) {
-    out_vals[r * k + i] = key2f(skey[i]);
-    out_idx[r * k + i] = (int64_t)sidx[i];
-  }
+  for (int i = tid; i < k; i += kBlock) emit(i, key2f(skey[i]), sidx[i]);
+}
+
+// one workgroup per row (rows short enough that a second stage would not pay)
+__global__ __launch_bounds__(kBlock) void topk_rows_kernel(const float* __restrict__ scores, int64_t ncols, int k,
+                                                           float* __restrict__ out_vals, int64_t* __restrict__ out_idx) {
+  const int64_t r = blockIdx.x;
+  topk_block(scores + r * ncols, ncols, k, [&](int i, float v, int32_t pos) {
+    out_vals[r * k + i] = v;
+    out_idx[r * k + i] = (int64_t)pos;
+  });
+}
+
+// Two stages for long rows.  Stage 1: the row is cut into nch chunks of C columns (the last one
+// takes the remainder, so every chunk holds >= k); workgroup (c, r) writes its chunk's exact top k
+// as (value, column) candidates.  Stage 2: one workgroup per row takes the top k of the nch * k
+// candidates.  Every member of the row's top k is in its chunk's top k, and among candidates of
+// equal value the position order is the column order (chunks in column order, each chunk's list
+// sorted by column among equal values), so breaking ties by position breaks them by column.
+__global__ __launch_bounds__(kBlock) void topk_chunks_kernel(const float* __restrict__ scores, int64_t ncols, int k,
+                                                             int64_t C, int nch, float* __restrict__ cand_val,
+                                                             int32_t* __restrict__ cand_idx) {
+  const int c = blockIdx.x;
+  const int64_t r = blockIdx.y;
+  const int64_t c0 = (int64_t)c * C, n = c + 1 < nch ? C : ncols - c0;
+  const int64_t o = (r * nch + c) * k;
+  topk_block(scores + r * ncols + c0, n, k, [&](int i, float v, int32_t pos) {
+    cand_val[o + i] = v;
+    cand_idx[o + i] = (int32_t)(c0 + pos);
+  });
+}
+
+__global__ __launch_bounds__(kBlock) void topk_merge_kernel(const float* __restrict__ cand_val,
+                                                            const int32_t* __restrict__ cand_idx, int nch, int k,
+                                                            float* __restrict__ out_vals, int64_t* __restrict__ out_idx) {
+  const int64_t r = blockIdx.x;
+  const int64_t m = (int64_t)nch * k;
+  const int32_t* ci = cand_idx + r * m;
+  topk_block(cand_val + r * m, m, k, [&](int i, float v, int32_t pos) {
+    out_vals[r * k + i] = v;
+    out_idx[r * k + i] = (int64_t)ci[pos];
+  });
+}
+
+// chunk length of the two-stage form: about sqrt(ncols k) (balances the stages), >= 2048 and
+// >= 2k; 0 when the row is too short for two stages
+inline int64_t topk_chunk(int64_t ncols, int k) {
+  int64_t C = 2048;
+  while (C * C < ncols * (int64_t)k) C <<= 1;
+  while (C < 2 * (int64_t)k) C <<= 1;
+  return ncols >= 4 * C ? C : 0;
 }
 
 }  // namespace
@@ -198,29 +321,72 @@ extern "C" int tt_cosine_scores(const float* q, int64_t nq, const float* docs, i
   if (nq == 0 || nd == 0) return TT_OK;
   TT_REQUIRE(q && docs && scores, "null pointer");
   TT_REQUIRE((reinterpret_cast<uintptr_t>(docs) & 15) == 0, "docs must be 16-byte aligned");
-  TT_REQUIRE((size_t)kQ * H * 4 <= 64 * 1024, "H=%d too large", H);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int64_t waves = nd;
-  const unsigned grid = (unsigned)std::min<int64_t>((waves + 3) / 4, 256 * 8);
-  for (int64_t i0 = 0; i0 < nq; i0 += kQ) {
-    const int n = (int)std::min<int64_t>(kQ, nq - i0);
-    cosine_scores_kernel<<<dim3(grid), dim3(kBlock), (size_t)n * H * 4, s>>>(q + i0 * H, n, docs, nd, H,
-                                                                            scores + i0 * nd, nd);
+  const int Hp = (H + kFC - 1) / kFC * kFC;
+  const int64_t ntiles = (nd + kDocsW - 1) / kDocsW;
+  // queries per pass: up to kQMax, as many (a power of two) as fit the LDS beside the document images
+  const size_t doc_lds = (size_t)(kBlock / kWave) * kDocsW * kRowF * 4, q_row = (size_t)Hp * 4;
+  int qcap = kQMax;
+  while (qcap > 1 && doc_lds + qcap * q_row > 160 * 1024) qcap >>= 1;
+  TT_REQUIRE(doc_lds + q_row <= 160 * 1024, "H=%d too large for the cosine kernel's LDS", H);
+  for (int64_t i0 = 0; i0 < nq; i0 += qcap) {
+    const int n = (int)std::min<int64_t>(qcap, nq - i0);
+    const int QP = n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : n <= 16 ? 16 : 32;
+    const size_t lds = doc_lds + (size_t)QP * q_row;
+    // one tile per wave until every CU holds a workgroup, then the waves walk tiles
+    const unsigned grid = (unsigned)std::min<int64_t>((ntiles + 3) / 4, 256 * 4);
+    const float* qi = q + i0 * H;
+    float* si = scores + i0 * nd;
+    switch (QP) {
+#define TT_COS_CASE(P)                                                                                         \
+  case P:                                                                                                      \
+    cosine_scores_kernel<P><<<dim3(grid), dim3(kBlock), lds, s>>>(qi, n, docs, nd, H, si, nd);                 \
+    break;
+      TT_COS_CASE(1) TT_COS_CASE(2) TT_COS_CASE(4) TT_COS_CASE(8) TT_COS_CASE(16) TT_COS_CASE(32)
+#undef TT_COS_CASE
+    }
     TT_LAUNCH_CHECK("tt_cosine_scores");
   }
   return TT_OK;
 }
 
-extern "C" int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float* out_vals,
-                            int64_t* out_idx, tt_stream_t stream) {
+extern "C" size_t tt_topk_rows_ws_size(int64_t nrows, int64_t ncols, int k) {
+  if (nrows <= 0 || k < 1) return 0;
+  const int64_t C = topk_chunk(ncols, k);
+  if (C == 0) return 0;
+  const int64_t nch = ncols / C;
+  return (size_t)nrows * nch * k * (sizeof(float) + sizeof(int32_t));
+}
+
+extern "C" int tt_topk_rows_ex(const float* scores, int64_t nrows, int64_t ncols, int k, void* ws, size_t ws_bytes,
+                               float* out_vals, int64_t* out_idx, tt_stream_t stream) {
   TT_REQUIRE(nrows >= 0 && ncols >= 0, "bad shape");
   TT_REQUIRE(k >= 1 && k <= kTopkMax && k <= ncols, "k=%d must be in [1, min(%d, ncols=%lld)]", k, kTopkMax,
              (long long)ncols);
   TT_REQUIRE(ncols < (int64_t(1) << 31), "ncols too large");
   if (nrows == 0) return TT_OK;
   TT_REQUIRE(scores && out_vals && out_idx, "null pointer");
-  topk_rows_kernel<<<dim3((unsigned)nrows), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(
-      scores, ncols, k, out_vals, out_idx);
-  TT_LAUNCH_CHECK("tt_topk_rows");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t need = tt_topk_rows_ws_size(nrows, ncols, k);
+  if (need == 0 || ws == nullptr) {  // short rows, or no workspace: one workgroup per row
+    topk_rows_kernel<<<dim3((unsigned)nrows), dim3(kBlock), 0, s>>>(scores, ncols, k, out_vals, out_idx);
+    TT_LAUNCH_CHECK("tt_topk_rows");
+    return TT_OK;
+  }
+  TT_REQUIRE(ws_bytes >= need, "topk workspace %zu bytes < %zu", ws_bytes, need);
+  TT_REQUIRE(nrows <= 65535, "nrows=%lld > 65535 (grid y)", (long long)nrows);
+  const int64_t C = topk_chunk(ncols, k);
+  const int nch = (int)(ncols / C);
+  float* cv = reinterpret_cast<float*>(ws);
+  int32_t* ci = reinterpret_cast<int32_t*>(cv + (size_t)nrows * nch * k);
+  topk_chunks_kernel<<<dim3((unsigned)nch, (unsigned)nrows), dim3(kBlock), 0, s>>>(scores, ncols, k, C, nch, cv, ci);
+  TT_LAUNCH_CHECK("tt_topk_rows (chunks)");
+  topk_merge_kernel<<<dim3((unsigned)nrows), dim3(kBlock), 0, s>>>(cv, ci, nch, k, out_vals, out_idx);
+  TT_LAUNCH_CHECK("tt_topk_rows (merge)");
   return TT_OK;
+}
+
+extern "C" int tt_topk_rows(const float* scores, int64_t nrows, int64_t ncols, int k, float* out_vals,
+                            int64_t* out_idx, tt_stream_t stream) {
+  return tt_topk_rows_ex(scores, nrows, ncols, k, nullptr, 0, out_vals, out_idx, stream);
 }

@@ -72,6 +72,7 @@ class DeviceTripletStore:
             raise ValueError(f"rows must be (3, N, L), got {tuple(rows.shape)}")
         self.rows = rows.to(torch.int32).contiguous()
         self.n, self.L = rows.shape[1], rows.shape[2]
+        self._bad, self._gen = None, 0
 
     @classmethod
     def from_dataset(cls, dataset, device="cuda") -> "DeviceTripletStore":
@@ -98,12 +99,19 @@ class DeviceTripletStore:
         B = index.shape[0]
         if out is None:
             out = torch.empty(3 * B, self.L, dtype=torch.int32, device=self.rows.device)
-        bad = torch.zeros(1, dtype=torch.int32, device=self.rows.device)
-        for k in range(3):
-            _lib.call("tt_gather_rows_i32", self.rows[k].data_ptr(), self.L, self.n, index.data_ptr(), B, self.L,
-                      out[k * B:].data_ptr(), self.L, bad.data_ptr(), _lib.stream_of(out))
-        self._bad = bad
+        if self._bad is None or self._bad.device != out.device:
+            self._bad = torch.zeros(1, dtype=torch.int32, device=out.device)
+        self._gen = self._gen % (2 ** 31 - 2) + 1  # a new tag per call: the flag is never cleared
+        if self._gen == 1:
+            self._bad.zero_()
+        _lib.call("tt_gather_rows_i32_ex", self.rows.data_ptr(), self.L, self.n, self.n * self.L, 3, index.data_ptr(),
+                  B, self.L, out.data_ptr(), self.L, B * self.L, self._bad.data_ptr(), self._gen, _lib.stream_of(out))
         return tuple(torch.split(out, B))
+
+    def bad_index(self) -> bool:
+        """Whether the last gather met an index outside [0, n) (its rows were written as padding).
+        Reads a device flag: a host sync."""
+        return self._bad is not None and int(self._bad.item()) == self._gen
 
     def order(self, seed: int = 0, shuffle: bool = True) -> torch.Tensor:
         if not shuffle:

@@ -1536,7 +1536,10 @@ def topk_rows(scores: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]
     n, m = scores.shape
     vals = torch.empty(n, k, dtype=_FLOAT, device=scores.device)
     idx = torch.empty(n, k, dtype=torch.int64, device=scores.device)
-    call("tt_topk_rows", ptr(scores), n, m, int(k), ptr(vals), ptr(idx), stream_of(scores))
+    nbytes = _lib.lib().tt_topk_rows_ws_size(n, m, int(k))
+    ws = WORKSPACE.get("topk", nbytes, scores.device) if nbytes else None
+    call("tt_topk_rows_ex", ptr(scores), n, m, int(k), ptr(ws) if ws is not None else None, nbytes, ptr(vals),
+         ptr(idx), stream_of(scores))
     return vals, idx
 
 
