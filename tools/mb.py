@@ -498,7 +498,7 @@ def next_rows(a):
     # f2 cosine scores over a 1M x 256 index, top-k of each query's row
     ND = 1_000_000
     docs = torch.nn.functional.normalize(torch.randn(ND, E, device=DEV, generator=g), dim=-1)
-    for nq in (1, 16, 64):
+    for nq in (1, 8, 16, 32, 64):
         q = torch.randn(nq, E, device=DEV, generator=g)
         dn = docs.norm(dim=1)
         t_us = graph_us(lambda: (q @ docs.t()) / (q.norm(dim=1, keepdim=True) * dn).clamp_min(1e-8), 10)
@@ -521,16 +521,28 @@ def next_rows(a):
     rec("f4_ln_l2_fwd", graph_us(lambda: ops.layernorm_l2_normalize(hproj, gam, bet, 1e-5), 20),
         R * H * 4 * 2 + R * 12, graph_us(lambda: torch.nn.functional.normalize(
             torch.nn.functional.layer_norm(hproj, (H,), gam, bet, 1e-5), dim=-1), 20))
-    hp = hproj.detach().requires_grad_(True)
-    gp, bp = gam.detach().requires_grad_(True), bet.detach().requires_grad_(True)
-    yv = ops.layernorm_l2_normalize(hp, gp, bp, 1e-5)
-    # backward passes timed eagerly (HIP events around back-to-back autograd calls)
-    rec("f4_ln_l2_bwd", event_us(lambda: torch.autograd.grad(yv, (hp, gp, bp), dy, retain_graph=True), 20),
-        R * H * 4 * 3 + R * 12 + 2 * H * 4)
-    xp, Wp, bb = x.detach().requires_grad_(True), W.detach().requires_grad_(True), b.detach().requires_grad_(True)
-    yl = ops.linear(xp, Wp, bb)
-    rec("f4_linear_bwd", event_us(lambda: torch.autograd.grad(yl, (xp, Wp, bb), dy, retain_graph=True), 20),
-        R * H * 4 * 2 + R * E * 4 * 2 + H * E * 4, note="dx (MFMA) + dW, db")
+    # backward launches called directly (autograd's own host time left out; graph replay)
+    stats = torch.empty(R, 3, device=DEV)
+    yv = torch.empty_like(hproj)
+    call("tt_ln_l2_fwd", ptr(hproj), R, H, ptr(gam), ptr(bet), 1e-5, ptr(yv), ptr(stats),
+         torch.cuda.current_stream().cuda_stream)
+    dxl, gx, gb = (torch.empty_like(hproj) for _ in range(3))
+
+    def ln_bwd():
+        call("tt_ln_l2_bwd", ptr(dy), ptr(hproj), R, H, ptr(gam), ptr(bet), ptr(stats), ptr(dxl), ptr(gx), ptr(gb),
+             torch.cuda.current_stream().cuda_stream)
+        return ops.colsum(gx), ops.colsum(gb)
+
+    rec("f4_ln_l2_bwd", graph_us(ln_bwd, 20), R * H * 4 * 3 + R * 12 + 2 * H * 4,
+        note="row pass (dx, and the per-row gamma / beta terms) + two column sums")
+    PWt = ops._planes(W, True)
+
+    def lin_bwd():
+        dx = ops._head_gemm(dy, PWt, 3, N=E)
+        return dx, ops.head_wgrad(dy, x)
+
+    rec("f4_linear_bwd", graph_us(lin_bwd, 20), R * H * 4 * 2 + R * E * 4 * 2 + H * E * 4,
+        note="dx (tt_head_gemm epi 3) + dW, db (tt_head_wgrad_ex)")
     path = a.shape
     if path:
         with open(path, "w") as f:

@@ -124,6 +124,96 @@ __global__ __launch_bounds__(kBlock) void cosine_scores_kernel(const float* __re
   }
 }
 
+// ---- cosine scores on the matrix cores, for passes of more than kVALUMaxQ queries: the same sums
+// as Q^ D^T with v_mfma_f32_32x32x2_f32 (fp32 products and accumulation).  A wave owns a tile of
+// 32 documents (the B operand, staged through its LDS image in kMFC-feature chunks) against the
+// pass's 32 or 64 normalised queries (the A operand, resident in LDS).  Step s of an 8-feature
+// block pairs features (8b + s, 8b + 4 + s): lane (row r32, half hh) supplies feature 8b + 4hh + s
+// of its query / document, so one 16-byte LDS read feeds four steps.  The document norms come
+// from the same staged chunks (each half sums its features, one exchange joins the halves), and
+// the accumulator layout gives each lane one document column: the division needs no shuffle.
+constexpr int kMDocs = 32;
+constexpr int kMFC = 64;
+constexpr int kMRowF = kMFC + 4;
+constexpr int kMLoads = kMDocs * kMFC / 4 / kWave;  // f32x4 staging loads per lane per chunk (8)
+constexpr int kVALUMaxQ = 8;
+
+template <int QT>
+__global__ __launch_bounds__(kBlock) void cosine_mfma_kernel(const float* __restrict__ q, int nq,
+                                                             const float* __restrict__ docs, int64_t nd, int H,
+                                                             float* __restrict__ scores, int64_t ld_scores) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int Hp = (H + kMFC - 1) / kMFC * kMFC, Hq = Hp + 4;
+  float* qs = smem;                                                // QT*32 x Hq normalised queries
+  const int lane = lane_id(), wid = threadIdx.x >> 6, r32 = lane & 31, hh = lane >> 5;
+  float* dl = smem + QT * 32 * Hq + wid * (kMDocs * kMRowF);
+  for (int i = wid; i < QT * 32; i += kBlock / kWave) {
+    float ss = 0.f;
+    if (i < nq)
+      for (int h = lane; h < H; h += kWave) ss += q[(int64_t)i * H + h] * q[(int64_t)i * H + h];
+    const float inv = 1.f / fmaxf(sqrtf(wave_sum(ss)), kCosEps);
+    for (int h = lane; h < Hp; h += kWave) qs[i * Hq + h] = (i < nq && h < H) ? q[(int64_t)i * H + h] * inv : 0.f;
+  }
+  __syncthreads();
+  const int nchunks = Hp / kMFC;
+  const int64_t ntiles = (nd + kMDocs - 1) / kMDocs;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / kWave);
+  const int srow = lane >> 4, scol = (lane & 15) * 4;  // staging: load u = row 4u + srow, features scol..+3
+  for (int64_t t = (int64_t)blockIdx.x * (kBlock / kWave) + wid; t < ntiles; t += wstride) {
+    const int64_t j0 = t * kMDocs;
+    auto load_chunk = [&](int c, f32x4 (&r)[kMLoads]) {
+#pragma unroll
+      for (int u = 0; u < kMLoads; ++u) {
+        int64_t j = j0 + 4 * u + srow;
+        j = j < nd ? j : nd - 1;  // rows past the end: a clamped row, never stored
+        const int f = c * kMFC + scol;
+        r[u] = f < H ? *reinterpret_cast<const f32x4*>(docs + j * H + f) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    f32x4 cur[kMLoads];
+    load_chunk(0, cur);
+    f32x16 acc[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) acc[qt] = f32x16{};
+    float ssp = 0.f;
+    for (int c = 0; c < nchunks; ++c) {
+#pragma unroll
+      for (int u = 0; u < kMLoads; ++u) *reinterpret_cast<f32x4*>(dl + (4 * u + srow) * kMRowF + scol) = cur[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (c + 1 < nchunks) load_chunk(c + 1, cur);
+#pragma unroll
+      for (int b = 0; b < kMFC / 8; ++b) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(dl + r32 * kMRowF + 8 * b + 4 * hh);
+        ssp += bv[0] * bv[0] + bv[1] * bv[1] + bv[2] * bv[2] + bv[3] * bv[3];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          const f32x4 av = *reinterpret_cast<const f32x4*>(qs + (qt * 32 + r32) * Hq + c * kMFC + 8 * b + 4 * hh);
+#pragma unroll
+          for (int st = 0; st < 4; ++st)
+            acc[qt] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], bv[st], acc[qt], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads of this image before the next writes
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const float ss = ssp + __shfl_xor(ssp, 32);
+    const float inv = 1.f / fmaxf(sqrtf(ss), kCosEps);
+    const int64_t j = j0 + r32;
+    if (j < nd) {
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int i = qt * 32 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+          if (i < nq) scores[(int64_t)i * ld_scores + j] = acc[qt][v] * inv;
+        }
+    }
+  }
+}
+
 // order-preserving image: larger float -> larger unsigned
 __device__ __forceinline__ uint32_t f2key(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -329,14 +419,33 @@ extern "C" int tt_cosine_scores(const float* q, int64_t nq, const float* docs, i
   int qcap = kQMax;
   while (qcap > 1 && doc_lds + qcap * q_row > 160 * 1024) qcap >>= 1;
   TT_REQUIRE(doc_lds + q_row <= 160 * 1024, "H=%d too large for the cosine kernel's LDS", H);
-  for (int64_t i0 = 0; i0 < nq; i0 += qcap) {
-    const int n = (int)std::min<int64_t>(qcap, nq - i0);
+  // the matrix-core form: 64 (or 32) queries per pass when its LDS fits
+  const int Hm = (H + kMFC - 1) / kMFC * kMFC;
+  const size_t mdoc_lds = (size_t)(kBlock / kWave) * kMDocs * kMRowF * 4, mq_rows = (size_t)(Hm + 4) * 4 * 32;
+  const int mqt = mdoc_lds + 2 * mq_rows <= 160 * 1024 ? 2 : mdoc_lds + mq_rows <= 160 * 1024 ? 1 : 0;
+  const int64_t mtiles = (nd + kMDocs - 1) / kMDocs;
+  for (int64_t i0 = 0; i0 < nq;) {
+    const int64_t rest = nq - i0;
+    const float* qi = q + i0 * H;
+    float* si = scores + i0 * nd;
+    if (mqt > 0 && rest > kVALUMaxQ) {
+      const int n = (int)std::min<int64_t>(32 * mqt, rest);
+      const int QT = n > 32 ? 2 : 1;
+      const size_t lds = mdoc_lds + QT * mq_rows;
+      const unsigned grid = (unsigned)std::min<int64_t>((mtiles + 3) / 4, 256 * 4);
+      if (QT == 2)
+        cosine_mfma_kernel<2><<<dim3(grid), dim3(kBlock), lds, s>>>(qi, n, docs, nd, H, si, nd);
+      else
+        cosine_mfma_kernel<1><<<dim3(grid), dim3(kBlock), lds, s>>>(qi, n, docs, nd, H, si, nd);
+      TT_LAUNCH_CHECK("tt_cosine_scores (mfma)");
+      i0 += n;
+      continue;
+    }
+    const int n = (int)std::min<int64_t>(qcap, rest);
     const int QP = n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : n <= 16 ? 16 : 32;
     const size_t lds = doc_lds + (size_t)QP * q_row;
     // one tile per wave until every CU holds a workgroup, then the waves walk tiles
     const unsigned grid = (unsigned)std::min<int64_t>((ntiles + 3) / 4, 256 * 4);
-    const float* qi = q + i0 * H;
-    float* si = scores + i0 * nd;
     switch (QP) {
 #define TT_COS_CASE(P)                                                                                         \
   case P:                                                                                                      \
@@ -346,6 +455,7 @@ extern "C" int tt_cosine_scores(const float* q, int64_t nq, const float* docs, i
 #undef TT_COS_CASE
     }
     TT_LAUNCH_CHECK("tt_cosine_scores");
+    i0 += n;
   }
   return TT_OK;
 }
