@@ -249,6 +249,13 @@ int tt_ln_l2_fwd(const float* x, int64_t rows, int H, const float* gamma, const 
                  float* stats, tt_stream_t stream);
 int tt_ln_l2_bwd(const float* dout, const float* x, int64_t rows, int H, const float* gamma, const float* beta,
                  const float* stats, float* dx, float* gx, float* gb, tt_stream_t stream);
+/* tt_ln_l2_bwd_ex: dx and the gamma / beta gradients themselves (the per-row terms folded over
+ * each workgroup's rows, then column-summed; fixed order), with a workspace of
+ * tt_ln_l2_bwd_ws_size bytes; H even, <= 1024. */
+size_t tt_ln_l2_bwd_ws_size(int64_t rows, int H);
+int tt_ln_l2_bwd_ex(const float* dout, const float* x, int64_t rows, int H, const float* gamma, const float* beta,
+                    const float* stats, float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+                    tt_stream_t stream);
 
 /* ---- column sum (bias gradient of nn.Linear: grad_out.sum(0); twotower/encoders.py:38-42) ----
  * out[c] = sum_r x[r, c] in a fixed order (deterministic): per-block partial sums over row

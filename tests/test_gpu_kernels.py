@@ -1118,7 +1118,7 @@ def test_device_feeder_gather_equals_index_select(N, L, B):
     assert not store.bad_index()
 
 
-@pytest.mark.parametrize("rows,H", [(37, 24), (1000, 256), (5, 1024)])
+@pytest.mark.parametrize("rows,H", [(37, 24), (1000, 256), (5, 1024), (24576, 128), (3000, 200), (7, 2048)])
 def test_layernorm_l2_normalize_vs_torch_fp64(rows, H):
     rng = np.random.default_rng(rows + H)
     x = rng.standard_normal((rows, H)).astype(np.float32) * 3 + 1

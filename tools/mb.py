@@ -528,13 +528,21 @@ def next_rows(a):
          torch.cuda.current_stream().cuda_stream)
     dxl, gx, gb = (torch.empty_like(hproj) for _ in range(3))
 
-    def ln_bwd():
+    def ln_bwd_unfolded():
         call("tt_ln_l2_bwd", ptr(dy), ptr(hproj), R, H, ptr(gam), ptr(bet), ptr(stats), ptr(dxl), ptr(gx), ptr(gb),
              torch.cuda.current_stream().cuda_stream)
         return ops.colsum(gx), ops.colsum(gb)
 
+    dg, dbt = torch.empty(H, device=DEV), torch.empty(H, device=DEV)
+    wsl = torch.empty(_lib.lib().tt_ln_l2_bwd_ws_size(R, H), dtype=torch.uint8, device=DEV)
+
+    def ln_bwd():
+        call("tt_ln_l2_bwd_ex", ptr(dy), ptr(hproj), R, H, ptr(gam), ptr(bet), ptr(stats), ptr(dxl), ptr(dg),
+             ptr(dbt), ptr(wsl), wsl.numel(), torch.cuda.current_stream().cuda_stream)
+
     rec("f4_ln_l2_bwd", graph_us(ln_bwd, 20), R * H * 4 * 3 + R * 12 + 2 * H * 4,
-        note="row pass (dx, and the per-row gamma / beta terms) + two column sums")
+        graph_us(ln_bwd_unfolded, 20), note="dx + dgamma, dbeta folded per workgroup, then column-summed (tt_ln_l2_bwd_ex); "
+        "torch_us column: the per-row terms written out + two tt_colsum launches (round 4 form)")
     PWt = ops._planes(W, True)
 
     def lin_bwd():

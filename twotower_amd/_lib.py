@@ -94,6 +94,8 @@ _SIGNATURES = {
                                        _vp, _c_int, _vp]),
     "tt_ln_l2_fwd": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_f32, _vp, _vp, _vp]),
     "tt_ln_l2_bwd": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "tt_ln_l2_bwd_ws_size": (_c_sz, [_c_i64, _c_int]),
+    "tt_ln_l2_bwd_ex": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_head_planes_bytes": (_c_sz, [_c_int, _c_int]),
     "tt_head_split": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "tt_head_split_ff": (_c_int, [_vp, _vp, _vp, _vp]),

@@ -132,6 +132,83 @@ __global__ __launch_bounds__(kBlock) void ln_l2_bwd_kernel(const float* __restri
   }
 }
 
+// The same backward with the gamma / beta terms folded over each workgroup's 4 rows before they
+// are written (ln_l2_bwd_kernel writes them per row for two column-sum launches: 2 x 2 full
+// passes of extra traffic).  One wave per row as there (lane l: columns l + 64 u); the
+// workgroup folds its 4 waves in a fixed order into row blockIdx.x of part (nwg x 2H: gamma
+// terms, then beta terms), whose columns the colsum kernels then sum in a fixed order.  dx is
+// the same arithmetic as ln_l2_bwd_kernel's, element for element.
+template <int U>
+__global__ __launch_bounds__(kBlock) void ln_l2_bwd_fold_kernel(const float* __restrict__ dout,
+                                                                const float* __restrict__ x, int64_t rows, int H,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta,
+                                                                const float* __restrict__ stats,
+                                                                float* __restrict__ dx, float* __restrict__ part) {
+  __shared__ float red[kWavesPerBlock][2][U * kWave];
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  float gam[U], bet[U], ga[U], ba[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = lane + kWave * u;
+    gam[u] = c < H ? gamma[c] : 0.f;
+    bet[u] = c < H ? beta[c] : 0.f;
+    ga[u] = ba[u] = 0.f;
+  }
+  const int64_t r = wave_row();
+  if (r < rows) {
+    const float mean = stats[3 * r], rstd = stats[3 * r + 1], nrm = stats[3 * r + 2];
+    const float den = fmaxf(nrm, 1e-12f);
+    float xh[U], d[U], sy = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = lane + kWave * u;
+      xh[u] = d[u] = 0.f;
+      if (c < H) {
+        xh[u] = (x[r * H + c] - mean) * rstd;
+        d[u] = dout[r * H + c];
+        sy += d[u] * (xh[u] * gam[u] + bet[u]);
+      }
+    }
+    const float coef = (nrm >= 1e-12f && nrm > 0.f) ? wave_sum(sy) / (den * den * nrm) : 0.f;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (lane + kWave * u < H) {
+        const float dy = d[u] / den - coef * (xh[u] * gam[u] + bet[u]);
+        ga[u] += dy * xh[u];
+        ba[u] += dy;
+        const float dxh = dy * gam[u];
+        a += dxh;
+        b += dxh * xh[u];
+        d[u] = dy;
+      }
+    }
+    a = wave_sum(a) / (float)H;
+    b = wave_sum(b) / (float)H;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = lane + kWave * u;
+      if (c < H) dx[r * H + c] = rstd * (d[u] * gam[u] - a - xh[u] * b);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    red[wid][0][lane + kWave * u] = ga[u];
+    red[wid][1][lane + kWave * u] = ba[u];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += kBlock) {
+    float g = red[0][0][c], bb = red[0][1][c];
+    for (int w = 1; w < kWavesPerBlock; ++w) {
+      g += red[w][0][c];
+      bb += red[w][1][c];
+    }
+    part[(int64_t)blockIdx.x * 2 * H + c] = g;
+    part[(int64_t)blockIdx.x * 2 * H + H + c] = bb;
+  }
+}
+
 struct CosStats {
   float dot, n1, n2;  // raw dot and unclamped norms
 };
@@ -561,6 +638,63 @@ extern "C" int tt_colsum(const float* x, int64_t rows, int cols, float* out, voi
   colsum_partial_kernel<<<dim3(nblk, (cols + 255) / 256), dim3(256), 0, s>>>(x, rows, cols, static_cast<float*>(ws));
   colsum_final_kernel<<<dim3((cols + 63) / 64), dim3(256), 0, s>>>(static_cast<const float*>(ws), nblk, cols, out);
   TT_LAUNCH_CHECK("tt_colsum");
+  return TT_OK;
+}
+
+extern "C" size_t tt_ln_l2_bwd_ws_size(int64_t rows, int H) {
+  const int64_t nwg = (std::max<int64_t>(rows, 1) + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int64_t nblk = (nwg + kColRows - 1) / kColRows;
+  return (size_t)(nwg + nblk) * 2 * (size_t)H * sizeof(float) + 2 * (size_t)H * sizeof(float);
+}
+
+// dgamma / dbeta land in the workspace's tail (2H floats) and are copied out: the column sums of
+// the (nwg x 2H) fold are one colsum over 2H columns (2H % 4 == 0: H even).
+__global__ void split_pair_kernel(const float* __restrict__ v, int H, float* __restrict__ a, float* __restrict__ b) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < H) {
+    a[c] = v[c];
+    b[c] = v[H + c];
+  }
+}
+
+extern "C" int tt_ln_l2_bwd_ex(const float* dout, const float* x, int64_t rows, int H, const float* gamma,
+                               const float* beta, const float* stats, float* dx, float* dgamma, float* dbeta, void* ws,
+                               size_t ws_bytes, tt_stream_t stream) {
+  TT_REQUIRE(rows >= 0 && H > 0 && H <= 16 * kWave && H % 2 == 0, "bad shape rows=%lld H=%d (H even, <= 1024)",
+             (long long)rows, H);
+  TT_REQUIRE(gamma && beta && dgamma && dbeta, "null pointer");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    TT_HIP(hipMemsetAsync(dgamma, 0, (size_t)H * 4, s), "memset dgamma");
+    TT_HIP(hipMemsetAsync(dbeta, 0, (size_t)H * 4, s), "memset dbeta");
+    return TT_OK;
+  }
+  TT_REQUIRE(dout && x && stats && dx && ws, "null pointer");
+  TT_REQUIRE(ws_bytes >= tt_ln_l2_bwd_ws_size(rows, H), "workspace too small");
+  const int64_t nwg = (rows + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int cols = 2 * H;
+  float* part = static_cast<float*>(ws);
+  float* cpart = part + nwg * cols;
+  float* both = cpart + ((nwg + kColRows - 1) / kColRows) * cols;
+  const int U = (H + kWave - 1) / kWave;
+#define TT_LNF(UU)                                                                                           \
+  ln_l2_bwd_fold_kernel<UU><<<dim3((unsigned)nwg), dim3(kBlock), 0, s>>>(dout, x, rows, H, gamma, beta, stats, dx, part)
+  if (U <= 1)
+    TT_LNF(1);
+  else if (U <= 2)
+    TT_LNF(2);
+  else if (U <= 4)
+    TT_LNF(4);
+  else if (U <= 8)
+    TT_LNF(8);
+  else
+    TT_LNF(16);
+#undef TT_LNF
+  const int nblk = (int)((nwg + kColRows - 1) / kColRows);
+  colsum_partial_kernel<<<dim3(nblk, (cols + 255) / 256), dim3(256), 0, s>>>(part, nwg, cols, cpart);
+  colsum_final_kernel<<<dim3((cols + 63) / 64), dim3(256), 0, s>>>(cpart, nblk, cols, both);
+  split_pair_kernel<<<dim3((H + 255) / 256), dim3(256), 0, s>>>(both, H, dgamma, dbeta);
+  TT_LAUNCH_CHECK("tt_ln_l2_bwd_ex");
   return TT_OK;
 }
 

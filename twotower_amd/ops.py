@@ -594,7 +594,15 @@ class LayerNormL2Normalize(torch.autograd.Function):
         x, gamma, beta, stats = ctx.saved_tensors
         dout = _contig_f32(dout, "dout")
         rows, H = x.shape
-        dx, gx, gb = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+        dx = torch.empty_like(x)
+        if H <= 1024 and H % 2 == 0:  # dgamma / dbeta folded per workgroup (tt_ln_l2_bwd_ex)
+            dg, db = torch.empty(H, dtype=_FLOAT, device=x.device), torch.empty(H, dtype=_FLOAT, device=x.device)
+            nbytes = _lib.lib().tt_ln_l2_bwd_ws_size(rows, H)
+            ws = WORKSPACE.get("ln_l2_bwd", nbytes, x.device)
+            call("tt_ln_l2_bwd_ex", ptr(dout), ptr(x), rows, H, ptr(gamma), ptr(beta), ptr(stats), ptr(dx), ptr(dg),
+                 ptr(db), ptr(ws), ws.numel(), stream_of(x))
+            return dx, dg, db, None
+        gx, gb = torch.empty_like(x), torch.empty_like(x)
         call("tt_ln_l2_bwd", ptr(dout), ptr(x), rows, H, ptr(gamma), ptr(beta), ptr(stats), ptr(dx), ptr(gx),
              ptr(gb), stream_of(x))
         return dx, colsum(gx), colsum(gb), None
