@@ -229,6 +229,7 @@ template <class Emit>
 __device__ __forceinline__ void topk_block(const float* __restrict__ row, int64_t ncols, int k, Emit emit) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t sel_prefix, sel_mask, sel_need;  // digits fixed so far, how many still to take
+  __shared__ uint32_t sel_all;  // every key under the fixed digits is taken: no further digit needed
   __shared__ uint32_t n_above, n_tie;
   __shared__ uint32_t skey[kTopkMax];
   __shared__ int32_t sidx[kTopkMax];
@@ -237,6 +238,7 @@ __device__ __forceinline__ void topk_block(const float* __restrict__ row, int64_
     sel_prefix = 0;
     sel_mask = 0;
     sel_need = (uint32_t)k;
+    sel_all = 0;
   }
   // 1. radix select of the k-th largest key, most significant digit first
   for (int shift = 24; shift >= 0; shift -= 8) {
@@ -272,9 +274,11 @@ __device__ __forceinline__ void topk_block(const float* __restrict__ row, int64_
         sel_prefix = pre | (d << shift);
         sel_mask = msk | (255u << shift);
         sel_need = need;  // how many keys equal to the final threshold are taken
+        sel_all = hist[d] == need;
       }
     }
     __syncthreads();
+    if (sel_all) break;  // the digit's whole bucket is taken: the lower digits decide nothing
   }
   const uint32_t thr = sel_prefix, take_eq = sel_need;
   // 2. collect: every key above the threshold, then the take_eq lowest-index keys equal to it
@@ -287,8 +291,22 @@ __device__ __forceinline__ void topk_block(const float* __restrict__ row, int64_
     sidx[i] = 0x7fffffff;
   }
   __syncthreads();
+  if (sel_all) {
+    // every key whose fixed digits reach the threshold's is taken (exactly k): slots in any order,
+    // the sort below orders them
+    const uint32_t msk = sel_mask;
+    for (int64_t j = tid; j < ncols; j += kBlock) {
+      const uint32_t key = f2key(row[j]);
+      if ((key & msk) >= thr) {
+        const uint32_t slot = atomicAdd(&n_above, 1u);
+        skey[slot] = key;
+        sidx[slot] = (int32_t)j;
+      }
+    }
+    __syncthreads();
+  }
   const uint32_t above_total = (uint32_t)k - take_eq;
-  for (int64_t j0 = 0; j0 < ncols; j0 += kBlock) {
+  for (int64_t j0 = 0; j0 < (sel_all ? 0 : ncols); j0 += kBlock) {
     const int64_t j = j0 + tid;
     uint32_t key = 0;
     bool eq = false;
