@@ -551,6 +551,26 @@ def next_rows(a):
 
     rec("f4_linear_bwd", graph_us(lin_bwd, 20), R * H * 4 * 2 + R * E * 4 * 2 + H * E * 4,
         note="dx (tt_head_gemm epi 3) + dW, db (tt_head_wgrad_ex)")
+    # a6 triplet loss (losses.py:9-44) at C3 rows: forward + backward kernels against the reference's
+    # torch expression (F.cosine_similarity, relu, mean) forward + backward
+    Bt, Ht = 8192, 256
+    qt_, pt_, nt_ = (torch.randn(Bt, Ht, device=DEV, generator=g) for _ in range(3))
+    dq_, dp_, dn_ = (torch.empty(Bt, Ht, device=DEV) for _ in range(3))
+    gl = torch.ones(1, device=DEV)
+
+    def trip():
+        ops._triplet_fwd(qt_, pt_, nt_, 0.2)
+        ops._triplet_bwd(qt_, pt_, nt_, 0.2, gl, dq_, dp_, dn_)
+
+    qr, pr, nr = (t.clone().requires_grad_(True) for t in (qt_, pt_, nt_))
+
+    def trip_torch():
+        F = torch.nn.functional
+        loss = F.relu(0.2 - F.cosine_similarity(qr, pr, dim=1) + F.cosine_similarity(qr, nr, dim=1)).mean()
+        return torch.autograd.grad(loss, (qr, pr, nr))
+
+    rec("a6_triplet_fwd_bwd", graph_us(trip, 20), Bt * Ht * 4 * 6, event_us(trip_torch, 20),
+        note="reads q, p, n twice (fwd, bwd), writes dq, dp, dn; torch_us: eager autograd of the reference expression")
     path = a.shape
     if path:
         with open(path, "w") as f:
