@@ -41,10 +41,10 @@ def _table_of(embedding: nn.Module) -> torch.Tensor | None:
 def _planes_in_gather(tower: nn.Module, ids: torch.Tensor):
     """The gather feeding this tower's hand-written head also forms the head's weight planes
     (ops.head_planes_in_gather)."""
-    if (ids.is_cuda and type(tower).encode_pooled is MeanPoolingTower.encode_pooled
-            and tower.hand_written_head()):
-        ff = tower.feed_forward
-        return ops.head_planes_in_gather(ff[0].weight, ff[2].weight)
+    if ids.is_cuda and type(tower).encode_pooled is MeanPoolingTower.encode_pooled:
+        ff = tower._layers()
+        if tower.hand_written_head(ff):
+            return ops.head_planes_in_gather(ff[0].weight, ff[2].weight)
     return contextlib.nullcontext()
 
 
@@ -92,27 +92,32 @@ class MeanPoolingTower(BaseTower):
         )
         self.log_params()
 
-    def _standard_ff(self) -> bool:
+    def _layers(self) -> tuple:
+        """feed_forward's modules (one dict read: nn.Sequential indexing costs a few us per item,
+        and the fused forward asks for the layers a dozen times per step)."""
         ff = self.feed_forward
+        return tuple(ff._modules.values()) if isinstance(ff, nn.Sequential) else ()
+
+    def _standard_ff(self, ff: tuple | None = None) -> bool:
+        ff = self._layers() if ff is None else ff
         return (len(ff) == 3 and isinstance(ff[0], nn.Linear) and isinstance(ff[1], nn.ReLU)
                 and isinstance(ff[2], nn.Linear) and ff[0].bias is not None and ff[2].bias is not None)
 
-    def hand_written_head(self) -> bool:
+    def hand_written_head(self, ff: tuple | None = None) -> bool:
         """The head runs on ops.tower_head (the hand-written split-bf16 GEMMs)."""
-        ff = self.feed_forward
-        return (self._standard_ff() and ff[0].out_features == ff[2].out_features == ff[2].in_features
+        ff = self._layers() if ff is None else ff
+        return (self._standard_ff(ff) and ff[0].out_features == ff[2].out_features == ff[2].in_features
                 in ops.HEAD_WIDTHS and ff[0].in_features in ops.EMB_WIDTHS)
 
     def encode_pooled(self, pooled: torch.Tensor) -> torch.Tensor:
-        ff = self.feed_forward
-        standard = self._standard_ff()
-        if self.hand_written_head():
+        ff = self._layers()
+        if self.hand_written_head(ff):
             # Linear-ReLU-Linear + F.normalize in two fused GEMM launches (encoders.py:38-42,77)
             return ops.tower_head(pooled.contiguous(), ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
-        if standard and ff[0].out_features % 4 == 0 and ff[2].out_features % 4 == 0:
+        if self._standard_ff(ff) and ff[0].out_features % 4 == 0 and ff[2].out_features % 4 == 0:
             y = ops.tower_ff(pooled.contiguous(), ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
         else:  # a user-modified head (or widths off the vec4 column-sum): run it as given
-            y = ff(pooled)
+            y = self.feed_forward(pooled)
         return ops.l2_normalize(y)  # encoders.py:77
 
 

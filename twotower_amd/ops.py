@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import functools
 import os
 
 import torch
@@ -74,6 +75,7 @@ _PLANES_REQ: list = []  # (W1, W2) whose planes the next bag gather forms (open 
 _PLANES_DONE: dict = {}  # (W1, W2 data_ptr) -> planes that gather formed, taken by that head's TowerHead
 
 
+@functools.lru_cache(maxsize=None)
 def _head_planes_bytes(E: int, H: int) -> tuple[int, int]:
     return _lib.lib().tt_head_planes_bytes(H, E), _lib.lib().tt_head_planes_bytes(H, H)
 
