@@ -577,10 +577,23 @@ def next_rows(a):
             json.dump(out, f, indent=1)
 
 
+def search_once(a):
+    """Cosine scores of 1 and of 64 queries over a 1M x 256 index and the top 10 of each row, five
+    times each, nothing else (counter passes: tools/profile_mb.sh)."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    docs = torch.randn(1_000_000, 256, device=DEV, generator=g)
+    for nq in (1, 64):
+        q = torch.randn(nq, 256, device=DEV, generator=g)
+        for _ in range(5):
+            ops.topk_rows(ops.cosine_scores(q, docs), 10)
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
-                                     "column_sync", "l2prep", "scorer_once", "head_once", "next_rows"])
+                                     "column_sync", "l2prep", "scorer_once", "head_once", "next_rows",
+                                     "search_once"])
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")
     ap.add_argument("--zipf", type=float, default=None)

@@ -113,16 +113,18 @@ def main(outdir: str, tag: str):
         with open(stats) as fh:
             ks = list(csv.DictReader(fh))
         scope = "the whole run (incl. warmup and set-up; no window markers in the trace)"
-    # steps profiled = calls of the bag forward kernel (one launch per step)
-    steps = max(int(r["Calls"]) for r in ks if "bag_fwd" in r["Name"])
+    # steps profiled = calls of the bag forward kernel (one launch per step); a trace without it
+    # (a tools/mb.py run, tools/profile_mb.sh) is reported per launch, "calls/step" = calls
+    steps = max((int(r["Calls"]) for r in ks if "bag_fwd" in r["Name"]), default=1)
     fetch = defaultdict(list)
     write = defaultdict(list)
     for n, v in pmc(os.path.join(outdir, "fetch"), "FETCH_SIZE"):
         fetch[n].append(v * 1024 * 2)
     for n, v in pmc(os.path.join(outdir, "write"), "WRITE_SIZE"):
         write[n].append(v * 1024)
-    lines = [f"# Profile {tag}", "", "Source: `tools/profile_round.sh` (rocprofv3 --kernel-trace --stats; separate "
-             "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes) over `bench.py`.", "",
+    lines = [f"# Profile {tag}", "", "Source: `tools/profile_round.sh` over `bench.py`, or `tools/profile_mb.sh` over `tools/mb.py` when "
+             "no bag kernel is in the trace (rocprofv3 --kernel-trace --stats; separate --pmc FETCH_SIZE and "
+             "--pmc WRITE_SIZE passes).", "",
              f"Steps covered: {steps}, {scope}", "",
              "| kernel | op | calls/step | avg us | us/step | fetch MB/launch | write MB/launch |",
              "|---|---|---|---|---|---|---|"]
