@@ -517,10 +517,12 @@ def parse():
                          "size 1, TT_DIST_FORCE=1), e.g. to check the N-rank step under HIP-graph capture on one GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--table-sync", default="auto", choices=["auto", "gather", "shard", "owner", "column"],
+    ap.add_argument("--table-sync", default="best", choices=["best", "auto", "gather", "shard", "owner", "column"],
                     help="N ranks: table update from gathered ids + row grads on every rank (gather), row-sharded "
-                         "AdamW after a gradient reduce-scatter (shard), or each rank's own rows from the gathered "
-                         "factored gradient (owner); auto picks gather up to 4 ranks")
+                         "AdamW after a gradient reduce-scatter (shard), each rank's own rows from the gathered "
+                         "factored gradient (owner), or each rank's own columns of every row (column); auto (the "
+                         "library default) picks gather up to 4 ranks, shard beyond; best (this bench's default) "
+                         "takes column wherever the width splits into the column kernels' slabs, else auto")
     ap.add_argument("--timing-steps", type=int, default=10, help="eager steps timed per op after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-batch", type=int, default=8192,
@@ -610,6 +612,8 @@ def main():
     V, d, L, B = cfg["V"], cfg["d"], cfg["L"], cfg["B"]
     scorer_dtype = args.scorer_dtype or cfg["dtype"]
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.table_sync == "best":  # the scaling choice, opt-in in the library
+        args.table_sync = "column" if dp and tt.distributed.column_ok(d, max(world, 1)) else "auto"
 
     emb, model = build_model(cfg, dev)
     K = cfg["negatives"]

@@ -176,6 +176,16 @@ int tt_bag_scale_rows(const float* d_pooled, const float* denom, int64_t nseq, i
 int tt_bag_col_reduce(const int32_t* seg_all, const int32_t* vals_all, int64_t nL, int nsrc, int64_t nseq,
                       const float* gs_all, int64_t V, int El, float* grad, float* slab, float* exp_avg,
                       float* exp_avg_sq, const void* adam_args, tt_stream_t stream);
+/* tt_bag_col_reduce with the hot-row path (embeddings.py:30 under Zipf ids; the 33-row character
+ * vocabulary of tokenisers.py:50,59): with a workspace of tt_bag_col_reduce_ws_size bytes, a row whose
+ * merged length exceeds 128 tokens is summed in pieces first (one sub-wave per piece, in the merged
+ * order), then folded -- the single-plan path's pieces and folds for rows of up to 32,768 merged tokens
+ * (bit for bit equal to tt_bag_mean_bwd(_adamw)_planned over the concatenated batch), up to 4,096
+ * pieces and a group level beyond.  ws == NULL: tt_bag_col_reduce (every row walked by one sub-wave). */
+size_t tt_bag_col_reduce_ws_size(int64_t V, int nsrc, int64_t nL, int El);
+int tt_bag_col_reduce_ex(const int32_t* seg_all, const int32_t* vals_all, int64_t nL, int nsrc, int64_t nseq,
+                         const float* gs_all, int64_t V, int El, float* grad, float* slab, float* exp_avg,
+                         float* exp_avg_sq, const void* adam_args, void* ws, size_t ws_bytes, tt_stream_t stream);
 
 /* ---- dense AdamW (torch.optim.AdamW, twotower/train.py:359, .step() :139) ---------
  * p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2*v + (1-b2)*g*g;

@@ -6,7 +6,8 @@ The reference's top-level package does not import here (twotower/__init__.py pul
 and a huggingface_hub API that no longer exists), so its leaf modules are loaded through a
 namespace stub — the same modules its train.py uses:
   twotower/embeddings.py, twotower/encoders.py, twotower/losses.py, twotower/tokenisers.py,
-  dataset_factory/synthetic_generators.py (C1 text), torch.optim.AdamW (twotower/train.py:359).
+  dataset_factory/synthetic_generators.py (C1 text), torch.optim.AdamW (twotower/train.py:359),
+  inference/search/two_tower.py (the search fixture).
 
     python tests/golden/make_golden.py [/root/reference]
 """
@@ -31,6 +32,12 @@ def load_reference(root: str):
         sys.modules[pkg] = m
     mods = {n: importlib.import_module(f"twotower.{n}") for n in ("embeddings", "encoders", "losses", "tokenisers")}
     mods["gen"] = importlib.import_module("dataset_factory.synthetic_generators")
+    # inference/search/two_tower.py (its package __init__ also imports the GloVe search: skipped)
+    for pkg, sub in (("inference", "inference"), ("inference.search", os.path.join("inference", "search"))):
+        m = types.ModuleType(pkg)
+        m.__path__ = [os.path.join(root, sub)]
+        sys.modules[pkg] = m
+    mods["search"] = importlib.import_module("inference.search.two_tower")
     return mods
 
 
@@ -240,8 +247,48 @@ def case_avg_pool(R):
     return out
 
 
+def case_search(R):
+    """inference/search/two_tower.py:37-115: a seeded C1-shaped tied model (E 64, H 128) and the
+    reference's char tokeniser over generator text; TwoTowerSearch.index_documents then .search for
+    a few queries (top 10).  Stored: the documents' and queries' padded ids (max_len 64, the
+    reference's), the weights, the document embeddings, each query's embedding and its results
+    (scores and document indices)."""
+    random.seed(5)
+    gen = R["gen"]
+    docs, queries = [], []
+    while len(docs) < 300:
+        q, pos = gen.create_positive_pair()
+        _, neg = gen.create_negative_pair(q)
+        docs += [pos, neg]
+        if len(queries) < 6:
+            queries.append(q)
+    queries.append(docs[17])  # a query that is one of the documents: its own score is the top
+    tok = R["tokenisers"].build("char")
+    tok.fit(docs + queries)
+    torch.manual_seed(21)
+    emb = R["embeddings"].build("lookup", vocab_size=tok.vocab_size, embedding_dim=64)
+    model = R["encoders"].build_two_tower("mean", emb, hidden_dim=128, tied_weights=True)
+    engine = R["search"].TwoTowerSearch(model, tok, device="cpu")
+    engine.index_documents(docs)
+    enc = lambda t: tok.truncate_and_pad(tok.encode(t), 64)  # noqa: E731 (two_tower.py:56-61, :89-90)
+    out = dict(doc_ids=np.array([enc(d) for d in docs], dtype=np.int64),
+               query_ids=np.array([enc(q) for q in queries], dtype=np.int64),
+               doc_emb=engine.document_embeddings.numpy().copy(), **tied_model_params(model))
+    scores, index = [], []
+    for q in queries:
+        res = engine.search(q, top_k=10)
+        scores.append([r["score"] for r in res])
+        index.append([docs.index(r["document"]) if docs.count(r["document"]) == 1 else -1 for r in res])
+    with torch.no_grad():
+        out["query_emb"] = model.query_tower(torch.tensor(out["query_ids"])).numpy()
+    out["top_scores"] = np.array(scores, dtype=np.float64)
+    out["top_index"] = np.array(index, dtype=np.int64)  # -1: a duplicated document text (index ambiguous)
+    return out
+
+
 CASES = (("bag_tiny", case_bag_tiny), ("c1_step", case_c1_step), ("trajectory", case_trajectory),
-         ("losses", case_losses), ("state_dict", case_state_dict), ("avg_pool", case_avg_pool))
+         ("losses", case_losses), ("state_dict", case_state_dict), ("avg_pool", case_avg_pool),
+         ("search", case_search))
 
 
 def main():

@@ -361,10 +361,13 @@ def test_column_table_exchanges_gloo():
 def test_column_mode_selection(monkeypatch):
     monkeypatch.setattr(D, "is_active", lambda group=None: True)
     monkeypatch.setattr(D.dist, "get_world_size", lambda group=None: 8)
-    assert D.table_sync_mode("auto", None, E=256) == "column"   # C3 / C4 / C5 at N = 8: 32 columns each
-    assert D.table_sync_mode("auto", None, E=48) == "shard"     # 6 columns: no column kernel
-    assert D.table_sync_mode("column", None, E=256) == "column"
+    # "column" is opt-in (its forwards and state_dict() are collective); "auto" keeps a
+    # replicated table: gather up to 4 ranks, shard beyond
+    assert D.table_sync_mode("auto", None, E=256) == "shard"
+    assert D.table_sync_mode("auto", None, E=48) == "shard"
+    assert D.table_sync_mode("column", None, E=256) == "column"  # C3 / C4 / C5 at N = 8: 32 columns each
     monkeypatch.setattr(D.dist, "get_world_size", lambda group=None: 2)
-    assert D.table_sync_mode("auto", None, E=256) == "column"   # 128 columns each
-    assert D.table_sync_mode("auto", None, E=1024) == "gather"  # 512 columns: past the kernels' slabs
+    assert D.table_sync_mode("auto", None, E=256) == "gather"
+    assert D.table_sync_mode("column", None, E=256) == "column"  # 128 columns each
+    assert D.column_ok(256, 8) and D.column_ok(256, 2) and not D.column_ok(1024, 2)  # 512 columns: past the slabs
     assert not D.column_ok(256, 3) and D.column_ok(128, 4)

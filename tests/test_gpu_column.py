@@ -3,9 +3,10 @@ W "ranks" each sort their own sequences (tt_bag_plan), the plans are concatenate
 would deliver them, and tt_bag_col_reduce forms the gradient of each rank's column slab from every
 rank's tokens.  Checked against the float64 oracle's dense table gradient of the global batch
 (oracle.reference_math.bag_mean_bwd: embeddings.py:30 via train.py:138) at 1e-5, and bit for bit
-against the single-plan reduce of the concatenated batch at the same columns (tt_bag_mean_bwd_planned,
-rows without pieces: the merged per-source order and interleaved partial sums are the same), and the
-fused AdamW form against tt_bag_mean_bwd_adamw_planned likewise."""
+against the single-plan reduce of the concatenated batch at the same columns (tt_bag_mean_bwd_planned:
+the merged per-source order and interleaved partial sums are the same, and with the hot-row path,
+tt_bag_col_reduce_ex, so are the pieces of rows up to 32,768 merged tokens), and the fused AdamW form
+against tt_bag_mean_bwd_adamw_planned likewise."""
 import ctypes
 
 import numpy as np
@@ -32,9 +33,22 @@ def _plan_arrays(ids: torch.Tensor, V: int, El: int):
     return seg.clone(), vals.clone()
 
 
-def _setup(W, E, V, nseq, L, seed):
+def _ids(rng, kind, V, n, L):
+    """uniform ids; Zipf(1.05) ids (SURVEY section 8(d): the hottest rows hold a few % of all tokens);
+    "char": a 34-row character vocabulary (tokenisers.py:50,59: every row is a hot row); "hot": 60 %
+    of the tokens on one row (a row past kPieceT * kMaxPieces merged tokens: the group level)."""
+    if kind == "zipf":
+        return np.minimum(rng.zipf(1.05, size=(n, L)), V - 1)
+    if kind == "hot":
+        ids = rng.integers(1, V, size=(n, L))
+        ids[rng.random((n, L)) < 0.6] = 5
+        return ids
+    return rng.integers(0, V, size=(n, L))
+
+
+def _setup(W, E, V, nseq, L, seed, kind="uniform"):
     rng = np.random.default_rng(seed)
-    ids = rng.integers(0, V, size=(W * nseq, L))
+    ids = _ids(rng, kind, V, W * nseq, L)
     ids[np.arange(L)[None, :] >= rng.integers(0, L + 1, size=W * nseq)[:, None]] = 0  # ragged
     ids[0, :] = 0                      # an all-padding sequence
     ids[1, :] = V - 1                  # the last row, repeated
@@ -64,6 +78,85 @@ def test_column_reduce_equals_single_plan_and_oracle(W, E):
         assert torch.equal(grad, want), (c, float((grad - want).abs().max()))
         o = oracle[:, c * El:(c + 1) * El]
         assert np.abs(grad.double().cpu().numpy() - o).max() / np.abs(o).max() < 1e-5
+
+
+def _col_reduce_ex(seg_all, vals_all, nL, W, nseq, gs_all, V, El, grad=None, slab=None, m=None, v=None, args=None):
+    n = _lib.lib().tt_bag_col_reduce_ws_size(V, W, nL, El)
+    ws = torch.empty(n, dtype=torch.uint8, device=DEV)
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    ops.call("tt_bag_col_reduce_ex", seg_all.data_ptr(), vals_all.data_ptr(), nL, W, nseq, gs_all.data_ptr(), V, El,
+             p(grad), p(slab), p(m), p(v), p(args), ws.data_ptr(), n, _lib.stream_of(gs_all))
+
+
+@pytest.mark.parametrize("kind,V", [("zipf", 3001), ("char", 34), ("uniform", 3001)])
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_column_reduce_hot_rows(kind, V, W):
+    """The hot-row path (tt_bag_col_reduce_ex: rows of more than 128 merged tokens summed in pieces,
+    one sub-wave each, then folded) under Zipf(1.05) ids and C1's 34-row character vocabulary, at
+    W = 2 / 4 / 8 (El 128 / 64 / 32): every row is at most 32,768 merged tokens here, where the piece
+    partition is the single plan's, so the gradient equals the single-plan reduce of the concatenated
+    batch bit for bit, and the float64 oracle's dense table gradient at 1e-5; the fused AdamW form
+    equals tt_bag_mean_bwd_adamw_planned bit for bit."""
+    E, nseq, L = 256, 192, 40
+    El = E // W
+    ids, ids_t, gs, seg_all, vals_all = _setup(W, E, V, nseq, L, seed=31 * W + V, kind=kind)
+    lens = np.bincount(ids[ids > 0].ravel(), minlength=V)
+    if kind != "uniform":
+        assert lens.max() > 128  # the piece path runs
+    assert lens.max() <= 128 * 256
+    whole = ops.bag_mean_backward_planned(gs, None, ops.BagPlan(ids_t, V, E, 0))
+    oracle = O.bag_mean_bwd(gs.double().cpu().numpy(), np.ones(W * nseq), ids, V, 0)
+    rng = np.random.default_rng(3)
+    tbl = torch.as_tensor(rng.standard_normal((V, E)).astype(np.float32), device=DEV)
+    m = torch.as_tensor(rng.standard_normal((V, E)).astype(np.float32) * 0.01, device=DEV)
+    v = torch.as_tensor(np.abs(rng.standard_normal((V, E))).astype(np.float32) * 1e-4, device=DEV)
+    step = torch.tensor(3.0, device=DEV)
+    args = torch.zeros(8, device=DEV)
+    ops.adam_prepare([(step, args)], lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01)
+    t1, m1, v1 = tbl.clone(), m.clone(), v.clone()
+    ops.bag_mean_backward_adamw_planned(gs, None, ops.BagPlan(ids_t, V, E, 0), t1, m1, v1, args)
+    for c in range(W):
+        sl = slice(c * El, (c + 1) * El)
+        gs_all = gs[:, sl].contiguous()
+        grad = torch.empty(V, El, device=DEV)
+        _col_reduce_ex(seg_all, vals_all, nseq * L, W, nseq, gs_all, V, El, grad=grad)
+        torch.cuda.synchronize()
+        assert torch.equal(grad, whole[:, sl]), (c, float((grad - whole[:, sl]).abs().max()))
+        o = oracle[:, sl]
+        assert np.abs(grad.double().cpu().numpy() - o).max() / np.abs(o).max() < 1e-5
+        ts, ms, vs = tbl[:, sl].contiguous(), m[:, sl].contiguous(), v[:, sl].contiguous()
+        _col_reduce_ex(seg_all, vals_all, nseq * L, W, nseq, gs_all, V, El, slab=ts, m=ms, v=vs, args=args)
+        torch.cuda.synchronize()
+        assert torch.equal(ts, t1[:, sl]) and torch.equal(ms, m1[:, sl]) and torch.equal(vs, v1[:, sl]), c
+
+
+@pytest.mark.parametrize("W", [2, 8])
+def test_column_reduce_row_past_single_plan_pieces(W):
+    """A row of more than 128 x 256 merged tokens (60 % of a global batch on one row): up to 4,096
+    pieces and the group level (groups of 256 piece partials), against the float64 oracle at 1e-5
+    (the single plan cuts such a row into 256 longer pieces, so the sums associate differently)."""
+    E, V, nseq, L = 256, 3001, 4096 // W, 64
+    El = E // W
+    ids, ids_t, gs, seg_all, vals_all = _setup(W, E, V, nseq, L, seed=77 + W, kind="hot")
+    lens = np.bincount(ids[ids > 0].ravel(), minlength=V)
+    assert lens.max() > 128 * 256
+    oracle = O.bag_mean_bwd(gs.double().cpu().numpy(), np.ones(W * nseq), ids, V, 0)
+    for c in (0, W - 1):
+        sl = slice(c * El, (c + 1) * El)
+        gs_all = gs[:, sl].contiguous()
+        grad = torch.empty(V, El, device=DEV)
+        _col_reduce_ex(seg_all, vals_all, nseq * L, W, nseq, gs_all, V, El, grad=grad)
+        torch.cuda.synchronize()
+        o = oracle[:, sl]
+        err = np.abs(grad.double().cpu().numpy() - o).max() / np.abs(o).max()
+        assert err < 1e-5, (c, float(err))
+        # and the row-without-pieces path is unchanged: the old entry walks the hot row serially
+        g0 = torch.empty(V, El, device=DEV)
+        ops.call("tt_bag_col_reduce", seg_all.data_ptr(), vals_all.data_ptr(), nseq * L, W, nseq, gs_all.data_ptr(), V,
+                 El, g0.data_ptr(), None, None, None, None, _lib.stream_of(g0))
+        torch.cuda.synchronize()
+        cold = lens <= 128
+        assert torch.equal(grad[torch.as_tensor(cold, device=DEV)], g0[torch.as_tensor(cold, device=DEV)])
 
 
 @pytest.mark.parametrize("W,E", [(2, 256), (8, 256), (2, 128)])

@@ -1030,6 +1030,20 @@ def test_topk_two_stage_ties_across_chunks(nq, ncols, k, levels):
     assert np.array_equal(vals.cpu().numpy(), np.take_along_axis(xs, order, 1))
 
 
+def test_topk_two_stage_more_rows_than_grid_y():
+    """the two-stage top-k puts rows on grid.y (at most 65,535); a query batch past that
+    goes in row blocks.  70,000 rows x 8,192 columns (two-stage at k = 10) against torch.topk (each row
+    a permutation: no ties), every row block's first and last rows included."""
+    nq, ncols, k = 70_000, 8192, 10
+    assert _lib.lib().tt_topk_rows_ws_size(nq, ncols, k) > 0
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand(nq, ncols, device=DEV, generator=g).argsort(dim=1).float()  # distinct values per row
+    vals, idx = ops.topk_rows(x, k)
+    tv, ti = torch.topk(x, k, dim=1)
+    assert torch.equal(vals, tv)
+    assert torch.equal(idx, ti)
+
+
 @pytest.mark.parametrize("nq,nd,H", [(40, 2049, 256), (70, 999, 64), (9, 300, 36), (33, 4097, 512), (5, 129, 1024)])
 def test_cosine_scores_many_queries_and_widths(nq, nd, H):
     """Query passes (up to 32 per pass, fewer at wide H), partial document tiles, H not a multiple
@@ -1049,6 +1063,58 @@ def test_topk_ties_and_extremes():
     assert idx.tolist() == [[1, 2, 4, 0]] and vals.tolist() == [[3.0, 3.0, 3.0, 1.0]]
     vals, idx = ops.topk_rows(x, 8)
     assert idx[0, -1].item() == 5
+
+
+def test_search_matches_reference_fixture(golden):
+    """inference/search/two_tower.py:37-115 pinned to the reference itself (tests/golden/search.npz:
+    its TwoTowerSearch.index_documents + search on a seeded C1-shaped model): the same weights in
+    twotower_amd's towers, the stored ids indexed and searched on the HIP path -- document and query
+    embeddings and the top-10 scores within 1e-5, the documents equal where the score is not tied
+    (within 1e-6) with its neighbour and the document text is unique; and search() on text returns
+    the reference's result dicts."""
+    g = golden("search")
+    V, E = g["table"].shape
+    H = g["W1"].shape[0]
+    emb = tt.embeddings.build("lookup", vocab_size=V, embedding_dim=E)
+    model = tt.build_two_tower("mean", emb, hidden_dim=H, tied_weights=True)
+    t = model.query_tower
+    with torch.no_grad():
+        t.embedding.embedding.weight.copy_(torch.as_tensor(g["table"]))
+        t.feed_forward[0].weight.copy_(torch.as_tensor(g["W1"]))
+        t.feed_forward[0].bias.copy_(torch.as_tensor(g["b1"]))
+        t.feed_forward[2].weight.copy_(torch.as_tensor(g["W2"]))
+        t.feed_forward[2].bias.copy_(torch.as_tensor(g["b2"]))
+    doc_ids = torch.as_tensor(g["doc_ids"], dtype=torch.int32)
+    engine = tt.search.TwoTowerSearch(model, device=DEV)
+    with _lib.record_calls() as calls:
+        engine.index_document_ids(doc_ids)
+        scores, idx = engine.search_ids(torch.as_tensor(g["query_ids"]), top_k=g["top_scores"].shape[1])
+    assert {"tt_cosine_scores", "tt_topk_rows_ex"} <= set(calls), calls
+    assert np.abs(engine.document_embeddings.cpu().numpy() - g["doc_emb"]).max() < 1e-5
+    q = engine.encode_queries(torch.as_tensor(g["query_ids"]))
+    assert np.abs(q.cpu().numpy() - g["query_emb"]).max() < 1e-5
+    sc, ix = scores.cpu().numpy(), idx.cpu().numpy()
+    assert np.abs(sc - g["top_scores"]).max() < 1e-5
+    ref_s, ref_i = g["top_scores"], g["top_index"]
+    gap = np.minimum(np.abs(np.diff(ref_s, axis=1, prepend=np.inf)), np.abs(np.diff(ref_s, axis=1, append=-np.inf)))
+    sure = (ref_i >= 0) & (gap > 1e-6)
+    assert sure.sum() > 0.8 * sure.size
+    assert np.array_equal(ix[sure], ref_i[sure])
+
+    class _FixtureTokenizer:  # the reference tokeniser's two calls, answered from the fixture's ids
+        def __init__(self, rows):
+            self.rows = {f"text{i}": list(r) for i, r in enumerate(rows)}
+
+        def encode(self, text):
+            return self.rows[text]
+
+        def truncate_and_pad(self, seq, max_len):
+            return seq[:max_len]
+
+    engine.tokenizer = _FixtureTokenizer(g["query_ids"])
+    res = engine.search("text0", top_k=5)
+    assert [r["document"] for r in res] == ix[0, :5].tolist()
+    assert np.abs(np.array([r["score"] for r in res]) - ref_s[0, :5]).max() < 1e-5
 
 
 def test_search_index_and_query(tmp_path):

@@ -258,3 +258,30 @@ def test_bench_op_report_shapes():
     kernels, roof = bench.op_report({"tt_bag_mean_fwd": op(0.34), "tt_multi_neg_fwd": op(0.026),
                                      "tt_multi_neg_bwd": op(0.031)}, 10, "c5", 1, "fp32", 2.0e6, 131_584, "stored")
     assert {k["abi"] for k in kernels} == {"tt_bag_mean_fwd", "tt_multi_neg_fwd", "tt_multi_neg_bwd"}
+
+
+# messages this stack raised for calls refused under HIP graph capture (tools/capture_messages.py on
+# an MI355X box, torch 2.10 + ROCm 7: gloo collectives on GPU tensors, host syncs); RCCL collectives
+# capture without error
+_SEEN_CAPTURE_MESSAGES = [
+    "HIP error: operation failed due to a previous error during capture\nSearch for "
+    "`hipErrorStreamCaptureInvalidated' in https://rocm.docs.amd.com/projects/HIP/en/latest/index.html",
+    "Cannot register the state during capturing stage. during CUDA graph capture. If you need this call to be "
+    "captured, please file an issue. Current hipStreamCaptureStatus: hipStreamCaptureStatusInvalidated",
+    "hipErrorStreamCaptureUnsupported: operation not permitted when stream is capturing",
+    "CUDA error: operation not permitted when stream is capturing",
+    "hipErrorCapturedEvent: operation not permitted on an event last recorded in a capturing stream",
+]
+
+
+def test_capture_error_messages():
+    """TrainStep falls back to eager only for capture refusals; these are the messages
+    actually seen on this stack, and errors of the step itself stay fatal."""
+    from twotower_amd.train_step import _is_capture_error
+
+    for m in _SEEN_CAPTURE_MESSAGES:
+        assert _is_capture_error(RuntimeError(m)), m
+    for m in ("tt_inbatch_fwd: workspace too small: need 10 have 5", "CUDA out of memory. Tried to allocate 2.00 GiB",
+              "HIP error: an illegal memory access was encountered", "Expected all tensors to be on the same device",
+              "NCCL error: unhandled system error"):
+        assert not _is_capture_error(RuntimeError(m)), m

@@ -115,3 +115,21 @@ def test_in_batch(golden):
         loss, (dq, dd), _ = O.in_batch_fwd_bwd(g[f"{tag}_q"].astype(np.float64), g[f"{tag}_d"].astype(np.float64), 0.1)
         assert abs(loss - g[f"{tag}_loss"]) < 1e-5 * max(1, abs(g[f"{tag}_loss"])), tag
         assert rel(dq, g[f"{tag}_dq"]) < 1e-5 and rel(dd, g[f"{tag}_dd"]) < 1e-5, tag
+
+
+def test_search_fixture_pins_oracle(golden):
+    """inference/search/two_tower.py (index_documents + search, captured from the reference): the
+    oracle's tower over the stored ids gives the reference's document and query embeddings, and its
+    cosine + index-ordered top-k the reference's scores and documents (where the text is unique)."""
+    g = golden("search")
+    p = params_of(g)
+    docs, _ = O.tower_fwd(p, g["doc_ids"])
+    qs, _ = O.tower_fwd(p, g["query_ids"])
+    assert rel(docs, g["doc_emb"]) < 1e-6
+    assert rel(qs, g["query_emb"]) < 1e-6
+    cos = (qs @ docs.T) / np.maximum(np.linalg.norm(qs, axis=1)[:, None] * np.linalg.norm(docs, axis=1)[None], 1e-8)
+    k = g["top_scores"].shape[1]
+    order = np.lexsort((np.arange(docs.shape[0])[None].repeat(len(qs), 0), -cos), axis=1)[:, :k]
+    assert np.abs(np.take_along_axis(cos, order, 1) - g["top_scores"]).max() < 1e-5
+    known = g["top_index"] >= 0
+    assert np.array_equal(order[known], g["top_index"][known])

@@ -284,10 +284,10 @@ def table_sync(a):
     table = torch.randn(V, E, device=DEV, generator=g) * 0.02
     m, v = torch.zeros_like(table), torch.zeros_like(table)
     _, args = adam_args()
-    own = ids_for(B, L, V, K)
+    own = ids_for(B, L, V, K, zipf=a.zipf)
     nown = own.shape[0]
     for R in (1, 2, 4, 8):
-        ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r) for r in range(1, R)]).contiguous()
+        ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r, zipf=a.zipf) for r in range(1, R)]).contiguous()
         N = ids.shape[0]
         d_pooled = torch.randn(N, E, device=DEV, generator=g)
         denom = (ids > 0).sum(1).float() + 1e-9
@@ -341,7 +341,7 @@ def column_sync(a):
     table = torch.randn(V, E, device=DEV, generator=g) * 0.02
     m, v = torch.zeros_like(table), torch.zeros_like(table)
     _, args = adam_args()
-    own = ids_for(B, L, V, K)
+    own = ids_for(B, L, V, K, zipf=a.zipf)
     nown = own.shape[0]
     st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     base = {}
@@ -356,7 +356,7 @@ def column_sync(a):
     del p1
     for R in (1, 2, 4, 8):
         El = E // R
-        ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r) for r in range(1, R)]).contiguous()
+        ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r, zipf=a.zipf) for r in range(1, R)]).contiguous()
         N = ids.shape[0]
         slab = table[:, :El].contiguous()
         ms, vs = torch.zeros_like(slab), torch.zeros_like(slab)
@@ -386,9 +386,19 @@ def column_sync(a):
             del pl
         seg_all, vals_all = torch.cat(segs), torch.cat(valss)
         gs_all = torch.randn(N, El, device=DEV, generator=g) * 1e-3
-        res["col_update_us"] = graph_us(lambda: call("tt_bag_col_reduce", ptr(seg_all), ptr(vals_all), nown * L, R, nown,
-                                                     ptr(gs_all), V, El, None, ptr(slab), ptr(ms), ptr(vs), ptr(args),
-                                                     st()))
+        nws = _lib.lib().tt_bag_col_reduce_ws_size(V, R, nown * L, El)
+        cws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+        res["col_update_us"] = graph_us(lambda: call("tt_bag_col_reduce_ex", ptr(seg_all), ptr(vals_all), nown * L, R,
+                                                     nown, ptr(gs_all), V, El, None, ptr(slab), ptr(ms), ptr(vs),
+                                                     ptr(args), ptr(cws), nws, st()))
+        # without the hot-row path (every row walked by one sub-wave: the round-5 kernel)
+        res["col_update_no_pieces_us"] = graph_us(lambda: call("tt_bag_col_reduce", ptr(seg_all), ptr(vals_all),
+                                                               nown * L, R, nown, ptr(gs_all), V, El, None, ptr(slab),
+                                                               ptr(ms), ptr(vs), ptr(args), st()))
+        lens = torch.bincount(ids[ids > 0].long().flatten(), minlength=V)
+        res["zipf"] = a.zipf
+        res["hottest_row_tokens"] = int(lens.max())
+        del cws
         res = {k: (round(x, 1) if isinstance(x, float) else x) for k, x in res.items()}
         res["link_MB_per_rank"] = {
             "ids_allgather": round((R - 1) * nown * L * 4 / 1e6, 1),

@@ -77,6 +77,9 @@ _SIGNATURES = {
     "tt_bag_scale_rows": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp]),
     "tt_bag_col_reduce": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp, _vp,
                                    _vp]),
+    "tt_bag_col_reduce_ws_size": (_c_sz, [_c_i64, _c_int, _c_i64, _c_int]),
+    "tt_bag_col_reduce_ex": (_c_int, [_vp, _vp, _c_i64, _c_int, _c_i64, _vp, _c_i64, _c_int, _vp, _vp, _vp, _vp,
+                                      _vp, _vp, _c_sz, _vp]),
     "tt_adam_prepare": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64, _vp]),
     "tt_adam_prepare_ex": (_c_int, [ctypes.POINTER(AdamSlot), _c_int, _c_f64, _c_f64, _c_f64, _c_f64, _c_f64,
                                     _c_int, _c_int, _vp]),

@@ -884,11 +884,160 @@ __device__ __forceinline__ void rotate_parts(f32x4 (&part)[U], int r) {
   }
 }
 
+// Hot rows of the column-sharded reduce (Zipf ids, a character vocabulary).  A row whose merged
+// length (every rank's tokens of it) exceeds kPieceT is cut into pieces of piece_len_col(len) merged
+// entries; one sub-wave per piece sums its gs rows in merged order (entry j of the piece -> partial
+// j % 4, folded 0 + 1 + 2 + 3), and the row's reduce folds the piece partials the same way.  Up to
+// kMaxPieces pieces (rows of <= kPieceT * kMaxPieces merged tokens) the partition and both folds
+// are the single-plan path's (bag_plan_pieces_kernel, bag_piece_sum_kernel, the sliced reduce), so
+// such rows equal the one-GPU reduce of the concatenated batch bit for bit.  Longer rows (only a
+// global batch of N ranks reaches them) take up to kColMaxPieces pieces and a middle level: groups
+// of kMaxPieces piece partials summed by one sub-wave each, the row folding its <= 16 group sums.
+// Every sum has a fixed order; only the slot numbering (atomic allocation) varies between runs.
+constexpr int kColMaxPieces = 4096;
+constexpr int kColLD = 16;  // entries loaded per sub-wave iteration (a multiple of 4)
+
+__device__ __forceinline__ int piece_len_col(int len) {
+  if (len <= kPieceT * kMaxPieces) return kPieceT;  // piece_len(len) there
+  const int t = (len + kColMaxPieces - 1) / kColMaxPieces;
+  return t > kPieceT ? t : kPieceT;
+}
+
+// One thread per row: merged length, piece count, piece / group slots (cnt[0] / cnt[1] counters,
+// zeroed by the launcher).  prow: the row of each piece slot; goff / gbeg / gend: a very long row's
+// group slots and their piece-slot ranges.
+__global__ __launch_bounds__(kBlock) void bag_col_pieces_kernel(const int32_t* __restrict__ seg, int nsrc, int64_t V,
+                                                                int32_t* __restrict__ nch, int32_t* __restrict__ off,
+                                                                int32_t* __restrict__ plen, int32_t* __restrict__ goff,
+                                                                int32_t* __restrict__ cnt, int32_t* __restrict__ prow,
+                                                                int32_t* __restrict__ gbeg, int32_t* __restrict__ gend) {
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= V) return;
+  int len = 0;
+  for (int src = 0; src < nsrc; ++src) {
+    const int32_t* sg = seg + (int64_t)src * (V + 1);
+    len += sg[r + 1] - sg[r];
+  }
+  const int t = piece_len_col(len);
+  const int np = len > kPieceT ? (len + t - 1) / t : 0;
+  nch[r] = np;
+  if (np == 0) return;
+  plen[r] = len;
+  const int k0 = atomicAdd(cnt, np);
+  off[r] = k0;
+  for (int k = 0; k < np; ++k) prow[k0 + k] = (int32_t)r;
+  if (np > kMaxPieces) {
+    const int ng = (np + kMaxPieces - 1) / kMaxPieces;
+    const int g0 = atomicAdd(cnt + 1, ng);
+    goff[r] = g0;
+    for (int g = 0; g < ng; ++g) {
+      gbeg[g0 + g] = k0 + g * kMaxPieces;
+      gend[g0 + g] = min(k0 + (g + 1) * kMaxPieces, k0 + np);
+    }
+  }
+}
+
+// Sum rows [b, e) of src (El floats each) into part[] with entry j -> part[j % 4] (j from 0), LD
+// loads in flight per iteration.  Zero rows pad the last iteration (x + 0 = x).
+template <int LPR>
+__device__ __forceinline__ void fold_rows(const float* __restrict__ src, int b, int e, int c, f32x4 (&part)[4]) {
+  constexpr int El = 4 * LPR;
+  for (int i = b; i < e; i += kColLD) {
+    f32x4 x[kColLD];
+#pragma unroll
+    for (int u = 0; u < kColLD; ++u)
+      x[u] = (i + u < e) ? reinterpret_cast<const f32x4*>(src + (int64_t)(i + u) * El)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < kColLD; ++u) part[u % 4] += x[u];
+  }
+}
+
+// One sub-wave (LPR lanes, El = 4 LPR columns) per piece: its merged entries [k t, min((k+1) t, len))
+// walked over the sources in rank order (source src's segment of the row is entries [acc, acc +
+// cnt) of the merged order), entry j of the piece into partial j % 4.
+template <int LPR>
+__global__ __launch_bounds__(kBlock) void bag_col_piece_sum_kernel(const int32_t* __restrict__ seg,
+                                                                   const int32_t* __restrict__ vals, int64_t nL,
+                                                                   int nsrc, int64_t nseq, const float* __restrict__ gs,
+                                                                   int64_t V, const int32_t* __restrict__ off,
+                                                                   const int32_t* __restrict__ plen,
+                                                                   const int32_t* __restrict__ cnt,
+                                                                   const int32_t* __restrict__ prow,
+                                                                   float* __restrict__ partial) {
+  constexpr int RPI = kWave / LPR;
+  constexpr int El = 4 * LPR;
+  const int lane = lane_id();
+  const int sub = lane / LPR, c = lane % LPR;
+  const int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  if (pc >= cnt[0]) return;
+  const int64_t r = prow[pc];
+  const int len = plen[r], t = piece_len_col(len);
+  const int b = (int)(pc - off[r]) * t, e = min(b + t, len);
+  f32x4 part[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int acc = 0, done = 0;
+  for (int src = 0; src < nsrc && acc < e; ++src) {
+    const int32_t* sg = seg + (int64_t)src * (V + 1);
+    const int st = sg[r], n = sg[r + 1] - st;
+    const int lo = max(b, acc), hi = min(e, acc + n);
+    if (lo < hi) {
+      const int32_t* vl = vals + (int64_t)src * nL + st - acc;  // merged entry m at vl[m]
+      const float* g = gs + (int64_t)src * nseq * El;
+      for (int i = lo; i < hi; i += kColLD) {
+        int sq[kColLD];
+#pragma unroll
+        for (int u = 0; u < kColLD; ++u) sq[u] = (i + u < hi) ? vl[i + u] : -1;
+        f32x4 x[kColLD];
+#pragma unroll
+        for (int u = 0; u < kColLD; ++u)
+          x[u] = (sq[u] >= 0) ? reinterpret_cast<const f32x4*>(g + (int64_t)sq[u] * El)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < kColLD; ++u) part[u % 4] += x[u];
+      }
+      done += hi - lo;
+      rotate_parts(part, (hi - lo) % 4);  // the next source's first entry goes to part[0]
+    }
+    acc += n;
+  }
+  rotate_parts(part, (4 - done % 4) % 4);  // back to part[j] = entries j (mod 4)
+  reinterpret_cast<f32x4*>(partial + pc * El)[c] = part[0] + part[1] + part[2] + part[3];
+}
+
+// One sub-wave per group of <= kMaxPieces piece partials (rows of more than kMaxPieces pieces).
+template <int LPR>
+__global__ __launch_bounds__(kBlock) void bag_col_group_sum_kernel(const int32_t* __restrict__ cnt,
+                                                                   const int32_t* __restrict__ gbeg,
+                                                                   const int32_t* __restrict__ gend,
+                                                                   const float* __restrict__ partial,
+                                                                   float* __restrict__ gpart) {
+  constexpr int RPI = kWave / LPR;
+  constexpr int El = 4 * LPR;
+  const int lane = lane_id();
+  const int sub = lane / LPR, c = lane % LPR;
+  const int64_t gc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
+  if (gc >= cnt[1]) return;
+  f32x4 part[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  fold_rows<LPR>(partial, gbeg[gc], gend[gc], c, part);
+  reinterpret_cast<f32x4*>(gpart + gc * El)[c] = part[0] + part[1] + part[2] + part[3];
+}
+
+struct ColPieces {  // the hot-row path's outputs (nch == nullptr: no pieces, every row merged)
+  const int32_t* nch;
+  const int32_t* off;
+  const int32_t* goff;
+  const float* partial;
+  const float* gpart;
+};
+
 template <int LPR, int U, bool FUSED, bool NT>
 __global__ __launch_bounds__(kBlock) void bag_col_reduce_kernel(
     const int32_t* __restrict__ seg, const int32_t* __restrict__ vals, int64_t nL, int nsrc, int64_t nseq,
     const float* __restrict__ gs, int64_t V, float* __restrict__ grad, float* __restrict__ param,
-    float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq, const AdamArgs* __restrict__ aa_dev) {
+    float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq, const AdamArgs* __restrict__ aa_dev,
+    ColPieces pcs) {
   constexpr int RPI = kWave / LPR;
   constexpr int El = 4 * LPR;
   const int lane = lane_id();
@@ -907,7 +1056,13 @@ __global__ __launch_bounds__(kBlock) void bag_col_reduce_kernel(
 #pragma unroll
   for (int u = 0; u < U; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   int64_t total = 0;
-  for (int src = 0; src < nsrc; ++src) {
+  const int np = pcs.nch ? pcs.nch[row] : 0;
+  if (np > 0) {  // a hot row: its piece partials (or, past kMaxPieces pieces, its group sums)
+    static_assert(U == 4, "piece folds are written for U = 4");
+    if (np <= kMaxPieces) fold_rows<LPR>(pcs.partial, pcs.off[row], pcs.off[row] + np, c, part);
+    else fold_rows<LPR>(pcs.gpart, pcs.goff[row], pcs.goff[row] + (np + kMaxPieces - 1) / kMaxPieces, c, part);
+  }
+  for (int src = 0; src < nsrc && np == 0; ++src) {
     const int32_t* sg = seg + (int64_t)src * (V + 1);
     const int st = sg[row], en = sg[row + 1];
     const int32_t* vl = vals + (int64_t)src * nL;
@@ -1527,9 +1682,64 @@ extern "C" int tt_bag_scale_rows(const float* d_pooled, const float* denom, int6
   return TT_OK;
 }
 
+namespace tt {
+namespace {
+struct ColWs {
+  int32_t *nch, *off, *plen, *goff, *cnt, *prow, *gbeg, *gend;
+  float *partial, *gpart;
+  int64_t maxp, maxg;
+  size_t total;
+};
+ColWs col_carve(void* base, int64_t V, int nsrc, int64_t nL, int El) {
+  ColWs w{};
+  const int64_t n = (int64_t)nsrc * nL;
+  w.maxp = max_pieces_for(n);
+  w.maxg = (w.maxp + kMaxPieces - 1) / kMaxPieces + 1;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align_up(o + bytes, 256);
+    return at;
+  };
+  const size_t onch = take((size_t)V * 4), ooff = take((size_t)V * 4), olen = take((size_t)V * 4),
+               ogoff = take((size_t)V * 4), ocnt = take(8), oprow = take((size_t)w.maxp * 4),
+               ogb = take((size_t)w.maxg * 4), oge = take((size_t)w.maxg * 4),
+               opart = take((size_t)w.maxp * El * 4), ogp = take((size_t)w.maxg * El * 4);
+  w.total = o + 256;
+  if (base) {
+    char* b = reinterpret_cast<char*>(align_up(reinterpret_cast<size_t>(base), 256));
+    w.nch = reinterpret_cast<int32_t*>(b + onch);
+    w.off = reinterpret_cast<int32_t*>(b + ooff);
+    w.plen = reinterpret_cast<int32_t*>(b + olen);
+    w.goff = reinterpret_cast<int32_t*>(b + ogoff);
+    w.cnt = reinterpret_cast<int32_t*>(b + ocnt);
+    w.prow = reinterpret_cast<int32_t*>(b + oprow);
+    w.gbeg = reinterpret_cast<int32_t*>(b + ogb);
+    w.gend = reinterpret_cast<int32_t*>(b + oge);
+    w.partial = reinterpret_cast<float*>(b + opart);
+    w.gpart = reinterpret_cast<float*>(b + ogp);
+  }
+  return w;
+}
+}  // namespace
+}  // namespace tt
+
+extern "C" size_t tt_bag_col_reduce_ws_size(int64_t V, int nsrc, int64_t nL, int El) {
+  if (V <= 0 || nsrc <= 0 || nL < 0 || El <= 0) return 0;
+  return col_carve(nullptr, V, nsrc, nL, El).total;
+}
+
 extern "C" int tt_bag_col_reduce(const int32_t* seg_all, const int32_t* vals_all, int64_t nL, int nsrc,
                                  int64_t nseq, const float* gs_all, int64_t V, int El, float* grad, float* slab,
                                  float* exp_avg, float* exp_avg_sq, const void* adam_args, tt_stream_t stream) {
+  return tt_bag_col_reduce_ex(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, El, grad, slab, exp_avg, exp_avg_sq,
+                              adam_args, nullptr, 0, stream);
+}
+
+extern "C" int tt_bag_col_reduce_ex(const int32_t* seg_all, const int32_t* vals_all, int64_t nL, int nsrc,
+                                    int64_t nseq, const float* gs_all, int64_t V, int El, float* grad, float* slab,
+                                    float* exp_avg, float* exp_avg_sq, const void* adam_args, void* ws,
+                                    size_t ws_bytes, tt_stream_t stream) {
   TT_REQUIRE(V > 0 && V < (int64_t(1) << 31) - 1 && nsrc > 0 && nseq >= 0 && nL >= 0 && nL < (int64_t(1) << 31),
              "tt_bag_col_reduce: bad shape (V=%lld nsrc=%d nseq=%lld nL=%lld)", (long long)V, nsrc, (long long)nseq,
              (long long)nL);
@@ -1542,14 +1752,34 @@ extern "C" int tt_bag_col_reduce(const int32_t* seg_all, const int32_t* vals_all
   const int LPR = El / 4, rpi = kWave / LPR;
   const int64_t waves = (V + rpi - 1) / rpi;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kBlock);
+  // hot rows (ws != NULL): piece plan, piece sums, group sums, then the reduce folds them
+  ColPieces pcs{};
+  ColWs w{};
+  if (ws) {
+    w = col_carve(ws, V, nsrc, nL, El);
+    TT_REQUIRE(ws_bytes >= w.total, "tt_bag_col_reduce_ex: workspace %zu bytes < %zu", ws_bytes, w.total);
+    TT_HIP(hipMemsetAsync(w.cnt, 0, 8, s), "memset piece counters");
+    bag_col_pieces_kernel<<<dim3((unsigned)((V + kBlock - 1) / kBlock)), block, 0, s>>>(
+        seg_all, nsrc, V, w.nch, w.off, w.plen, w.goff, w.cnt, w.prow, w.gbeg, w.gend);
+    TT_LAUNCH_CHECK("tt_bag_col_reduce (pieces)");
+    pcs = ColPieces{w.nch, w.off, w.goff, w.partial, w.gpart};
+  }
+  auto sub_grid = [&](int64_t n) {  // n sub-wave jobs of El columns each
+    return dim3((unsigned)std::max<int64_t>(1, ((n + rpi - 1) / rpi + kWavesPerBlock - 1) / kWavesPerBlock));
+  };
 #define TT_COL(L)                                                                                             \
   do {                                                                                                        \
+    if (ws) {                                                                                                 \
+      bag_col_piece_sum_kernel<L><<<sub_grid(w.maxp), block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
+                                                                     w.off, w.plen, w.cnt, w.prow, w.partial); \
+      bag_col_group_sum_kernel<L><<<sub_grid(w.maxg), block, 0, s>>>(w.cnt, w.gbeg, w.gend, w.partial, w.gpart); \
+    }                                                                                                         \
     if (fused)                                                                                                \
       bag_col_reduce_kernel<L, 4, true, false><<<grid, block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
-                                                                     nullptr, slab, exp_avg, exp_avg_sq, aa);  \
+                                                                     nullptr, slab, exp_avg, exp_avg_sq, aa, pcs); \
     else                                                                                                      \
       bag_col_reduce_kernel<L, 4, false, false><<<grid, block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
-                                                                      grad, nullptr, nullptr, nullptr, nullptr); \
+                                                                      grad, nullptr, nullptr, nullptr, nullptr, pcs); \
   } while (0)
   switch (El) {
     case 32: TT_COL(8); break;

@@ -502,15 +502,22 @@ extern "C" int tt_topk_rows_ex(const float* scores, int64_t nrows, int64_t ncols
     return TT_OK;
   }
   TT_REQUIRE(ws_bytes >= need, "topk workspace %zu bytes < %zu", ws_bytes, need);
-  TT_REQUIRE(nrows <= 65535, "nrows=%lld > 65535 (grid y)", (long long)nrows);
   const int64_t C = topk_chunk(ncols, k);
   const int nch = (int)(ncols / C);
   float* cv = reinterpret_cast<float*>(ws);
   int32_t* ci = reinterpret_cast<int32_t*>(cv + (size_t)nrows * nch * k);
-  topk_chunks_kernel<<<dim3((unsigned)nch, (unsigned)nrows), dim3(kBlock), 0, s>>>(scores, ncols, k, C, nch, cv, ci);
-  TT_LAUNCH_CHECK("tt_topk_rows (chunks)");
-  topk_merge_kernel<<<dim3((unsigned)nrows), dim3(kBlock), 0, s>>>(cv, ci, nch, k, out_vals, out_idx);
-  TT_LAUNCH_CHECK("tt_topk_rows (merge)");
+  // rows ride grid.y (at most 65,535): longer query batches go in row blocks of that many
+  constexpr int64_t kRowBlock = 65535;
+  for (int64_t r0 = 0; r0 < nrows; r0 += kRowBlock) {
+    const int64_t nr = std::min<int64_t>(kRowBlock, nrows - r0);
+    const size_t co = (size_t)r0 * nch * k;
+    topk_chunks_kernel<<<dim3((unsigned)nch, (unsigned)nr), dim3(kBlock), 0, s>>>(scores + r0 * ncols, ncols, k, C,
+                                                                                   nch, cv + co, ci + co);
+    TT_LAUNCH_CHECK("tt_topk_rows (chunks)");
+    topk_merge_kernel<<<dim3((unsigned)nr), dim3(kBlock), 0, s>>>(cv + co, ci + co, nch, k, out_vals + r0 * k,
+                                                                  out_idx + r0 * k);
+    TT_LAUNCH_CHECK("tt_topk_rows (merge)");
+  }
   return TT_OK;
 }
 

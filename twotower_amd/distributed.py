@@ -103,14 +103,16 @@ def table_sync_mode(requested: str, group=None, E: int | None = None) -> str:
                   pooled and d_pooled column blocks exchanged all-to-all, no table row ever crosses
                   the links, 1/N of the update per rank (C5 at N = 8: ~0.26 GB per rank and step,
                   against 1.3-1.8 GB for owner / shard).
-    "auto": "column" when the width splits into the column kernels' slabs (E / N in 32..256: C3/C4/C5
-    at N = 2, 4, 8), else gather up to 4 ranks, shard beyond."""
+    "auto": gather up to 4 ranks, shard beyond.  Both keep a replicated, current table on every
+    rank, so evaluation, search and state_dict() stay local (rank 0 alone may run them).
+    "column" is the scaling choice (bench.py --gpus N takes it wherever column_ok) but opt-in:
+    with a column-sharded table every forward that runs while the table is stale (after a step,
+    until materialize() / state_dict()) is collective -- ids all-gather + pooled all-to-all --
+    and state_dict() itself is collective (it materialises the slabs)."""
     if not is_active(group):
         return "local"
     if requested == "auto":
         world = dist.get_world_size(group)
-        if E is not None and column_ok(E, world):
-            return "column"
         return "gather" if world <= 4 else "shard"
     if requested not in ("gather", "shard", "owner", "column"):
         raise ValueError(f"table_sync must be 'auto', 'gather', 'shard', 'owner' or 'column', got {requested!r}")

@@ -522,18 +522,25 @@ def bag_col_update(col, parts, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, 
     bag calls (BagMeanPoolColumn): one fused launch for one call (tt_bag_col_reduce, grad NULL); for
     several calls on the table, their gradient rows are summed first, then one dense AdamW."""
     slab = col.slab
+
+    def ws_for(cp):  # the hot-row path's scratch (pieces of rows longer than 128 merged tokens)
+        n = _lib.lib().tt_bag_col_reduce_ws_size(col.V, col.world, cp.nL, col.El)
+        return WORKSPACE.get("col_reduce", n, slab.device), n
+
     if len(parts) == 1:
         _, gs_all, nseq, cp = parts[0]
         cp.wait()
-        call("tt_bag_col_reduce", ptr(cp.seg_all), ptr(cp.vals_all), cp.nL, col.world, nseq, ptr(gs_all), col.V,
-             col.El, None, ptr(slab), ptr(exp_avg), ptr(exp_avg_sq), ptr(adam_args), stream_of(slab))
+        ws, n = ws_for(cp)
+        call("tt_bag_col_reduce_ex", ptr(cp.seg_all), ptr(cp.vals_all), cp.nL, col.world, nseq, ptr(gs_all), col.V,
+             col.El, None, ptr(slab), ptr(exp_avg), ptr(exp_avg_sq), ptr(adam_args), ptr(ws), n, stream_of(slab))
     else:
         g = torch.zeros_like(slab)
         for _, gs_all, nseq, cp in parts:
             cp.wait()
             gi = torch.empty_like(slab)
-            call("tt_bag_col_reduce", ptr(cp.seg_all), ptr(cp.vals_all), cp.nL, col.world, nseq, ptr(gs_all), col.V,
-                 col.El, ptr(gi), None, None, None, None, stream_of(slab))
+            ws, n = ws_for(cp)
+            call("tt_bag_col_reduce_ex", ptr(cp.seg_all), ptr(cp.vals_all), cp.nL, col.world, nseq, ptr(gs_all),
+                 col.V, col.El, ptr(gi), None, None, None, None, ptr(ws), n, stream_of(slab))
             g += gi
         adamw_multi([(slab, g, exp_avg, exp_avg_sq, adam_args)])
     col.stale = True
@@ -542,10 +549,11 @@ def bag_col_update(col, parts, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, 
 def bag_mean_pool(weight: torch.Tensor, ids: torch.Tensor, padding_idx: int | None = 0,
                   scatter_mode: int = _lib.TT_SCATTER_SORTED) -> torch.Tensor:
     col = getattr(weight, "_tt_column", None)
-    if col is not None:  # data parallel, column-sharded table (distributed.ColumnTable)
-        want = torch.is_grad_enabled() and weight.requires_grad
-        return BagMeanPoolColumn.apply(weight, ids, padding_idx, col, want)
     want_plan = torch.is_grad_enabled() and weight.requires_grad
+    if col is not None and (want_plan or col.stale):  # data parallel, column-sharded table (ColumnTable):
+        # collective.  A forward without gradient on a materialised table (after state_dict() or
+        # materialize()) reads the full local weight instead: rank-local evaluation and search.
+        return BagMeanPoolColumn.apply(weight, ids, padding_idx, col, want_plan)
     return BagMeanPool.apply(weight, ids, padding_idx, scatter_mode, want_plan)
 
 

@@ -77,14 +77,23 @@ class AdamW(torch.optim.Optimizer):
 
     def release_tables(self) -> None:
         """Return the tables to ordinary dense gradients (and every gradient to the current stream);
-        a column-sharded table is materialized first (collective)."""
+        a column-sharded table is materialized first and a sharded table's moments are gathered to
+        the full table (both collective), so the next dense step updates V x E moments."""
         for w in self._tables:
             if hasattr(w, "_tt_deferred"):
                 del w._tt_deferred
             col = self._columns.pop(id(w), None)
+            sh = self._shards.pop(id(w), None)
+            st = self.state.get(w)
             if col is not None:
                 col.materialize()
                 del w._tt_column
+            if st and (col is not None or sh is not None):
+                for k in ("exp_avg", "exp_avg_sq"):
+                    m = st[k]
+                    self._sharded_moments.pop(id(m), None)
+                    full = col.gather_cols(m) if col is not None else sh.gather_full(m)[:w.shape[0]]
+                    st[k] = full.contiguous().clone()
         self._tables = []
         for g in self.param_groups:
             for p in g["params"]:
@@ -237,6 +246,7 @@ class AdamW(torch.optim.Optimizer):
             if p.grad.is_sparse:
                 raise RuntimeError("AdamW does not support sparse gradients")
             st = self._state(p, False)
+            _check_dense_moments(p, st)
             st["step"] += 1
             ops.adamw_step(p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], lr=lr, beta1=b1,
                            beta2=b2, eps=eps, weight_decay=wd, step=int(st["step"]))
@@ -277,6 +287,7 @@ class AdamW(torch.optim.Optimizer):
                 if not t.is_cuda or t.dtype != torch.float32:
                     raise ValueError(f"capturable AdamW needs float32 GPU tensors ({nm} is {t.dtype} on {t.device})")
             st = self._state(p, True)
+            _check_dense_moments(p, st)
             a = self._adam_args(p)
             slots.append((st["step"], a))
             dense.append((p.data, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], a))
@@ -634,6 +645,15 @@ class _ArgsRing:
 
 
 _ARGS_RING = _ArgsRing()
+
+
+def _check_dense_moments(p: torch.Tensor, st: dict) -> None:
+    """A dense update reads and writes p.numel() moment elements: a moment left in a sharded (rows
+    or columns) layout would be overrun, so refuse it instead of launching."""
+    for k in ("exp_avg", "exp_avg_sq"):
+        if st[k].shape != p.shape:
+            raise RuntimeError(f"AdamW: {k} has shape {tuple(st[k].shape)} but the parameter is {tuple(p.shape)} "
+                               "(sharded table moments; release_tables() gathers them before a dense step)")
 
 
 def _host_adam_args(lr, b1, b2, eps, wd, step, device) -> torch.Tensor:

@@ -209,7 +209,16 @@ _CAPTURE_ERRORS = (
     "during cuda graph capture",
     "during hip graph capture",
     "while a stream is capturing",
+    "hiperrorcapturedevent",  # an event recorded in a capturing stream, queried / synchronised
+    "cudaerrorcapturedevent",
+    "stream is capturing",
+    "stream capture",  # "... not allowed during stream capture", "stream capture invalidated" ...
+    "graph capture",  # torch's / c10d's own guards ("... is not supported during (CUDA) graph capture")
+    "is_current_stream_capturing",
+    "capture_begin",
 )
+# (the error-code enum names torch embeds in HIP/CUDA runtime errors cover the rest; messages seen
+# on this stack from collectives refused under capture: tests/test_host_cpu.py::test_capture_error_messages)
 
 
 def _is_capture_error(e: BaseException) -> bool:
