@@ -347,6 +347,18 @@ def op_report(ops_t: dict, timing_steps: int, config: str, world: int, scorer_dt
     add("step tail: head weight-gradient slab sums + dense AdamW + next scalars", "tt_adamw_multi_ex",
         28 * tower_params + 2 * 32 * 256 * 257 * 4 + 2 * 256 * 257 * 4, "GB/s", HBM_PEAK_GBS, "hbm",
         "28 bytes per parameter + 2*32*256*257*4 partial bytes read + 2*256*257*4 gradient bytes written")
+    # the tower head (encoders.py:38-42,77) on split-bf16 MFMA: six bf16 products per fp32 product,
+    # so its MFMA peak is the dense bf16 peak / 6; algorithmic flops = the fp32 GEMM's 2 * rows * K * N
+    split_peak = MFMA_PEAK_TFLOPS["bf16"] / 6.0
+    add("tower head activation GEMMs (Linear-ReLU-Linear fwd, dh / dx bwd; split-bf16 MFMA, fused epilogues)",
+        "tt_head_gemm", 2.0 * nseq * d * d, "TFLOP/s", split_peak, "mfma",
+        "2*rows*E*H fp32-GEMM flops per launch (4 launches per step); peak = 2.5 PF bf16 / 6 (six bf16 products "
+        "per fp32 product)")
+    add("tower head weight + bias gradients (dW1, dW2 as one launch; side stream beside the table update)",
+        "tt_head_wgrad2", 4.0 * nseq * d * d, "TFLOP/s", split_peak, "mfma",
+        "2 x 2*rows*E*H fp32-GEMM flops (dW1 and dW2 = G^T X); peak = 2.5 PF bf16 / 6", side_stream=True)
+    add("tower head weight + bias gradient (one Linear)", "tt_head_wgrad_ex", 2.0 * nseq * d * d, "TFLOP/s",
+        split_peak, "mfma", "2*rows*E*H fp32-GEMM flops (dW = G^T X); peak = 2.5 PF bf16 / 6", side_stream=True)
     main_stream = [k for k in kernels if "stream" not in k]
     dominant = max(main_stream, key=lambda k: k["mean_ms"] * k["calls_per_step"]) if main_stream else None
     roofline = None

@@ -86,20 +86,41 @@ def main():
                     work, link = exch(mode, r, bw)
                     t = base + extra_scorer + (work + link) / 1e3
                     rows.append((cfg, N, mode, bw, round(t, 3), round(N * step / t, 2)))
+    def scorer_growth(cfg, N):
+        """Extra per-rank scorer ms at N ranks (global negatives): the N-rank shape's passes minus the
+        one-GPU shape's, from tools/mb.py scorer_dp (the triplet form's M = N 2B; the pairs form's
+        M = N B is the triplet shape at N / 2, and its one-GPU shape half the triplet's)."""
+        if not sdp:
+            return 0.0
+        w1 = sdp[1]["fwd_us"] + sdp[1]["bwd_us"]
+        key = N if cfg == "c3" else N // 2
+        return (sdp[key]["fwd_us"] + sdp[key]["bwd_us"] - (w1 if cfg == "c3" else w1 / 2)) / 1e3
+
     for r in load(a.column) if a.column else []:
         N = r["ranks"]
         if N < 2:
             continue
         cfg = r["config"]
+        zipf = r.get("zipf")
         step, upd = (a.step_ms[2], a.update_ms[2]) if cfg == "c5" else (a.step_ms[0], a.update_ms[0])
         work = (r["col_gather_us"] - r["gather_own_us"] + r["permute_pooled_us"] + r["permute_grad_us"]
                 + r["col_update_us"])
         mb = r["link_MB_per_rank"]
         exposed_mb = mb["ids_allgather"] + mb["pooled_alltoall"] + mb["grad_alltoall"]
-        for bw in a.bw:
-            t = step - upd + (work + exposed_mb * 1e6 / (bw * 1e9) * 1e6) / 1e3
-            rows.append((cfg + ("" if cfg == "c5" else " (per-sample losses)"), N, "column", bw, round(t, 3),
-                         round(N * step / t, 2)))
+        # C5 and C3 with per-sample losses (no cross-rank term); the in-batch loss the driver scales
+        # (bench.py --gpus N at C3: the triplet form, M = N 2B) and C4's pairs form (M = N B) add the
+        # per-rank scorer growth of global negatives (its candidate all-gather overlaps the local
+        # launch of the two-launch forward and is not charged)
+        forms = [("c5" + (f" (Zipf {zipf} ids)" if zipf else ""), step, upd, 0.0)] if cfg == "c5" else [
+            ("c3 (per-sample losses)", step, upd, 0.0),
+            ("c3 in-batch, M = N 2B (bench --gpus N)", step, upd, scorer_growth("c3", N)),
+            ("c4 pairs, M = N B", a.step_ms[1], a.update_ms[1], scorer_growth("c4p", N))]
+        for label, st, up, extra in forms:
+            if extra is None:
+                continue
+            for bw in a.bw:
+                t = st - up + extra + (work + exposed_mb * 1e6 / (bw * 1e9) * 1e6) / 1e3
+                rows.append((label, N, "column", bw, round(t, 3), round(N * st / t, 2)))
     print("| workload | N | table exchange | RCCL GB/s per rank | forecast ms/step | speedup vs 1 GPU |")
     print("|---|---|---|---|---|---|")
     for cfg, N, mode, bw, t, s in rows:

@@ -1,7 +1,7 @@
 """Microbenchmarks of the step's kernels on one GPU, one driver with a subcommand per op family
 (device times from HIP graph replay of back-to-back calls, or HIP events per C-ABI call).
 
-  python tools/mb.py bag_bwd [--zipf S]          fused table update (scale rows + per-row reduce +
+  python tools/mb.py bag_bwd [c3|c5] [--zipf S]  fused table update (scale rows + per-row reduce +
                                                  AdamW) at C3, against a dense AdamW, a device copy and
                                                  the dense-gradient apply on the same buffers
   python tools/mb.py plan [c3|c5]                the backward's sort plan (tt_bag_plan), uniform and Zipf
@@ -91,8 +91,9 @@ def ids_for(B, L, V, K=1, seed=0, zipf=None):
 
 # ------------------------------------------------------------------------------------------------
 def bag_bwd(a):
-    B, L, V, E = 8192, 64, 200_000, 256
-    ids = ids_for(B, L, V, zipf=a.zipf)
+    B, L, E = 8192, 64, 256
+    V, K = (1_000_000, 4) if a.shape == "c5" else (200_000, 1)  # C5: multi_pos_multi_neg, 1M rows
+    ids = ids_for(B, L, V, K, zipf=a.zipf)
     N = ids.shape[0]
     g = torch.Generator(device=DEV).manual_seed(0)
     table = torch.randn(V, E, device=DEV, generator=g) * 0.02
@@ -104,7 +105,23 @@ def bag_bwd(a):
     _, args = adam_args()
     us = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, denom, plan, table, m, v, args), 20)
     algo = N * E * 4 + N * 4 + 24 * V * E
-    print(f"fused update (zipf={a.zipf}): {us:.1f} us, algorithmic {algo / us / 1e3:.0f} GB/s")
+    print(f"fused update ({a.shape or 'c3'}, zipf={a.zipf}): {us:.1f} us, algorithmic {algo / us / 1e3:.0f} GB/s")
+    # where the gathers are served from: the same plan with every sorted sequence
+    # index folded into the first K sequences, so the gathered gs rows fit an XCD's L2 (K = 4096: a
+    # 1 MB slice per XCD) or the Infinity Cache, at the same row structure and counts.  Timing only
+    # (the sums are of other rows): if the real plan runs as fast as the L2-resident one, the
+    # gathers that miss L2 cost no HBM time.
+    offs = (ctypes.c_int64 * 3)()
+    call("tt_bag_plan_layout", plan.nseq, plan.L, plan.V, plan.E, offs)
+    b0 = (-plan.buf.data_ptr()) % 256
+    vals = plan.buf[b0 + offs[1]: b0 + offs[1] + 4 * plan.nseq * plan.L].view(torch.int32)
+    keep = vals.clone()
+    for K in (4096, 16384, N):
+        vals.copy_(torch.remainder(keep, K))
+        us_k = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, denom, plan, table, m, v, args), 20)
+        print(f"fused update, gathers from the first {K} sequences ({K * E // 4 / 1e6:.1f} MB per XCD slice): "
+              f"{us_k:.1f} us")
+    vals.copy_(keep)
     grad = torch.randn(V, E, device=DEV, generator=g)
     dst = torch.empty_like(table)
     dense = lambda: call("tt_adamw", ptr(table), ptr(grad), ptr(m), ptr(v), V * E, 1e-3, 0.9, 0.999, 1e-8,  # noqa
@@ -317,7 +334,7 @@ def table_sync(a):
                                                                                       m[:Vs], v[:Vs], args))
         del po, own_ids
         seq_b = L * 4 + E * 4 + 4  # ids + d_pooled + denom per sequence
-        res = {k: (round(x, 1) if isinstance(x, float) else x) for k, x in res.items()}
+        res = {k: (round(x, 1) if isinstance(x, float) and k != "zipf" else x) for k, x in res.items()}
         res["link_MB_per_rank"] = {"gather": round((R - 1) * nown * seq_b / 1e6, 1),
                                    "shard": round(2 * (R - 1) / R * V * E * 4 / 1e6, 1),
                                    "owner": round(((R - 1) * nown * seq_b + (R - 1) / R * V * E * 4) / 1e6, 1)}
@@ -399,7 +416,7 @@ def column_sync(a):
         res["zipf"] = a.zipf
         res["hottest_row_tokens"] = int(lens.max())
         del cws
-        res = {k: (round(x, 1) if isinstance(x, float) else x) for k, x in res.items()}
+        res = {k: (round(x, 1) if isinstance(x, float) and k != "zipf" else x) for k, x in res.items()}
         res["link_MB_per_rank"] = {
             "ids_allgather": round((R - 1) * nown * L * 4 / 1e6, 1),
             "pooled_alltoall": round((R - 1) / R * nown * E * 4 / 1e6, 1),

@@ -783,9 +783,13 @@ __device__ __forceinline__ float combine_rowv(int64_t i, float l, GetO get_o, fl
   constexpr int H = V * kWave;
   using FV = typename RowVec<V>::f;
   using BV = typename RowVec<V>::b;
-  l = __builtin_fmaf(-(float)n_pad, __builtin_amdgcn_exp2f(-sh), l);  // pad rows: X = 0 exactly
   const DT* qr = Qmat + i * H;
   const DT* dl = Dmat + (i + label_off) * H;
+  // every load of the row issued here, before l is needed (round 6): one memory round trip per row
+  // instead of three (l, then q / d, then the split partials); the exact path below ignores them
+  const FV qv = loadv<V>(qr, lane), dv = loadv<V>(dl, lane);
+  const FV o = dqu ? get_o() : FV{};
+  l = __builtin_fmaf(-(float)n_pad, __builtin_amdgcn_exp2f(-sh), l);  // pad rows: X = 0 exactly
   if (!(l >= 7.888609052210118e-31f)) {  // l < 2^-100 (or NaN): the bound overshot, redo the row exactly
     float m2, lx, o[4];
     exact_row(qr, Dmat, M, H, c2, lane, m2, lx, o);
@@ -812,7 +816,6 @@ __device__ __forceinline__ float combine_rowv(int64_t i, float l, GetO get_o, fl
   }
   const float lse2_i = sh + log2f(l);  // log2 units, for the backward engine
   const float lse_i = lse2_i * kLn2;
-  const FV qv = loadv<V>(qr, lane), dv = loadv<V>(dl, lane);
   const float dot = wave_sum(dotv<V>(qv, dv));
   if (qs) {  // q~ 2^(shift - lse2): the backward's G = P_stored * that factor, folded into q~
     const float f = __builtin_amdgcn_exp2f(sh - lse2_i);
@@ -839,7 +842,6 @@ __device__ __forceinline__ float combine_rowv(int64_t i, float l, GetO get_o, fl
   }
   if (dqu) {
     const float inv_l = 1.f / l;
-    const FV o = get_o();
     FV r;
 #pragma unroll
     for (int u = 0; u < V; ++u) r[u] = __builtin_fmaf(o[u], inv_l, -dv[u]);
