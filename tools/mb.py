@@ -119,7 +119,7 @@ def bag_bwd(a):
     for K in (4096, 16384, N):
         vals.copy_(torch.remainder(keep, K))
         us_k = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, denom, plan, table, m, v, args), 20)
-        print(f"fused update, gathers from the first {K} sequences ({K * E // 4 / 1e6:.1f} MB per XCD slice): "
+        print(f"fused update, gathers from the first {K} sequences ({K * E / 1e6:.1f} MB per XCD slice): "
               f"{us_k:.1f} us")
     vals.copy_(keep)
     grad = torch.randn(V, E, device=DEV, generator=g)
