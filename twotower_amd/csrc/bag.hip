@@ -939,16 +939,17 @@ __global__ __launch_bounds__(kBlock) void bag_col_pieces_kernel(const int32_t* _
 
 // Sum rows [b, e) of src (El floats each) into part[] with entry j -> part[j % 4] (j from 0), LD
 // loads in flight per iteration.  Zero rows pad the last iteration (x + 0 = x).
-template <int LPR>
+template <int LPR, int LD = kColLD>
 __device__ __forceinline__ void fold_rows(const float* __restrict__ src, int b, int e, int c, f32x4 (&part)[4]) {
+  static_assert(LD % 4 == 0, "entry j goes to part[j % 4]: LD a multiple of 4");
   constexpr int El = 4 * LPR;
-  for (int i = b; i < e; i += kColLD) {
-    f32x4 x[kColLD];
+  for (int i = b; i < e; i += LD) {
+    f32x4 x[LD];
 #pragma unroll
-    for (int u = 0; u < kColLD; ++u)
+    for (int u = 0; u < LD; ++u)
       x[u] = (i + u < e) ? reinterpret_cast<const f32x4*>(src + (int64_t)(i + u) * El)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < kColLD; ++u) part[u % 4] += x[u];
+    for (int u = 0; u < LD; ++u) part[u % 4] += x[u];
   }
 }
 
@@ -1059,8 +1060,11 @@ __global__ __launch_bounds__(kBlock) void bag_col_reduce_kernel(
   const int np = pcs.nch ? pcs.nch[row] : 0;
   if (np > 0) {  // a hot row: its piece partials (or, past kMaxPieces pieces, its group sums)
     static_assert(U == 4, "piece folds are written for U = 4");
-    if (np <= kMaxPieces) fold_rows<LPR>(pcs.partial, pcs.off[row], pcs.off[row] + np, c, part);
-    else fold_rows<LPR>(pcs.gpart, pcs.goff[row], pcs.goff[row] + (np + kMaxPieces - 1) / kMaxPieces, c, part);
+    // 4 partial rows in flight: the row reduce keeps its register count (and so its occupancy, which
+    // the merged per-source path of every other row needs) at the round-5 kernel's; only hot rows
+    // come here, and their waves overlap the rest of the launch
+    if (np <= kMaxPieces) fold_rows<LPR, 4>(pcs.partial, pcs.off[row], pcs.off[row] + np, c, part);
+    else fold_rows<LPR, 4>(pcs.gpart, pcs.goff[row], pcs.goff[row] + (np + kMaxPieces - 1) / kMaxPieces, c, part);
   }
   for (int src = 0; src < nsrc && np == 0; ++src) {
     const int32_t* sg = seg + (int64_t)src * (V + 1);
