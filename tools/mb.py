@@ -371,7 +371,7 @@ def column_sync(a):
     p1.wait()
     base["update_own_us"] = graph_us(lambda: ops.bag_mean_backward_adamw_planned(d_pooled, None, p1, table, m, v, args))
     del p1
-    for R in (1, 2, 4, 8):
+    for R in (a.ranks or (1, 2, 4, 8)):
         El = E // R
         ids = torch.cat([own] + [ids_for(B, L, V, K, seed=1000 * r, zipf=a.zipf) for r in range(1, R)]).contiguous()
         N = ids.shape[0]
@@ -409,9 +409,10 @@ def column_sync(a):
                                                      nown, ptr(gs_all), V, El, None, ptr(slab), ptr(ms), ptr(vs),
                                                      ptr(args), ptr(cws), nws, st()))
         # without the hot-row path (every row walked by one sub-wave: the round-5 kernel)
-        res["col_update_no_pieces_us"] = graph_us(lambda: call("tt_bag_col_reduce", ptr(seg_all), ptr(vals_all),
-                                                               nown * L, R, nown, ptr(gs_all), V, El, None, ptr(slab),
-                                                               ptr(ms), ptr(vs), ptr(args), st()))
+        if not a.no_serial:
+            res["col_update_no_pieces_us"] = graph_us(lambda: call("tt_bag_col_reduce", ptr(seg_all), ptr(vals_all),
+                                                                   nown * L, R, nown, ptr(gs_all), V, El, None,
+                                                                   ptr(slab), ptr(ms), ptr(vs), ptr(args), st()))
         lens = torch.bincount(ids[ids > 0].long().flatten(), minlength=V)
         res["zipf"] = a.zipf
         res["hottest_row_tokens"] = int(lens.max())
@@ -624,6 +625,8 @@ def main():
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")
     ap.add_argument("--zipf", type=float, default=None)
+    ap.add_argument("--ranks", type=int, nargs="*", default=None, help="column_sync: only these rank counts")
+    ap.add_argument("--no-serial", action="store_true", help="column_sync: skip the round-5 serial-row timing")
     a = ap.parse_args()
     if a.what == "scorer_once" and len(a.rest) > 3:  # a variant library (tools/build_variants.sh)
         _lib.LIB_PATH = os.path.abspath(a.rest[3])

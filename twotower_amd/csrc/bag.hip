@@ -895,7 +895,11 @@ __device__ __forceinline__ void rotate_parts(f32x4 (&part)[U], int r) {
 // of kMaxPieces piece partials summed by one sub-wave each, the row folding its <= 16 group sums.
 // Every sum has a fixed order; only the slot numbering (atomic allocation) varies between runs.
 constexpr int kColMaxPieces = 4096;
-constexpr int kColLD = 16;  // entries loaded per sub-wave iteration (a multiple of 4)
+constexpr int kColLD = 16;  // partial rows loaded per sub-wave iteration of a group sum (a multiple of 4)
+#ifndef TT_COL_PIECE_LD
+#define TT_COL_PIECE_LD 16  // (8 / 32: C5 N = 8 at Zipf 1.05 606 / 607-615 us against 572-580, profiles/r06j_col_piece_ld_ab.txt)
+#endif
+constexpr int kColPieceLD = TT_COL_PIECE_LD;  // entries per iteration of a piece sum (its next indices prefetched)
 
 __device__ __forceinline__ int piece_len_col(int len) {
   if (len <= kPieceT * kMaxPieces) return kPieceT;  // piece_len(len) there
@@ -903,14 +907,19 @@ __device__ __forceinline__ int piece_len_col(int len) {
   return t > kPieceT ? t : kPieceT;
 }
 
-// One thread per row: merged length, piece count, piece / group slots (cnt[0] / cnt[1] counters,
-// zeroed by the launcher).  prow: the row of each piece slot; goff / gbeg / gend: a very long row's
-// group slots and their piece-slot ranges.
+// One thread per row: merged length and piece count.  A long row takes its piece slots and its entry
+// in the hot-row list with ONE 64-bit atomic add on {rows, pieces}: list index idx and first slot k0
+// come back together, so hot_k0 increases with idx and a piece slot finds its row by a binary search
+// over the list (no per-slot descriptors: a 4,096-piece row written by one thread took ~40 us).
+// Rows of more than kMaxPieces pieces likewise take group slots from a second {rows, groups} counter.
 __global__ __launch_bounds__(kBlock) void bag_col_pieces_kernel(const int32_t* __restrict__ seg, int nsrc, int64_t V,
                                                                 int32_t* __restrict__ nch, int32_t* __restrict__ off,
                                                                 int32_t* __restrict__ plen, int32_t* __restrict__ goff,
-                                                                int32_t* __restrict__ cnt, int32_t* __restrict__ prow,
-                                                                int32_t* __restrict__ gbeg, int32_t* __restrict__ gend) {
+                                                                unsigned long long* __restrict__ cnt,
+                                                                int32_t* __restrict__ hot_row,
+                                                                int32_t* __restrict__ hot_k0,
+                                                                int32_t* __restrict__ grp_row,
+                                                                int32_t* __restrict__ grp_g0) {
   const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (r >= V) return;
   int len = 0;
@@ -923,18 +932,30 @@ __global__ __launch_bounds__(kBlock) void bag_col_pieces_kernel(const int32_t* _
   nch[r] = np;
   if (np == 0) return;
   plen[r] = len;
-  const int k0 = atomicAdd(cnt, np);
+  const unsigned long long o = atomicAdd(cnt, (1ull << 32) | (unsigned)np);
+  const int idx = (int)(o >> 32), k0 = (int)(o & 0xffffffffu);
   off[r] = k0;
-  for (int k = 0; k < np; ++k) prow[k0 + k] = (int32_t)r;
+  hot_row[idx] = (int32_t)r;
+  hot_k0[idx] = k0;
   if (np > kMaxPieces) {
     const int ng = (np + kMaxPieces - 1) / kMaxPieces;
-    const int g0 = atomicAdd(cnt + 1, ng);
+    const unsigned long long og = atomicAdd(cnt + 1, (1ull << 32) | (unsigned)ng);
+    const int gi = (int)(og >> 32), g0 = (int)(og & 0xffffffffu);
     goff[r] = g0;
-    for (int g = 0; g < ng; ++g) {
-      gbeg[g0 + g] = k0 + g * kMaxPieces;
-      gend[g0 + g] = min(k0 + (g + 1) * kMaxPieces, k0 + np);
-    }
+    grp_row[gi] = (int32_t)r;
+    grp_g0[gi] = g0;
   }
+}
+
+// The list entry whose slot range holds slot k: the last idx < n with first[idx] <= k (first[] ascending).
+__device__ __forceinline__ int hot_entry(const int32_t* __restrict__ first, int n, int64_t k) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first[mid] <= k) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
 }
 
 // Sum rows [b, e) of src (El floats each) into part[] with entry j -> part[j % 4] (j from 0), LD
@@ -960,20 +981,23 @@ template <int LPR>
 __global__ __launch_bounds__(kBlock) void bag_col_piece_sum_kernel(const int32_t* __restrict__ seg,
                                                                    const int32_t* __restrict__ vals, int64_t nL,
                                                                    int nsrc, int64_t nseq, const float* __restrict__ gs,
-                                                                   int64_t V, const int32_t* __restrict__ off,
-                                                                   const int32_t* __restrict__ plen,
-                                                                   const int32_t* __restrict__ cnt,
-                                                                   const int32_t* __restrict__ prow,
+                                                                   int64_t V, const int32_t* __restrict__ plen,
+                                                                   const unsigned long long* __restrict__ cnt,
+                                                                   const int32_t* __restrict__ hot_row,
+                                                                   const int32_t* __restrict__ hot_k0,
                                                                    float* __restrict__ partial) {
   constexpr int RPI = kWave / LPR;
   constexpr int El = 4 * LPR;
+  constexpr int LD = kColPieceLD;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
   const int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
-  if (pc >= cnt[0]) return;
-  const int64_t r = prow[pc];
+  const unsigned long long n = *cnt;
+  if (pc >= (int64_t)(n & 0xffffffffu)) return;
+  const int h = hot_entry(hot_k0, (int)(n >> 32), pc);
+  const int64_t r = hot_row[h];
   const int len = plen[r], t = piece_len_col(len);
-  const int b = (int)(pc - off[r]) * t, e = min(b + t, len);
+  const int b = (int)(pc - hot_k0[h]) * t, e = min(b + t, len);
   f32x4 part[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -985,16 +1009,24 @@ __global__ __launch_bounds__(kBlock) void bag_col_piece_sum_kernel(const int32_t
     if (lo < hi) {
       const int32_t* vl = vals + (int64_t)src * nL + st - acc;  // merged entry m at vl[m]
       const float* g = gs + (int64_t)src * nseq * El;
-      for (int i = lo; i < hi; i += kColLD) {
-        int sq[kColLD];
+      // the next chunk's sequence indices are loaded before this chunk's gathers: one dependent
+      // memory round trip per chunk instead of two
+      int nq[LD];
 #pragma unroll
-        for (int u = 0; u < kColLD; ++u) sq[u] = (i + u < hi) ? vl[i + u] : -1;
-        f32x4 x[kColLD];
+      for (int u = 0; u < LD; ++u) nq[u] = (lo + u < hi) ? vl[lo + u] : -1;
+      for (int i = lo; i < hi; i += LD) {
+        int sq[LD];
 #pragma unroll
-        for (int u = 0; u < kColLD; ++u)
+        for (int u = 0; u < LD; ++u) {
+          sq[u] = nq[u];
+          nq[u] = (i + LD + u < hi) ? vl[i + LD + u] : -1;
+        }
+        f32x4 x[LD];
+#pragma unroll
+        for (int u = 0; u < LD; ++u)
           x[u] = (sq[u] >= 0) ? reinterpret_cast<const f32x4*>(g + (int64_t)sq[u] * El)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int u = 0; u < kColLD; ++u) part[u % 4] += x[u];
+        for (int u = 0; u < LD; ++u) part[u % 4] += x[u];
       }
       done += hi - lo;
       rotate_parts(part, (hi - lo) % 4);  // the next source's first entry goes to part[0]
@@ -1007,9 +1039,11 @@ __global__ __launch_bounds__(kBlock) void bag_col_piece_sum_kernel(const int32_t
 
 // One sub-wave per group of <= kMaxPieces piece partials (rows of more than kMaxPieces pieces).
 template <int LPR>
-__global__ __launch_bounds__(kBlock) void bag_col_group_sum_kernel(const int32_t* __restrict__ cnt,
-                                                                   const int32_t* __restrict__ gbeg,
-                                                                   const int32_t* __restrict__ gend,
+__global__ __launch_bounds__(kBlock) void bag_col_group_sum_kernel(const unsigned long long* __restrict__ cnt,
+                                                                   const int32_t* __restrict__ grp_row,
+                                                                   const int32_t* __restrict__ grp_g0,
+                                                                   const int32_t* __restrict__ nch,
+                                                                   const int32_t* __restrict__ off,
                                                                    const float* __restrict__ partial,
                                                                    float* __restrict__ gpart) {
   constexpr int RPI = kWave / LPR;
@@ -1017,11 +1051,16 @@ __global__ __launch_bounds__(kBlock) void bag_col_group_sum_kernel(const int32_t
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
   const int64_t gc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
-  if (gc >= cnt[1]) return;
+  const unsigned long long n = cnt[1];
+  if (gc >= (int64_t)(n & 0xffffffffu)) return;
+  const int h = hot_entry(grp_g0, (int)(n >> 32), gc);
+  const int64_t r = grp_row[h];
+  const int k0 = off[r], np = nch[r];
+  const int b = k0 + (int)(gc - grp_g0[h]) * kMaxPieces, e = min(b + kMaxPieces, k0 + np);
   f32x4 part[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  fold_rows<LPR>(partial, gbeg[gc], gend[gc], c, part);
+  fold_rows<LPR>(partial, b, e, c, part);
   reinterpret_cast<f32x4*>(gpart + gc * El)[c] = part[0] + part[1] + part[2] + part[3];
 }
 
@@ -1689,7 +1728,8 @@ extern "C" int tt_bag_scale_rows(const float* d_pooled, const float* denom, int6
 namespace tt {
 namespace {
 struct ColWs {
-  int32_t *nch, *off, *plen, *goff, *cnt, *prow, *gbeg, *gend;
+  int32_t *nch, *off, *plen, *goff, *hot_row, *hot_k0, *grp_row, *grp_g0;
+  unsigned long long* cnt;  // {hot rows, pieces}, {group rows, groups}
   float *partial, *gpart;
   int64_t maxp, maxg;
   size_t total;
@@ -1698,7 +1738,9 @@ ColWs col_carve(void* base, int64_t V, int nsrc, int64_t nL, int El) {
   ColWs w{};
   const int64_t n = (int64_t)nsrc * nL;
   w.maxp = max_pieces_for(n);
-  w.maxg = (w.maxp + kMaxPieces - 1) / kMaxPieces + 1;
+  // groups: sum over rows of more than kMaxPieces pieces of ceil(np / kMaxPieces) <= maxp / 256 + (rows of
+  // more than 32,768 tokens, at most n / 32,768 <= maxp / 512)
+  w.maxg = 2 * ((w.maxp + kMaxPieces - 1) / kMaxPieces) + 1;
   size_t o = 0;
   auto take = [&](size_t bytes) {
     const size_t at = o;
@@ -1706,8 +1748,8 @@ ColWs col_carve(void* base, int64_t V, int nsrc, int64_t nL, int El) {
     return at;
   };
   const size_t onch = take((size_t)V * 4), ooff = take((size_t)V * 4), olen = take((size_t)V * 4),
-               ogoff = take((size_t)V * 4), ocnt = take(8), oprow = take((size_t)w.maxp * 4),
-               ogb = take((size_t)w.maxg * 4), oge = take((size_t)w.maxg * 4),
+               ogoff = take((size_t)V * 4), ocnt = take(16), ohr = take((size_t)w.maxp * 4),
+               ohk = take((size_t)w.maxp * 4), ogr = take((size_t)w.maxg * 4), ogg = take((size_t)w.maxg * 4),
                opart = take((size_t)w.maxp * El * 4), ogp = take((size_t)w.maxg * El * 4);
   w.total = o + 256;
   if (base) {
@@ -1716,10 +1758,11 @@ ColWs col_carve(void* base, int64_t V, int nsrc, int64_t nL, int El) {
     w.off = reinterpret_cast<int32_t*>(b + ooff);
     w.plen = reinterpret_cast<int32_t*>(b + olen);
     w.goff = reinterpret_cast<int32_t*>(b + ogoff);
-    w.cnt = reinterpret_cast<int32_t*>(b + ocnt);
-    w.prow = reinterpret_cast<int32_t*>(b + oprow);
-    w.gbeg = reinterpret_cast<int32_t*>(b + ogb);
-    w.gend = reinterpret_cast<int32_t*>(b + oge);
+    w.cnt = reinterpret_cast<unsigned long long*>(b + ocnt);
+    w.hot_row = reinterpret_cast<int32_t*>(b + ohr);
+    w.hot_k0 = reinterpret_cast<int32_t*>(b + ohk);
+    w.grp_row = reinterpret_cast<int32_t*>(b + ogr);
+    w.grp_g0 = reinterpret_cast<int32_t*>(b + ogg);
     w.partial = reinterpret_cast<float*>(b + opart);
     w.gpart = reinterpret_cast<float*>(b + ogp);
   }
@@ -1762,9 +1805,9 @@ extern "C" int tt_bag_col_reduce_ex(const int32_t* seg_all, const int32_t* vals_
   if (ws) {
     w = col_carve(ws, V, nsrc, nL, El);
     TT_REQUIRE(ws_bytes >= w.total, "tt_bag_col_reduce_ex: workspace %zu bytes < %zu", ws_bytes, w.total);
-    TT_HIP(hipMemsetAsync(w.cnt, 0, 8, s), "memset piece counters");
+    TT_HIP(hipMemsetAsync(w.cnt, 0, 16, s), "memset piece counters");
     bag_col_pieces_kernel<<<dim3((unsigned)((V + kBlock - 1) / kBlock)), block, 0, s>>>(
-        seg_all, nsrc, V, w.nch, w.off, w.plen, w.goff, w.cnt, w.prow, w.gbeg, w.gend);
+        seg_all, nsrc, V, w.nch, w.off, w.plen, w.goff, w.cnt, w.hot_row, w.hot_k0, w.grp_row, w.grp_g0);
     TT_LAUNCH_CHECK("tt_bag_col_reduce (pieces)");
     pcs = ColPieces{w.nch, w.off, w.goff, w.partial, w.gpart};
   }
@@ -1775,8 +1818,9 @@ extern "C" int tt_bag_col_reduce_ex(const int32_t* seg_all, const int32_t* vals_
   do {                                                                                                        \
     if (ws) {                                                                                                 \
       bag_col_piece_sum_kernel<L><<<sub_grid(w.maxp), block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
-                                                                     w.off, w.plen, w.cnt, w.prow, w.partial); \
-      bag_col_group_sum_kernel<L><<<sub_grid(w.maxg), block, 0, s>>>(w.cnt, w.gbeg, w.gend, w.partial, w.gpart); \
+                                                                     w.plen, w.cnt, w.hot_row, w.hot_k0, w.partial); \
+      bag_col_group_sum_kernel<L><<<sub_grid(w.maxg), block, 0, s>>>(w.cnt, w.grp_row, w.grp_g0, w.nch, w.off,  \
+                                                                     w.partial, w.gpart);                      \
     }                                                                                                         \
     if (fused)                                                                                                \
       bag_col_reduce_kernel<L, 4, true, false><<<grid, block, 0, s>>>(seg_all, vals_all, nL, nsrc, nseq, gs_all, V, \
