@@ -218,6 +218,45 @@ __device__ __forceinline__ void stage_fill(char* smem, int buf, const ET* __rest
   }
 }
 
+// Write-through (sc1) stores for the bytes a launch hands to the next one (the split partials, the
+// forward's stored probabilities): the line leaves the XCD's L2 as it is written, so the launch
+// ends without dirty L2 lines to write back at its boundary (MI355X_MICROARCH.md price list,
+// 'boundary': + dirty bytes / 6 TB/s; 'publish-large': 16-B sc1 stores cost the same as plain).
+// A buffer store: the cache-policy bits are the builtin's operand (sc1 = 16 on gfx950) and the
+// compiler keeps the data registers live as for any store.  -DTT_WT_STORES=0: plain stores.
+#ifndef TT_WT_STORES
+#define TT_WT_STORES 1
+#endif
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+// a wave-uniform address as the compiler's SGPR pair (readfirstlane returns int: each half goes
+// through uint32_t, or the low half would sign-extend over the high one)
+__device__ __forceinline__ uint64_t uniform_addr(const void* p) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)p);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uintptr_t)p >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+template <typename V16>
+__device__ __forceinline__ void store16(void* base, uint32_t byte_off, const V16& v) {
+  static_assert(sizeof(V16) == 16, "16-B stores");
+#if TT_WT_STORES
+  // base is wave-uniform at every call site; readfirstlane says so to the compiler (no waterfall)
+  const uint64_t b = uniform_addr(base);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)0xffffffffu, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, byte_off, 0, 16 /* sc1 */);
+#else
+  *reinterpret_cast<V16*>(static_cast<char*>(base) + byte_off) = v;
+#endif
+}
+__device__ __forceinline__ void store4(void* base, uint32_t byte_off, float v) {
+#if TT_WT_STORES
+  const uint64_t b = uniform_addr(base);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)0xffffffffu, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 16 /* sc1 */);
+#else
+  *reinterpret_cast<float*>(static_cast<char*>(base) + byte_off) = v;
+#endif
+}
+
 template <int MODE, int H>
 __device__ __forceinline__ void write_partials(const f32x16 (&acc)[H / 32], float l_run, int split, int64_t nC,
                                                int64_t my_col, int hh, float* acc_part, float* l_part) {
@@ -260,16 +299,16 @@ __device__ __forceinline__ void write_partials_t(const f32x16 (&acc)[H / 32], fl
           f32x4{acc[ht][4 * g4], acc[ht][4 * g4 + 1], acc[ht][4 * g4 + 2], acc[ht][4 * g4 + 3]};
     }
   const int lane = lane_id(), rl = lane / NCH, ch = lane % NCH;
+  float* const blk = acc_part + ((int64_t)split * nC + col0) * H;  // this wave's 32 rows (wave-uniform)
 #pragma unroll
   for (int k = 0; k < 32 / RPI; ++k) {
     const int row = k * RPI + rl;
     const f32x4 v = *(const lds_f32x4_t*)(img + row * (H * 4) + ((ch ^ (row & 15)) << 4));
-    const int64_t col = col0 + row;
-    if (col < nC) *reinterpret_cast<f32x4*>(acc_part + ((int64_t)split * nC + col) * H + 4 * ch) = v;
+    if (col0 + row < nC) store16(blk, (uint32_t)((row * H + 4 * ch) * 4), v);
   }
   if constexpr (MODE == FWD) {
     l_run += __shfl_xor(l_run, 32);
-    if (col0 + r32 < nC && hh == 0) l_part[(int64_t)split * nC + col0 + r32] = l_run;
+    if (col0 + r32 < nC && hh == 0) store4(l_part + (int64_t)split * nC + col0, (uint32_t)(r32 * 4), l_run);
   }
 }
 
@@ -656,9 +695,9 @@ __device__ __forceinline__ void p_transpose_step(int st, int w1, const PStore& p
       asm volatile("" ::"v"(v), "v"(blk + ps.g + 1024 * s2));
       continue;
 #endif
-      // default cache policy: the backward, right after, finds part of P still in the Infinity Cache
-      // (measured: non-temporal stores and loads cost the backward 10 us at C3)
-      *reinterpret_cast<bf16x8*>(blk + ps.g + 1024 * s2) = v;
+      // not non-temporal: the backward, right after, finds part of P still in the Infinity Cache
+      // (measured: nt stores and loads cost the backward 10 us at C3); write-through (sc1) keeps that
+      store16(blk, (uint32_t)(ps.g + 1024 * s2), v);
     }
 }
 
