@@ -17,6 +17,34 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// Write-through (sc1) 16-B / 4-B stores: the line leaves the XCD's L2 as it is written, so a launch
+// that hands large outputs to the next one ends without dirty L2 lines to write back at the
+// boundary (MI355X_MICROARCH.md price list, 'boundary': + dirty bytes / 6 TB/s; 'publish-large':
+// 16-B sc1 stores cost what plain ones do; 4-B sc1 stores cost ~6x per byte, so only 16-B sites
+// use them).  A buffer store: the cache-policy bits are the builtin's operand (sc1 = 16 on gfx950)
+// and the compiler keeps the data registers live as for any store.  `base` must be wave-uniform
+// (an array base); the byte offset is per lane and below 4 GiB.
+typedef unsigned tt_u32x4 __attribute__((ext_vector_type(4)));
+// a wave-uniform address as the compiler's SGPR pair (readfirstlane returns int: each half goes
+// through uint32_t, or the low half would sign-extend over the high one)
+__device__ __forceinline__ uint64_t uniform_addr(const void* p) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)p);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uintptr_t)p >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+template <typename V16>
+__device__ __forceinline__ void store16_wt(void* base, uint32_t byte_off, const V16& v) {
+  static_assert(sizeof(V16) == 16, "16-B stores");
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)uniform_addr(base), 0, (int)0xffffffffu, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tt_u32x4, v), r, byte_off, 0, 16 /* sc1 */);
+}
+__device__ __forceinline__ void store4_wt(void* base, uint32_t byte_off, float v) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)uniform_addr(base), 0, (int)0xffffffffu, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 16 /* sc1 */);
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
 // v0^2 + v1^2 + v2^2 + v3^2 with its fma chain spelled out, so every kernel that forms a row

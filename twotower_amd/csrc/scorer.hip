@@ -218,40 +218,23 @@ __device__ __forceinline__ void stage_fill(char* smem, int buf, const ET* __rest
   }
 }
 
-// Write-through (sc1) stores for the bytes a launch hands to the next one (the split partials, the
-// forward's stored probabilities): the line leaves the XCD's L2 as it is written, so the launch
-// ends without dirty L2 lines to write back at its boundary (MI355X_MICROARCH.md price list,
-// 'boundary': + dirty bytes / 6 TB/s; 'publish-large': 16-B sc1 stores cost the same as plain).
-// A buffer store: the cache-policy bits are the builtin's operand (sc1 = 16 on gfx950) and the
-// compiler keeps the data registers live as for any store.  -DTT_WT_STORES=0: plain stores.
+// The scorer's hand-offs (split partials, stored probabilities) written through (common.hpp
+// store16_wt): round 6, scorer -4 us in the C3 step (profiles/r06n_wt_stores_ab.txt);
+// -DTT_WT_STORES=0: plain stores.
 #ifndef TT_WT_STORES
 #define TT_WT_STORES 1
 #endif
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-// a wave-uniform address as the compiler's SGPR pair (readfirstlane returns int: each half goes
-// through uint32_t, or the low half would sign-extend over the high one)
-__device__ __forceinline__ uint64_t uniform_addr(const void* p) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)p);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uintptr_t)p >> 32));
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
 template <typename V16>
 __device__ __forceinline__ void store16(void* base, uint32_t byte_off, const V16& v) {
-  static_assert(sizeof(V16) == 16, "16-B stores");
 #if TT_WT_STORES
-  // base is wave-uniform at every call site; readfirstlane says so to the compiler (no waterfall)
-  const uint64_t b = uniform_addr(base);
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)0xffffffffu, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, byte_off, 0, 16 /* sc1 */);
+  store16_wt(base, byte_off, v);
 #else
   *reinterpret_cast<V16*>(static_cast<char*>(base) + byte_off) = v;
 #endif
 }
 __device__ __forceinline__ void store4(void* base, uint32_t byte_off, float v) {
 #if TT_WT_STORES
-  const uint64_t b = uniform_addr(base);
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)b, 0, (int)0xffffffffu, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, byte_off, 0, 16 /* sc1 */);
+  store4_wt(base, byte_off, v);
 #else
   *reinterpret_cast<float*>(static_cast<char*>(base) + byte_off) = v;
 #endif
