@@ -515,25 +515,6 @@ int tt_head_gemm(const float* A, int64_t rows, int64_t lda, int K, const void* p
                  const float* bias, uint32_t* relu_mask, float* out, float* norms, void* ws, size_t ws_bytes,
                  tt_stream_t stream);
 
-/* ---- tower head as two fused chains (MeanPoolingTower, twotower/encoders.py:38-42,77; E in {64, 128, 256},
- * H in {128, 256}): one launch per pass instead of two GEMM launches (and the normalise pass), the first
- * product's rows kept in registers as the second product's operand, same split-bf16 products as
- * tt_head_gemm.
- * tt_head_fwd_chain: h = relu(x W1^T + b1) (stored, rows x H; ReLU bits into relu_bits, an opaque layout
- *   of tt_head_chain_bits_bytes(rows, H) read back by tt_head_bwd_chain), y = h W2^T + b2 and, normalize:
- *   out = y / max(|y|, 1e-12), norms[r] = |y_r| (F.normalize); otherwise out = y (tt_inbatch_l2_prep
- *   normalises).  planes_w1 / planes_w2: tt_head_split planes of W1 (H x E), W2 (H x H).
- * tt_head_bwd_chain: dh = (dy W2) * relu'(h) (stored, rows x H: the input of dW1), dx = dh W1, divided
- *   row by row by row_div when it is not NULL (the bag backward's d_pooled / denom, encoders.py:72, IEEE
- *   division).  planes_w2t / planes_w1t: the planes of W2^T (H x H) and W1^T (E x H). */
-size_t tt_head_chain_bits_bytes(int64_t rows, int H);
-int tt_head_fwd_chain(const float* x, int64_t rows, int64_t ldx, int E, int H, const void* planes_w1,
-                      const void* planes_w2, const float* b1, const float* b2, uint32_t* relu_bits, float* h,
-                      float* out, float* norms, int normalize, tt_stream_t stream);
-int tt_head_bwd_chain(const float* dy, int64_t rows, int64_t lddy, int E, int H, const void* planes_w2t,
-                      const void* planes_w1t, const uint32_t* relu_bits, const float* row_div, float* dh, float* dx,
-                      tt_stream_t stream);
-
 #ifdef __cplusplus
 }
 #endif

@@ -719,11 +719,15 @@ def test_plan_sort_equals_stable_sort(case):
         ids[5:50, 3] = 7
     wk, ws, wst = O.bag_plan(ids.cpu().numpy(), V, pad)
     n = ids.numel()
-    for split in (False, True):  # split: tt_bag_plan_part 0, then 1 (queued by flush_plans / wait)
-        plan = ops.BagPlan(ids, V, 64, pad, split=split)
+    plan = ops.BagPlan(ids, V, 64, pad)
+    plan.wait()
+    for split in (False, True):  # split: the ABI's two halves (tt_bag_plan_part 0, then 1) redo it
         if split:
-            ops.flush_plans()
-        plan.wait()
+            plan.buf.zero_()
+            for part in (0, 1):
+                ops.call("tt_bag_plan_part", plan.ids.data_ptr(), _lib.ids_dtype_code(plan.ids), plan.nseq, plan.L,
+                         plan.L, V, 64, plan.pad, plan.buf.data_ptr(), plan.buf.numel(), part,
+                         torch.cuda.current_stream().cuda_stream)
         keys, seqs, starts = _plan_out(plan, n)
         assert np.array_equal(keys, wk), split
         assert np.array_equal(seqs, ws), split

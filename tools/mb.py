@@ -158,31 +158,6 @@ def head(a):
     print(f"split planes: {graph_us(lambda: ops._planes(W, True), 20):.1f} us")
     print(f"torch addmm (hipBLASLt): {graph_us(lambda: torch.addmm(b, x, W.t()), 20):.1f} us")
     print(f"head_wgrad (dW + db): {graph_us(lambda: ops.head_wgrad(g2, x), 20):.1f} us")
-    # the fused chains (head_chain.hip) against the launches they replace, same rows (C3: 3 B rows)
-    W2 = torch.randn(256, 256, device=DEV) / 16
-    P2, P1t, P2t = ops._planes(W2, False), ops._planes(W, True), ops._planes(W2, True)
-    h, y, dh, dx = (torch.empty(N, 256, device=DEV) for _ in range(4))
-    bits = torch.empty(_lib.lib().tt_head_chain_bits_bytes(N, 256) // 4, dtype=torch.int32, device=DEV)
-    den = torch.full((N,), 40.0, device=DEV)
-    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
-
-    def fwd(norm):
-        return lambda: call("tt_head_fwd_chain", ptr(x), N, 256, 256, 256, ptr(P), ptr(P2), ptr(b), ptr(b), ptr(bits),
-                            ptr(h), ptr(y), ptr(norms), norm, st())
-
-    bwd = lambda: call("tt_head_bwd_chain", ptr(g2), N, 256, 256, 256, ptr(P2t), ptr(P1t), ptr(bits), ptr(den),  # noqa: E731
-                       ptr(dh), ptr(dx), st())
-    unf_f = graph_us(lambda: (ops._head_gemm(x, P, 0, bias=b, mask=mask), ops._head_gemm(h, P2, 4, bias=b)), 20)
-    unf_f1 = graph_us(lambda: (ops._head_gemm(x, P, 0, bias=b, mask=mask), ops._head_gemm(h, P2, 1, bias=b,
-                                                                                         norms=norms)), 20)
-    unf_b = graph_us(lambda: (ops._head_gemm(g2, P2t, 2, mask=mask), ops._head_gemm(dh, P1t, 5, bias=den)), 20)
-    print(json.dumps({"rows": N, "fwd_chain_bias_us": round(graph_us(fwd(0), 20), 1),
-                      "fwd_chain_l2_us": round(graph_us(fwd(1), 20), 1), "bwd_chain_rowdiv_us": round(graph_us(bwd, 20), 1),
-                      "unfused_fwd_bias_us": round(unf_f, 1), "unfused_fwd_l2_us": round(unf_f1, 1),
-                      "unfused_bwd_rowdiv_us": round(unf_b, 1),
-                      # two GEMMs per pass, six 32x32x16 MFMAs of 32 cycles per 32 x 32 x 16 block, 1024 SIMDs
-                      "mfma_floor_us_at_2GHz_per_pass": round(2 * (N / 32) * 8 * 16 * 6 / 1024 * 32 / 2e9 * 1e6, 1)}),
-          flush=True)
 
 
 def scorer(a):
@@ -466,28 +441,6 @@ def scorer_once(a):
     torch.cuda.synchronize()
 
 
-def head_once(a):
-    """One round of the head's fused chains and the unfused launches at C3's rows (counter passes)."""
-    N, E = 24576, 256
-    g = torch.Generator(device=DEV).manual_seed(0)
-    x, g2 = torch.randn(N, E, device=DEV, generator=g), torch.randn(N, E, device=DEV, generator=g)
-    W, W2 = (torch.randn(E, E, device=DEV, generator=g) / 16 for _ in range(2))
-    b = torch.randn(E, device=DEV, generator=g)
-    P, P2, P1t, P2t = ops._planes(W, False), ops._planes(W2, False), ops._planes(W, True), ops._planes(W2, True)
-    h, y, dh, dx = (torch.empty(N, E, device=DEV) for _ in range(4))
-    norms, den = torch.empty(N, device=DEV), torch.full((N,), 40.0, device=DEV)
-    mask = torch.empty(N, 8, dtype=torch.int32, device=DEV)
-    bits = torch.empty(_lib.lib().tt_head_chain_bits_bytes(N, E) // 4, dtype=torch.int32, device=DEV)
-    st = torch.cuda.current_stream().cuda_stream
-    for _ in range(3):
-        call("tt_head_fwd_chain", ptr(x), N, E, E, E, ptr(P), ptr(P2), ptr(b), ptr(b), ptr(bits), ptr(h), ptr(y),
-             ptr(norms), 0, st)
-        call("tt_head_bwd_chain", ptr(g2), N, E, E, E, ptr(P2t), ptr(P1t), ptr(bits), ptr(den), ptr(dh), ptr(dx), st)
-        ops._head_gemm(x, P, 0, bias=b, mask=mask)
-        ops._head_gemm(h, P2, 4, bias=b)
-    torch.cuda.synchronize()
-
-
 def next_rows(a):
     """each op's device time (graph replay), algorithmic bytes and the fraction of 8 TB/s,
     with the torch expression of the same result beside it."""
@@ -620,7 +573,7 @@ def search_once(a):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("what", choices=["bag_bwd", "plan", "head", "scorer", "scorer_dp", "split_fwd", "table_sync",
-                                     "column_sync", "l2prep", "scorer_once", "head_once", "next_rows",
+                                     "column_sync", "l2prep", "scorer_once", "next_rows",
                                      "search_once"])
     ap.add_argument("shape", nargs="?", default=None)
     ap.add_argument("rest", nargs="*")

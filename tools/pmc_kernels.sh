@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel stats + two SQ counter passes (each its own rocprofv3 run, --kernel-trace only) over one
-# tools/mb.py invocation.  Usage: tools/pmc_kernels.sh OUTDIR mb-args...   (e.g. head_once)
+# tools/mb.py invocation.  Usage: tools/pmc_kernels.sh OUTDIR mb-args...   (e.g. scorer_once)
 # Summarise with: python3 tools/pmc_report.py OUTDIR --match <kernel-name-substring>
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -105,10 +105,6 @@ _SIGNATURES = {
     "tt_head_split_ff2": (_c_int, [_vp, _vp, _c_int, _c_int, _vp, _vp]),
     "tt_head_gemm_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_relu_mask_bytes": (_c_sz, [_c_i64]),
-    "tt_head_chain_bits_bytes": (_c_sz, [_c_i64, _c_int]),
-    "tt_head_fwd_chain": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int,
-                                   _vp]),
-    "tt_head_bwd_chain": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tt_head_wgrad_ws_size": (_c_sz, [_c_i64, _c_int]),
     "tt_head_wgrad": (_c_int, [_vp, _vp, _c_i64, _c_int, _vp, _vp, _vp, _c_sz, _vp]),
     "tt_head_wgrad_ex_ws_size": (_c_sz, [_c_i64, _c_int, _c_int]),

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void bag_fwd_kernel(
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
-  // a capped grid (TT_GATHER_GRID) walks the sequences; the default grid has one wave per sequence
+  // one wave per sequence (the loop also covers a grid smaller than the sequences)
   const int64_t nwaves = (int64_t)(gridDim.x - split_blocks) * kWavesPerBlock;
   for (int64_t seq = (int64_t)(blockIdx.x - split_blocks) * kWavesPerBlock + (threadIdx.x >> 6); seq < nseq;
        seq += nwaves) {
@@ -1277,12 +1277,7 @@ int launch_fwd(const float* table, int64_t V, int E, const IdT* ids, int64_t nse
     for (int j = 0; j < 4; ++j) big = std::max<int64_t>(big, (int64_t)sj.n[j] * sj.k[j]);
     nsplit = (int)((big + kBlock - 1) / kBlock);
   }
-  static const int64_t gather_grid = [] {
-    const char* e = getenv("TT_GATHER_GRID");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  int64_t gblocks = (nseq + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (gather_grid > 0 && gather_grid < gblocks) gblocks = gather_grid;
+  const int64_t gblocks = (nseq + kWavesPerBlock - 1) / kWavesPerBlock;
   const dim3 grid((unsigned)(nsplit + gblocks)), block(kBlock);
 #define TT_FWD(LPR, NV, U) \
   bag_fwd_kernel<IdT, LPR, NV, U><<<grid, block, 0, s>>>(table, V, E, ids, nseq, L, ld, pooled, denom, sj, planes, nsplit)
@@ -1385,13 +1380,9 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   // (keys_in, vals_in) otherwise, so the last pass lands in the _out arrays
   const SortShape sh = sort_shape(n, V);
   const int nd = 1 << sh.D;
-  // TT_PLAN_GRID > 0: count / scatter launch at most that many workgroups, each walking tiles
-  // (fewer slots held beside the gather and the first head GEMM); 0: one workgroup per tile
-  static const int64_t plan_grid = [] {
-    const char* e = getenv("TT_PLAN_GRID");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  const unsigned sgrid = (unsigned)(plan_grid > 0 && plan_grid < sh.ntiles ? plan_grid : sh.ntiles);
+  // one workgroup per tile (capped grids whose workgroups walk several tiles measured slower in
+  // the step: profiles/r05n_plan_grid_ab.txt)
+  const unsigned sgrid = (unsigned)sh.ntiles;
   int32_t* cnt = static_cast<int32_t*>(w.sort_tmp);
   int32_t* total = cnt + (size_t)nd * sh.ntiles;
   SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr, L > 0 ? 1.0 / (double)L : 0.0};

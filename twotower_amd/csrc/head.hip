@@ -83,7 +83,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
   // LDS-DMA writes each 1 KiB piece linearly (lane l -> byte 16 l = row n0 + l / kCH, slot
   // l % kCH), so the swizzle goes on the source: slot s of row n holds chunk s ^ (n % kCH).
   // kSliceB / 4 KiB pieces per wave (24 at K = 256), all in flight together, no staging registers.
-#ifndef TT_HABL_NOFILL
   {
     constexpr int kPiecesW = kSliceB / 1024 / kWaves;
     constexpr int kRowsPiece = 1024 / kRowB;
@@ -100,23 +99,14 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
                    : "memory");
     }
   }
-#endif
   // this wave's tiles: rows g*tiles*128 + t*128 + wid*32 + [0, 32)
   const int64_t wrow0 = (int64_t)g * tiles * (kWaves * kTileRows) + wid * kTileRows;
   auto a_src = [&](int t) {
     int64_t r = wrow0 + (int64_t)t * (kWaves * kTileRows) + r32;
     r = r < rows ? r : rows - 1;  // rows past the end are computed from a clamped row, never stored
-#ifdef TT_HABL_ACOAL
-    r = (r - r32) / 32 * 32;  // timing ablation: instruction i reads row r + i/2.. contiguously
-    return reinterpret_cast<const f32x4*>(A + r * lda + lane * 4 - 4 * (hh * 8) / 4 * 0);
-#endif
     return reinterpret_cast<const f32x4*>(A + r * lda + hh * 8);
   };
-#ifdef TT_HABL_ACOAL
-  constexpr int kAStep = 2 * 64, kAHalf = 64;  // f32x4 units: rows of 256 floats
-#else
   constexpr int kAStep = 4, kAHalf = 1;
-#endif
   // A chunks in flight: the whole next tile (kAR = kSteps: 128 VGPRs at K = 256, one wave per SIMD
   // with the rest), or TT_HEAD_AHALF: half a tile ahead (kAR = kSteps / 2, ~64 VGPRs less, so the
   // kernel fits 256 registers and other kernels' waves can share its SIMDs)
@@ -142,11 +132,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
   // B operand of column tile ct, plane p, step j: local column n = 32 ct + r32, chunk 2 j + hh
   const lds_char_t* bbase = lds + r32 * kRowB;
   auto rdb = [&](int ct, int p, int j) {  // (32 ct + r32) % kCH == r32 % kCH picks the swizzle
-#ifdef TT_HABL_NOLDS
-    bf16x8 z;
-    asm volatile("" : "=v"(z));
-    return z;
-#endif
     return *reinterpret_cast<const lds_bf16x8_t*>(bbase + ct * 32 * kRowB + p * kPlaneB +
                                                   (((2 * j + hh) ^ (r32 % kCH)) << 4));
   };
@@ -181,13 +166,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
       asm volatile("" : "+v"(w[2][i]));
     }
   };
-#ifdef TT_HABL_NOSPLIT
-  auto split_all = [&](const f32x4 (&ar)[2], u32x4 (&w)[3]) {
-    w[0] = __builtin_bit_cast(u32x4, ar[0]);
-    w[1] = w[0];
-    w[2] = w[0];
-  };
-#endif
   u32x4 ca[3];
   bf16x8 cb[2][3];
   {
@@ -244,16 +222,9 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
       {
         const int c = j + kAR;  // (j is a compile-time constant after unrolling: so is the branch)
         const f32x4* rs = c < kSteps ? csrc + c * kAStep : nsrc + (c - kSteps) * kAStep;
-#ifndef TT_HABL_NOALOAD
         areg[j % kAR][0] = *rs;
         areg[j % kAR][1] = *(rs + kAHalf);
-#else
-        asm volatile("" : "+v"(areg[j % kAR][0]), "+v"(areg[j % kAR][1]));
-#endif
       }
-#ifdef TT_HABL_NOSPLIT
-      split_all(areg[jn % kAR], na);
-#endif
       __builtin_amdgcn_sched_barrier(0);
       const bf16x8 a0 = __builtin_bit_cast(bf16x8, ca[0]), a1 = __builtin_bit_cast(bf16x8, ca[1]),
                    a2 = __builtin_bit_cast(bf16x8, ca[2]);
@@ -262,9 +233,6 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
         const int ct = m / 6;
         f32x16& C = acc[ct];
         const bf16x8(&b)[3] = cb[ct];
-#ifdef TT_HABL_NOMFMA
-        asm volatile("" ::"v"(a0), "v"(a1), "v"(a2), "v"(b[0]), "v"(b[1]), "v"(b[2]));
-#else
         switch (m % 6) {
           case 0: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[0], C, 0, 0, 0); break;
           case 1: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[1], C, 0, 0, 0); break;
@@ -273,10 +241,7 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
           case 4: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[1], C, 0, 0, 0); break;
           default: C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0], C, 0, 0, 0); break;
         }
-#endif
-#ifndef TT_HABL_NOSPLIT
         split_piece(areg[jn % kAR], m, st, na);
-#endif
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
@@ -307,12 +272,10 @@ __global__ __launch_bounds__(256, 1) void head_gemm_kernel(const float* __restri
     }
     float* orow = out + trow0 * N + c * kColsWG + r32;
     if (__builtin_amdgcn_readfirstlane((int)(trow0 + kTileRows <= rows))) {
-#ifndef TT_HABL_NOSTORE
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int v = 0; v < 16; ++v) orow[((v & 3) + 8 * (v >> 2) + 4 * hh) * N + ct * 32] = acc[ct][v];
-#endif
     } else {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
@@ -477,11 +440,6 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
   auto rd = [&](int buf, int mat, int plane, int tile) {
     const lds_char_t* b = lds + buf * kWgBuf + mat * 3 * kWgPlane + plane * kWgPlane;
     const int col = 32 * tile + 16 * gh + 4 * pp;
-#ifdef TT_WABL_NOREAD
-    bf16x8 z;
-    asm volatile("" : "=v"(z) : "v"(b), "v"(col));
-    return z;
-#endif
     const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(b + wg_off(8 * kh + q, col)));
     const bf16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(b + wg_off(8 * kh + 4 + q, col)));
     return bf16x8{t1[0], t1[1], t1[2], t1[3], t2[0], t2[1], t2[2], t2[3]};
@@ -508,20 +466,12 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
         ga[t][p] = rd(buf, 0, p, 2 * wi + t);
         xb[t][p] = rd(buf, 1, p, 2 * wj + t);
       }
-#ifndef TT_WABL_NOSTAGE
     stage_chunk(next, ch + 1, buf ^ 1);  // past the end: zeros into the unused buffer
-#else
-    asm volatile("" ::"v"(next[0]), "v"(next[1]), "v"(next[2]), "v"(next[3]));
-#endif
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
       for (int tj = 0; tj < 2; ++tj) {
         f32x16& C = acc[ti][tj];
-#ifdef TT_WABL_NOMFMA
-        asm volatile("" ::"v"(ga[ti][0]), "v"(ga[ti][1]), "v"(ga[ti][2]), "v"(xb[tj][0]), "v"(xb[tj][1]), "v"(xb[tj][2]));
-        continue;
-#endif
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][2], xb[tj][0], C, 0, 0, 0);
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][1], xb[tj][1], C, 0, 0, 0);
         C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ti][0], xb[tj][2], C, 0, 0, 0);
@@ -547,9 +497,6 @@ __global__ __launch_bounds__(256, 1) void head_wgrad_kernel(const float* __restr
         const int i = 128 * bi + 32 * (2 * wi + ti) + (v & 3) + 8 * (v >> 2) + 4 * kh;
         const int j = 128 * bj + 32 * (2 * wj + tj) + (lane & 31);
         if (NX < kWgBlk && 32 * (2 * wj + tj) >= XW) continue;  // zero columns past a narrow X
-#ifdef TT_WABL_NOSTORE
-        if (acc[ti][tj][v] == 12345.678f)
-#endif
         pw[i * NX + j] = acc[ti][tj][v];
       }
   if (bj == 0 && part_b) {  // fold the 8 row groups (lr) of each column group in LDS, fixed order

@@ -376,11 +376,7 @@ struct MapState {
   __device__ __forceinline__ void slot(int v, const f32x16& xa, bf16x8 (&bh)[2], bf16x8 (&bl)[2]) {
     if (kDeferPair && (v & 1) == 0 && (v & 7) != 0) pair(v - 2, bh, bl);  // before this slot's exp
     const float y = __builtin_fmaf(xa[v], c2, -sub[v]);
-#ifdef TT_ABLATE_EXP
-    e[v] = y;
-#else
     e[v] = __builtin_amdgcn_exp2f(y);
-#endif
     asm volatile("" : "+v"(e[v]));  // side-effecting use: keeps the exp inside this step
     if ((v & 1) && (!kDeferPair || (v & 7) == 7)) pair(v & ~1, bh, bl);
   }
@@ -391,9 +387,6 @@ struct MapState {
 // 16 chunks (+256 B) and tile jt adds 32 rows: immediates.  Acc chain: the transposed 4-row
 // blocks of rows r0 and r0 + 8 at chunk (4 ht + cbase) ^ swz = 4 (ht ^ (swz >> 2)) + (cbase ^
 // (swz & 3)) for ht = 0..3; ht >= 4 (+256 B), the second 16-row half and jt: immediates.
-#ifndef TT_LDS_HI
-#define TT_LDS_HI 1
-#endif
 template <int H>
 struct LdsOffs {
   using T = Tile<__bf16, H>;
@@ -401,11 +394,9 @@ struct LdsOffs {
   static constexpr int NA4 = (H / 32) < 4 ? (H / 32) : 4;
   unsigned s[NS8];
   unsigned a0[NA4], a1[NA4];
-#if TT_LDS_HI
   // the same offsets + 64 KiB: a ds_read's offset field holds 16 bits, so reads of the ring slots
   // at 64 KiB and above take these (lds_at) instead of a v_add_u32 per read address
   unsigned sh[NS8], a0h[NA4], a1h[NA4];
-#endif
   __device__ __forceinline__ void init(int lane) {
     const int r32 = lane & 31, hh = lane >> 5, x = T::swz(r32);
 #pragma unroll
@@ -419,7 +410,6 @@ struct LdsOffs {
       a0[ht] = r0 * T::ROWB + bo + (((4 * ht + cbase) ^ x0) << 4);
       a1[ht] = (r0 + 8) * T::ROWB + bo + (((4 * ht + cbase) ^ x1) << 4);
     }
-#if TT_LDS_HI
 #pragma unroll
     for (int k = 0; k < NS8; ++k) {
       sh[k] = s[k] + 65536u;
@@ -431,7 +421,6 @@ struct LdsOffs {
       a1h[ht] = a1[ht] + 65536u;
       asm volatile("" : "+v"(a0h[ht]), "+v"(a1h[ht]));
     }
-#endif
   }
 };
 
@@ -440,13 +429,8 @@ struct LdsOffs {
 // and above go through the +64 KiB offsets, so offset + immediate stays inside the 16-bit field.
 __device__ __forceinline__ const lds_char_t* lds_at(const lds_char_t* base, const lds_char_t* tile, unsigned vo,
                                                     unsigned vo_hi) {
-#if TT_LDS_HI
   const int off = (int)(tile - base);
   if (off >= 65536) return base + (off - 65536) + vo_hi;
-#else
-  (void)base;
-  (void)vo_hi;
-#endif
   return tile + vo;
 }
 
@@ -476,25 +460,13 @@ constexpr int kSdFor = TT_SD < H / 8 ? TT_SD : H / 8;  // <= NSTEP: never past t
 #define TT_FWD_MAP_S 1
 #endif
 constexpr bool kMapInS = TT_FWD_MAP_S != 0;
-#ifndef TT_FWD_UNROLL4
-#define TT_FWD_UNROLL4 1
-#endif
 
-#ifdef TT_S_BUILTIN  // diagnostic: the S chain through the builtin (compiler-placed accumulators)
-__device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
-  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, f32x16{}, 0, 0, 0);
-}
-__device__ __forceinline__ void mfma_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
-  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, d, 0, 0, 0);
-}
-#else
 __device__ __forceinline__ void mfma_v_first(f32x16& d, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void mfma_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
 }
-#endif
 
 template <int H>
 struct UnitSrc {
@@ -512,14 +484,7 @@ __device__ __forceinline__ bf16x8 unit_operand(int i, const UnitSrc<H>& u, const
   constexpr int NK = H / 16, NHT = H / 32, NSA = 2 * NHT, NSTEP = NK + NSA;
   const bool nxt = i >= NSTEP;
   const int w = nxt ? i - NSTEP : i;
-#ifdef TT_ABLATE_LDSREAD  // timing ablation (never in a real build): no operand reads
-  return bf16x8{(__bf16)(float)w, (__bf16)(float)(lo.s[0] & 7), 0, 0, 0, 0, 0, (__bf16)(float)nxt};
-#endif
-#if TT_LDS_HI
 #define TT_LO_HI(f, i) lo.f##h[i]
-#else
-#define TT_LO_HI(f, i) lo.f[i]
-#endif
   if (w < NK) {
     const lds_char_t* tb = nxt ? u.n : u.s;
     return *reinterpret_cast<const lds_bf16x8_t*>(lds_at(u.base, tb, lo.s[w & 7], TT_LO_HI(s, w & 7)) +
@@ -674,10 +639,6 @@ __device__ __forceinline__ void p_transpose_step(int st, int w1, const PStore& p
     if (st == at(w1 + 5 + 2 * s2)) {
       const bf16x8 v = bf16x8{pt[s2][0][0], pt[s2][0][1], pt[s2][0][2], pt[s2][0][3],
                               pt[s2][1][0], pt[s2][1][1], pt[s2][1][2], pt[s2][1][3]};
-#ifdef TT_ABLATE_PSTORE  // timing ablation (never in a real build): no P stores
-      asm volatile("" ::"v"(v), "v"(blk + ps.g + 1024 * s2));
-      continue;
-#endif
       // not non-temporal: the backward, right after, finds part of P still in the Infinity Cache
       // (measured: nt stores and loads cost the backward 10 us at C3); write-through (sc1) keeps that
       store16(blk, (uint32_t)(ps.g + 1024 * s2), v);
@@ -712,18 +673,11 @@ __device__ __forceinline__ typename RowVec<V>::f loadv(const __bf16* p, int lane
 // sum over s < S of w_s p[s * stride] (w_s = f_loc for s < S_loc, else 1: the product is skipped,
 // x * 1 == x), added in the order s = 0, 1, ... as the plain loop does (the same bits), with up to
 // eight loads in flight instead of one dependent round trip per split.
-// (-DTT_COMBINE_BATCHED=0: one load per step, the loop before round 3's end; C2 0.4299 vs 0.4273
-// ms/step batched, same box, profiles/r03zp_c2_combine_ab.txt)
-#ifndef TT_COMBINE_BATCHED
-#define TT_COMBINE_BATCHED 1
-#endif
+// (one load per step, the loop before round 3's end: C2 0.4299 vs 0.4273 ms/step batched, same
+// box, profiles/r03zp_c2_combine_ab.txt)
 __device__ __forceinline__ float sum_parts1(const float* __restrict__ p, int64_t stride, int S, int S_loc = 0,
                                             float f_loc = 1.f) {
   float o = 0.f;
-#if !TT_COMBINE_BATCHED
-  for (int s = 0; s < S; ++s) o += s < S_loc ? f_loc * p[(int64_t)s * stride] : p[(int64_t)s * stride];
-  return o;
-#endif
   for (int s0 = 0; s0 < S; s0 += 8) {  // up to 8 splits' loads in one round (S <= 8 by plan_for)
     float v[8];
 #pragma unroll
@@ -930,9 +884,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // scalar per wave
   auto piece = [&](int c, int b, int64_t r0) {  // piece c of the stage at row r0 into buffer b
-#ifdef TT_ABLATE_FILL  // timing ablation (never in a real build): stages after the prologue keep stale data
-    if (r0 != row_begin || b != 0) return;
-#endif
     if (c < T::NI) {
       glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024);
     } else if constexpr (MODE == DD) {  // every wave loads the lse row (same bytes): uniform vmcnt
@@ -999,7 +950,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
   constexpr int NSTEP = NK + 2 * NHT;
   if (MODE == FWD) TT_KTRACE_K(1, 1);
   // One stage.  bufc: the ring slot (t & 3) as a compile-time constant when the loop is unrolled
-  // over the ring (TT_FWD_UNROLL4), so every LDS operand address is a per-lane offset plus an
+  // over the ring, so every LDS operand address is a per-lane offset plus an
   // immediate (no per-read address add); -1: the slot computed at run time.
   auto stage = [&](int64_t t, auto bufc) {
     constexpr int bc = decltype(bufc)::value;
@@ -1016,9 +967,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     else
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + (STOREP ? kPStores * NJ : 0)) : "memory");
     TT_TRACE(1);
-#ifndef TT_ABLATE_BARRIER
     asm volatile("s_barrier" ::: "memory");
-#endif
     TT_TRACE(2);
     auto unit = [&](auto jtc, const f32x16& xin, f32x16& xout) {
       constexpr int jt = decltype(jtc)::value;
@@ -1046,16 +995,12 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_bf16_kernel(
     unit(std::integral_constant<int, 0>{}, xa, xb);
     unit(std::integral_constant<int, 1>{}, xb, xa);
   };
-#if TT_FWD_UNROLL4
   for (int64_t t = 0; t < ntiles; t += 4) {  // wave-uniform conditions: the ring slot of each call is constant
     stage(t, std::integral_constant<int, 0>{});
     if (t + 1 < ntiles) stage(t + 1, std::integral_constant<int, 1>{});
     if (t + 2 < ntiles) stage(t + 2, std::integral_constant<int, 2>{});
     if (t + 3 < ntiles) stage(t + 3, std::integral_constant<int, 3>{});
   }
-#else
-  for (int64_t t = 0; t < ntiles; ++t) stage(t, std::integral_constant<int, -1>{});
-#endif
   if (MODE == FWD) TT_KTRACE_K(1, 2);
   drain_dma();  // no LDS-DMA may outlive the workgroup
   __syncthreads();  // every wave is past its last ring read: the ring takes the partial images
@@ -1082,10 +1027,6 @@ template <int s2, int imm_extra = 0>
 __device__ __forceinline__ bf16x8 p_load(const char* sbase, unsigned voff) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   i32x4 r;
-#ifdef TT_ABLATE_PLOAD  // timing ablation (never in a real build): no P loads
-  r = i32x4{(int)voff, s2, imm_extra, (int)(uintptr_t)sbase};
-  return __builtin_bit_cast(bf16x8, r);
-#endif
   asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "n"(1024 * s2 + imm_extra)
                : "memory");
   return __builtin_bit_cast(bf16x8, r);
@@ -1127,9 +1068,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
   const unsigned wbase = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);
   auto stage_row = [&](int64_t t) { return t < ntiles ? row_begin + t * T::BJ : row_begin; };
   auto fill = [&](int c, int b, int64_t r0) {
-#ifdef TT_ABLATE_FILL  // timing ablation (never in a real build): stages after the prologue keep stale data
-    if (r0 != row_begin || b > 2) return;
-#endif
     glds_dwordx4_s(fo.v[c], R + r0 * H, wbase + b * T::STAGE_B + c * NW * 1024);
   };
   // a lane's fragment of a P block: candidate r32, queries 16 s2 + 8 (j >> 2) + 4 hh + (j & 3) (PStore)
@@ -1160,11 +1098,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) asm volatile("" : "+v"(x.v[jt][c][s2]));
   };
-#ifdef TT_ABLATE_PLOAD
-  constexpr int kPl = 0;
-#else
   constexpr int kPl = NPL;
-#endif
   // prologue in steady-state order: [P(k), fills(k)] for k = 0, 1, 2, but only the first half
   // of fills(2): the second half of every stage's fills comes from the first tile of the stage
   // two before it (below)
@@ -1219,9 +1153,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
         TT_TRACE_B(1);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPC + 2 * kPl) : "memory");
         TT_TRACE_B(2);
-#ifndef TT_ABLATE_BARRIER
         asm volatile("s_barrier" ::: "memory");
-#endif
         TT_TRACE_B(3);
         tie(next);
       }
@@ -1296,7 +1228,7 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 // consumes X register t directly as its B operand (k = row of X held by register t).
 // Waves per SIMD the H = 128 fp32 engine is compiled for.  Round 2: two waves spilled 80 B/lane of
 // scratch (256 VGPRs), so the forward ran at one (217 VGPRs + 64 AGPRs).  Round 3: the Acc chain's
-// LDS addresses come from four per-lane offsets plus immediates (TT_F32_AOFF; hipcc had held
+// LDS addresses come from four per-lane offsets plus immediates (hipcc had held
 // 16 x NHT loop-invariant addresses in VGPRs across the loop), so both passes fit two waves with no
 // scratch (225 / 221 VGPRs): C2 forward 205 -> 175 us, backward 180 -> 160 us, bit-identical,
 // step 0.520 -> 0.469 ms (profiles/r03t_f32_variants.txt, r03t_c2_ab.txt).
@@ -1305,9 +1237,6 @@ __global__ __launch_bounds__(NT, (H <= 128 ? 2 : 1)) void score_ddp_kernel(
 #endif
 #ifndef TT_F32_MINW128_DD
 #define TT_F32_MINW128_DD 2
-#endif
-#ifndef TT_F32_AOFF
-#define TT_F32_AOFF 1
 #endif
 // Waves per SIMD of the fp32 backward from stored probabilities (no X chain: fewer registers), by H
 #ifndef TT_F32_MINW_LOADP128
@@ -1384,12 +1313,10 @@ void score_f32_kernel(
   for (int t = 0; t < NHT; ++t) acc[t] = f32x16{};
   float l_run = 0.f;
   const int rx = T::swz(r32);
-#if TT_F32_AOFF
   static_assert(T::SWM == 7, "the Acc chain's offsets assume the f32 tile's 3-bit row XOR");
   unsigned aoff[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) aoff[u] = (u + 4 * hh) * T::ROWB + (((r32 >> 2) ^ (u + 4 * hh)) << 4) + (r32 & 3) * 4;
-#endif
   drain_dma();
   __syncthreads();
 
@@ -1428,16 +1355,10 @@ void score_f32_kernel(
     for (int ht = 0; ht < NHT; ++ht) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-#if TT_F32_AOFF
         // row = (v & 3) + 8 (v >> 2) + 4 hh and swz(row) = row & 7 = (v & 3) + 4 hh, so the XOR only
         // touches the chunk's low three bits: four per-lane offsets (one per v & 3, kernel-constant)
         // plus immediates, instead of 16 x NHT loop-invariant addresses held across the loop
         const float a = *reinterpret_cast<const lds_float_t*>(tile + aoff[v & 3] + 8 * (v >> 2) * T::ROWB + 128 * ht);
-#else
-        const int row = acc_row(v, hh);
-        const float a = *reinterpret_cast<const lds_float_t*>(
-            tile + row * T::ROWB + (((8 * ht + (r32 >> 2)) ^ T::swz(row)) << 4) + (r32 & 3) * 4);
-#endif
         acc[ht] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, e[v], acc[ht], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);

@@ -130,13 +130,9 @@ class BagPlan:
 
     __slots__ = ("ids", "buf", "ready", "nseq", "L", "V", "E", "pad")
 
-    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None, gather_group=None,
-                 split: bool = False):
+    def __init__(self, ids: torch.Tensor, V: int, E: int, padding_idx: int | None, gather_group=None):
         """gather_group: data parallel with a replicated table update -- the plan covers the ids
-        of every rank (all-gathered here, on the side stream, rank-major).  split: only the first
-        half of the sort here (tt_bag_plan_part 0); the second half is queued by finish() (the next
-        loss forward calls flush_plans(), or wait() does), so it runs beside the loss instead of
-        beside the head and the scorer's operand prep."""
+        of every rank (all-gathered here, on the side stream, rank-major)."""
         dev = ids.device
         self.V, self.E = V, E
         main = torch.cuda.current_stream(dev)
@@ -156,55 +152,15 @@ class BagPlan:
             self.nseq, self.L = ids.shape
             nbytes = _lib.lib().tt_bag_plan_ws_size(self.nseq, self.L, V, E)
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            if split:
-                call("tt_bag_plan_part", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E,
-                     self.pad, ptr(self.buf), self.buf.numel(), 0, side.cuda_stream)
-            else:
-                call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, self.pad,
-                     ptr(self.buf), self.buf.numel(), side.cuda_stream)
-        self.ready = None
-        if split:
-            flush_plans()  # (at most one plan waits for its second half)
-            _PENDING_PLANS.append(self)
-        else:
-            self.ready = torch.cuda.Event()
-            self.ready.record(side)
-
-    def finish(self) -> None:
-        """Queue the second half of a split plan on the side stream, behind the current stream's
-        work so far (idempotent)."""
-        if self.ready is not None:
-            return
-        dev = self.buf.device
-        side = _lib.side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        call("tt_bag_plan_part", ptr(self.ids), _lib.ids_dtype_code(self.ids), self.nseq, self.L, self.L, self.V,
-             self.E, self.pad, ptr(self.buf), self.buf.numel(), 1, side.cuda_stream)
+            call("tt_bag_plan", ptr(ids), _lib.ids_dtype_code(ids), self.nseq, self.L, self.L, V, E, self.pad,
+                 ptr(self.buf), self.buf.numel(), side.cuda_stream)
         self.ready = torch.cuda.Event()
         self.ready.record(side)
-        if self in _PENDING_PLANS:
-            _PENDING_PLANS.remove(self)
 
     def wait(self) -> None:
-        self.finish()
         cur = torch.cuda.current_stream(self.buf.device)
         cur.wait_event(self.ready)
         self.buf.record_stream(cur)  # allocated on the side stream, read here
-
-
-_PENDING_PLANS: list = []  # split plans whose second half is not queued yet
-
-
-def flush_plans() -> None:
-    """Queue the second half of every split plan (called by the loss forwards: the sort's last
-    pass then runs beside the loss, not beside the head and the scorer's operand prep)."""
-    while _PENDING_PLANS:
-        _PENDING_PLANS[0].finish()
-
-
-def plan_split() -> bool:
-    """TT_PLAN_SPLIT=1: split plans (BagPlan split=True) for the tower bag's sort."""
-    return os.environ.get("TT_PLAN_SPLIT", "0") == "1"
 
 
 def plan_fork_early(table_bytes: int) -> bool:
@@ -336,8 +292,7 @@ class BagMeanPool(torch.autograd.Function):
         if early:
             deferred = getattr(weight, "_tt_deferred", None)
             group = deferred.gather_group if deferred is not None else None
-            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group,
-                               split=plan_split())
+            ctx.plan = BagPlan(ids, weight.shape[0], weight.shape[1], padding_idx, gather_group=group)
         pooled, denom = bag_mean_forward(weight, ids)
         if plan_now and not early:
             # forked after the gather: the sort runs beside the towers and the scorer (forked
@@ -780,17 +735,9 @@ class TowerHead(torch.autograd.Function):
         norm = torch.empty(rows, dtype=_FLOAT, device=x.device)
         req = _SCORER_PREP[-1] if _SCORER_PREP and _prep_fusable(width, _SCORER_PREP[-1][1]) else None
         prep = req is not None and 0 < req[0] < rows
-        ctx.chain = head_chain()
-        if ctx.chain:  # both Linears (and F.normalize) in one launch, h never re-read (head_chain.hip)
-            mask = torch.empty(_lib.lib().tt_head_chain_bits_bytes(rows, H) // 4, dtype=torch.int32, device=x.device)
-            h = torch.empty(rows, H, dtype=_FLOAT, device=x.device)
-            out = torch.empty(rows, H, dtype=_FLOAT, device=x.device)
-            call("tt_head_fwd_chain", ptr(x), rows, x.stride(0), E, H, ptr(p_w1), ptr(p_w2), ptr(_contig_f32(b1, "b1")),
-                 ptr(_contig_f32(b2, "b2")), ptr(mask), ptr(h), ptr(out), ptr(norm), int(not prep), stream_of(x))
-        else:
-            mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
-            h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
-            out = _head_gemm(h, p_w2, 4, bias=b2) if prep else _head_gemm(h, p_w2, 1, bias=b2, norms=norm)
+        mask = torch.empty(_lib.lib().tt_head_relu_mask_bytes(rows) // 4, dtype=torch.int32, device=x.device)
+        h = _head_gemm(x, p_w1, 0, bias=b1, mask=mask, N=H)
+        out = _head_gemm(h, p_w2, 4, bias=b2) if prep else _head_gemm(h, p_w2, 1, bias=b2, norms=norm)
         if prep:
             nq, dt = req  # normalise pass fused with the in-batch scorer's operand prep
             ws = torch.empty(_lib.lib().tt_inbatch_ws_size(nq, rows - nq, width, dt), dtype=torch.uint8,
@@ -854,23 +801,12 @@ class TowerHead(torch.autograd.Function):
 
         tok, ctx.bag_token = ctx.bag_token, None
         dx = None
-        if ctx.chain:  # dh and dx (/ denom for the bag backward) in one launch (head_chain.hip)
-            dh = torch.empty(dy.shape[0], H, dtype=_FLOAT, device=dy.device)
-            dxc = torch.empty(dy.shape[0], E, dtype=_FLOAT, device=dy.device)
-            div = tok.denom if (ctx.needs_input_grad[0] and tok is not None) else None
-            call("tt_head_bwd_chain", ptr(dy), dy.shape[0], dy.stride(0), E, H, ptr(p_w2t), ptr(p_w1t), ptr(mask),
-                 ptr(div), ptr(dh), ptr(dxc), stream_of(dy))
-            if ctx.needs_input_grad[0]:
-                dx = dxc
-                if tok is not None:
-                    tok.grad = dx
-        else:
-            dh = _head_gemm(dy, p_w2t, 2, mask=mask, N=H)
-            if ctx.needs_input_grad[0] and tok is not None:  # dx / denom for the bag backward (epi 5)
-                dx = _head_gemm(dh, p_w1t, 5, bias=tok.denom, N=E)
-                tok.grad = dx
-            elif ctx.needs_input_grad[0]:
-                dx = _head_gemm(dh, p_w1t, 3, N=E)
+        dh = _head_gemm(dy, p_w2t, 2, mask=mask, N=H)
+        if ctx.needs_input_grad[0] and tok is not None:  # dx / denom for the bag backward (epi 5)
+            dx = _head_gemm(dh, p_w1t, 5, bias=tok.denom, N=E)
+            tok.grad = dx
+        elif ctx.needs_input_grad[0]:
+            dx = _head_gemm(dh, p_w1t, 3, N=E)
         two = E == H  # square heads: both weight gradients in one launch (tt_head_wgrad2)
         if not on_side:
             if two:
@@ -902,14 +838,6 @@ class TowerHead(torch.autograd.Function):
         done.record(aux)
         side.add(done, zip(ctx.params, (dW1, db1, dW2, db2)))
         return dx, dW1, db1, dW2, db2
-
-
-def head_chain() -> bool:
-    """TT_HEAD_CHAIN=1: the tower head runs as two fused chains (tt_head_fwd_chain /
-    tt_head_bwd_chain: one launch per pass).  Off by default: at C3's 24,576 rows the chains take
-    54.6 / 56.2 us per pass against 46.7 / 46.8 us for the two tt_head_gemm launches they replace
-    (profiles/r05h_head_chain_ablations.txt); the outputs are bit-identical either way."""
-    return os.environ.get("TT_HEAD_CHAIN", "0") == "1"
 
 
 def head_wgrad(G: torch.Tensor, X: torch.Tensor, dW: torch.Tensor | None = None,
@@ -1026,7 +954,6 @@ def _triplet_bwd(q, p, n, margin, g, dq, dp, dn):
 class TripletLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, p, n, margin):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(q, p, n)
         q, p, n = (_contig_f32(t, nm) for t, nm in ((q, "q"), (p, "p"), (n, "n")))
         ctx.save_for_backward(q, p, n)
@@ -1047,7 +974,6 @@ class TripletLossPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qpn, margin):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(qpn)
         qpn = _contig_f32(qpn, "qpn")
         q, p, n = torch.chunk(qpn, 3)
@@ -1068,7 +994,6 @@ class TripletLossPacked(torch.autograd.Function):
 class MultiNegLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, p, negs, inv_tau):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(q, p, negs)
         q, p, negs = _contig_f32(q, "q"), _contig_f32(p, "p"), _contig_f32(negs, "negs")
         B, H = q.shape
@@ -1100,7 +1025,6 @@ class MultiNegLossPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qpn, B, K, inv_tau):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(qpn)
         qpn = _contig_f32(qpn, "qpn")
         H = qpn.shape[1]
@@ -1189,7 +1113,6 @@ def _inbatch_bwd(meta, q, d, lse, dqu, ws, g, dq, dd, mean=None):
 class InBatchSoftmaxLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, d, inv_tau, label_off, compute_dtype, grad_scale):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(q, d)
         q, d = _contig_f32(q, "q"), _contig_f32(d, "d")
         want_grad = bool(ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
@@ -1212,7 +1135,6 @@ class InBatchSoftmaxLossPacked(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qd, nq, inv_tau, compute_dtype, grad_scale):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         require_gpu(qd)
         prep = qd.__dict__.pop("_tt_inbatch_prep", None)  # taken once (TowerHead under scorer_prep)
         qd = _contig_f32(qd, "qd")
@@ -1319,7 +1241,6 @@ class InBatchSoftmaxLossOwned(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q, d, inv_tau, compute_dtype, grad_scale, group):
-        flush_plans()  # a split sort plan's second half runs beside the loss
         from .distributed import all_gather_rows
 
         require_gpu(q, d)
