@@ -203,6 +203,7 @@ int tt_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
  * TT_ADAM_MAX_TENSORS tensors in one launch, each with its own args. */
 #define TT_ADAM_ARGS_BYTES 32
 #define TT_ADAM_MAX_TENSORS 16
+#define TT_ADAM_TICKET_WORDS 16 /* tt_adamw_multi_ex's ticket: zeroed device words (it uses 9) */
 typedef struct {
   float* step;
   void* args;
@@ -229,8 +230,9 @@ int tt_adamw_multi(const tt_adamw_tensor* tensors, int count, tt_stream_t stream
  * part[s * stride + k], s < slabs, the same sum tt_head_wgrad2_reduce forms, written to
  * tensors[i].grad (which must then be writable, 16-byte aligned, n % 4 == 0) and used -- and
  * (2) run tt_adam_prepare_ex(next, nnext, ..., increment 1, ahead 1) in the same launch, after
- * every update has read its scalars (the last workgroup to finish, by a ticket: `ticket` is one
- * zeroed device unsigned the kernel leaves zeroed).  parts may be NULL; nnext 0 skips (2).
+ * every update has read its scalars (the last workgroup to finish, by a ticket: `ticket` is
+ * TT_ADAM_TICKET_WORDS zeroed device unsigneds the kernel leaves zeroed).  parts may be NULL;
+ * nnext 0 skips (2).
  * The tail of a step as one launch instead of slab sums + updates + prepare. */
 typedef struct {
   const float* part;

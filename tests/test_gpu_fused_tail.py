@@ -8,7 +8,7 @@ import pytest
 import torch
 
 import twotower_amd as tt
-from twotower_amd import ops
+from twotower_amd import _lib, ops
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -45,10 +45,10 @@ def test_adamw_multi_ex_equals_reduce_update_prepare(rows):
         if fused:
             sums = ops._Wgrad2Sums(ws, [p for p, _, _ in params]).grad_parts()
             parts = [sums[id(p)] for p, _, _ in params] + [None]
-            ticket = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ticket = torch.zeros(_lib.TT_ADAM_TICKET_WORDS, dtype=torch.int32, device=DEV)
             ops.adamw_multi_ex(items, parts, slots, ticket=ticket, **hyper)
             torch.cuda.synchronize()
-            assert int(ticket.item()) == 0  # left zeroed for the next launch
+            assert not bool(ticket.any())  # left zeroed for the next launch
         else:
             ops.head_wgrad2_reduce(ws, *grads)
             ops.adamw_multi(items)
@@ -67,7 +67,7 @@ def test_adamw_multi_ex_prepare_only():
     for fused in (False, True):
         st, a = torch.full((), 2.0, device=DEV), torch.zeros(8, device=DEV)
         if fused:
-            ops.adamw_multi_ex([], None, [(st, a)], ticket=torch.zeros(1, dtype=torch.int32, device=DEV), **hyper)
+            ops.adamw_multi_ex([], None, [(st, a)], ticket=torch.zeros(_lib.TT_ADAM_TICKET_WORDS, dtype=torch.int32, device=DEV), **hyper)
         else:
             ops.adam_prepare([(st, a)], increment=1, ahead=1, **hyper)
         torch.cuda.synchronize()

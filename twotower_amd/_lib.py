@@ -31,6 +31,7 @@ _c_f64 = ctypes.c_double
 
 TT_ADAM_ARGS_BYTES = 32
 TT_ADAM_MAX_TENSORS = 16
+TT_ADAM_TICKET_WORDS = 16
 
 
 class AdamSlot(ctypes.Structure):

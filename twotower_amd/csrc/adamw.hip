@@ -111,12 +111,15 @@ __global__ void adam_prepare_kernel(PrepArgs pa, int count, double lr, double be
 // tt_adamw_multi_ex: tensors with slab partials form their gradient first (the sums of
 // tt_head_wgrad2_reduce, bit for bit), write it to .grad and update; the last workgroup to
 // finish (ticket) advances the counters and forms the next step's scalars (prepare_slot with
-// increment 1, ahead 1), after every workgroup has read this step's.
+// increment 1, ahead 1), after every workgroup has read this step's.  One flat grid: tensor i
+// owns blocks [start[i], start[i + 1]), sized to its own work (a bias takes two, not as many as
+// the largest tensor).
 struct MultiExArgs {
   tt_adamw_tensor t[TT_ADAM_MAX_TENSORS];
   tt_adamw_grad_parts g[TT_ADAM_MAX_TENSORS];
   tt_adam_slot next[TT_ADAM_MAX_TENSORS];
-  int nnext;
+  int start[TT_ADAM_MAX_TENSORS + 1];
+  int count, nnext;
   double lr, beta1, beta2, eps, wd;
   unsigned* ticket;
 };
@@ -136,11 +139,37 @@ __device__ __forceinline__ void adam_update4(f32x4* p, f32x4* m, f32x4* v, int64
   v[i] = vv;
 }
 
+// Was this workgroup the last of the launch to finish?  Two levels of relaxed device-scope
+// counters: ticket[b % 8] counts the workgroups of one of eight groups, the last of a group
+// counts into ticket[8].  One counter taking every workgroup's increment serialises them at the
+// memory side (round 2: ≈ 10 us over ~1,000 workgroups, MI355X_MICROARCH.md 'dequeue': one word
+// saturates at ≈ 88 increments per us); eight words take an eighth each.  Every wave has waited
+// for its own loads before the increment, so the last workgroup's writes follow every read.
+__device__ bool last_workgroup(unsigned* ticket, unsigned b, unsigned total) {
+  __shared__ unsigned last;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = b & 7u, groups = total < 8u ? total : 8u;
+    const unsigned in_group = (total - g + 7u) / 8u;
+    bool l = false;
+    if (__hip_atomic_fetch_add(ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_group - 1u)
+      l = __hip_atomic_fetch_add(ticket + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1u;
+    last = l;
+  }
+  __syncthreads();
+  return last;
+}
+
 __global__ __launch_bounds__(kBlock) void adamw_multi_ex_kernel(MultiExArgs ma) {
   __shared__ f32x4 red[kRedQ][64];
-  const tt_adamw_tensor& t = ma.t[blockIdx.y];
-  const tt_adamw_grad_parts& gp = ma.g[blockIdx.y];
-  if (t.n > 0) {
+  const int b = blockIdx.x;
+  int ti = 0;
+  while (ti < ma.count && b >= ma.start[ti + 1]) ++ti;  // wave-uniform: <= 16 compares
+  if (ti < ma.count && ma.t[ti].n > 0) {
+    const tt_adamw_tensor& t = ma.t[ti];
+    const tt_adamw_grad_parts& gp = ma.g[ti];
+    const int64_t lb = b - ma.start[ti], nb = ma.start[ti + 1] - ma.start[ti];
     const AdamArgs a = *static_cast<const AdamArgs*>(t.args);
     f32x4* p4 = reinterpret_cast<f32x4*>(t.param);
     f32x4* m4 = reinterpret_cast<f32x4*>(t.exp_avg);
@@ -154,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void adamw_multi_ex_kernel(MultiExArgs ma) 
       const int s0 = qq * per, s1 = min(gp.slabs, s0 + per);
       const int64_t n4 = t.n / 4;
       const f32x4* part4 = reinterpret_cast<const f32x4*>(gp.part);
-      for (int64_t base = (int64_t)blockIdx.x * 64; base < n4; base += (int64_t)gridDim.x * 64) {
+      for (int64_t base = lb * 64; base < n4; base += nb * 64) {
         const int64_t i = base + o;
         red[qq][o] = i < n4 ? sum_slabs(part4 + i, (size_t)gp.stride / 4, s0, s1) : f32x4{0.f, 0.f, 0.f, 0.f};
         __syncthreads();
@@ -169,10 +198,10 @@ __global__ __launch_bounds__(kBlock) void adamw_multi_ex_kernel(MultiExArgs ma) 
       const bool vec = ((reinterpret_cast<uintptr_t>(t.param) | reinterpret_cast<uintptr_t>(t.grad) |
                          reinterpret_cast<uintptr_t>(t.exp_avg) | reinterpret_cast<uintptr_t>(t.exp_avg_sq)) & 15) == 0;
       const int64_t n4 = vec ? t.n / 4 : 0;
-      const int64_t stride = (int64_t)gridDim.x * kBlock;
-      for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride)
+      const int64_t stride = nb * kBlock;
+      for (int64_t i = lb * kBlock + threadIdx.x; i < n4; i += stride)
         adam_update4(p4, m4, v4, i, reinterpret_cast<const f32x4*>(t.grad)[i], a);
-      for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < t.n; i += stride) {
+      for (int64_t i = n4 * 4 + lb * kBlock + threadIdx.x; i < t.n; i += stride) {
         float pp = t.param[i], mm = t.exp_avg[i], vv = t.exp_avg_sq[i];
         adam_update(pp, t.grad[i], mm, vv, a);
         t.param[i] = pp;
@@ -182,23 +211,11 @@ __global__ __launch_bounds__(kBlock) void adamw_multi_ex_kernel(MultiExArgs ma) 
     }
   }
   if (ma.nnext == 0) return;
-  __shared__ unsigned last;
-  // The ticket orders only this launch's reads of the scalars before the last workgroup's
-  // writes of the next ones (the counters it reads were written by earlier launches): every
-  // wave waits for its own loads, then one relaxed device-scope increment per workgroup.  (A
-  // device-scope fence per workgroup, i.e. an L2 write-back on each of 1,000 workgroups right
-  // after the table update, made the launch 68 us instead of a few.)
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned total = gridDim.x * gridDim.y;
-    last = __hip_atomic_fetch_add(ma.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
-  }
-  __syncthreads();
-  if (!last) return;
+  if (!last_workgroup(ma.ticket, (unsigned)b, gridDim.x)) return;
   if ((int)threadIdx.x < ma.nnext)
     prepare_slot(ma.next[threadIdx.x], ma.lr, ma.beta1, ma.beta2, ma.eps, ma.wd, 1.f, 1.f);
-  if (threadIdx.x == 0) __hip_atomic_store(ma.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 9)  // every count is in: reset the nine words for the next launch
+    __hip_atomic_store(ma.ticket + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 static_assert(sizeof(AdamArgs) <= TT_ADAM_ARGS_BYTES, "AdamArgs does not fit TT_ADAM_ARGS_BYTES");
@@ -288,7 +305,6 @@ extern "C" int tt_adamw_multi_ex(const tt_adamw_tensor* tensors, const tt_adamw_
   TT_REQUIRE(count == 0 || tensors != nullptr, "null tensors");
   TT_REQUIRE(nnext == 0 || (next != nullptr && ticket != nullptr), "nnext=%d needs slots and a ticket", nnext);
   MultiExArgs ma{};
-  int64_t nmax = 0;
   for (int i = 0; i < count; ++i) {
     const tt_adamw_tensor& t = tensors[i];
     TT_REQUIRE(t.n >= 0, "tensor %d: n=%lld", i, (long long)t.n);
@@ -304,13 +320,13 @@ extern "C" int tt_adamw_multi_ex(const tt_adamw_tensor* tensors, const tt_adamw_
                  "tensor %d: slab partials need 16-byte aligned buffers", i);
       ma.g[i] = g;
     }
-    nmax = std::max(nmax, t.n);
   }
   for (int i = 0; i < nnext; ++i) {
     TT_REQUIRE(next[i].step && next[i].args, "null step/args in slot %d", i);
     TT_REQUIRE((reinterpret_cast<uintptr_t>(next[i].args) & 3) == 0, "args of slot %d misaligned", i);
     ma.next[i] = next[i];
   }
+  ma.count = count;
   ma.nnext = nnext;
   ma.lr = lr;
   ma.beta1 = beta1;
@@ -319,12 +335,19 @@ extern "C" int tt_adamw_multi_ex(const tt_adamw_tensor* tensors, const tt_adamw_
   ma.wd = weight_decay;
   ma.ticket = ticket;
   if (count == 0 && nnext == 0) return TT_OK;
-  int64_t bx = (nmax / 4 + kBlock - 1) / kBlock + 1;
-  for (int i = 0; i < count; ++i)
-    if (ma.g[i].part) bx = std::max<int64_t>(bx, (tensors[i].n / 4 + 63) / 64);
-  bx = std::min<int64_t>(bx, 512);
-  adamw_multi_ex_kernel<<<dim3((unsigned)bx, (unsigned)std::max(count, 1)), dim3(kBlock), 0,
-                          reinterpret_cast<hipStream_t>(stream)>>>(ma);
+  // blocks per tensor: its own vec4 grid-stride cover (+1 for a scalar tail), or one block per 64
+  // outputs when it sums slab partials; at most 512 each
+  int total = 0;
+  for (int i = 0; i < count; ++i) {
+    ma.start[i] = total;
+    const int64_t n = tensors[i].n;
+    int64_t nb = n > 0 ? (n / 4 + kBlock - 1) / kBlock + 1 : 0;
+    if (ma.g[i].part) nb = std::max<int64_t>(nb, (n / 4 + 63) / 64);
+    total += (int)std::min<int64_t>(nb, 512);
+  }
+  ma.start[count] = total;
+  if (total == 0) total = 1;  // scalars only: one workgroup
+  adamw_multi_ex_kernel<<<dim3((unsigned)total), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream)>>>(ma);
   TT_LAUNCH_CHECK("tt_adamw_multi_ex");
   return TT_OK;
 }

@@ -336,8 +336,8 @@ class AdamW(torch.optim.Optimizer):
         # form the head weight gradients from their side-stream slab partials themselves (the sums
         # of tt_head_wgrad2_reduce, bit for bit, also written to .grad; tt_adamw_multi_ex).  The
         # next step's scalars stay a launch of their own: formed by the same launch's last
-        # workgroup they cost more than that launch (round 2: one same-address device-scope
-        # increment per workgroup, 1,000 of them, serialising at the memory side).
+        # workgroup (two-level ticket) the step measured the same, 0.8446-0.8486 against
+        # 0.8407-0.8484 ms (profiles/r06s_prepare_in_tail_ab.txt; round 2's single counter cost more).
         fuse = (os.environ.get("TT_FUSED_TAIL", "1") != "0" and len(dense) <= _lib.TT_ADAM_MAX_TENSORS
                 and len(slots) <= _lib.TT_ADAM_MAX_TENSORS and (dense or ahead))
         parts = self._side_grads.join(claim={i for i in dense_ids if i is not None} if fuse else None)
@@ -345,7 +345,7 @@ class AdamW(torch.optim.Optimizer):
             dev = (dense[0][0] if dense else slots[0][0]).device
             ticket = self._tickets.get(dev)
             if ticket is None:
-                ticket = self._tickets[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+                ticket = self._tickets[dev] = torch.zeros(_lib.TT_ADAM_TICKET_WORDS, dtype=torch.int32, device=dev)
             ops.adamw_multi_ex(dense, [parts.get(i) if i is not None else None for i in dense_ids], [], lr=lr,
                                beta1=b1, beta2=b2, eps=eps, weight_decay=wd, ticket=ticket)
             join_shards()
