@@ -517,8 +517,8 @@ def plain_loop_entry(cfg, loss_fn, batches, dev, steps: int, trainstep_ms: float
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)  # >= 50 timed steps after 10 warm-up
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--scorer-dtype", default=None, help="override: fp32 | bf16 | bf16_split")
     ap.add_argument("--no-cpu-baseline", action="store_true")

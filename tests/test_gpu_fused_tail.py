@@ -60,6 +60,39 @@ def test_adamw_multi_ex_equals_reduce_update_prepare(rows):
     assert all(float(s) == 5.0 for s in runs[1][-10::2])
 
 
+@pytest.mark.parametrize("sizes", [(1000,), (1000, 3000, 50), (1000,) * 5, (70000, 5, 9)])
+def test_adamw_multi_ex_ticket_any_grid(sizes):
+    """The two-level last-workgroup ticket on grids of 2, 8, 10 and 74 workgroups (fewer than,
+    equal to and not a multiple of its eight groups; odd sizes take the scalar tail): the update
+    and the next scalars equal the separate launches, and the nine ticket words are left zeroed
+    for the next launch."""
+    hyper = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01)
+    runs = []
+    for fused in (False, True):
+        r = np.random.default_rng(11)
+        items, slots = [], []
+        for n in sizes:
+            p, m, v = _state((n,), r)
+            g = torch.as_tensor(r.standard_normal(n).astype(np.float32)).to(DEV)
+            st, a = torch.full((), 2.0, device=DEV), torch.zeros(8, device=DEV)
+            ops.adam_prepare([(st, a)], increment=0, ahead=1, **hyper)
+            items.append((p, g, m, v, a))
+            slots.append((st, a))
+        ticket = torch.zeros(_lib.TT_ADAM_TICKET_WORDS, dtype=torch.int32, device=DEV)
+        for _ in range(3):  # the ticket is reused across launches
+            if fused:
+                ops.adamw_multi_ex(items, None, slots, ticket=ticket, **hyper)
+            else:
+                ops.adamw_multi(items)
+                ops.adam_prepare(slots, increment=1, ahead=1, **hyper)
+        torch.cuda.synchronize()
+        assert not bool(ticket.any())
+        runs.append([t.clone() for it in items for t in it[:4]] + [t.clone() for sl in slots for t in sl])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    assert all(float(s) == 5.0 for s in runs[1][-2 * len(sizes)::2])
+
+
 def test_adamw_multi_ex_prepare_only():
     """No tensors, only the next step's scalars (a launch of one workgroup)."""
     hyper = dict(lr=2e-3, beta1=0.8, beta2=0.99, eps=1e-6, weight_decay=0.1)
