@@ -291,7 +291,9 @@ __device__ __forceinline__ int piece_len(int len) {
 //           offset) + the entry's rank among the tile's entries of its digit, in entry order, so
 //           every pass is stable and the result is THE stable sort of (key, seq) by key.
 // Pass 0 reads the ids directly (the key and the sequence index are formed on the fly), so no
-// keys/values arrays are staged.  The in-tile rank: entry j of a tile sits at wave j / 256,
+// keys/values arrays are staged, and drops the masked slots (pads, ids >= V: 46 % of C3's slots),
+// so the later passes and the segment starts handle the tokens only; the tokens' order is the
+// same as when the masked slots sorted last under key V.  The in-tile rank: entry j of a tile sits at wave j / 256,
 // step (j / 64) % 4, lane j % 64; a wave forms each step's same-digit lane set with D ballots,
 // and keeps its running per-digit counts in its own LDS row; the wave offsets per digit are an
 // exclusive scan over the waves' rows.  Bytes per pass: keys (+ values) read twice, written once.
@@ -309,6 +311,13 @@ struct SortSrc {  // pass 0: ids (keys == nullptr); later passes: the previous p
   const uint32_t* keys;
   const int32_t* vals;
   double inv_L;  // 1 / L: the entry -> (sequence, position) split without a 64-bit division
+  const int32_t* nvalid;  // passes after the first: the first pass's output length (device)
+  // entries this pass reads: every id slot in the first pass (masked ones are dropped there),
+  // the first pass's valid entries after it
+  __device__ __forceinline__ int64_t count(int64_t n) const { return keys ? (int64_t)*nvalid : n; }
+  // an entry the pass keeps: the first pass drops the masked slots (key V: pads, ids >= V), so
+  // the later passes and the segment starts see only the tokens (stable: their order is kept)
+  __device__ __forceinline__ bool keep(uint32_t key) const { return keys || key != (uint32_t)V; }
   __device__ __forceinline__ void load(int64_t i, uint32_t& key, int32_t& val) const {
     if (keys) {
       key = keys[i];
@@ -357,6 +366,7 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
                                                                        int32_t* __restrict__ cnt) {
   __shared__ int32_t h[1 << kSortMaxD];
   const int nd = 1 << D;
+  const int64_t ne = src.count(n);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // (a capped grid walks tiles)
     for (int d = threadIdx.x; d < nd; d += kSortThreads) h[d] = 0;
     __syncthreads();
@@ -364,11 +374,11 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
 #pragma unroll
     for (int k = 0; k < kSortIPT; ++k) {
       const int64_t i = base + k * kSortThreads + threadIdx.x;
-      if (i < n) {
+      if (i < ne) {
         uint32_t key;
         int32_t val;
         src.load(i, key, val);
-        atomicAdd(&h[(key >> shift) & (nd - 1)], 1);
+        if (src.keep(key)) atomicAdd(&h[(key >> shift) & (nd - 1)], 1);
       }
     }
     __syncthreads();
@@ -422,7 +432,8 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
                                                                          const int32_t* __restrict__ cnt,
                                                                          const int32_t* __restrict__ total,
                                                                          uint32_t* __restrict__ keys_out,
-                                                                         int32_t* __restrict__ vals_out) {
+                                                                         int32_t* __restrict__ vals_out,
+                                                                         int32_t* __restrict__ nvalid_out) {
   constexpr int ND = 1 << D;
   constexpr int DPT = (ND + kSortThreads - 1) / kSortThreads;  // digits per thread in the digit scans
   __shared__ int32_t hw[kSortWaves][ND];  // per-wave running counts, then per-wave tile offsets
@@ -432,26 +443,28 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
   __shared__ int32_t sv[kSortTile];       // writes of a digit's run are consecutive lanes)
   __shared__ int32_t wsum[kSortWaves];
   const int w = threadIdx.x >> 6, lane = lane_id();
+  const int64_t ne = src.count(n);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // (a capped grid walks tiles)
     for (int d = threadIdx.x; d < kSortWaves * ND; d += kSortThreads) (&hw[0][0])[d] = 0;
     __syncthreads();
 
     const int64_t base = (int64_t)tile * kSortTile;
     const int64_t wbase = base + (int64_t)w * (kWave * kSortIPT);
-    const int tile_n = (int)(n - base < kSortTile ? n - base : kSortTile);
     const uint64_t lt = (uint64_t(1) << lane) - 1;
     uint32_t key[kSortIPT];
     int32_t val[kSortIPT], rk[kSortIPT];
+    bool kept[kSortIPT];
   #pragma unroll
     for (int k = 0; k < kSortIPT; ++k) {
       const int64_t i = wbase + k * kWave + lane;
       key[k] = 0;
       val[k] = 0;
-      if (i < n) src.load(i, key[k], val[k]);
+      if (i < ne) src.load(i, key[k], val[k]);
+      kept[k] = i < ne && src.keep(key[k]);
     }
   #pragma unroll
     for (int k = 0; k < kSortIPT; ++k) {
-      const bool ok = wbase + k * kWave + lane < n;
+      const bool ok = kept[k];
       const int d = (int)((key[k] >> shift) & (ND - 1));
       uint64_t peers = __ballot(ok);
   #pragma unroll
@@ -485,8 +498,10 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
       part += tv[j];
       tpart += tl[j];
     }
-    int32_t run = sort_block_excl_scan(part, wsum, nullptr);
-    int32_t trun = sort_block_excl_scan(tpart, wsum, nullptr);
+    int32_t all = 0, tile_n = 0;  // every digit's total (the pass's output length), this tile's share
+    int32_t run = sort_block_excl_scan(part, wsum, &all);
+    int32_t trun = sort_block_excl_scan(tpart, wsum, &tile_n);
+    if (nvalid_out && tile == 0 && threadIdx.x == 0) *nvalid_out = all;
   #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const int d = threadIdx.x * DPT + j;
@@ -500,7 +515,7 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
     __syncthreads();
   #pragma unroll
     for (int k = 0; k < kSortIPT; ++k) {
-      if (wbase + k * kWave + lane < n) {
+      if (kept[k]) {
         const int d = (int)((key[k] >> shift) & (ND - 1));
         const int lp = tst[d] + hw[w][d] + rk[k];
         sk[lp] = key[k];
@@ -530,9 +545,11 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
 // allocates from.  (Round 3: one thread per boundary, 6,144 workgroups at C3, 4.8 us alone but
 // 25 us beside the gather; four per thread dispatch a quarter of the workgroups.)
 constexpr int kStartsPT = 4;
-__global__ __launch_bounds__(kBlock) void bag_plan_starts_kernel(const uint32_t* __restrict__ keys, int64_t n,
-                                                                 int64_t V, int32_t* __restrict__ seg_start,
+__global__ __launch_bounds__(kBlock) void bag_plan_starts_kernel(const uint32_t* __restrict__ keys,
+                                                                 const int32_t* __restrict__ nvalid, int64_t V,
+                                                                 int32_t* __restrict__ seg_start,
                                                                  int32_t* __restrict__ n_pieces) {
+  const int64_t n = *nvalid;  // the sorted tokens (masked slots were dropped by the first pass)
   const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kStartsPT;
   if (i0 == 0) *n_pieces = 0;
   if (i0 > n) return;
@@ -1263,7 +1280,8 @@ SortShape sort_shape(int64_t n, int64_t V) {
 }
 size_t sort_tmp_bytes(int64_t n, int64_t V) {
   const SortShape sh = sort_shape(n, V);
-  return align_up(((size_t)sh.ntiles + 1) * ((size_t)1 << sh.D) * 4, 256);
+  // digit-major tile counts, the digit totals, then the first pass's output length
+  return align_up((((size_t)sh.ntiles + 1) * ((size_t)1 << sh.D) + 1) * 4, 256);
 }
 
 // planes != nullptr: the split workgroups of tt_bag_mean_fwd_split first (E in the templated set)
@@ -1385,7 +1403,8 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   const unsigned sgrid = (unsigned)sh.ntiles;
   int32_t* cnt = static_cast<int32_t*>(w.sort_tmp);
   int32_t* total = cnt + (size_t)nd * sh.ntiles;
-  SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr, L > 0 ? 1.0 / (double)L : 0.0};
+  int32_t* nvalid = total + nd;  // written by the first pass's scatter
+  SortSrc<IdT> src{ids, L, ld, V, padding_idx, nullptr, nullptr, L > 0 ? 1.0 / (double)L : 0.0, nvalid};
   const int p_begin = part == 1 ? sh.P - 1 : 0, p_end = part == 0 ? sh.P - 1 : sh.P;
   if (p_begin > 0) {  // the previous pass's output (pass p writes _out when P - 1 - p is even)
     const bool prev_out = ((sh.P - 1 - (p_begin - 1)) & 1) == 0;
@@ -1408,7 +1427,8 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   case DD:                                                                                                \
     plan_sort_scatter_kernel<IdT, DD><<<dim3(sgrid), dim3(kSortThreads), 0, s>>>(src, n, shift,            \
                                                                                              sh.ntiles, cnt, \
-                                                                                             total, ko, vo);  \
+                                                                                             total, ko, vo,   \
+                                                                                             p == 0 ? nvalid : nullptr); \
     break;
       TT_SC(1) TT_SC(2) TT_SC(3) TT_SC(4) TT_SC(5) TT_SC(6) TT_SC(7) TT_SC(8) TT_SC(9) TT_SC(10) TT_SC(11)
 #undef TT_SC
@@ -1420,8 +1440,8 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
   }
   if (part == 0) return TT_OK;
   const int64_t nst = (n + 1 + kStartsPT - 1) / kStartsPT;
-  bag_plan_starts_kernel<<<dim3((unsigned)((nst + kBlock - 1) / kBlock)), block, 0, s>>>(w.keys_out, n, V, w.seg_start,
-                                                                                       w.piece_off + V);
+  bag_plan_starts_kernel<<<dim3((unsigned)((nst + kBlock - 1) / kBlock)), block, 0, s>>>(w.keys_out, nvalid, V,
+                                                                                       w.seg_start, w.piece_off + V);
   TT_LAUNCH_CHECK("bag_plan_starts");
   bag_plan_pieces_kernel<<<dim3((unsigned)((V + 1 + kBlock - 1) / kBlock)), block, 0, s>>>(
       w.seg_start, V, w.nch, w.piece_off, w.piece_beg, w.piece_end);
