@@ -367,7 +367,10 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
   __shared__ int32_t h[1 << kSortMaxD];
   const int nd = 1 << D;
   const int64_t ne = src.count(n);
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // (a capped grid walks tiles)
+  // tiles past the entries (a later pass reads fewer entries than the grid was sized for): no
+  // counts -- the scan and the scatter stop at the last tile that holds entries
+  const int64_t nt = (ne + kSortTile - 1) / kSortTile;
+  for (int64_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {  // (a capped grid walks tiles)
     for (int d = threadIdx.x; d < nd; d += kSortThreads) h[d] = 0;
     __syncthreads();
     const int64_t base = tile * kSortTile;
@@ -397,11 +400,14 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_count_kernel(SortSrc<I
 constexpr int kScanWaves = 2;
 constexpr int kScanChunks = 16;  // chunks of 64 tiles held per lane: 1,024 tiles per round
 __global__ __launch_bounds__(kScanWaves * kWave) void plan_sort_scan_kernel(int32_t* __restrict__ cnt, int64_t ntiles,
-                                                                            int nd, int32_t* __restrict__ total) {
+                                                                            int nd, int32_t* __restrict__ total,
+                                                                            const int32_t* __restrict__ nvalid) {
   const int d = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
   if (d >= nd) return;
   const int lane = lane_id();
-  int32_t* row = cnt + (int64_t)d * ntiles;
+  int32_t* row = cnt + (int64_t)d * ntiles;  // (rows keep the grid's stride)
+  // a later pass: only the tiles holding the first pass's output (the rest were not counted)
+  if (nvalid) ntiles = ((int64_t)*nvalid + kSortTile - 1) / kSortTile;
   int32_t carry = 0;
   for (int64_t t0 = 0; t0 < ntiles; t0 += kScanChunks * kWave) {
     int32_t x[kScanChunks];
@@ -444,6 +450,8 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
   __shared__ int32_t wsum[kSortWaves];
   const int w = threadIdx.x >> 6, lane = lane_id();
   const int64_t ne = src.count(n);
+  const int64_t row_stride = ntiles;  // the count matrix's digit rows keep the grid's stride
+  ntiles = (ne + kSortTile - 1) / kSortTile;  // tiles past the entries: nothing to place
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {  // (a capped grid walks tiles)
     for (int d = threadIdx.x; d < kSortWaves * ND; d += kSortThreads) (&hw[0][0])[d] = 0;
     __syncthreads();
@@ -506,7 +514,7 @@ __global__ __launch_bounds__(kSortThreads) void plan_sort_scatter_kernel(SortSrc
     for (int j = 0; j < DPT; ++j) {
       const int d = threadIdx.x * DPT + j;
       if (d < ND) {
-        gdst[d] = run + cnt[(int64_t)d * ntiles + tile];
+        gdst[d] = run + cnt[(int64_t)d * row_stride + tile];
         tst[d] = trun;
       }
       run += tv[j];
@@ -1420,7 +1428,7 @@ int plan_front(const IdT* ids, int64_t nseq, int L, int64_t ld, int64_t V, int64
                                                                                        sh.ntiles, cnt);
     TT_LAUNCH_CHECK("plan_sort_count");
     plan_sort_scan_kernel<<<dim3((unsigned)((nd + kScanWaves - 1) / kScanWaves)), dim3(kScanWaves * kWave), 0, s>>>(
-        cnt, sh.ntiles, nd, total);
+        cnt, sh.ntiles, nd, total, p == 0 ? nullptr : nvalid);
     TT_LAUNCH_CHECK("plan_sort_scan");
     switch (sh.D) {
 #define TT_SC(DD)                                                                                         \
