@@ -192,7 +192,13 @@ class TrainStep:
             dst.copy_(src)
         graph = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(graph):
+        # thread-local capture mode: a process group's watchdog thread polls the events of the
+        # collectives issued before the capture (hipEventQuery); under the default global mode
+        # that query is refused while this thread captures and the watchdog aborts the process
+        # (seen once in the one-rank RCCL graph test: "operation not permitted when stream is
+        # capturing" from the ProcessGroupNCCL watchdog).  Calls made by this thread are checked
+        # as before.
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             static_loss = self.eager(*static_in)
         return graph, static_all, static_loss
 
