@@ -619,8 +619,9 @@ __global__ __launch_bounds__(kBlock) void bag_piece_sum_kernel(const int32_t* __
   constexpr int RPI = kWave / LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
-  const int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
-  if (pc >= piece_off[V]) return;
+  const int64_t np = piece_off[V];
+  const int64_t pstride = (int64_t)gridDim.x * kWavesPerBlock * RPI;
+  for (int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub; pc < np; pc += pstride) {
   const int st = piece_beg[pc], en = piece_end[pc];
   f32x4 part[U][NV];
 #pragma unroll
@@ -650,6 +651,7 @@ __global__ __launch_bounds__(kBlock) void bag_piece_sum_kernel(const int32_t* __
     for (int u = 1; u < U; ++u) a += part[u][k];
     reinterpret_cast<f32x4*>(partial + pc * E)[k * LPR + c] = a;
   }
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void bag_piece_sum_generic_kernel(const int32_t* __restrict__ piece_off,
@@ -658,13 +660,15 @@ __global__ __launch_bounds__(kBlock) void bag_piece_sum_generic_kernel(const int
                                                                        const int32_t* __restrict__ vals,
                                                                        const float* __restrict__ gs, int E,
                                                                        float* __restrict__ partial) {
-  const int64_t pc = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (pc >= piece_off[V]) return;
-  const int st = piece_beg[pc], en = piece_end[pc];
-  for (int c = lane_id(); c < E; c += kWave) {
-    float acc = 0.f;
-    for (int e = st; e < en; ++e) acc += gs[(int64_t)vals[e] * E + c];
-    partial[pc * E + c] = acc;
+  const int64_t np = piece_off[V];
+  for (int64_t pc = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); pc < np;
+       pc += (int64_t)gridDim.x * kWavesPerBlock) {
+    const int st = piece_beg[pc], en = piece_end[pc];
+    for (int c = lane_id(); c < E; c += kWave) {
+      float acc = 0.f;
+      for (int e = st; e < en; ++e) acc += gs[(int64_t)vals[e] * E + c];
+      partial[pc * E + c] = acc;
+    }
   }
 }
 
@@ -1018,9 +1022,10 @@ __global__ __launch_bounds__(kBlock) void bag_col_piece_sum_kernel(const int32_t
   constexpr int LD = kColPieceLD;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
-  const int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   const unsigned long long n = *cnt;
-  if (pc >= (int64_t)(n & 0xffffffffu)) return;
+  const int64_t npc = (int64_t)(n & 0xffffffffu), pstride = (int64_t)gridDim.x * kWavesPerBlock * RPI;
+  for (int64_t pc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub; pc < npc;
+       pc += pstride) {  // (a grid of at most one round: its sub-waves walk the pieces)
   const int h = hot_entry(hot_k0, (int)(n >> 32), pc);
   const int64_t r = hot_row[h];
   const int len = plen[r], t = piece_len_col(len);
@@ -1062,6 +1067,7 @@ __global__ __launch_bounds__(kBlock) void bag_col_piece_sum_kernel(const int32_t
   }
   rotate_parts(part, (4 - done % 4) % 4);  // back to part[j] = entries j (mod 4)
   reinterpret_cast<f32x4*>(partial + pc * El)[c] = part[0] + part[1] + part[2] + part[3];
+  }
 }
 
 // One sub-wave per group of <= kMaxPieces piece partials (rows of more than kMaxPieces pieces).
@@ -1077,9 +1083,10 @@ __global__ __launch_bounds__(kBlock) void bag_col_group_sum_kernel(const unsigne
   constexpr int El = 4 * LPR;
   const int lane = lane_id();
   const int sub = lane / LPR, c = lane % LPR;
-  const int64_t gc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub;
   const unsigned long long n = cnt[1];
-  if (gc >= (int64_t)(n & 0xffffffffu)) return;
+  const int64_t ngc = (int64_t)(n & 0xffffffffu), gstride = (int64_t)gridDim.x * kWavesPerBlock * RPI;
+  for (int64_t gc = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * RPI + sub; gc < ngc;
+       gc += gstride) {
   const int h = hot_entry(grp_g0, (int)(n >> 32), gc);
   const int64_t r = grp_row[h];
   const int k0 = off[r], np = nch[r];
@@ -1089,6 +1096,7 @@ __global__ __launch_bounds__(kBlock) void bag_col_group_sum_kernel(const unsigne
   for (int u = 0; u < 4; ++u) part[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   fold_rows<LPR>(partial, b, e, c, part);
   reinterpret_cast<f32x4*>(gpart + gc * El)[c] = part[0] + part[1] + part[2] + part[3];
+  }
 }
 
 struct ColPieces {  // the hot-row path's outputs (nch == nullptr: no pieces, every row merged)
@@ -1368,10 +1376,15 @@ int launch_reduce(const BwdWs& w, int64_t V, int E, float* grad, float* param, f
   return TT_OK;
 }
 
+constexpr int64_t kPieceSumMaxBlocks = 2048;  // 8 per CU: one round
+
 int launch_piece_sum(const BwdWs& w, int64_t V, int E, hipStream_t s) {
+  // the pieces are counted on the device (piece_off[V]); the grid covers the most a batch can have
+  // up to one round of waves on the chip (kPieceSumMaxBlocks), whose waves walk any further pieces:
+  // a batch without long rows (C3's uniform ids) then costs one short launch, not 6,000 workgroups
   auto grid_for = [&](int rpi) {
     const int64_t waves = (w.max_pieces + rpi - 1) / rpi;
-    return dim3((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+    return dim3((unsigned)std::min<int64_t>((waves + kWavesPerBlock - 1) / kWavesPerBlock, kPieceSumMaxBlocks));
   };
   const dim3 block(kBlock);
   switch (E) {
@@ -1832,8 +1845,9 @@ extern "C" int tt_bag_col_reduce_ex(const int32_t* seg_all, const int32_t* vals_
     TT_LAUNCH_CHECK("tt_bag_col_reduce (pieces)");
     pcs = ColPieces{w.nch, w.off, w.goff, w.partial, w.gpart};
   }
-  auto sub_grid = [&](int64_t n) {  // n sub-wave jobs of El columns each
-    return dim3((unsigned)std::max<int64_t>(1, ((n + rpi - 1) / rpi + kWavesPerBlock - 1) / kWavesPerBlock));
+  auto sub_grid = [&](int64_t n) {  // n sub-wave jobs of El columns each, at most one round of waves
+    return dim3((unsigned)std::min<int64_t>(
+        kPieceSumMaxBlocks, std::max<int64_t>(1, ((n + rpi - 1) / rpi + kWavesPerBlock - 1) / kWavesPerBlock)));
   };
 #define TT_COL(L)                                                                                             \
   do {                                                                                                        \
