@@ -110,10 +110,12 @@ int tt_bag_mean_bwd_planned(const float* d_pooled, const float* denom, int64_t n
                             int64_t V, int E, const void* plan, size_t plan_bytes,
                             float* grad_table, tt_stream_t stream);
 /* Where the plan's sorted output lies inside `plan` (byte offsets from the plan pointer rounded
- * up to 256 B): offs[0] the sorted row keys (nseq*L uint32), offs[1] their sequence indices
- * (nseq*L int32), offs[2] seg_start (V + 1 int32: row r's entries are [seg_start[r],
- * seg_start[r + 1]), r = V the masked tail).  The sort is the stable sort of the (row, seq) pairs
- * by row, so these are fixed by the ids: what the parity tests compare with a CPU stable sort. */
+ * up to 256 B): offs[0] the sorted row keys (room for nseq*L uint32), offs[1] their sequence
+ * indices (room for nseq*L int32), offs[2] seg_start (V + 1 int32: row r's entries are
+ * [seg_start[r], seg_start[r + 1])).  The sort is the stable sort of the kept (row, seq) pairs by
+ * row, so these are fixed by the ids: what the parity tests compare with a CPU stable sort.  The
+ * masked slots (pads, padding_idx, ids outside (0, V)) are dropped: seg_start[V] entries are
+ * written, the rest of the two arrays is unspecified. */
 int tt_bag_plan_layout(int64_t nseq, int L, int64_t V, int E, int64_t* offs);
 /* tt_bag_plan in two halves on one stream (same plan, same bytes): part 0 runs every sort pass
  * but the last, part 1 the last pass, the segment starts and the pieces, so a caller can place the
