@@ -222,6 +222,8 @@ _CAPTURE_ERRORS = (
     "graph capture",  # torch's / c10d's own guards ("... is not supported during (CUDA) graph capture")
     "is_current_stream_capturing",
     "capture_begin",
+    "hipstreamcapturestatus",  # torch's capture_end assert when another call invalidated the capture
+    "cudastreamcapturestatus",
 )
 # (the error-code enum names torch embeds in HIP/CUDA runtime errors cover the rest; messages seen
 # on this stack from collectives refused under capture: tests/test_host_cpu.py::test_capture_error_messages)
