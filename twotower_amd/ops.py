@@ -1391,9 +1391,14 @@ def adamw_multi_ex(items, parts: list | None, next_slots: list, *, lr: float, be
                    weight_decay: float, ticket: torch.Tensor) -> None:
     """One tt_adamw_multi_ex launch (at most 16 tensors, 16 next slots): items as adamw_multi;
     parts[i] None or (part pointer, stride, slabs, owner) whose fixed-order sum becomes items[i]'s
-    gradient; then the next step's scalars of next_slots (increment 1, ahead 1)."""
+    gradient; then the next step's scalars of next_slots (increment 1, ahead 1), formed by the
+    launch's last workgroup: `ticket` is a zeroed device int32 tensor of at least
+    TT_ADAM_TICKET_WORDS elements, left zeroed."""
     if len(items) > _lib.TT_ADAM_MAX_TENSORS or len(next_slots) > _lib.TT_ADAM_MAX_TENSORS:
         raise ValueError("adamw_multi_ex: at most 16 tensors and 16 slots per launch")
+    if next_slots and (ticket.dtype != torch.int32 or ticket.numel() < _lib.TT_ADAM_TICKET_WORDS
+                       or not ticket.is_contiguous()):
+        raise ValueError(f"adamw_multi_ex: ticket must be {_lib.TT_ADAM_TICKET_WORDS} contiguous int32 words")
     if not items and not next_slots:
         return
     stream = stream_of(items[0][0] if items else next_slots[0][0])
